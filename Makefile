@@ -1,0 +1,53 @@
+# Build recipe for the product library (libesgd.so, gfx950) and the CPU oracle.
+#   make            -> both
+#   make lib        -> eager-sgd_amd/esgd/libesgd.so
+#   make oracle     -> oracle/libffref.so
+# No -ffast-math anywhere: parity with fflib2 is bitwise (SURVEY.md §7 "Hard parts").
+
+ROCM      ?= /opt/rocm
+HIPCC     ?= $(ROCM)/bin/hipcc
+ARCH      ?= gfx950
+PKG       := eager-sgd_amd
+CSRC      := $(PKG)/csrc
+OUTLIB    := $(PKG)/esgd/libesgd.so
+BUILD     := build/obj
+
+HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off \
+             -Iinclude -I$(CSRC) -Wall -Wno-unused-result -D__HIP_PLATFORM_AMD__
+CXXFLAGS  := -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -I$(CSRC) \
+             -I$(ROCM)/include -D__HIP_PLATFORM_AMD__ -Wall
+LDFLAGS   := -shared -L$(ROCM)/lib -lamdhip64 -lrccl -lpthread -lrt \
+             -Wl,--no-undefined -Wl,-soname,libesgd.so \
+             -Wl,--version-script=$(CSRC)/exports.map
+
+HIP_SRCS  := $(wildcard $(CSRC)/*.hip)
+CPP_SRCS  := $(wildcard $(CSRC)/*.cpp)
+OBJS      := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.hip.o,$(HIP_SRCS)) \
+             $(patsubst $(CSRC)/%.cpp,$(BUILD)/%.cpp.o,$(CPP_SRCS))
+HDRS      := $(wildcard include/*.h) $(wildcard $(CSRC)/*.h)
+
+.PHONY: all lib oracle clean
+all: lib oracle
+
+lib: $(OUTLIB)
+
+$(BUILD)/%.hip.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(CXXFLAGS) -x c++ -c $< -o $@
+
+$(OUTLIB): $(OBJS) $(CSRC)/exports.map
+	$(HIPCC) --offload-arch=$(ARCH) $(OBJS) $(LDFLAGS) -o $@
+
+# ---- CPU oracle (test infrastructure only) ----
+oracle: oracle/libffref.so
+
+oracle/libffref.so: oracle/ffref.c oracle/ffref.h
+	gcc -O3 -ftree-vectorize -ffp-contract=off -fno-fast-math -fPIC -shared -std=c11 \
+	    -Wall -o $@ oracle/ffref.c -lpthread
+
+clean:
+	rm -rf $(BUILD) $(OUTLIB) oracle/libffref.so

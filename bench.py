@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GB/s of gradient buckets reduced, device-resident.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N = 1 (default): config C2 of BASELINE.json — one MI355X sums 8 staged 64 MiB fp32
+buckets into one output with the hand-written HIP tree kernel (esgd_reduce).
+N > 1 (launched by torch.distributed.run, one rank per GPU): solo-allreduce of one
+256 MiB fp32 bucket per rank (config C3) through the esgd data plane.
+
+value = bucket bytes reduced per second over the whole job = (#contributing buckets
+x bucket bytes) / wall time of the K timed steps (max over ranks), inputs resident in
+HBM before the timed region.  roofline = the dominant kernel's algorithmic bytes per
+launch / its average launch time from HIP events on its own stream.  cpu_baseline =
+the oracle's restatement of fflib2's recursive doubling (oracle/ffref.c) timed on
+this host's cores for the same workload shape (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "eager-sgd_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+XGMI_LINK_GBS = 153.0      # per-link figure used by SURVEY.md §8d
+SEED = 0x5EEDE56D
+MiB = 1 << 20
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--buckets", type=int, default=8, help="N=1: staged buckets (fan-in k)")
+    ap.add_argument("--bucket-mib", type=float, default=None,
+                    help="bucket size (default 64 at N=1, 256 at N>1)")
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--schedule", choices=["solo", "majority", "allreduce"], default="solo")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
+    ap.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)
+    return ap.parse_args()
+
+
+def cpu_baseline(k: int, count: int):
+    """fflib2's recursive doubling restated (oracle/ffref.c), one pthread per simulated
+    rank, on this host: the reference's CPU path for the same k x bucket workload."""
+    from oracle import ffref
+    threads = k
+    t1 = ffref.time_allreduce(k, count, threads, 1)          # warm + size the sample
+    reps = max(1, min(20, int(10.0 / max(t1, 1e-3))))
+    t = ffref.time_allreduce(k, count, threads, reps)
+    gbs = k * count * 4 / t / 1e9
+    return {"value": round(gbs, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"full workload: {k}-rank recursive-doubling allreduce of {count*4/MiB:.0f} MiB "
+                      f"fp32 (oracle/ffref.c, 1 pthread/rank, best of {reps}; {t*1e3:.1f} ms each)",
+            "host_cpus": os.cpu_count()}
+
+
+def pmc_traffic(args):
+    """HBM bytes per launch of the dominant kernel from rocprofv3 PMC counters, in
+    separate passes (FETCH_SIZE, WRITE_SIZE), corrected as MI355X_MICROARCH.md §HBM
+    prescribes: gfx950 FETCH_SIZE counts half the bytes of a wide streaming read."""
+    out = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(ROOT, "gpurun_out", f"bench_pmc_{ctr}")
+        os.makedirs(d, exist_ok=True)
+        cmd = ["rocprofv3", "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+               sys.executable, os.path.abspath(__file__), "--pmc-child", "1",
+               "--buckets", str(args.buckets), "--bucket-mib", str(args.bucket_mib),
+               "--dtype", args.dtype]
+        subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL,
+                       stderr=subprocess.DEVNULL, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"))
+        vals = []
+        for dp, _, files in os.walk(d):
+            for fn in files:
+                if fn.endswith("counter_collection.csv"):
+                    import csv
+                    with open(os.path.join(dp, fn)) as f:
+                        for row in csv.DictReader(f):
+                            if "k_tree_sum" in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                                vals.append(float(row["Counter_Value"]))
+        if not vals:
+            return None
+        out[ctr] = sorted(vals)[len(vals) // 2]   # median over dispatches, KiB units
+    # FETCH_SIZE/WRITE_SIZE are in KiB; FETCH_SIZE x2 on gfx950 for 16-B streaming loads
+    return 2 * out["FETCH_SIZE"] * 1024 + out["WRITE_SIZE"] * 1024
+
+
+def run_local(args, esgd, dev):
+    """N = 1: k staged buckets -> 1 output (config C2)."""
+    from esgd import _lib
+    k = args.buckets
+    dt = _lib.FLOAT if args.dtype == "fp32" else _lib.BF16
+    es = _lib.dtype_size(dt)
+    count = int(args.bucket_mib * MiB) // es
+    s = dev.Stream()
+    bufs = [dev.DeviceBuffer(count, dt) for _ in range(k)]
+    for r, b in enumerate(bufs):
+        dev.fill_uniform(b, SEED, r, stream=s)
+    out = dev.DeviceBuffer(count, dt)
+    ptrs = [b.ptr for b in bufs]
+    s.synchronize()
+
+    if args.pmc_child:
+        for _ in range(5):
+            dev.reduce(dt, ptrs, out, count, stream=s)
+        s.synchronize()
+        return None
+
+    for _ in range(args.warmup):
+        dev.reduce(dt, ptrs, out, count, stream=s)
+    s.synchronize()
+
+    evs = [dev.Event() for _ in range(args.steps + 1)]
+    dev.device_synchronize()
+    t0 = time.perf_counter()
+    evs[0].record(s)
+    for i in range(args.steps):
+        dev.reduce(dt, ptrs, out, count, stream=s)
+        evs[i + 1].record(s)
+    s.synchronize()
+    dev.device_synchronize()
+    wall = time.perf_counter() - t0
+    per_launch_ms = evs[0].elapsed_ms(evs[-1]) / args.steps
+
+    # parity spot-check outside the timed region: first 1 Mi elements vs the oracle
+    parity = "skipped"
+    if dt == _lib.FLOAT:
+        from oracle import ffref
+        import numpy as np
+        m = min(count, 1 << 20)
+        got = out.download()[:m]
+        want = ffref.tree_sum([ffref.fill_uniform(SEED, r, m) for r in range(k)])
+        parity = "bitwise" if np.array_equal(got.view(np.uint32), want.view(np.uint32)) else "MISMATCH"
+
+    bucket_bytes = count * es
+    algo_bytes = (k + 1) * bucket_bytes        # k reads + 1 write per launch
+    achieved = algo_bytes / (per_launch_ms * 1e-3) / 1e9
+    return {
+        "value": k * bucket_bytes * args.steps / wall / 1e9,
+        "ms_per_step": wall * 1e3 / args.steps,
+        "kernel_ms": per_launch_ms,
+        "achieved_gbs": achieved,
+        "algo_bytes": algo_bytes,
+        "count": count,
+        "bucket_bytes": bucket_bytes,
+        "k": k,
+        "parity": parity,
+    }
+
+
+def main():
+    args = parse()
+    if args.bucket_mib is None:
+        args.bucket_mib = 64.0 if args.gpus == 1 else 256.0
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not args.pmc_child:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+
+    import esgd
+    from esgd import device as dev
+    esgd.check(esgd.lib().esgd_set_device(local_rank), "esgd_set_device")
+
+    if world > 1:
+        from esgd import dataplane
+        res = dataplane.bench_allreduce(args, rank, world, local_rank)
+        if rank == 0:
+            print(json.dumps(res))
+        return
+
+    res = run_local(args, esgd, dev)
+    if args.pmc_child:
+        return
+    line = {
+        "metric": "GB/s grad-bucket reduced (device-resident), solo/majority-allreduce 1-8 GPU",
+        "value": round(res["value"], 2),
+        "unit": "GB/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(res["ms_per_step"], 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if args.dtype == "fp32" else "bf16 (f32 accumulate)",
+        "data": "synthetic (splitmix64 uniform [-1,1), generated on device)",
+        "config": {"workload": f"C2: local reduction of {res['k']} staged "
+                               f"{args.bucket_mib:g} MiB {args.dtype} buckets -> 1 (tree order)",
+                   "buckets": res["k"], "bucket_bytes": res["bucket_bytes"],
+                   "parallelism": "single GPU", "kernel": "esgd_reduce (k_tree_sum)"},
+        "parity": res["parity"],
+    }
+    traffic = None
+    if not args.no_pmc:
+        try:
+            traffic = pmc_traffic(args)
+        except Exception as e:  # profiler missing or refused: report, keep the line
+            line["pmc_error"] = str(e)[:200]
+    line["roofline"] = {
+        "bound": "hbm", "achieved": round(res["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
+        "unit": "GB/s", "frac": round(res["achieved_gbs"] / HBM_PEAK_GBS, 4),
+        "traffic": traffic, "algo_bytes_per_launch": res["algo_bytes"],
+        "kernel_ms": round(res["kernel_ms"], 5),
+    }
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(res["k"], res["count"] if args.dtype == "fp32"
+                                            else res["count"])
+    print(json.dumps(line))
+
+
+if __name__ == "__main__":
+    main()

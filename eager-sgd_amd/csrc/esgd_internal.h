@@ -1,0 +1,40 @@
+// esgd_internal.h — shared helpers for libesgd.so (not installed).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "esgd.h"
+
+namespace esgd {
+
+// Per-thread message of the last failure; esgd_last_error() returns it.
+void set_error(const char *fmt, ...);
+void clear_error();
+
+// Map a HIP status onto the ABI's codes, recording where it failed.
+int hip_fail(hipError_t e, const char *what, const char *file, int line);
+
+// Lazily-created library stream for the current device (NULL stream argument).
+hipStream_t default_stream();
+
+// Fails with ESGD_NO_DEVICE (and a message) if no HIP device is usable.
+int require_device();
+
+inline hipStream_t as_stream(void *s) { return s ? static_cast<hipStream_t>(s) : default_stream(); }
+
+}  // namespace esgd
+
+#define ESGD_HIP(call)                                                          \
+    do {                                                                        \
+        hipError_t esgd_e_ = (call);                                            \
+        if (esgd_e_ != hipSuccess) return esgd::hip_fail(esgd_e_, #call, __FILE__, __LINE__); \
+    } while (0)
+
+#define ESGD_ARG(cond, ...)                                                     \
+    do {                                                                        \
+        if (!(cond)) { esgd::set_error(__VA_ARGS__); return ESGD_INVALID_ARG; } \
+    } while (0)

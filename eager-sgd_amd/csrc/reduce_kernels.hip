@@ -1,0 +1,394 @@
+// reduce_kernels.hip — the gradient-bucket reduction, hand-written for gfx950.
+//
+// Reference behaviour (fflib2, /root/reference/eager-SGD-modules/fflib2):
+//   * FFSUM on a pair of buffers, c = a + b, is a scalar C loop strip-mined in 1024s
+//     on the progress pthread (src/components/gcomp/ffop_gcomp_operator.c:8-25, 33-58).
+//   * ffallreduce applies it log2(P) times in recursive-doubling order
+//     (src/colls/ffallreduce.c:138-171), so every rank ends with the hypercube tree
+//     ((x0+x1)+(x2+x3))+((x4+x5)+(x6+x7)).
+// Here the whole tree is one pass: each lane loads 16 B from each of the k inputs,
+// folds them in exactly that tree order in registers and stores 16 B once.  The
+// result is bit-identical to the reference for fp32/fp64/int32/int64 (no FMA, no
+// reassociation, denormals kept — hipcc's default f32 denorm mode).
+//
+// MI355X mapping: pure HBM streaming (k reads + 1 write per element, ~0.2 FLOP/B),
+// so the design goal is bytes in flight: 64-wide waves, 16-B loads per lane
+// (1 KiB per wave-instruction), U independent vectors per input per lane, a
+// grid-stride loop over <= 8 blocks per CU, optional non-temporal loads/stores so
+// the once-read buckets do not churn L2 / Infinity Cache.  No LDS: there is no
+// reuse to stage, and a round trip through it would only add instructions
+// (cdna_hip_programming.md Appendix B "Element-wise").
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+
+#include "esgd_internal.h"
+
+namespace esgd {
+
+using raw16 = __attribute__((ext_vector_type(4))) unsigned int;  // one 16-B access
+
+struct InputSet {
+    const void *p[ESGD_MAX_FANIN];
+};
+
+// ---- element traits: T = storage, A = accumulator, E = elements per 16 B ----
+struct F32 {
+    using T = float; using A = float; static constexpr int E = 4;
+    __device__ static A load(T x) { return x; }
+    __device__ static T store(A a) { return a; }
+};
+struct F64 {
+    using T = double; using A = double; static constexpr int E = 2;
+    __device__ static A load(T x) { return x; }
+    __device__ static T store(A a) { return a; }
+};
+struct I32 {  // wrapping two's-complement add, like the reference's int32 SUM
+    using T = uint32_t; using A = uint32_t; static constexpr int E = 4;
+    __device__ static A load(T x) { return x; }
+    __device__ static T store(A a) { return a; }
+};
+struct I64 {
+    using T = uint64_t; using A = uint64_t; static constexpr int E = 2;
+    __device__ static A load(T x) { return x; }
+    __device__ static T store(A a) { return a; }
+};
+struct BF16 {  // extension: fp32 accumulate, one round-to-nearest-even at the end
+    using T = uint16_t; using A = float; static constexpr int E = 8;
+    __device__ static A load(T x) { return __uint_as_float(uint32_t(x) << 16); }
+    __device__ static T store(A a) {
+        uint32_t u = __float_as_uint(a);
+        if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu))
+            return uint16_t((u >> 16) | 0x0040u);            // NaN stays a (quiet) NaN
+        u += 0x7fffu + ((u >> 16) & 1u);
+        return uint16_t(u >> 16);
+    }
+};
+
+// The hypercube tree of ffallreduce.c:138-171 as rank 0 evaluates it: at distance s
+// the partner's partial (operand a, `tmp`) is added to the local one (operand b, `rb`).
+template <class Tr, int K>
+__device__ __forceinline__ void tree_fold(typename Tr::A (&v)[K]) {
+#pragma unroll
+    for (int s = 1; s < K; s <<= 1) {
+#pragma unroll
+        for (int j = 0; j + s < K; j += 2 * s) v[j] = v[j + s] + v[j];
+    }
+}
+
+template <bool NT>
+__device__ __forceinline__ raw16 ld16(const void *base, uint64_t i) {
+    const raw16 *p = static_cast<const raw16 *>(base) + i;
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16(void *base, uint64_t i, raw16 v) {
+    raw16 *p = static_cast<raw16 *>(base) + i;
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// fold one 16-B column of K inputs
+template <class Tr, int K, bool SCALE>
+__device__ __forceinline__ raw16 fold16(const raw16 (&r)[K], float scale) {
+    using T = typename Tr::T;
+    using A = typename Tr::A;
+    constexpr int E = Tr::E;
+    T out[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        A v[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            T x;
+            __builtin_memcpy(&x, reinterpret_cast<const char *>(&r[j]) + e * sizeof(T), sizeof(T));
+            v[j] = Tr::load(x);
+        }
+        tree_fold<Tr, K>(v);
+        if constexpr (SCALE) v[0] = v[0] * scale;
+        out[e] = Tr::store(v[0]);
+    }
+    raw16 o;
+    __builtin_memcpy(&o, out, 16);
+    return o;
+}
+
+// Vector body: `nvec` 16-B columns; the ragged tail (< E elements) is folded by
+// block 0 with scalar accesses.
+template <class Tr, int K, int U, bool NT, bool SCALE>
+__global__ __launch_bounds__(256) void k_tree_sum(InputSet in, void *out, uint64_t nvec,
+                                                   uint64_t count, float scale) {
+    constexpr int B = 256;
+    const uint64_t stride = uint64_t(gridDim.x) * B * U;
+    uint64_t i = uint64_t(blockIdx.x) * B * U + threadIdx.x;
+    for (; i + uint64_t(U - 1) * B < nvec; i += stride) {
+        raw16 r[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j) r[u][j] = ld16<NT>(in.p[j], i + u * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) st16<NT>(out, i + u * B, fold16<Tr, K, SCALE>(r[u], scale));
+    }
+    // partial last iteration of this lane (only when U > 1)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t c = i + u * B;
+        if (c < nvec) {
+            raw16 r[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) r[j] = ld16<NT>(in.p[j], c);
+            st16<NT>(out, c, fold16<Tr, K, SCALE>(r, scale));
+        }
+    }
+    using T = typename Tr::T;
+    using A = typename Tr::A;
+    const uint64_t tail0 = nvec * Tr::E;
+    if (blockIdx.x == 0 && tail0 + threadIdx.x < count) {
+        const uint64_t e = tail0 + threadIdx.x;
+        A v[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) v[j] = Tr::load(static_cast<const T *>(in.p[j])[e]);
+        tree_fold<Tr, K>(v);
+        if constexpr (SCALE) v[0] = v[0] * scale;
+        static_cast<T *>(out)[e] = Tr::store(v[0]);
+    }
+}
+
+// Fallback for pointers that are not 16-B aligned: one element per lane.
+template <class Tr, int K, bool SCALE>
+__global__ __launch_bounds__(256) void k_tree_sum_scalar(InputSet in, void *out, uint64_t count,
+                                                          float scale) {
+    using T = typename Tr::T;
+    using A = typename Tr::A;
+    const uint64_t stride = uint64_t(gridDim.x) * 256;
+    for (uint64_t e = uint64_t(blockIdx.x) * 256 + threadIdx.x; e < count; e += stride) {
+        A v[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) v[j] = Tr::load(static_cast<const T *>(in.p[j])[e]);
+        tree_fold<Tr, K>(v);
+        if constexpr (SCALE) v[0] = v[0] * scale;
+        static_cast<T *>(out)[e] = Tr::store(v[0]);
+    }
+}
+
+// ---- synthetic inputs (same generator as oracle/ffref.c) ----
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ float uniform_pm1(uint64_t base, uint64_t i) {
+    const float u = float(splitmix64(base ^ i) >> 40) * (1.0f / 16777216.0f);
+    return __fsub_rn(__fmul_rn(2.0f, u), 1.0f);
+}
+
+__global__ void k_fill_uniform_f32(uint64_t base, float *out, uint64_t n) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = uniform_pm1(base, i);
+}
+
+__global__ void k_fill_uniform_bf16(uint64_t base, uint16_t *out, uint64_t n) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = BF16::store(uniform_pm1(base, i));
+}
+
+// ---- launch configuration ----
+static int g_unroll = 0;   // 0 -> default per type
+static int g_grid = 0;     // 0 -> auto
+static int g_nt = -1;      // -1 -> default (on)
+
+static int cu_count() {
+    static int cus[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        hipDeviceProp_t p;
+        cus[dev] = (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0)
+                       ? p.multiProcessorCount : 256;
+    }
+    return cus[dev];
+}
+
+static unsigned grid_for(uint64_t items_per_block_pass, uint64_t items) {
+    if (g_grid > 0) return unsigned(g_grid);
+    uint64_t need = (items + items_per_block_pass - 1) / items_per_block_pass;
+    uint64_t cap = uint64_t(cu_count()) * 8;   // 8 x 256-thread blocks per CU
+    if (need < 1) need = 1;
+    return unsigned(need < cap ? need : cap);
+}
+
+template <class Tr, int K, int U, bool NT, bool SCALE>
+static int launch_vec(const InputSet &in, void *out, uint64_t count, float scale, hipStream_t s) {
+    const uint64_t nvec = count / Tr::E;
+    unsigned grid = grid_for(uint64_t(256) * U, nvec ? nvec : 1);
+    hipLaunchKernelGGL((k_tree_sum<Tr, K, U, NT, SCALE>), dim3(grid), dim3(256), 0, s, in, out,
+                       nvec, count, scale);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+template <class Tr, int K, bool SCALE>
+static int launch_scalar(const InputSet &in, void *out, uint64_t count, float scale, hipStream_t s) {
+    unsigned grid = grid_for(256, count);
+    hipLaunchKernelGGL((k_tree_sum_scalar<Tr, K, SCALE>), dim3(grid), dim3(256), 0, s, in, out,
+                       count, scale);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+template <class Tr, int K, bool SCALE>
+static int dispatch_u(const InputSet &in, void *out, uint64_t count, float scale, bool aligned,
+                      hipStream_t s) {
+    if (!aligned) return launch_scalar<Tr, K, SCALE>(in, out, count, scale, s);
+    const bool nt = g_nt != 0;
+    int u = g_unroll ? g_unroll : 2;
+    if constexpr (sizeof(typename Tr::T) == 2) u = 1;  // bf16: 8 accumulators per vector already
+    if (u >= 4) return nt ? launch_vec<Tr, K, 4, true, SCALE>(in, out, count, scale, s)
+                          : launch_vec<Tr, K, 4, false, SCALE>(in, out, count, scale, s);
+    if (u == 2) return nt ? launch_vec<Tr, K, 2, true, SCALE>(in, out, count, scale, s)
+                          : launch_vec<Tr, K, 2, false, SCALE>(in, out, count, scale, s);
+    return nt ? launch_vec<Tr, K, 1, true, SCALE>(in, out, count, scale, s)
+              : launch_vec<Tr, K, 1, false, SCALE>(in, out, count, scale, s);
+}
+
+template <class Tr, bool SCALE>
+static int dispatch_k(int k, const InputSet &in, void *out, uint64_t count, float scale,
+                      bool aligned, hipStream_t s) {
+    switch (k) {
+    case 1: return dispatch_u<Tr, 1, SCALE>(in, out, count, scale, aligned, s);
+    case 2: return dispatch_u<Tr, 2, SCALE>(in, out, count, scale, aligned, s);
+    case 3: return dispatch_u<Tr, 3, SCALE>(in, out, count, scale, aligned, s);
+    case 4: return dispatch_u<Tr, 4, SCALE>(in, out, count, scale, aligned, s);
+    case 5: return dispatch_u<Tr, 5, SCALE>(in, out, count, scale, aligned, s);
+    case 6: return dispatch_u<Tr, 6, SCALE>(in, out, count, scale, aligned, s);
+    case 7: return dispatch_u<Tr, 7, SCALE>(in, out, count, scale, aligned, s);
+    case 8: return dispatch_u<Tr, 8, SCALE>(in, out, count, scale, aligned, s);
+    default: break;
+    }
+    set_error("esgd_reduce: fan-in %d outside [1, %d]", k, ESGD_MAX_FANIN);
+    return ESGD_INVALID_ARG;
+}
+
+static int reduce_impl(int dtype, int k, const void *const *inputs, void *out, uint64_t count,
+                       float scale, bool scaled, void *stream) {
+    ESGD_ARG(k >= 1 && k <= ESGD_MAX_FANIN, "esgd_reduce: fan-in %d outside [1, %d]", k,
+             ESGD_MAX_FANIN);
+    ESGD_ARG(inputs && out, "esgd_reduce: null inputs/out");
+    if (count == 0) return ESGD_SUCCESS;
+    if (int rc = require_device()) return rc;
+    InputSet in;
+    std::memset(&in, 0, sizeof(in));
+    bool aligned = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+    for (int j = 0; j < k; ++j) {
+        ESGD_ARG(inputs[j], "esgd_reduce: input %d is null", j);
+        in.p[j] = inputs[j];
+        aligned = aligned && (reinterpret_cast<uintptr_t>(inputs[j]) & 15) == 0;
+    }
+    hipStream_t s = as_stream(stream);
+    switch (dtype) {
+    case ESGD_FLOAT:
+        return scaled ? dispatch_k<F32, true>(k, in, out, count, scale, aligned, s)
+                      : dispatch_k<F32, false>(k, in, out, count, scale, aligned, s);
+    case ESGD_BF16:
+        return scaled ? dispatch_k<BF16, true>(k, in, out, count, scale, aligned, s)
+                      : dispatch_k<BF16, false>(k, in, out, count, scale, aligned, s);
+    case ESGD_DOUBLE:
+        ESGD_ARG(!scaled, "esgd_reduce_scaled: FLOAT/BF16 only");
+        return dispatch_k<F64, false>(k, in, out, count, scale, aligned, s);
+    case ESGD_INT32:
+        ESGD_ARG(!scaled, "esgd_reduce_scaled: FLOAT/BF16 only");
+        return dispatch_k<I32, false>(k, in, out, count, scale, aligned, s);
+    case ESGD_INT64:
+        ESGD_ARG(!scaled, "esgd_reduce_scaled: FLOAT/BF16 only");
+        return dispatch_k<I64, false>(k, in, out, count, scale, aligned, s);
+    default: break;
+    }
+    set_error("esgd_reduce: unsupported dtype %d", dtype);
+    return ESGD_INVALID_ARG;
+}
+
+}  // namespace esgd
+
+using namespace esgd;
+
+extern "C" {
+
+int esgd_reduce(int dtype, int k, const void *const *inputs, void *out, uint64_t count,
+                void *stream) {
+    return reduce_impl(dtype, k, inputs, out, count, 1.0f, false, stream);
+}
+
+int esgd_reduce_scaled(int dtype, int k, const void *const *inputs, void *out, uint64_t count,
+                       float scale, void *stream) {
+    if (scale == 1.0f) return reduce_impl(dtype, k, inputs, out, count, 1.0f, false, stream);
+    return reduce_impl(dtype, k, inputs, out, count, scale, true, stream);
+}
+
+int esgd_vsum(int dtype, const void *a, const void *b, void *c, uint64_t count, void *stream) {
+    // tree order for k=2 is x1 + x0; with x0 = b (rb) and x1 = a (tmp) this is exactly
+    // the reference's c = a + b (ffop_gcomp_operator.c:13).
+    const void *in[2] = {b, a};
+    return reduce_impl(dtype, 2, in, c, count, 1.0f, false, stream);
+}
+
+int esgd_fill_uniform_f32(uint64_t seed, int rank, float *out, uint64_t n, void *stream) {
+    ESGD_ARG(out || n == 0, "esgd_fill_uniform_f32: null output");
+    if (!n) return ESGD_SUCCESS;
+    if (int rc = require_device()) return rc;
+    const uint64_t base = seed ^ (uint64_t(uint32_t(rank)) << 40);
+    hipLaunchKernelGGL(k_fill_uniform_f32, dim3(grid_for(256, n)), dim3(256), 0, as_stream(stream),
+                       base, out, n);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+int esgd_fill_uniform_bf16(uint64_t seed, int rank, uint16_t *out, uint64_t n, void *stream) {
+    ESGD_ARG(out || n == 0, "esgd_fill_uniform_bf16: null output");
+    if (!n) return ESGD_SUCCESS;
+    if (int rc = require_device()) return rc;
+    const uint64_t base = seed ^ (uint64_t(uint32_t(rank)) << 40);
+    hipLaunchKernelGGL(k_fill_uniform_bf16, dim3(grid_for(256, n)), dim3(256), 0,
+                       as_stream(stream), base, out, n);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+int esgd_set_tuning(const char *key, int value) {
+    ESGD_ARG(key, "esgd_set_tuning: null key");
+    if (!std::strcmp(key, "unroll")) {
+        ESGD_ARG(value == 0 || value == 1 || value == 2 || value == 4, "unroll must be 0/1/2/4");
+        g_unroll = value;
+    } else if (!std::strcmp(key, "grid")) {
+        ESGD_ARG(value >= 0, "grid must be >= 0");
+        g_grid = value;
+    } else if (!std::strcmp(key, "nt")) {
+        g_nt = value ? 1 : 0;
+    } else {
+        set_error("esgd_set_tuning: unknown key '%s'", key);
+        return ESGD_INVALID_ARG;
+    }
+    return ESGD_SUCCESS;
+}
+
+int esgd_get_tuning(const char *key, int *value) {
+    ESGD_ARG(key && value, "esgd_get_tuning: null argument");
+    if (!std::strcmp(key, "unroll")) *value = g_unroll;
+    else if (!std::strcmp(key, "grid")) *value = g_grid;
+    else if (!std::strcmp(key, "nt")) *value = g_nt;
+    else {
+        set_error("esgd_get_tuning: unknown key '%s'", key);
+        return ESGD_INVALID_ARG;
+    }
+    return ESGD_SUCCESS;
+}
+
+}  // extern "C"

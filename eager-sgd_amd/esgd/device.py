@@ -1,0 +1,172 @@
+"""Thin Python handles over libesgd's device plumbing and the reduction kernels.
+
+Nothing here computes on the host: every reduction is a HIP launch through the C ABI
+(esgd_reduce / esgd_vsum).  Buffers are raw device allocations owned by libesgd, so
+the module works without PyTorch; `as_ptr` also accepts torch tensors (data_ptr()).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+NP_DTYPE = {
+    _lib.INT32: np.int32,
+    _lib.INT64: np.int64,
+    _lib.DOUBLE: np.float64,
+    _lib.FLOAT: np.float32,
+    _lib.BF16: np.uint16,  # raw bf16 bits
+}
+
+
+def as_ptr(x) -> int:
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "ptr"):
+        return int(x.ptr)
+    if hasattr(x, "data_ptr"):
+        return int(x.data_ptr())
+    raise TypeError(f"cannot take a device pointer of {type(x)!r}")
+
+
+class Stream:
+    def __init__(self):
+        s = C.c_void_p()
+        check(lib().esgd_stream_create(C.byref(s)), "esgd_stream_create")
+        self.handle = s.value
+
+    def synchronize(self):
+        check(lib().esgd_stream_synchronize(self.handle), "esgd_stream_synchronize")
+
+    def close(self):
+        if self.handle:
+            lib().esgd_stream_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Event:
+    def __init__(self):
+        e = C.c_void_p()
+        check(lib().esgd_event_create(C.byref(e)), "esgd_event_create")
+        self.handle = e.value
+
+    def record(self, stream=None):
+        check(lib().esgd_event_record(self.handle, _sh(stream)), "esgd_event_record")
+
+    def synchronize(self):
+        check(lib().esgd_event_synchronize(self.handle), "esgd_event_synchronize")
+
+    def elapsed_ms(self, stop: "Event") -> float:
+        ms = C.c_float()
+        check(lib().esgd_event_elapsed_ms(self.handle, stop.handle, C.byref(ms)), "elapsed")
+        return float(ms.value)
+
+    def close(self):
+        if self.handle:
+            lib().esgd_event_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _sh(stream):
+    if stream is None:
+        return None
+    return stream.handle if isinstance(stream, Stream) else int(stream)
+
+
+class DeviceBuffer:
+    """A device allocation of `count` elements of an esgd dtype."""
+
+    def __init__(self, count: int, dtype: int = _lib.FLOAT):
+        self.count, self.dtype = int(count), dtype
+        self.nbytes = self.count * _lib.dtype_size(dtype)
+        p = C.c_void_p()
+        check(lib().esgd_malloc(C.byref(p), self.nbytes), "esgd_malloc")
+        self.ptr = p.value
+
+    def upload(self, arr: np.ndarray, stream=None, sync=True):
+        arr = np.ascontiguousarray(arr, dtype=NP_DTYPE[self.dtype])
+        assert arr.size == self.count, (arr.size, self.count)
+        check(lib().esgd_memcpy_async(self.ptr, arr.ctypes.data, self.nbytes, 0, _sh(stream)), "h2d")
+        if sync:
+            synchronize(stream)
+        return self
+
+    def download(self, stream=None) -> np.ndarray:
+        out = np.empty(self.count, dtype=NP_DTYPE[self.dtype])
+        check(lib().esgd_memcpy_async(out.ctypes.data, self.ptr, self.nbytes, 1, _sh(stream)), "d2h")
+        synchronize(stream)
+        return out
+
+    def zero(self, stream=None):
+        check(lib().esgd_memset_async(self.ptr, 0, self.nbytes, _sh(stream)), "memset")
+
+    def close(self):
+        if self.ptr:
+            lib().esgd_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def synchronize(stream=None):
+    if stream is None:
+        check(lib().esgd_stream_synchronize(None), "esgd_stream_synchronize")
+    else:
+        check(lib().esgd_stream_synchronize(_sh(stream)), "esgd_stream_synchronize")
+
+
+def device_synchronize():
+    check(lib().esgd_device_synchronize(), "esgd_device_synchronize")
+
+
+def reduce(dtype: int, inputs, out, count: int, stream=None, scale: float | None = None):
+    """out = tree(inputs) on the device (esgd_reduce / esgd_reduce_scaled)."""
+    ptrs = _lib.ptr_array([as_ptr(x) for x in inputs])
+    if scale is None:
+        rc = lib().esgd_reduce(dtype, len(inputs), ptrs, as_ptr(out), count, _sh(stream))
+    else:
+        rc = lib().esgd_reduce_scaled(dtype, len(inputs), ptrs, as_ptr(out), count, scale, _sh(stream))
+    return check(rc, "esgd_reduce")
+
+
+def vsum(dtype: int, a, b, c, count: int, stream=None):
+    return check(lib().esgd_vsum(dtype, as_ptr(a), as_ptr(b), as_ptr(c), count, _sh(stream)), "esgd_vsum")
+
+
+def fill_uniform(buf: DeviceBuffer, seed: int, rank: int, stream=None):
+    if buf.dtype == _lib.FLOAT:
+        rc = lib().esgd_fill_uniform_f32(seed, rank, buf.ptr, buf.count, _sh(stream))
+    elif buf.dtype == _lib.BF16:
+        rc = lib().esgd_fill_uniform_bf16(seed, rank, buf.ptr, buf.count, _sh(stream))
+    else:
+        raise ValueError("fill_uniform: FLOAT or BF16 only")
+    return check(rc, "esgd_fill_uniform")
+
+
+def set_tuning(key: str, value: int):
+    check(lib().esgd_set_tuning(key.encode(), int(value)), "esgd_set_tuning")
+
+
+def get_tuning(key: str) -> int:
+    v = C.c_int()
+    check(lib().esgd_get_tuning(key.encode(), C.byref(v)), "esgd_get_tuning")
+    return v.value

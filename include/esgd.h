@@ -1,0 +1,111 @@
+/*
+ * esgd.h — C ABI of libesgd.so, the MI355X-native gradient-bucket reduction
+ * behind eager-SGD's partial allreduce.
+ *
+ * Every entry point is `extern "C"`, takes plain pointers and sizes, and returns an
+ * int status with the reference's error numbering (src/ff.h:4-10 in
+ * /root/reference/eager-SGD-modules/fflib2): 0 success, -1 error, -2 invalid
+ * argument, -4 out of memory.  esgd_last_error() gives the message of the calling
+ * thread's last failure.  Streams and events are opaque `void *` (hipStream_t /
+ * hipEvent_t); NULL means the library's default stream for the current device.
+ *
+ * The reference-shaped entry points (ffinit, ffallreduce, ffsolo_allreduce,
+ * ffrand_allreduce, ffschedule_*) live in esgd_ff.h; the deep500 operator ABI in
+ * esgd_deep500.h.  This header holds the device-resident hot path those build on.
+ */
+#ifndef ESGD_H
+#define ESGD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (src/ff.h:4-10) ---- */
+#define ESGD_SUCCESS 0
+#define ESGD_ERROR -1
+#define ESGD_INVALID_ARG -2
+#define ESGD_ENOMEM -4
+#define ESGD_NO_DEVICE -6 /* extension: no usable gfx950 device / HIP runtime error */
+
+/* ---- element types: numbering of src/ff.h:21-31, plus bf16 (extension) ---- */
+#define ESGD_INT32 0
+#define ESGD_INT64 1
+#define ESGD_DOUBLE 2
+#define ESGD_FLOAT 3
+#define ESGD_BF16 16 /* not in the reference (parity unpinned): fp32 accumulate, one RNE */
+
+/* largest fan-in of one local-reduction launch */
+#define ESGD_MAX_FANIN 8
+
+const char *esgd_last_error(void);
+int esgd_version(void);                 /* 100 * major + minor */
+size_t esgd_dtype_size(int dtype);      /* 0 for unsupported */
+
+/* ---- device plumbing (replaces the reference's host buffers; no reference
+ *      equivalent — fflib2 is CPU-only) ---- */
+int esgd_device_count(int *n);
+int esgd_set_device(int dev);
+int esgd_get_device(int *dev);
+int esgd_device_arch(int dev, char *name, size_t len); /* e.g. "gfx950:sramecc+:xnack-" */
+int esgd_malloc(void **ptr, size_t bytes);
+int esgd_free(void *ptr);
+int esgd_host_alloc(void **ptr, size_t bytes);           /* pinned host memory */
+int esgd_host_free(void *ptr);
+int esgd_host_register(void *ptr, size_t bytes);         /* pin caller-owned memory */
+int esgd_host_unregister(void *ptr);
+/* kind: 0 host->device, 1 device->host, 2 device->device, 3 inferred */
+int esgd_memcpy_async(void *dst, const void *src, size_t bytes, int kind, void *stream);
+int esgd_memset_async(void *dst, int value, size_t bytes, void *stream);
+int esgd_stream_create(void **stream);
+int esgd_stream_destroy(void *stream);
+int esgd_stream_synchronize(void *stream);
+int esgd_device_synchronize(void);
+int esgd_event_create(void **event);                     /* timing-enabled */
+int esgd_event_destroy(void *event);
+int esgd_event_record(void *event, void *stream);
+int esgd_event_synchronize(void *event);
+int esgd_event_elapsed_ms(void *start, void *stop, float *ms);
+int esgd_stream_wait_event(void *stream, void *event);
+
+/* ---- the hot path: element-wise bucket reduction (device pointers) ----
+ *
+ * esgd_reduce: out[i] = tree(x_0[i], ..., x_{k-1}[i]) for i < count, where tree is
+ * the hypercube order of fflib2's recursive doubling as rank 0 sees it
+ * (src/colls/ffallreduce.c:138-171): ((x0+x1)+(x2+x3))+((x4+x5)+(x6+x7)).
+ * For power-of-two k that is bit-identical to what every rank of the reference
+ * holds after ffallreduce; for other k it is rank 0's (complete) result.
+ * `inputs` is a HOST array of k device pointers; `out` may alias any input.
+ * dtype: ESGD_FLOAT / ESGD_DOUBLE / ESGD_INT32 / ESGD_INT64 (wrapping) / ESGD_BF16.
+ * Stream-ordered; returns after the launch is queued. */
+int esgd_reduce(int dtype, int k, const void *const *inputs, void *out,
+                uint64_t count, void *stream);
+
+/* c = a + b element-wise: the reference's FFSUM operator
+ * (src/components/gcomp/ffop_gcomp_operator.c:33-58) on device memory. */
+int esgd_vsum(int dtype, const void *a, const void *b, void *c, uint64_t count,
+              void *stream);
+
+/* Scaled variant used by the optimizer wrapper: out = tree(x) * scale, the
+ * division by comm size of opt_esgd_solo_imagenet_imbalance.py:40 fused into the
+ * sum (FLOAT / BF16 only).  scale == 1 is exactly esgd_reduce. */
+int esgd_reduce_scaled(int dtype, int k, const void *const *inputs, void *out,
+                       uint64_t count, float scale, void *stream);
+
+/* Synthetic gradient generator shared with the oracle: x[i] = 2*u - 1 with
+ * u = (splitmix64(seed ^ (rank << 40) ^ i) >> 40) / 2^24  (SURVEY.md §8d). */
+int esgd_fill_uniform_f32(uint64_t seed, int rank, float *out, uint64_t n, void *stream);
+int esgd_fill_uniform_bf16(uint64_t seed, int rank, uint16_t *out, uint64_t n, void *stream);
+
+/* Tuning knobs for the reduction launch (benchmarks only; 0 = default).
+ * key: "unroll" (16-B vectors per thread per input: 1,2,4), "grid" (blocks, 0 = auto),
+ *      "nt" (1 = non-temporal loads/stores).  Unknown keys -> ESGD_INVALID_ARG. */
+int esgd_set_tuning(const char *key, int value);
+int esgd_get_tuning(const char *key, int *value);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ESGD_H */

@@ -1,0 +1,71 @@
+"""The C ABI: libesgd.so loads and exports every function the public headers declare.
+
+No compute calls here (the container has no GPU); instead the product path is checked
+to refuse loudly, with a message, when no device is present.
+"""
+import ctypes
+import glob
+import os
+import re
+
+import pytest
+
+from conftest import LIB, ROOT
+
+DECL = re.compile(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b([a-z_][a-z0-9_]*)\s*\(", re.M)
+
+
+def declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        text = re.sub(r"//[^\n]*", "", text)
+        text = re.sub(r"^\s*#.*$", "", text, flags=re.M)
+        for m in DECL.finditer(text):
+            name = m.group(1)
+            if name in ("if", "while", "for", "return", "sizeof", "typedef"):
+                continue
+            names.add(name)
+    return sorted(names)
+
+
+def test_headers_declare_something():
+    names = declared_functions()
+    assert "esgd_reduce" in names and len(names) > 20
+
+
+def test_every_declared_symbol_is_exported():
+    lib = ctypes.CDLL(LIB)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, f"declared in include/*.h but not exported: {missing}"
+
+
+def test_internal_symbols_hidden():
+    out = os.popen(f"nm -D --defined-only {LIB}").read()
+    exported = [l.split()[-1] for l in out.splitlines() if " T " in l]
+    bad = [s for s in exported if s.startswith("_ZN4esgd")]
+    assert not bad, f"C++ internals leak from the ABI: {bad[:5]}"
+
+
+def test_no_device_fails_loudly():
+    from esgd import _lib
+    if _lib.device_count() > 0:
+        pytest.skip("a GPU is present")
+    lib = _lib.lib()
+    ptrs = _lib.ptr_array([0x1000, 0x2000])
+    rc = lib.esgd_reduce(_lib.FLOAT, 2, ptrs, ctypes.c_void_p(0x3000), 16, None)
+    assert rc == _lib.NO_DEVICE
+    assert "no HIP device" in _lib.last_error()
+
+
+def test_argument_validation_without_device():
+    from esgd import _lib
+    lib = _lib.lib()
+    ptrs = _lib.ptr_array([0x1000] * 9)
+    assert lib.esgd_reduce(_lib.FLOAT, 9, ptrs, ctypes.c_void_p(0x3000), 16, None) == _lib.INVALID_ARG
+    assert lib.esgd_reduce(_lib.FLOAT, 0, ptrs, ctypes.c_void_p(0x3000), 16, None) == _lib.INVALID_ARG
+    assert lib.esgd_reduce(99, 2, ptrs, ctypes.c_void_p(0x3000), 16, None) in (_lib.INVALID_ARG, _lib.NO_DEVICE)
+    assert lib.esgd_dtype_size(_lib.BF16) == 2 and lib.esgd_dtype_size(7) == 0
+    assert lib.esgd_set_tuning(b"unroll", 3) == _lib.INVALID_ARG
+    assert lib.esgd_set_tuning(b"bogus", 1) == _lib.INVALID_ARG

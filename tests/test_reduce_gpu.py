@@ -1,0 +1,175 @@
+"""Parity of the HIP reduction (esgd_reduce / esgd_vsum) with the CPU oracle.
+
+Bar: bit-exact for fp32/fp64/int32/int64 against oracle/ffref.c's restatement of
+fflib2's recursive doubling (NaN compared as NaN); bf16 (an extension the reference
+lacks, parity unpinned) bit-exact against the oracle's fp32-accumulate + single-RNE
+convention.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from esgd import _lib
+from esgd.device import DeviceBuffer, Stream, fill_uniform, reduce, set_tuning, synchronize, vsum
+from oracle import ffref
+
+pytestmark = pytest.mark.gpu
+
+NP = {_lib.FLOAT: np.float32, _lib.DOUBLE: np.float64, _lib.INT32: np.int32, _lib.INT64: np.int64}
+U = {np.dtype(np.float32): np.uint32, np.dtype(np.float64): np.uint64,
+     np.dtype(np.int32): np.uint32, np.dtype(np.int64): np.uint64, np.dtype(np.uint16): np.uint16}
+
+
+def bits_equal(a: np.ndarray, b: np.ndarray):
+    assert a.shape == b.shape and a.dtype == b.dtype
+    if a.dtype.kind == "f":
+        na, nb = np.isnan(a), np.isnan(b)
+        assert np.array_equal(na, nb), "NaN positions differ"
+        a, b = np.where(na, 0, a).astype(a.dtype), np.where(nb, 0, b).astype(b.dtype)
+    ua, ub = a.view(U[a.dtype]), b.view(U[b.dtype])
+    bad = np.nonzero(ua != ub)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:5]}: {a[bad[:5]]} vs {b[bad[:5]]}"
+
+
+def gpu_reduce(xs, dtype, out_alias=False, offset=0, scale=None):
+    n = xs[0].size
+    bufs = [DeviceBuffer(n + offset, dtype) for _ in xs]
+    for b, x in zip(bufs, xs):
+        host = np.zeros(n + offset, dtype=x.dtype)
+        host[offset:] = x
+        b.upload(host)
+    es = _lib.dtype_size(dtype)
+    ins = [b.ptr + offset * es for b in bufs]
+    if out_alias:
+        out, optr = bufs[0], ins[0]
+    else:
+        out = DeviceBuffer(n + offset, dtype)
+        optr = out.ptr + offset * es
+    reduce(dtype, ins, optr, n, scale=scale)
+    synchronize()
+    return out.download()[offset:]
+
+
+def rand_input(dt, k, n, seed):
+    rng = np.random.default_rng(seed)
+    if np.dtype(dt).kind == "f":
+        return [(rng.standard_normal(n) * 10.0 ** rng.integers(-2, 3)).astype(dt) for _ in range(k)]
+    info = np.iinfo(dt)
+    return [rng.integers(info.min, info.max, n, dtype=dt, endpoint=True) for _ in range(k)]
+
+
+@pytest.mark.parametrize("dtype", [_lib.FLOAT, _lib.DOUBLE, _lib.INT32, _lib.INT64])
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("n", [1, 5, 1023, 4099, 65536 + 3])
+def test_reduce_matches_oracle(dtype, k, n):
+    xs = rand_input(NP[dtype], k, n, seed=k * 1000 + n)
+    bits_equal(gpu_reduce(xs, dtype), ffref.tree_sum(xs))
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_golden_every_rank(golden_dir, P):
+    g = np.load(os.path.join(golden_dir, f"tree_f32_p{P}.npz"))
+    for name in ("gauss", "special"):
+        x, rb = g[f"{name}_x"], g[f"{name}_rb"]
+        out = gpu_reduce(list(x), _lib.FLOAT)
+        for r in range(P):  # the one device result equals every reference rank's buffer
+            bits_equal(out, rb[r])
+
+
+def test_golden_known_int32(golden_dir):
+    g = np.load(os.path.join(golden_dir, "known_int32.npz"))
+    for key in g.files:
+        if key.endswith("_x"):
+            out = gpu_reduce(list(g[key]), _lib.INT32)
+            np.testing.assert_array_equal(out, g[key[:-2] + "_rb"][0])
+
+
+@pytest.mark.parametrize("k", [2, 8])
+def test_misaligned_and_inplace(k):
+    xs = rand_input(np.float32, k, 10001, seed=7)
+    want = ffref.tree_sum(xs)
+    bits_equal(gpu_reduce(xs, _lib.FLOAT, offset=1), want)       # scalar path
+    bits_equal(gpu_reduce(xs, _lib.FLOAT, out_alias=True), want)  # rb = tmp + rb style
+
+
+def test_zero_count_is_noop():
+    b = DeviceBuffer(4)
+    reduce(_lib.FLOAT, [b.ptr, b.ptr], b.ptr, 0)
+    synchronize()
+
+
+@pytest.mark.parametrize("dtype", [_lib.FLOAT, _lib.INT32, _lib.DOUBLE, _lib.INT64])
+def test_vsum_matches_ffsum(dtype):
+    a, b = rand_input(NP[dtype], 2, 5003, seed=11)
+    da, db, dc = (DeviceBuffer(5003, dtype).upload(a), DeviceBuffer(5003, dtype).upload(b),
+                  DeviceBuffer(5003, dtype))
+    vsum(dtype, da, db, dc, 5003)
+    bits_equal(dc.download(), ffref.vsum(a, b))
+
+
+def test_bf16_golden(golden_dir):
+    g = np.load(os.path.join(golden_dir, "tree_bf16_p8.npz"))
+    out = gpu_reduce(list(g["x"]), _lib.BF16)
+    np.testing.assert_array_equal(out, g["out"])
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 8])
+def test_bf16_matches_oracle(k):
+    rng = np.random.default_rng(k)
+    xs = [ffref.f32_to_bf16(rng.standard_normal(9001).astype(np.float32)) for _ in range(k)]
+    xs[0][:8] = ffref.f32_to_bf16(np.array([np.nan, np.inf, -np.inf, 0, -0.0, 1e-39, 3e38, -3e38],
+                                           np.float32))
+    np.testing.assert_array_equal(gpu_reduce(xs, _lib.BF16), ffref.tree_sum_bf16(xs))
+
+
+@pytest.mark.parametrize("dtype", [_lib.FLOAT, _lib.BF16])
+def test_scaled_reduce(dtype):
+    # opt_esgd_solo_imagenet_imbalance.py:40 divides by comm size; fused here as one
+    # fp32 multiply after the tree (exact IEEE product, then storage rounding)
+    rng = np.random.default_rng(5)
+    xf = [rng.standard_normal(7777).astype(np.float32) for _ in range(8)]
+    if dtype == _lib.BF16:
+        xs = [ffref.f32_to_bf16(x) for x in xf]
+        acc = ffref.bf16_to_f32(np.zeros(1, np.uint16))  # noqa: F841
+        t = [ffref.bf16_to_f32(x) for x in xs]
+        tree = ffref.tree_sum(t)
+        want = ffref.f32_to_bf16(tree * np.float32(0.125))
+    else:
+        xs = xf
+        want = ffref.tree_sum(xs) * np.float32(0.125)
+    bits_equal(gpu_reduce(xs, dtype, scale=0.125), want)
+
+
+def test_fill_uniform_bitwise():
+    for rank in (0, 3, 7):
+        b = DeviceBuffer(100003)
+        fill_uniform(b, 0x5EEDE56D, rank)
+        bits_equal(b.download(), ffref.fill_uniform(0x5EEDE56D, rank, 100003))
+
+
+@pytest.mark.parametrize("unroll,nt,grid", [(1, 0, 0), (2, 1, 0), (4, 1, 0), (4, 0, 7), (2, 1, 1)])
+def test_tuning_variants_identical(unroll, nt, grid):
+    xs = rand_input(np.float32, 8, 300007, seed=3)
+    want = ffref.tree_sum(xs)
+    try:
+        set_tuning("unroll", unroll); set_tuning("nt", nt); set_tuning("grid", grid)
+        bits_equal(gpu_reduce(xs, _lib.FLOAT), want)
+    finally:
+        set_tuning("unroll", 0); set_tuning("nt", 1); set_tuning("grid", 0)
+
+
+def test_full_size_c2_bitwise():
+    """Config C2 at full size: 8 staged 64 MiB fp32 buckets -> 1, generated on device
+    by the shared splitmix generator and checked element-for-element."""
+    n, k, seed = 16 * 1024 * 1024, 8, 0x5EEDE56D
+    s = Stream()
+    bufs = [DeviceBuffer(n) for _ in range(k)]
+    for r, b in enumerate(bufs):
+        fill_uniform(b, seed, r, stream=s)
+    out = DeviceBuffer(n)
+    reduce(_lib.FLOAT, [b.ptr for b in bufs], out, n, stream=s)
+    s.synchronize()
+    got = out.download()
+    xs = [ffref.fill_uniform(seed, r, n) for r in range(k)]
+    bits_equal(got, ffref.tree_sum(xs))
