@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--schedule", choices=["solo", "majority", "allreduce"], default="solo")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
+    ap.add_argument("--no-gate", action="store_true", help="skip the 8 x 256 MiB gate shape")
     ap.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -111,6 +112,7 @@ def run_local(args, esgd, dev):
     s.synchronize()
 
     if args.pmc_child:
+        args.no_gate = True
         for _ in range(5):
             dev.reduce(dt, ptrs, out, count, stream=s)
         s.synchronize()
@@ -120,17 +122,18 @@ def run_local(args, esgd, dev):
         dev.reduce(dt, ptrs, out, count, stream=s)
     s.synchronize()
 
-    evs = [dev.Event() for _ in range(args.steps + 1)]
+    # HIP event pair around every launch, on the launch stream: kernel time per launch
+    evs = [(dev.Event(), dev.Event()) for _ in range(args.steps)]
     dev.device_synchronize()
     t0 = time.perf_counter()
-    evs[0].record(s)
     for i in range(args.steps):
+        evs[i][0].record(s)
         dev.reduce(dt, ptrs, out, count, stream=s)
-        evs[i + 1].record(s)
+        evs[i][1].record(s)
     s.synchronize()
     dev.device_synchronize()
     wall = time.perf_counter() - t0
-    per_launch_ms = evs[0].elapsed_ms(evs[-1]) / args.steps
+    per_launch_ms = sum(a.elapsed_ms(b) for a, b in evs) / args.steps
 
     # parity spot-check outside the timed region: first 1 Mi elements vs the oracle
     parity = "skipped"
@@ -142,6 +145,9 @@ def run_local(args, esgd, dev):
         want = ffref.tree_sum([ffref.fill_uniform(SEED, r, m) for r in range(k)])
         parity = "bitwise" if np.array_equal(got.view(np.uint32), want.view(np.uint32)) else "MISMATCH"
 
+    gate = None
+    if not args.no_gate:
+        gate = gate_256(dev, dt, es, k, s)
     bucket_bytes = count * es
     algo_bytes = (k + 1) * bucket_bytes        # k reads + 1 write per launch
     achieved = algo_bytes / (per_launch_ms * 1e-3) / 1e9
@@ -155,7 +161,36 @@ def run_local(args, esgd, dev):
         "bucket_bytes": bucket_bytes,
         "k": k,
         "parity": parity,
+        "gate": gate,
     }
+
+
+def gate_256(dev, dt, es, k, s, iters=20):
+    """BASELINE.json's 1-GPU gate shape (k x 256 MiB buckets, no Infinity-Cache reuse
+    possible): per-launch time from HIP event pairs on the launch stream."""
+    count = (256 * MiB) // es
+    bufs = [dev.DeviceBuffer(count, dt) for _ in range(k)]
+    for r, b in enumerate(bufs):
+        dev.fill_uniform(b, SEED, r, stream=s)
+    out = dev.DeviceBuffer(count, dt)
+    ptrs = [b.ptr for b in bufs]
+    for _ in range(3):
+        dev.reduce(dt, ptrs, out, count, stream=s)
+    ev = [dev.Event() for _ in range(2 * iters)]
+    for i in range(iters):
+        ev[2 * i].record(s)
+        dev.reduce(dt, ptrs, out, count, stream=s)
+        ev[2 * i + 1].record(s)
+    s.synchronize()
+    ts = sorted(ev[2 * i].elapsed_ms(ev[2 * i + 1]) for i in range(iters))
+    med = ts[iters // 2]
+    algo = (k + 1) * count * es
+    for b in bufs:
+        b.close()
+    out.close()
+    return {"workload": f"{k} x 256 MiB -> 1", "kernel_ms_median": round(med, 4),
+            "achieved_GBs": round(algo / (med * 1e-3) / 1e9, 1),
+            "frac": round(algo / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 def main():
@@ -201,6 +236,8 @@ def main():
                    "parallelism": "single GPU", "kernel": "esgd_reduce (k_tree_sum)"},
         "parity": res["parity"],
     }
+    if res.get("gate"):
+        line["gate_256MiB"] = res["gate"]
     traffic = None
     if not args.no_pmc:
         try:

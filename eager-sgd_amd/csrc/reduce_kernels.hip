@@ -23,6 +23,7 @@
 #include <cstdint>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 
 #include "esgd_internal.h"
 
@@ -117,8 +118,9 @@ __device__ __forceinline__ raw16 fold16(const raw16 (&r)[K], float scale) {
     return o;
 }
 
-// Vector body: `nvec` 16-B columns; the ragged tail (< E elements) is folded by
-// block 0 with scalar accesses.
+// Flat-address body for buckets past the descriptor's 32-bit byte range (> 2 GiB) and
+// for A/B runs (policy 0): `nvec` 16-B columns; the ragged tail (< E elements) is
+// folded by block 0 with scalar accesses.
 template <class Tr, int K, int U, bool NT, bool SCALE>
 __global__ __launch_bounds__(256) void k_tree_sum(InputSet in, void *out, uint64_t nvec,
                                                    uint64_t count, float scale) {
@@ -148,6 +150,52 @@ __global__ __launch_bounds__(256) void k_tree_sum(InputSet in, void *out, uint64
     using T = typename Tr::T;
     using A = typename Tr::A;
     const uint64_t tail0 = nvec * Tr::E;
+    if (blockIdx.x == 0 && tail0 + threadIdx.x < count) {
+        const uint64_t e = tail0 + threadIdx.x;
+        A v[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) v[j] = Tr::load(static_cast<const T *>(in.p[j])[e]);
+        tree_fold<Tr, K>(v);
+        if constexpr (SCALE) v[0] = v[0] * scale;
+        static_cast<T *>(out)[e] = Tr::store(v[0]);
+    }
+}
+
+// Production body: buffer-descriptor loads/stores (`buffer_load_dwordx4 ... offen`) with
+// explicit cache-policy bits (aux: 1 = sc0, 2 = nt, 16 = sc1).  Measured on MI355X
+// (profiles/r01/sweep_policy.md): nt loads + sc1 (write-through, not retained in L2)
+// stores move 6.5 TB/s at k = 8 x 256 MiB against 5.9 TB/s for plain global
+// loads/stores — the once-read inputs and the once-written output stop competing for
+// L2 / Infinity Cache.  The descriptor's range check (num_records = bytes of the vector
+// body) turns the ragged last iteration into zero-fill loads and dropped stores, so the
+// loop has no per-element branch (cdna_hip_programming.md §5 item 4c).
+template <class Tr, int K, int U, int LAUX, int SAUX, bool SCALE>
+__global__ __launch_bounds__(256) void k_tree_sum_buf(InputSet in, void *out, uint32_t nvec,
+                                                       uint64_t count, float scale) {
+    constexpr int B = 256;
+    const int bytes = int(nvec * 16u);
+    __amdgpu_buffer_rsrc_t rs[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(in.p[j]), (short)0, bytes,
+                                                  0x00020000);
+    __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, bytes, 0x00020000);
+    const uint32_t step = gridDim.x * (B * U);
+    for (uint32_t i = blockIdx.x * (B * U) + threadIdx.x; i < nvec; i += step) {
+        raw16 r[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                r[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs[j], (i + u * B) * 16, 0, LAUX);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_raw_buffer_store_b128(fold16<Tr, K, SCALE>(r[u], scale), ws,
+                                                   (i + u * B) * 16, 0, SAUX);
+    }
+    using T = typename Tr::T;
+    using A = typename Tr::A;
+    const uint64_t tail0 = uint64_t(nvec) * Tr::E;
     if (blockIdx.x == 0 && tail0 + threadIdx.x < count) {
         const uint64_t e = tail0 + threadIdx.x;
         A v[K];
@@ -202,9 +250,11 @@ __global__ void k_fill_uniform_bf16(uint64_t base, uint16_t *out, uint64_t n) {
 }
 
 // ---- launch configuration ----
-static int g_unroll = 0;   // 0 -> default per type
-static int g_grid = 0;     // 0 -> auto
-static int g_nt = -1;      // -1 -> default (on)
+static int g_unroll = 0;   // 0 -> default (4 x 16 B per input per lane)
+static int g_grid = 0;     // 0 -> auto: 8 blocks of 256 per CU, grid-stride
+static int g_nt = -1;      // flat path only: -1/1 -> nt loads/stores
+static int g_policy = -1;  // -1 -> production policy (nt loads, sc1 stores); 0 -> flat path;
+                           // 1..8 -> cache-policy table below (F32, k = 8 only; sweeps)
 
 static int cu_count() {
     static int cus[64] = {};
@@ -218,16 +268,27 @@ static int cu_count() {
     return cus[dev];
 }
 
-static unsigned grid_for(uint64_t items_per_block_pass, uint64_t items) {
+// Grid-stride launches are sized to what is resident at once (CUs x blocks per CU that
+// the kernel's registers admit): a second, queued wave of blocks only adds a tail
+// (profiles/r01/sweep_grid.md: 1024 blocks = 4/CU beat 2048 at 98 VGPRs).
+static unsigned grid_for(uint64_t items_per_block_pass, uint64_t items, int blocks_per_cu = 8) {
     if (g_grid > 0) return unsigned(g_grid);
     uint64_t need = (items + items_per_block_pass - 1) / items_per_block_pass;
-    uint64_t cap = uint64_t(cu_count()) * 8;   // 8 x 256-thread blocks per CU
+    uint64_t cap = uint64_t(cu_count()) * uint64_t(blocks_per_cu > 0 ? blocks_per_cu : 1);
     if (need < 1) need = 1;
     return unsigned(need < cap ? need : cap);
 }
 
+template <typename KernelT>
+static int resident_blocks(KernelT kernel) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, 256, 0) != hipSuccess || nb <= 0)
+        nb = 4;
+    return nb < 8 ? nb : 8;
+}
+
 template <class Tr, int K, int U, bool NT, bool SCALE>
-static int launch_vec(const InputSet &in, void *out, uint64_t count, float scale, hipStream_t s) {
+static int launch_flat(const InputSet &in, void *out, uint64_t count, float scale, hipStream_t s) {
     const uint64_t nvec = count / Tr::E;
     unsigned grid = grid_for(uint64_t(256) * U, nvec ? nvec : 1);
     hipLaunchKernelGGL((k_tree_sum<Tr, K, U, NT, SCALE>), dim3(grid), dim3(256), 0, s, in, out,
@@ -235,6 +296,20 @@ static int launch_vec(const InputSet &in, void *out, uint64_t count, float scale
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;
 }
+
+template <class Tr, int K, int U, int LA, int SA, bool SCALE>
+static int launch_buf(const InputSet &in, void *out, uint64_t count, float scale, hipStream_t s) {
+    const uint64_t nvec = count / Tr::E;
+    static const int per_cu = resident_blocks(k_tree_sum_buf<Tr, K, U, LA, SA, SCALE>);
+    unsigned grid = grid_for(uint64_t(256) * U, nvec ? nvec : 1, per_cu);
+    hipLaunchKernelGGL((k_tree_sum_buf<Tr, K, U, LA, SA, SCALE>), dim3(grid), dim3(256), 0, s, in,
+                       out, uint32_t(nvec), count, scale);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+// alternative {load aux, store aux} pairs kept for sweeps (tools/sweep_reduce.py)
+#define ESGD_POLICIES(X) X(1, 2, 16) X(2, 2, 17) X(3, 2, 18) X(4, 2, 19) X(5, 0, 16) X(6, 3, 16) X(7, 18, 16) X(8, 16, 16)
 
 template <class Tr, int K, bool SCALE>
 static int launch_scalar(const InputSet &in, void *out, uint64_t count, float scale, hipStream_t s) {
@@ -249,15 +324,28 @@ template <class Tr, int K, bool SCALE>
 static int dispatch_u(const InputSet &in, void *out, uint64_t count, float scale, bool aligned,
                       hipStream_t s) {
     if (!aligned) return launch_scalar<Tr, K, SCALE>(in, out, count, scale, s);
+    // bf16 folds 8 lanes per 16 B: two vectors per input keep it under 128 VGPRs
+    constexpr int UD = sizeof(typename Tr::T) == 2 ? 2 : 4;
+    const bool fits32 = count / Tr::E * 16 + uint64_t(UD) * 256 * 16 < (1ull << 31);
+    if (g_policy != 0 && fits32) {
+        if constexpr (std::is_same<Tr, F32>::value && K == 8) {
+            switch (g_policy) {
+#define ESGD_CASE(ID, LA, SA) \
+            case ID: return launch_buf<Tr, K, 4, LA, SA, SCALE>(in, out, count, scale, s);
+            ESGD_POLICIES(ESGD_CASE)
+#undef ESGD_CASE
+            default: break;
+            }
+        }
+        if (g_unroll == 2 || g_unroll == 1)
+            return launch_buf<Tr, K, 2, 2, 16, SCALE>(in, out, count, scale, s);
+        return launch_buf<Tr, K, UD, 2, 16, SCALE>(in, out, count, scale, s);
+    }
     const bool nt = g_nt != 0;
-    int u = g_unroll ? g_unroll : 2;
-    if constexpr (sizeof(typename Tr::T) == 2) u = 1;  // bf16: 8 accumulators per vector already
-    if (u >= 4) return nt ? launch_vec<Tr, K, 4, true, SCALE>(in, out, count, scale, s)
-                          : launch_vec<Tr, K, 4, false, SCALE>(in, out, count, scale, s);
-    if (u == 2) return nt ? launch_vec<Tr, K, 2, true, SCALE>(in, out, count, scale, s)
-                          : launch_vec<Tr, K, 2, false, SCALE>(in, out, count, scale, s);
-    return nt ? launch_vec<Tr, K, 1, true, SCALE>(in, out, count, scale, s)
-              : launch_vec<Tr, K, 1, false, SCALE>(in, out, count, scale, s);
+    if (g_unroll == 1) return nt ? launch_flat<Tr, K, 1, true, SCALE>(in, out, count, scale, s)
+                                 : launch_flat<Tr, K, 1, false, SCALE>(in, out, count, scale, s);
+    return nt ? launch_flat<Tr, K, 2, true, SCALE>(in, out, count, scale, s)
+              : launch_flat<Tr, K, 2, false, SCALE>(in, out, count, scale, s);
 }
 
 template <class Tr, bool SCALE>
@@ -372,6 +460,9 @@ int esgd_set_tuning(const char *key, int value) {
         g_grid = value;
     } else if (!std::strcmp(key, "nt")) {
         g_nt = value ? 1 : 0;
+    } else if (!std::strcmp(key, "policy")) {
+        ESGD_ARG(value >= -1 && value <= 8, "policy must be -1..8");
+        g_policy = value;
     } else {
         set_error("esgd_set_tuning: unknown key '%s'", key);
         return ESGD_INVALID_ARG;
@@ -384,6 +475,7 @@ int esgd_get_tuning(const char *key, int *value) {
     if (!std::strcmp(key, "unroll")) *value = g_unroll;
     else if (!std::strcmp(key, "grid")) *value = g_grid;
     else if (!std::strcmp(key, "nt")) *value = g_nt;
+    else if (!std::strcmp(key, "policy")) *value = g_policy;
     else {
         set_error("esgd_get_tuning: unknown key '%s'", key);
         return ESGD_INVALID_ARG;

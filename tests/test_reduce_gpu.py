@@ -131,7 +131,6 @@ def test_scaled_reduce(dtype):
     xf = [rng.standard_normal(7777).astype(np.float32) for _ in range(8)]
     if dtype == _lib.BF16:
         xs = [ffref.f32_to_bf16(x) for x in xf]
-        acc = ffref.bf16_to_f32(np.zeros(1, np.uint16))  # noqa: F841
         t = [ffref.bf16_to_f32(x) for x in xs]
         tree = ffref.tree_sum(t)
         want = ffref.f32_to_bf16(tree * np.float32(0.125))
@@ -148,15 +147,19 @@ def test_fill_uniform_bitwise():
         bits_equal(b.download(), ffref.fill_uniform(0x5EEDE56D, rank, 100003))
 
 
-@pytest.mark.parametrize("unroll,nt,grid", [(1, 0, 0), (2, 1, 0), (4, 1, 0), (4, 0, 7), (2, 1, 1)])
-def test_tuning_variants_identical(unroll, nt, grid):
-    xs = rand_input(np.float32, 8, 300007, seed=3)
+@pytest.mark.parametrize("policy,unroll,nt,grid", [
+    (-1, 0, 1, 0), (-1, 2, 1, 7), (-1, 4, 1, 1), (0, 1, 0, 0), (0, 2, 1, 0), (0, 4, 0, 7),
+    (1, 0, 1, 0), (3, 0, 1, 5), (5, 0, 1, 0), (8, 0, 1, 3)])
+@pytest.mark.parametrize("k", [2, 8])
+def test_tuning_variants_identical(policy, unroll, nt, grid, k):
+    xs = rand_input(np.float32, k, 300007, seed=3)
     want = ffref.tree_sum(xs)
     try:
-        set_tuning("unroll", unroll); set_tuning("nt", nt); set_tuning("grid", grid)
+        set_tuning("policy", policy); set_tuning("unroll", unroll); set_tuning("nt", nt)
+        set_tuning("grid", grid)
         bits_equal(gpu_reduce(xs, _lib.FLOAT), want)
     finally:
-        set_tuning("unroll", 0); set_tuning("nt", 1); set_tuning("grid", 0)
+        set_tuning("policy", -1); set_tuning("unroll", 0); set_tuning("nt", 1); set_tuning("grid", 0)
 
 
 def test_full_size_c2_bitwise():
@@ -171,5 +174,21 @@ def test_full_size_c2_bitwise():
     reduce(_lib.FLOAT, [b.ptr for b in bufs], out, n, stream=s)
     s.synchronize()
     got = out.download()
+    xs = [ffref.fill_uniform(seed, r, n) for r in range(k)]
+    bits_equal(got, ffref.tree_sum(xs))
+
+
+def test_full_size_gate_256mib_bitwise():
+    """The 1-GPU gate shape of BASELINE.json: 8 x 256 MiB fp32 buckets, checked in full."""
+    n, k, seed = 64 * 1024 * 1024, 8, 0x5EEDE56D
+    s = Stream()
+    bufs = [DeviceBuffer(n) for _ in range(k)]
+    for r, b in enumerate(bufs):
+        fill_uniform(b, seed, r, stream=s)
+    out = DeviceBuffer(n)
+    reduce(_lib.FLOAT, [b.ptr for b in bufs], out, n, stream=s)
+    s.synchronize()
+    got = out.download()
+    del bufs
     xs = [ffref.fill_uniform(seed, r, n) for r in range(k)]
     bits_equal(got, ffref.tree_sum(xs))

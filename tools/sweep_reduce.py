@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Interleaved A/B sweep of the reduction launch parameters in ONE process
+(cdna_hip_programming.md §5.4 rule 24): every variant is timed once per round, for
+several rounds, and the median/min per-launch time from HIP event pairs is reported.
+
+  python tools/sweep_reduce.py [--k 8] [--mib 64] [--rounds 7] [--iters 30]
+"""
+import argparse
+import itertools
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "eager-sgd_amd"))
+
+import esgd  # noqa: E402
+from esgd import device as dev  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--k", type=int, default=8)
+ap.add_argument("--mib", type=float, default=64)
+ap.add_argument("--rounds", type=int, default=7)
+ap.add_argument("--iters", type=int, default=30)
+ap.add_argument("--dtype", default="fp32")
+ap.add_argument("--grids", default="0,1024,2048,4096,8192,16384")
+ap.add_argument("--unrolls", default="2,4")
+ap.add_argument("--nts", default="0,1")
+ap.add_argument("--policies", default="-1")
+ap.add_argument("--stagger", type=int, default=0,
+                help="bytes between consecutive buckets in one arena (0 = separate allocations)")
+a = ap.parse_args()
+
+dt = esgd.FLOAT if a.dtype == "fp32" else esgd.BF16
+es = 4 if dt == esgd.FLOAT else 2
+count = int(a.mib * (1 << 20)) // es
+s = dev.Stream()
+if a.stagger:
+    pitch = count * es + a.stagger
+    arena = dev.DeviceBuffer((pitch * (a.k + 1)) // es + 1, dt)
+    ptrs = [arena.ptr + r * pitch for r in range(a.k)]
+    out = arena.ptr + a.k * pitch
+    for r, p in enumerate(ptrs):
+        esgd.check(esgd.lib().esgd_fill_uniform_f32(0x5EEDE56D, r, p, count, s.handle))
+else:
+    bufs = [dev.DeviceBuffer(count, dt) for _ in range(a.k)]
+    for r, b in enumerate(bufs):
+        dev.fill_uniform(b, 0x5EEDE56D, r, stream=s)
+    out = dev.DeviceBuffer(count, dt)
+    ptrs = [b.ptr for b in bufs]
+s.synchronize()
+variants = list(itertools.product([int(x) for x in a.unrolls.split(",")],
+                                  [int(x) for x in a.nts.split(",")],
+                                  [int(x) for x in a.grids.split(",")],
+                                  [int(x) for x in a.policies.split(",")]))
+ev = [dev.Event() for _ in range(2 * a.iters)]
+times = {v: [] for v in variants}
+for rnd in range(a.rounds):
+    for v in variants:
+        u, nt, g, pol = v
+        dev.set_tuning("unroll", u); dev.set_tuning("nt", nt); dev.set_tuning("grid", g)
+        dev.set_tuning("policy", pol)
+        for _ in range(3):
+            dev.reduce(dt, ptrs, out, count, stream=s)
+        for i in range(a.iters):
+            ev[2 * i].record(s)
+            dev.reduce(dt, ptrs, out, count, stream=s)
+            ev[2 * i + 1].record(s)
+        s.synchronize()
+        times[v].extend(ev[2 * i].elapsed_ms(ev[2 * i + 1]) for i in range(a.iters))
+algo = (a.k + 1) * count * es
+rows = []
+for v, t in times.items():
+    med, mn = statistics.median(t), min(t)
+    rows.append({"unroll": v[0], "nt": v[1], "grid": v[2], "policy": v[3],
+                 "median_us": round(med * 1e3, 2),
+                 "min_us": round(mn * 1e3, 2), "median_GBs": round(algo / (med * 1e-3) / 1e9, 1),
+                 "frac_of_8TBs": round(algo / (med * 1e-3) / 8e12, 4)})
+rows.sort(key=lambda r: r["median_us"])
+for r in rows:
+    r.update(k=a.k, mib=a.mib, stagger=a.stagger)
+    print(json.dumps(r))
