@@ -1,0 +1,125 @@
+// comm_api.cpp — C ABI of the node communicator and the persistent schedules (esgd.h).
+#include <cstring>
+
+#include "engine.h"
+#include "esgd_internal.h"
+
+namespace esgd {
+Transport *ipc_transport();
+Transport *null_transport();
+hipStream_t sched_stream(Sched &s);
+}  // namespace esgd
+
+using namespace esgd;
+
+static Sched *handle_to_sched(esgd_sched_h h) {
+    Sched *s = sched_lookup(h);
+    if (!s) set_error("unknown or deleted schedule handle 0x%llx", (unsigned long long)h);
+    return s;
+}
+
+extern "C" {
+
+int esgd_comm_init(const char *job_id, int rank, int world) {
+    ESGD_ARG(job_id && *job_id, "esgd_comm_init: empty job id");
+    return engine_init(job_id, rank, world, true);
+}
+
+int esgd_comm_finalize(void) { return engine_finalize(); }
+
+int esgd_comm_rank(int *rank) {
+    ESGD_ARG(rank, "esgd_comm_rank: null pointer");
+    *rank = engine_rank();
+    return ESGD_SUCCESS;
+}
+
+int esgd_comm_size(int *size) {
+    ESGD_ARG(size, "esgd_comm_size: null pointer");
+    *size = engine_ready() ? engine_world() : 1;
+    return ESGD_SUCCESS;
+}
+
+int esgd_barrier(void) { return engine_barrier(); }
+
+int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t count, int dtype,
+                         int async, unsigned seed, esgd_sched_h *out) {
+    ESGD_ARG(out, "esgd_schedule_create: null output");
+    ESGD_ARG(buf == ESGD_BUF_DEVICE || buf == ESGD_BUF_HOST || buf == ESGD_BUF_NONE,
+             "esgd_schedule_create: bad buffer kind %d", buf);
+    ESGD_ARG(esgd_dtype_size(dtype) > 0, "esgd_schedule_create: unsupported dtype %d", dtype);
+    ESGD_ARG(buf == ESGD_BUF_NONE || rb || count == 0, "esgd_schedule_create: null receive buffer");
+    Transport *tp = buf == ESGD_BUF_NONE ? null_transport() : ipc_transport();
+    Sched *s = nullptr;
+    int rc = sched_create(kind, dtype, count, const_cast<void *>(sb), rb, buf == ESGD_BUF_HOST,
+                          async, seed, tp, &s);
+    if (rc) return rc;
+    *out = reinterpret_cast<esgd_sched_h>(s);
+    return ESGD_SUCCESS;
+}
+
+int esgd_schedule_post(esgd_sched_h h, void *producer_stream, int *role) {
+    Sched *s = handle_to_sched(h);
+    if (!s) return ESGD_INVALID_ARG;
+    return sched_post(s, producer_stream, role);
+}
+
+int esgd_schedule_wait(esgd_sched_h h) {
+    Sched *s = handle_to_sched(h);
+    if (!s) return ESGD_INVALID_ARG;
+    return sched_wait(s);
+}
+
+int esgd_schedule_test(esgd_sched_h h, int *flag) {
+    Sched *s = handle_to_sched(h);
+    if (!s) return ESGD_INVALID_ARG;
+    return sched_test(s, flag);
+}
+
+int esgd_schedule_delete(esgd_sched_h h) {
+    Sched *s = handle_to_sched(h);
+    if (!s) return ESGD_INVALID_ARG;
+    return sched_delete(s);
+}
+
+int esgd_schedule_stats(esgd_sched_h h, esgd_sched_stats_t *out) {
+    ESGD_ARG(out, "esgd_schedule_stats: null output");
+    Sched *s = handle_to_sched(h);
+    if (!s) return ESGD_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(s->mu);
+    out->posted = s->posted.load();
+    out->joined = s->joined;
+    out->completed = s->completed;
+    out->waited = s->waited;
+    out->activated = s->sh->activated.load();
+    out->last_activator = s->sh->last_activator.load();
+    out->fresh_rounds = s->n_fresh;
+    out->auto_rounds = s->n_auto;
+    out->activations = s->n_activated;
+    return ESGD_SUCCESS;
+}
+
+int esgd_schedule_log(esgd_sched_h h, uint32_t *rounds, uint8_t *fresh, uint8_t *sync,
+                      int16_t *activator, uint32_t cap, uint32_t *n) {
+    Sched *s = handle_to_sched(h);
+    if (!s) return ESGD_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(s->mu);
+    const uint32_t total = uint32_t(s->log.size());
+    for (uint32_t i = 0; i < total && i < cap; ++i) {
+        if (rounds) rounds[i] = s->log[i].round;
+        if (fresh) fresh[i] = s->log[i].fresh;
+        if (sync) sync[i] = s->log[i].sync;
+        if (activator) activator[i] = s->log[i].activator;
+    }
+    if (n) *n = total;
+    return ESGD_SUCCESS;
+}
+
+int esgd_schedule_stream(esgd_sched_h h, void **stream) {
+    ESGD_ARG(stream, "esgd_schedule_stream: null output");
+    Sched *s = handle_to_sched(h);
+    if (!s) return ESGD_INVALID_ARG;
+    *stream = sched_stream(*s);
+    return ESGD_SUCCESS;
+}
+
+}  // extern "C"

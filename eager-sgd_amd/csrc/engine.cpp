@@ -1,0 +1,385 @@
+// engine.cpp — partial-allreduce schedules, the round protocol and the progress thread.
+//
+// Per schedule and round t, every rank walks the same stages (engine.h: Stage):
+//   join -> snapshot (move sb -> rb)      -> publish ready[r]   = t
+//        -> all ready  -> reduce-scatter  -> publish reduced[r] = t
+//        -> all reduced -> all-gather     -> publish done[r]    = t
+//        -> all done   -> copy-out        -> completed = t, wake wait()
+// "Join" is decided by the activation rules of fflib2 (see engine.h).  The three
+// all-rank conditions are epochs in the node segment; they are what fflib2's matched
+// MPI send/recv pairs guarantee implicitly (src/colls/ffallreduce.c:145-162: a send of
+// rb happens after the previous comp, the comp after the recv).
+#include "engine.h"
+
+#include <hip/hip_runtime.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+
+#include "esgd_internal.h"
+
+namespace esgd {
+
+static Segment *g_seg = nullptr;
+static int g_rank = 0, g_world = 1, g_device = -1;
+static std::string g_job;
+static double g_timeout = 600.0;
+static std::mutex g_reg_mu;
+static std::vector<Sched *> g_reg;
+static std::mutex g_create_mu;
+static int g_next_id = 0;
+static std::thread g_thread;
+static std::atomic<bool> g_running{false};
+static std::atomic<uint32_t> g_wake{0};
+
+bool engine_ready() { return g_seg != nullptr; }
+int engine_rank() { return g_rank; }
+int engine_world() { return g_world; }
+Segment *engine_segment() { return g_seg; }
+double engine_timeout() { return g_timeout; }
+
+int engine_barrier() {
+    if (!g_seg) { set_error("esgd: communicator not initialised"); return ESGD_ERROR; }
+    return shm_barrier(g_seg, g_world, g_timeout);
+}
+
+bool round_is_sync(const Sched &s, uint32_t round) {
+    switch (s.kind) {
+    case KIND_SOLO:  // limiter: posts 1..async asynchronous, post async+1 synchronous
+        return s.async <= 0 || round % uint32_t(s.async + 1) == 0;
+    case KIND_MAJORITY: return false;
+    default: return true;
+    }
+}
+
+static void progress_main() {
+    if (g_device >= 0) (void)hipSetDevice(g_device);
+    unsigned polls = 0;
+    uint32_t seen = g_wake.load();
+    while (g_running.load(std::memory_order_acquire)) {
+        if (engine_progress_once()) { polls = 0; continue; }
+        const uint32_t w = g_wake.load(std::memory_order_acquire);
+        if (w != seen) { seen = w; polls = 0; continue; }
+        backoff(polls);
+    }
+}
+
+int engine_init(const char *job, int rank, int world, bool start_progress) {
+    if (g_seg) {
+        if (rank == g_rank && world == g_world) return ESGD_SUCCESS;
+        set_error("esgd: already initialised as rank %d/%d", g_rank, g_world);
+        return ESGD_INVALID_ARG;
+    }
+    if (const char *t = getenv("ESGD_TIMEOUT_S")) g_timeout = atof(t) > 0 ? atof(t) : g_timeout;
+    Segment *seg = shm_attach(job, rank, world, g_timeout);
+    if (!seg) return ESGD_ERROR;
+    g_seg = seg; g_rank = rank; g_world = world; g_job = job;
+    int dev = -1;
+    if (start_progress && hipGetDevice(&dev) == hipSuccess) g_device = dev;
+    seg->device[rank].store(g_device);
+    if (int rc = shm_barrier(seg, world, g_timeout)) { g_seg = nullptr; shm_detach(seg, job, rank); return rc; }
+    // every rank is attached: drop the name so nothing outlives the job in /dev/shm
+    if (rank == 0) shm_unlink_name(job);
+    if (start_progress) {
+        g_running.store(true);
+        g_thread = std::thread(progress_main);
+    }
+    return ESGD_SUCCESS;
+}
+
+int engine_finalize() {
+    if (!g_seg) return ESGD_SUCCESS;
+    int rc = shm_barrier(g_seg, g_world, g_timeout);
+    if (g_running.exchange(false)) g_thread.join();
+    std::vector<Sched *> left;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        left.swap(g_reg);
+    }
+    for (Sched *s : left) {
+        if (s->tp) s->tp->teardown(*s);
+        delete s;
+    }
+    shm_detach(g_seg, nullptr, -1);
+    g_seg = nullptr;
+    g_next_id = 0;
+    return rc;
+}
+
+// ---- schedules -------------------------------------------------------------------
+
+static void fail_locked(Sched &s, int rc, const char *msg) {
+    s.error = rc ? rc : ESGD_ERROR;
+    snprintf(s.errmsg, sizeof(s.errmsg), "schedule %d round %u: %s", s.id, s.cur, msg);
+    s.cv.notify_all();
+}
+
+int sched_create(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
+                 int async, unsigned seed, Transport *tp, Sched **out) {
+    ESGD_ARG(out, "schedule create: null output");
+    ESGD_ARG(kind >= KIND_ALLREDUCE && kind <= KIND_MAJORITY, "schedule create: bad kind %d", kind);
+    ESGD_ARG(tp, "schedule create: no transport");
+    if (!g_seg) { set_error("esgd: communicator not initialised (ffinit / esgd_comm_init)"); return ESGD_ERROR; }
+    std::lock_guard<std::mutex> clk(g_create_mu);
+    if (g_next_id >= kMaxSched) { set_error("schedule create: more than %d schedules", kMaxSched); return ESGD_ENOMEM; }
+    Sched *s = new Sched();
+    s->id = g_next_id++;
+    s->kind = kind; s->dtype = dtype; s->count = count; s->esize = esgd_dtype_size(dtype);
+    s->sb = sb; s->rb = rb; s->host_mode = host_mode; s->in_place = (sb == nullptr || sb == rb);
+    s->async = async; s->seed = seed;
+    s->rank = g_rank; s->world = g_world;
+    s->sh = &g_seg->sched[s->id];
+    s->tp = tp;
+    int rc = shm_barrier(g_seg, g_world, g_timeout);
+    if (!rc && g_rank == 0) {
+        SchedShm *sh = s->sh;
+        sh->kind.store(uint32_t(kind));
+        sh->activated.store(0);
+        sh->last_activator.store(-1);
+        for (int r = 0; r < kMaxRanks; ++r) {
+            sh->ready[r].store(0); sh->reduced[r].store(0); sh->done[r].store(0);
+            sh->joined[r].store(0); sh->activations[r].store(0);
+        }
+        sh->gen.fetch_add(1, std::memory_order_acq_rel);
+    }
+    if (!rc) rc = shm_barrier(g_seg, g_world, g_timeout);
+    if (!rc && s->sh->kind.load() != uint32_t(kind)) {
+        set_error("schedule create: rank %d kind %d differs from rank 0's %u (creation order must match)",
+                  g_rank, kind, s->sh->kind.load());
+        rc = ESGD_INVALID_ARG;
+    }
+    s->gen = s->sh->gen.load();
+    if (!rc) rc = tp->setup(*s);   // collective registration (has its own barriers)
+    int rc2 = shm_barrier(g_seg, g_world, g_timeout);
+    if (!rc) rc = rc2;
+    if (rc) { delete s; return rc; }
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        g_reg.push_back(s);
+    }
+    *out = s;
+    return ESGD_SUCCESS;
+}
+
+static void activate_max(SchedShm *sh, uint32_t round, int rank, bool *raised) {
+    uint32_t cur = sh->activated.load(std::memory_order_acquire);
+    *raised = false;
+    while (cur < round) {
+        if (sh->activated.compare_exchange_weak(cur, round, std::memory_order_acq_rel)) {
+            *raised = true;
+            sh->last_activator.store(rank, std::memory_order_relaxed);
+            sh->activations[rank].fetch_add(1, std::memory_order_relaxed);
+            break;
+        }
+    }
+}
+
+int sched_post(Sched *s, void *producer_stream, int *role) {
+    ESGD_ARG(s, "schedule post: null schedule");
+    int r = 0;
+    {
+        std::lock_guard<std::mutex> lk(s->mu);
+        if (s->error) { set_error("%s", s->errmsg); return s->error; }
+        const uint32_t t = s->posted.load() + 1;
+        if (producer_stream)
+            if (int rc = s->tp->note_producer(*s, t, producer_stream)) return rc;
+        s->posted.store(t, std::memory_order_release);
+        if (s->kind == KIND_MAJORITY) {
+            // colls/ffrand_allreduce.c:88 — the same glibc draw on every rank
+            const int act = int(unsigned(rand_r(&s->seed)) % unsigned(s->world));
+            if (act == s->rank) {
+                bool raised;
+                activate_max(s->sh, t, s->rank, &raised);
+                s->passive = 0;   // catch-up of :93-96 is implicit in the round counter
+                r = 1;
+                if (raised) ++s->n_activated;
+            } else {
+                ++s->passive;
+                r = 0;
+            }
+        } else if (round_is_sync(*s, t)) {
+            r = 2;
+        } else {
+            bool raised;
+            activate_max(s->sh, t, s->rank, &raised);   // first poster activates the round
+            r = raised ? 1 : 0;
+            if (raised) ++s->n_activated;
+        }
+    }
+    g_wake.fetch_add(1, std::memory_order_acq_rel);
+    if (role) *role = r;
+    return ESGD_SUCCESS;
+}
+
+int sched_wait(Sched *s) {
+    ESGD_ARG(s, "schedule wait: null schedule");
+    std::unique_lock<std::mutex> lk(s->mu);
+    const uint32_t target = s->waited + 1;
+    const double t0 = now_s();
+    while (s->completed < target && !s->error) {
+        s->cv.wait_for(lk, std::chrono::milliseconds(50));
+        if (now_s() - t0 > g_timeout) {
+            fail_locked(*s, ESGD_ERROR, "wait timed out (a peer never posted / activated?)");
+            break;
+        }
+    }
+    if (s->error) { set_error("%s", s->errmsg); return s->error; }
+    s->waited = target;
+    return ESGD_SUCCESS;
+}
+
+int sched_test(Sched *s, int *flag) {
+    ESGD_ARG(s && flag, "schedule test: null argument");
+    std::lock_guard<std::mutex> lk(s->mu);
+    if (s->error) { set_error("%s", s->errmsg); return s->error; }
+    *flag = s->completed >= s->waited + 1;
+    if (*flag) ++s->waited;
+    return ESGD_SUCCESS;
+}
+
+int sched_delete(Sched *s) {
+    ESGD_ARG(s, "schedule delete: null schedule");
+    const double t0 = now_s();
+    for (;;) {   // let an in-flight round finish (peers may still need our flags)
+        {
+            std::lock_guard<std::mutex> lk(s->mu);
+            if (s->stage == ST_IDLE || s->error) { s->live.store(false); break; }
+        }
+        if (now_s() - t0 > g_timeout) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        g_reg.erase(std::remove(g_reg.begin(), g_reg.end(), s), g_reg.end());
+    }
+    int rc = shm_barrier(g_seg, g_world, g_timeout);
+    s->tp->teardown(*s);
+    int rc2 = shm_barrier(g_seg, g_world, g_timeout);
+    delete s;
+    return rc ? rc : rc2;
+}
+
+Sched *sched_lookup(uint64_t handle) {
+    Sched *p = reinterpret_cast<Sched *>(handle);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (Sched *s : g_reg)
+        if (s == p) return s;
+    return nullptr;
+}
+
+// ---- the progress step -------------------------------------------------------------
+
+static bool all_at_least(const std::atomic<uint32_t> *v, int world, uint32_t round) {
+    for (int r = 0; r < world; ++r)
+        if (v[r].load(std::memory_order_acquire) < round) return false;
+    return true;
+}
+
+static bool step(Sched &s) {
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (s.error || !s.live.load()) return false;
+    SchedShm *sh = s.sh;
+    auto enter = [&](Stage st) { s.stage = st; s.stage_t0 = now_s(); };
+    auto check = [&](int rc, const char *what) {
+        if (rc < 0) {
+            std::string m = std::string(what) + ": " + esgd_last_error();
+            fail_locked(s, rc, m.c_str());
+            return false;
+        }
+        return true;
+    };
+    auto timed_out = [&](const char *what) {
+        if (now_s() - s.stage_t0 > g_timeout) {
+            fail_locked(s, ESGD_ERROR, what);
+            return true;
+        }
+        return false;
+    };
+    switch (s.stage) {
+    case ST_IDLE: {
+        const uint32_t next = s.joined + 1;
+        const bool sync = round_is_sync(s, next);
+        const uint32_t posted = s.posted.load(std::memory_order_acquire);
+        const bool go = sync ? posted >= next : sh->activated.load(std::memory_order_acquire) >= next;
+        if (!go) return false;
+        s.cur = next;
+        s.cur_fresh = posted >= next;
+        s.joined = next;
+        sh->joined[s.rank].store(next, std::memory_order_release);
+        if (s.cur_fresh) ++s.n_fresh; else ++s.n_auto;
+        if (s.log.size() < 65536)
+            s.log.push_back({next, uint8_t(s.cur_fresh), uint8_t(sync),
+                             int16_t(sync ? -1 : sh->last_activator.load())});
+        if (!check(s.tp->snapshot(s, next, s.cur_fresh), "snapshot")) return true;
+        enter(ST_SNAPSHOT);
+        return true;
+    }
+    case ST_SNAPSHOT: {
+        int q = s.tp->query(s);
+        if (!check(q, "snapshot")) return true;
+        if (!q) return false;
+        sh->ready[s.rank].store(s.cur, std::memory_order_release);
+        enter(ST_WAIT_READY);
+        return true;
+    }
+    case ST_WAIT_READY:
+        if (!all_at_least(sh->ready, s.world, s.cur)) return timed_out("peers never published their snapshot");
+        if (!check(s.tp->reduce_scatter(s), "reduce-scatter")) return true;
+        enter(ST_RS);
+        return true;
+    case ST_RS: {
+        int q = s.tp->query(s);
+        if (!check(q, "reduce-scatter")) return true;
+        if (!q) return false;
+        sh->reduced[s.rank].store(s.cur, std::memory_order_release);
+        enter(ST_WAIT_REDUCED);
+        return true;
+    }
+    case ST_WAIT_REDUCED:
+        if (!all_at_least(sh->reduced, s.world, s.cur)) return timed_out("peers never finished reduce-scatter");
+        if (!check(s.tp->all_gather(s), "all-gather")) return true;
+        enter(ST_AG);
+        return true;
+    case ST_AG: {
+        int q = s.tp->query(s);
+        if (!check(q, "all-gather")) return true;
+        if (!q) return false;
+        sh->done[s.rank].store(s.cur, std::memory_order_release);
+        enter(ST_WAIT_DONE);
+        return true;
+    }
+    case ST_WAIT_DONE:
+        if (!all_at_least(sh->done, s.world, s.cur)) return timed_out("peers never finished all-gather");
+        if (!check(s.tp->finish(s), "copy-out")) return true;
+        enter(ST_FINISH);
+        return true;
+    case ST_FINISH: {
+        int q = s.tp->query(s);
+        if (!check(q, "copy-out")) return true;
+        if (!q) return false;
+        s.completed = s.cur;
+        s.stage = ST_IDLE;
+        s.cv.notify_all();
+        return true;
+    }
+    }
+    return false;
+}
+
+bool engine_progress_once() {
+    std::vector<Sched *> snap;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        snap = g_reg;
+    }
+    bool any = false;
+    for (Sched *s : snap)
+        while (step(*s)) any = true;   // run a schedule until it has to wait
+    return any;
+}
+
+}  // namespace esgd

@@ -1,0 +1,127 @@
+// engine.h — persistent partial-allreduce schedules and the progress thread.
+//
+// Observable contract restated from fflib2 (paths under
+// /root/reference/eager-SGD-modules/fflib2/src):
+//   * A schedule is created collectively and reused every round
+//     (colls/ffsolo_allreduce.c:20-95, colls/ffrand_allreduce.c:27-75).
+//   * Solo: post() of round t goes through the limiter (colls/ffsolo_limiter.c:4-35):
+//     rounds 1..async are asynchronous, round async+1 is synchronous, then repeat.
+//     An asynchronous round is activated by the FIRST rank that posts it; the
+//     activation floods to every rank (colls/ffactivation.c:11-106), and each rank joins
+//     with whatever its send buffer holds at that moment (the `move` of
+//     colls/ffallreduce.c:126-130).  A synchronous round is joined by each rank when it
+//     posts (no activation).
+//   * Majority: round t is activated by rank rand_r(&seed) % P, the same draw on every
+//     rank (colls/ffrand_allreduce.c:83-103); the others only count passive rounds.
+//   * Plain allreduce: every round synchronous (colls/ffallreduce.c).
+//   * wait() returns once the next round not yet waited for has completed locally
+//     (ffop.c:143-177 waits for version wait_version+1 of allreduce_ends).
+// The fflib2 op-DAG/version machinery that implements this is not rebuilt: a round
+// counter per schedule in shared memory plays the role of the op versions.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <mutex>
+#include <vector>
+
+#include "shm.h"
+
+namespace esgd {
+
+enum Kind { KIND_ALLREDUCE = 0, KIND_SOLO = 1, KIND_MAJORITY = 2 };
+
+enum Stage {
+    ST_IDLE = 0,      // between rounds
+    ST_SNAPSHOT,      // move sb -> rb queued
+    ST_WAIT_READY,    // waiting for every rank's snapshot
+    ST_RS,            // reduce-scatter queued
+    ST_WAIT_REDUCED,  // waiting for every rank's reduced shard
+    ST_AG,            // all-gather queued
+    ST_WAIT_DONE,     // waiting for every rank's gather (buffers free again)
+    ST_FINISH,        // copy-out queued
+};
+
+struct Sched;
+
+// Data movement of one round.  Every step only *queues* work; query() reports whether
+// the last queued step has finished (1), is pending (0) or failed (< 0).
+struct Transport {
+    virtual ~Transport() {}
+    virtual const char *name() const = 0;
+    virtual int setup(Sched &s) = 0;          // collective: called between barriers
+    virtual int note_producer(Sched &s, uint32_t round, void *stream) = 0;
+    virtual int snapshot(Sched &s, uint32_t round, bool fresh) = 0;
+    virtual int reduce_scatter(Sched &s) = 0;
+    virtual int all_gather(Sched &s) = 0;
+    virtual int finish(Sched &s) = 0;
+    virtual int query(Sched &s) = 0;
+    virtual void teardown(Sched &s) = 0;
+};
+
+struct RoundLog {      // per-round record kept for tests / stats (bounded ring)
+    uint32_t round;
+    uint8_t fresh;     // this rank had posted the round before it joined
+    uint8_t sync;
+    int16_t activator; // -1 for synchronous rounds
+};
+
+struct Sched {
+    int id = -1, kind = KIND_ALLREDUCE, async = 0, dtype = 3;
+    unsigned seed = 0;
+    uint64_t count = 0;
+    size_t esize = 4;
+    int rank = 0, world = 1;
+    SchedShm *sh = nullptr;
+    uint32_t gen = 0;
+    Transport *tp = nullptr;
+    void *tstate = nullptr;
+
+    // caller buffers (captured at creation, like colls/ffallreduce.c:113-115)
+    void *sb = nullptr, *rb = nullptr;
+    bool host_mode = false, in_place = false;
+
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<uint32_t> posted{0};
+    uint32_t joined = 0, completed = 0, waited = 0;
+    Stage stage = ST_IDLE;
+    uint32_t cur = 0;
+    bool cur_fresh = false;
+    double stage_t0 = 0;
+    int error = 0;
+    char errmsg[256] = {0};
+    uint32_t passive = 0;      // majority: passive rounds since the last activation
+    uint64_t n_fresh = 0, n_auto = 0, n_activated = 0;
+    std::vector<RoundLog> log;
+    std::atomic<bool> live{true};
+};
+
+// Round kind / activator rules (pure functions of the schedule parameters).
+bool round_is_sync(const Sched &s, uint32_t round);
+
+// Engine lifetime: attach to the node segment and start the progress thread.
+int engine_init(const char *job, int rank, int world, bool start_progress);
+int engine_finalize();
+bool engine_ready();
+int engine_rank();
+int engine_world();
+Segment *engine_segment();
+int engine_barrier();
+double engine_timeout();
+
+// Schedules (collective create/delete, same order on every rank).
+int sched_create(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
+                 int async, unsigned seed, Transport *tp, Sched **out);
+int sched_post(Sched *s, void *producer_stream, int *role);
+int sched_wait(Sched *s);
+int sched_test(Sched *s, int *flag);
+int sched_delete(Sched *s);
+Sched *sched_lookup(uint64_t handle);
+
+// One polling pass over all schedules (the progress thread calls it in a loop; tests
+// without a thread may call it directly).  Returns true if anything advanced.
+bool engine_progress_once();
+
+}  // namespace esgd

@@ -1,0 +1,113 @@
+// ff_api.cpp — fflib2's collective entry points (include/esgd_ff.h) on the esgd engine.
+//
+// The caller the reference ships (the deep500 op embedded in
+// test-models/tf-models-r1.11/official/utils/opt_esgd_solo_imagenet_imbalance.py:277-346)
+// calls ffinit once, builds 161 persistent schedules over host buckets, then per step
+// post / wait.  Those calls map 1:1 onto esgd schedules with host buffers.
+#include <hip/hip_runtime.h>
+#include <unistd.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "engine.h"
+#include "esgd_ff.h"
+#include "esgd_internal.h"
+
+using namespace esgd;
+
+static int env_int(std::initializer_list<const char *> names, int dflt) {
+    for (const char *n : names)
+        if (const char *v = getenv(n))
+            if (*v) return atoi(v);
+    return dflt;
+}
+
+static bool g_ff_owns_comm = false;
+
+static int make_schedule(int kind, void *sndbuff, void *rcvbuff, int count, ffoperator_h op,
+                         ffdatatype_h dt, int options, int async, unsigned seed, ffschedule_h *sched) {
+    ESGD_ARG(sched, "fflib: null schedule output");
+    ESGD_ARG(count >= 0, "fflib: negative count");
+    ESGD_ARG(op == FFSUM, "fflib: only FFSUM is reduced by libesgd (operator %d)", op);
+    ESGD_ARG(!(options & FFCOLL_BUFFERS), "fflib: FFCOLL_BUFFERS (ffbuffer_h) is not supported");
+    ESGD_ARG(dt == FFINT32 || dt == FFINT64 || dt == FFDOUBLE || dt == FFFLOAT || dt == ESGD_FFBF16,
+             "fflib: unsupported datatype %d", dt);
+    if (!engine_ready()) {
+        if (int rc = ffinit(nullptr, nullptr)) return rc;
+    }
+    const int buf = (options & ESGD_FF_DEVICE_BUFFERS) ? ESGD_BUF_DEVICE : ESGD_BUF_HOST;
+    void *sb = sndbuff == FFINPLACE ? nullptr : sndbuff;
+    esgd_sched_h h = 0;
+    int rc = esgd_schedule_create(kind, buf, sb, rcvbuff, uint64_t(count), dt, async, seed, &h);
+    if (rc) return rc;
+    *sched = h;
+    return FFSUCCESS;
+}
+
+extern "C" {
+
+int ffinit(int *, char ***) {
+    if (engine_ready()) return FFSUCCESS;   // already joined (esgd_comm_init / earlier ffinit)
+    const int rank = env_int({"ESGD_RANK", "RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID"}, 0);
+    const int world = env_int({"ESGD_WORLD_SIZE", "WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE",
+                               "SLURM_NTASKS"}, 1);
+    const int local = env_int({"ESGD_LOCAL_RANK", "LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK",
+                               "SLURM_LOCALID"}, rank);
+    std::string job;
+    if (const char *j = getenv("ESGD_JOB_ID")) job = j;
+    else if (const char *t = getenv("TORCHELASTIC_RUN_ID")) job = std::string(t) + "-" + (getenv("MASTER_PORT") ? getenv("MASTER_PORT") : "0");
+    else if (const char *p = getenv("MASTER_PORT")) job = std::string("port-") + p;
+    else if (world == 1) job = "single-" + std::to_string(getpid());
+    else {
+        set_error("ffinit: %d ranks but no job id (set ESGD_JOB_ID or run under torch.distributed.run)", world);
+        return FFINVALID_ARG;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0) {
+        const int dev = env_int({"ESGD_DEVICE"}, local % ndev);
+        ESGD_HIP(hipSetDevice(dev));
+    }
+    int rc = engine_init(job.c_str(), rank, world, true);
+    if (!rc) g_ff_owns_comm = true;
+    return rc;
+}
+
+int fffinalize(void) {
+    g_ff_owns_comm = false;
+    return engine_finalize();
+}
+
+int ffrank(int *rank) { return esgd_comm_rank(rank); }
+int ffsize(int *size) { return esgd_comm_size(size); }
+
+int ffallreduce(void *sndbuff, void *rcvbuff, int count, int16_t, ffoperator_h op,
+                ffdatatype_h datatype, int options, ffschedule_h *sched) {
+    return make_schedule(KIND_ALLREDUCE, sndbuff, rcvbuff, count, op, datatype, options, 0, 0, sched);
+}
+
+int ffsolo_allreduce(void *sndbuff, void *rcvbuff, int count, int16_t, ffoperator_h op,
+                     ffdatatype_h datatype, int options, int async, ffschedule_h *sched) {
+    return make_schedule(KIND_SOLO, sndbuff, rcvbuff, count, op, datatype, options, async, 0, sched);
+}
+
+int ffrand_allreduce(void *sndbuff, void *rcvbuff, int count, int16_t, ffoperator_h op,
+                     ffdatatype_h datatype, int options, int seed, int async, ffschedule_h *sched) {
+    return make_schedule(KIND_MAJORITY, sndbuff, rcvbuff, count, op, datatype, options, async,
+                         unsigned(seed), sched);
+}
+
+// The reference posts the auto-activator here so activation receives are armed
+// (colls/ffsolo_allreduce.c:97-101); the progress thread is always armed.
+int ffschedule_start(ffschedule_h sched) {
+    return sched_lookup(sched) ? FFSUCCESS : FFINVALID_ARG;
+}
+
+int ffschedule_post(ffschedule_h sched) { return esgd_schedule_post(sched, nullptr, nullptr); }
+int ffschedule_post_stream(ffschedule_h sched, void *stream) { return esgd_schedule_post(sched, stream, nullptr); }
+int ffschedule_wait(ffschedule_h sched) { return esgd_schedule_wait(sched); }
+int ffschedule_test(ffschedule_h sched, int *flag) { return esgd_schedule_test(sched, flag); }
+int ffschedule_delete(ffschedule_h sched) { return esgd_schedule_delete(sched); }
+
+}  // extern "C"

@@ -23,6 +23,7 @@
 #include <cstdint>
 #include <cstring>
 #include <mutex>
+#include <algorithm>
 #include <type_traits>
 
 #include "esgd_internal.h"
@@ -224,6 +225,47 @@ __global__ __launch_bounds__(256) void k_tree_sum_scalar(InputSet in, void *out,
     }
 }
 
+// ---- all-gather of peer shards (data plane phase 2) ----
+// Copies up to kMaxSeg segments (one per peer shard) in one launch; blockIdx.y picks
+// the segment.  Sources are peer memory mapped over xGMI: loads carry system scope
+// (sc0 sc1) so no stale line of a previous round can be served from this device's L2;
+// stores are local and write-through (sc1).
+constexpr int kMaxSeg = 16;
+struct GatherSet {
+    const void *src[kMaxSeg];
+    void *dst[kMaxSeg];
+    uint32_t nvec[kMaxSeg];
+    uint32_t tail[kMaxSeg];   // bytes after the last full 16-B vector
+};
+
+template <int U>
+__global__ __launch_bounds__(256) void k_gather(GatherSet g) {
+    constexpr int B = 256;
+    const int seg = blockIdx.y;
+    const uint32_t nvec = g.nvec[seg];
+    const int bytes = int(nvec * 16u);
+    if (nvec) {
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(g.src[seg]), (short)0,
+                                                                     bytes, 0x00020000);
+        __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(g.dst[seg], (short)0, bytes, 0x00020000);
+        const uint32_t step = gridDim.x * (B * U);
+        for (uint32_t i = blockIdx.x * (B * U) + threadIdx.x; i < nvec; i += step) {
+            raw16 r[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                r[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (i + u * B) * 16, 0, 19);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                __builtin_amdgcn_raw_buffer_store_b128(r[u], ws, (i + u * B) * 16, 0, 16);
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < g.tail[seg]) {
+        const uint8_t *src = static_cast<const uint8_t *>(g.src[seg]) + size_t(nvec) * 16;
+        uint8_t *dst = static_cast<uint8_t *>(g.dst[seg]) + size_t(nvec) * 16;
+        dst[threadIdx.x] = __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // ---- synthetic inputs (same generator as oracle/ffref.c) ----
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -322,11 +364,19 @@ static int launch_scalar(const InputSet &in, void *out, uint64_t count, float sc
 
 template <class Tr, int K, bool SCALE>
 static int dispatch_u(const InputSet &in, void *out, uint64_t count, float scale, bool aligned,
-                      hipStream_t s) {
-    if (!aligned) return launch_scalar<Tr, K, SCALE>(in, out, count, scale, s);
+                      hipStream_t s, bool remote = false) {
     // bf16 folds 8 lanes per 16 B: two vectors per input keep it under 128 VGPRs
     constexpr int UD = sizeof(typename Tr::T) == 2 ? 2 : 4;
     const bool fits32 = count / Tr::E * 16 + uint64_t(UD) * 256 * 16 < (1ull << 31);
+    if (remote) {
+        // inputs live in peer HBM (IPC over xGMI): system-scope nt loads, local sc1 stores
+        if (!aligned || !fits32) {
+            set_error("remote reduce: shard must be 16-B aligned and < 2 GiB");
+            return ESGD_INVALID_ARG;
+        }
+        return launch_buf<Tr, K, UD, 19, 16, SCALE>(in, out, count, scale, s);
+    }
+    if (!aligned) return launch_scalar<Tr, K, SCALE>(in, out, count, scale, s);
     if (g_policy != 0 && fits32) {
         if constexpr (std::is_same<Tr, F32>::value && K == 8) {
             switch (g_policy) {
@@ -350,16 +400,16 @@ static int dispatch_u(const InputSet &in, void *out, uint64_t count, float scale
 
 template <class Tr, bool SCALE>
 static int dispatch_k(int k, const InputSet &in, void *out, uint64_t count, float scale,
-                      bool aligned, hipStream_t s) {
+                      bool aligned, hipStream_t s, bool remote = false) {
     switch (k) {
-    case 1: return dispatch_u<Tr, 1, SCALE>(in, out, count, scale, aligned, s);
-    case 2: return dispatch_u<Tr, 2, SCALE>(in, out, count, scale, aligned, s);
-    case 3: return dispatch_u<Tr, 3, SCALE>(in, out, count, scale, aligned, s);
-    case 4: return dispatch_u<Tr, 4, SCALE>(in, out, count, scale, aligned, s);
-    case 5: return dispatch_u<Tr, 5, SCALE>(in, out, count, scale, aligned, s);
-    case 6: return dispatch_u<Tr, 6, SCALE>(in, out, count, scale, aligned, s);
-    case 7: return dispatch_u<Tr, 7, SCALE>(in, out, count, scale, aligned, s);
-    case 8: return dispatch_u<Tr, 8, SCALE>(in, out, count, scale, aligned, s);
+    case 1: return dispatch_u<Tr, 1, SCALE>(in, out, count, scale, aligned, s, remote);
+    case 2: return dispatch_u<Tr, 2, SCALE>(in, out, count, scale, aligned, s, remote);
+    case 3: return dispatch_u<Tr, 3, SCALE>(in, out, count, scale, aligned, s, remote);
+    case 4: return dispatch_u<Tr, 4, SCALE>(in, out, count, scale, aligned, s, remote);
+    case 5: return dispatch_u<Tr, 5, SCALE>(in, out, count, scale, aligned, s, remote);
+    case 6: return dispatch_u<Tr, 6, SCALE>(in, out, count, scale, aligned, s, remote);
+    case 7: return dispatch_u<Tr, 7, SCALE>(in, out, count, scale, aligned, s, remote);
+    case 8: return dispatch_u<Tr, 8, SCALE>(in, out, count, scale, aligned, s, remote);
     default: break;
     }
     set_error("esgd_reduce: fan-in %d outside [1, %d]", k, ESGD_MAX_FANIN);
@@ -367,7 +417,7 @@ static int dispatch_k(int k, const InputSet &in, void *out, uint64_t count, floa
 }
 
 static int reduce_impl(int dtype, int k, const void *const *inputs, void *out, uint64_t count,
-                       float scale, bool scaled, void *stream) {
+                       float scale, bool scaled, void *stream, bool remote = false) {
     ESGD_ARG(k >= 1 && k <= ESGD_MAX_FANIN, "esgd_reduce: fan-in %d outside [1, %d]", k,
              ESGD_MAX_FANIN);
     ESGD_ARG(inputs && out, "esgd_reduce: null inputs/out");
@@ -384,24 +434,55 @@ static int reduce_impl(int dtype, int k, const void *const *inputs, void *out, u
     hipStream_t s = as_stream(stream);
     switch (dtype) {
     case ESGD_FLOAT:
-        return scaled ? dispatch_k<F32, true>(k, in, out, count, scale, aligned, s)
-                      : dispatch_k<F32, false>(k, in, out, count, scale, aligned, s);
+        return scaled ? dispatch_k<F32, true>(k, in, out, count, scale, aligned, s, remote)
+                      : dispatch_k<F32, false>(k, in, out, count, scale, aligned, s, remote);
     case ESGD_BF16:
-        return scaled ? dispatch_k<BF16, true>(k, in, out, count, scale, aligned, s)
-                      : dispatch_k<BF16, false>(k, in, out, count, scale, aligned, s);
+        return scaled ? dispatch_k<BF16, true>(k, in, out, count, scale, aligned, s, remote)
+                      : dispatch_k<BF16, false>(k, in, out, count, scale, aligned, s, remote);
     case ESGD_DOUBLE:
         ESGD_ARG(!scaled, "esgd_reduce_scaled: FLOAT/BF16 only");
-        return dispatch_k<F64, false>(k, in, out, count, scale, aligned, s);
+        return dispatch_k<F64, false>(k, in, out, count, scale, aligned, s, remote);
     case ESGD_INT32:
         ESGD_ARG(!scaled, "esgd_reduce_scaled: FLOAT/BF16 only");
-        return dispatch_k<I32, false>(k, in, out, count, scale, aligned, s);
+        return dispatch_k<I32, false>(k, in, out, count, scale, aligned, s, remote);
     case ESGD_INT64:
         ESGD_ARG(!scaled, "esgd_reduce_scaled: FLOAT/BF16 only");
-        return dispatch_k<I64, false>(k, in, out, count, scale, aligned, s);
+        return dispatch_k<I64, false>(k, in, out, count, scale, aligned, s, remote);
     default: break;
     }
     set_error("esgd_reduce: unsupported dtype %d", dtype);
     return ESGD_INVALID_ARG;
+}
+
+// ---- internal entry points of the data plane (dataplane_ipc.cpp) ----
+int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64_t count,
+                  float scale, hipStream_t s) {
+    return reduce_impl(dtype, k, inputs, out, count, scale, scale != 1.0f, s, true);
+}
+
+int gather_remote(int n, const void *const *src, void *const *dst, const uint64_t *bytes,
+                  hipStream_t s) {
+    ESGD_ARG(n >= 0 && n <= kMaxSeg, "gather: %d segments", n);
+    if (n == 0) return ESGD_SUCCESS;
+    GatherSet g;
+    std::memset(&g, 0, sizeof(g));
+    uint64_t maxvec = 0;
+    for (int i = 0; i < n; ++i) {
+        ESGD_ARG(bytes[i] / 16 < (1ull << 27), "gather: segment of %llu bytes too large",
+                 (unsigned long long)bytes[i]);
+        ESGD_ARG(((reinterpret_cast<uintptr_t>(src[i]) | reinterpret_cast<uintptr_t>(dst[i])) & 15) == 0,
+                 "gather: segment %d not 16-B aligned", i);
+        g.src[i] = src[i]; g.dst[i] = dst[i];
+        g.nvec[i] = uint32_t(bytes[i] / 16);
+        g.tail[i] = uint32_t(bytes[i] % 16);
+        maxvec = std::max<uint64_t>(maxvec, g.nvec[i]);
+    }
+    unsigned gx = grid_for(256 * 4, maxvec ? maxvec : 1, 8);
+    unsigned per_seg = std::max(1u, (unsigned(cu_count()) * 4 + n - 1) / unsigned(n));
+    if (gx > per_seg) gx = per_seg;
+    hipLaunchKernelGGL(k_gather<4>, dim3(gx, n), dim3(256), 0, s, g);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
 }
 
 }  // namespace esgd

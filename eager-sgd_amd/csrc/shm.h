@@ -1,0 +1,73 @@
+// shm.h — node-local shared segment that replaces fflib2's MPI control traffic.
+//
+// fflib2 moves activation tokens and completion through MPI point-to-point messages
+// polled by a progress pthread (src/colls/ffactivation.c:11-106,
+// src/components/mpi/ffop_mpi_progresser.c:34-104).  All ranks of this build live on
+// one MI355X node, so the same information is a handful of atomics in a /dev/shm
+// segment: activation counters (the "versions" of ffop.c), per-rank ready/done epochs
+// of every round, IPC handles of the registered buckets, and a sense-reversing barrier
+// (the reference's MPI_Barrier, opt_esgd_solo_imagenet_imbalance.py:295).
+#pragma once
+
+#include <atomic>
+#include <cstddef>
+#include <cstdint>
+
+namespace esgd {
+
+constexpr int kMaxRanks = 16;     // ranks per node
+constexpr int kMaxSched = 2048;   // persistent schedules per job (the ResNet-50 wrapper uses 161)
+constexpr uint64_t kShmMagic = 0x314d4853444753ull;  // "ESGDSHM1"
+
+// One registered device buffer: the allocation's IPC handle plus the offset of the
+// buffer inside it (torch's caching allocator hands out sub-allocations).
+struct alignas(64) IpcSlot {
+    uint8_t handle[64];
+    uint64_t offset;
+    uint64_t bytes;
+    std::atomic<uint32_t> gen;    // == schedule generation when valid
+};
+
+struct alignas(64) SchedShm {
+    std::atomic<uint32_t> gen;            // bumped by each collective (re)creation
+    std::atomic<uint32_t> kind;
+    std::atomic<uint32_t> activated;      // highest round activated (solo async / majority)
+    std::atomic<int32_t> last_activator;  // rank that activated `activated`
+    std::atomic<uint32_t> ready[kMaxRanks];   // round whose input snapshot rank r has published
+    std::atomic<uint32_t> reduced[kMaxRanks]; // round whose phase 1 (reduce-scatter) is done
+    std::atomic<uint32_t> done[kMaxRanks];    // round whose phase 2 (all-gather) is done
+    std::atomic<uint32_t> joined[kMaxRanks];  // diagnostics: last round rank r joined
+    std::atomic<uint32_t> activations[kMaxRanks];  // diagnostics: rounds activated by r
+    IpcSlot slot[kMaxRanks];
+};
+
+struct Segment {
+    uint64_t magic;
+    uint32_t world;
+    uint32_t bytes;
+    std::atomic<uint32_t> attached;
+    std::atomic<uint32_t> bar_count;
+    std::atomic<uint32_t> bar_gen;
+    std::atomic<uint32_t> aborted;
+    std::atomic<uint32_t> nccl_ready;
+    uint8_t nccl_id[128];
+    std::atomic<int32_t> pid[kMaxRanks];
+    std::atomic<int32_t> device[kMaxRanks];
+    SchedShm sched[kMaxSched];
+};
+
+// Attach (rank 0 creates) the segment /dev/shm/esgd-<job>.  Returns nullptr and sets
+// the error message on failure / timeout.
+Segment *shm_attach(const char *job, int rank, int world, double timeout_s);
+void shm_detach(Segment *seg, const char *job, int rank);
+void shm_unlink_name(const char *job);
+
+// Sense-reversing barrier over the segment; ESGD_ERROR on timeout or abort.
+int shm_barrier(Segment *seg, int world, double timeout_s);
+
+// Seconds since an arbitrary epoch (steady clock).
+double now_s();
+// Spin-then-yield-then-sleep backoff for polling loops.
+void backoff(unsigned &polls);
+
+}  // namespace esgd

@@ -1,0 +1,180 @@
+"""Node communicator and persistent partial-allreduce schedules (esgd.h C ABI).
+
+Mirrors fflib2's collective surface (src/ff.h:161-165, src/ffschedule.c) one level
+below the optimizer wrapper:
+
+    comm.init()                                   # ffinit (rendezvous + progress thread)
+    s = comm.Schedule(comm.SOLO, sb, rb, count, async_=32)   # ffsolo_allreduce
+    s.post(); s.wait()                            # ffschedule_post / ffschedule_wait
+
+Buffers are device pointers (ints, DeviceBuffer or torch tensors), host numpy arrays
+(host staging mode, the reference's contract) or None with buf=NONE (control plane only).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import uuid
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+ALLREDUCE, SOLO, MAJORITY = 0, 1, 2
+BUF_DEVICE, BUF_HOST, BUF_NONE = 0, 1, 2
+
+
+class SchedStats(C.Structure):
+    _fields_ = [("posted", C.c_uint32), ("joined", C.c_uint32), ("completed", C.c_uint32),
+                ("waited", C.c_uint32), ("activated", C.c_uint32), ("last_activator", C.c_int32),
+                ("fresh_rounds", C.c_uint64), ("auto_rounds", C.c_uint64),
+                ("activations", C.c_uint64)]
+
+
+def _bind(h):
+    vp, i, u32, u64 = C.c_void_p, C.c_int, C.c_uint32, C.c_uint64
+    sigs = {
+        "esgd_comm_init": (i, [C.c_char_p, i, i]),
+        "esgd_comm_finalize": (i, []),
+        "esgd_comm_rank": (i, [C.POINTER(i)]),
+        "esgd_comm_size": (i, [C.POINTER(i)]),
+        "esgd_barrier": (i, []),
+        "esgd_schedule_create": (i, [i, i, vp, vp, u64, i, i, C.c_uint, C.POINTER(u64)]),
+        "esgd_schedule_post": (i, [u64, vp, C.POINTER(i)]),
+        "esgd_schedule_wait": (i, [u64]),
+        "esgd_schedule_test": (i, [u64, C.POINTER(i)]),
+        "esgd_schedule_delete": (i, [u64]),
+        "esgd_schedule_stats": (i, [u64, C.POINTER(SchedStats)]),
+        "esgd_schedule_log": (i, [u64, C.POINTER(u32), C.POINTER(C.c_uint8), C.POINTER(C.c_uint8),
+                                  C.POINTER(C.c_int16), u32, C.POINTER(u32)]),
+        "esgd_schedule_stream": (i, [u64, C.POINTER(vp)]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(h, name)
+        fn.restype, fn.argtypes = res, args
+
+
+_lib.register_signatures(_bind)
+
+_state = {"init": False}
+
+
+def _default_job_id(rank: int, world: int) -> str:
+    """A job id every rank agrees on: broadcast over torch.distributed when it is up,
+    else derived from the launcher's environment."""
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            obj = [uuid.uuid4().hex if dist.get_rank() == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            return obj[0]
+    except Exception:
+        pass
+    if os.environ.get("ESGD_JOB_ID"):
+        return os.environ["ESGD_JOB_ID"]
+    if os.environ.get("TORCHELASTIC_RUN_ID"):
+        return f"{os.environ['TORCHELASTIC_RUN_ID']}-{os.environ.get('MASTER_PORT', '0')}"
+    if world == 1:
+        return f"single-{os.getpid()}"
+    raise RuntimeError("esgd.comm.init: no job id (pass job_id= or set ESGD_JOB_ID)")
+
+
+def init(job_id: str | None = None, rank: int | None = None, world: int | None = None):
+    """Join the node communicator (collective).  Uses the current HIP device."""
+    if rank is None:
+        rank = int(os.environ.get("RANK", "0"))
+    if world is None:
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+    if job_id is None:
+        job_id = _default_job_id(rank, world)
+    check(lib().esgd_comm_init(job_id.encode(), rank, world), "esgd_comm_init")
+    _state["init"] = True
+    return rank, world
+
+
+def finalize():
+    if _state["init"]:
+        check(lib().esgd_comm_finalize(), "esgd_comm_finalize")
+        _state["init"] = False
+
+
+def rank() -> int:
+    v = C.c_int()
+    check(lib().esgd_comm_rank(C.byref(v)))
+    return v.value
+
+
+def world() -> int:
+    v = C.c_int()
+    check(lib().esgd_comm_size(C.byref(v)))
+    return v.value
+
+
+def barrier():
+    check(lib().esgd_barrier(), "esgd_barrier")
+
+
+def _buf_arg(x, buf):
+    if x is None:
+        return None
+    if buf == BUF_HOST:
+        assert isinstance(x, np.ndarray) and x.flags.c_contiguous
+        return x.ctypes.data
+    from .device import as_ptr
+    return as_ptr(x)
+
+
+class Schedule:
+    """A persistent schedule (ffallreduce / ffsolo_allreduce / ffrand_allreduce)."""
+
+    def __init__(self, kind: int, sb, rb, count: int, dtype: int = _lib.FLOAT,
+                 async_: int = 0, seed: int = 0, buf: int | None = None):
+        if buf is None:
+            buf = BUF_HOST if isinstance(rb, np.ndarray) else BUF_NONE if rb is None else BUF_DEVICE
+        self.kind, self.buf, self.count, self.dtype = kind, buf, int(count), dtype
+        self._keep = (sb, rb)   # host arrays must outlive the schedule
+        h = C.c_uint64()
+        check(lib().esgd_schedule_create(kind, buf, _buf_arg(sb, buf), _buf_arg(rb, buf),
+                                         self.count, dtype, int(async_), int(seed) & 0xFFFFFFFF,
+                                         C.byref(h)), "esgd_schedule_create")
+        self.handle = h.value
+
+    def post(self, stream=None) -> int:
+        role = C.c_int()
+        s = None if stream is None else (stream.handle if hasattr(stream, "handle") else int(stream))
+        check(lib().esgd_schedule_post(self.handle, s, C.byref(role)), "esgd_schedule_post")
+        return role.value
+
+    def wait(self):
+        check(lib().esgd_schedule_wait(self.handle), "esgd_schedule_wait")
+
+    def test(self) -> bool:
+        f = C.c_int()
+        check(lib().esgd_schedule_test(self.handle, C.byref(f)), "esgd_schedule_test")
+        return bool(f.value)
+
+    def stats(self) -> dict:
+        st = SchedStats()
+        check(lib().esgd_schedule_stats(self.handle, C.byref(st)), "esgd_schedule_stats")
+        return {k: getattr(st, k) for k, _ in SchedStats._fields_}
+
+    def log(self):
+        n = C.c_uint32()
+        check(lib().esgd_schedule_log(self.handle, None, None, None, None, 0, C.byref(n)))
+        cap = n.value
+        r = (C.c_uint32 * cap)(); f = (C.c_uint8 * cap)(); s = (C.c_uint8 * cap)()
+        a = (C.c_int16 * cap)()
+        check(lib().esgd_schedule_log(self.handle, r, f, s, a, cap, C.byref(n)))
+        return [{"round": r[i], "fresh": bool(f[i]), "sync": bool(s[i]), "activator": a[i]}
+                for i in range(min(cap, n.value))]
+
+    def stream(self) -> int:
+        v = C.c_void_p()
+        check(lib().esgd_schedule_stream(self.handle, C.byref(v)))
+        return v.value or 0
+
+    def delete(self):
+        if self.handle:
+            check(lib().esgd_schedule_delete(self.handle), "esgd_schedule_delete")
+            self.handle = 0

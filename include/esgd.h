@@ -109,6 +109,64 @@ int esgd_fill_uniform_bf16(uint64_t seed, int rank, uint16_t *out, uint64_t n, v
 int esgd_set_tuning(const char *key, int value);
 int esgd_get_tuning(const char *key, int *value);
 
+/* ---- node communicator (replaces MPI_Init / MPI_Barrier of the reference:
+ *      src/components/mpi/ffmpi.c:11-31, opt_esgd_solo_imagenet_imbalance.py:295) ----
+ * Collective over the `world` processes of one node that pass the same job id; each
+ * process drives the HIP device current at the call.  A node-local shared segment
+ * carries activations, round epochs and IPC handles; a progress thread drives rounds. */
+int esgd_comm_init(const char *job_id, int rank, int world);
+int esgd_comm_finalize(void);
+int esgd_comm_rank(int *rank);
+int esgd_comm_size(int *size);
+int esgd_barrier(void);
+
+/* ---- persistent partial-allreduce schedules ----
+ * kind: ESGD_SCHED_ALLREDUCE (every round synchronous, src/colls/ffallreduce.c),
+ *       ESGD_SCHED_SOLO (first poster activates; every (async+1)-th round synchronous,
+ *                        src/colls/ffsolo_allreduce.c + ffsolo_limiter.c),
+ *       ESGD_SCHED_MAJORITY (activator rand_r(&seed) % P, src/colls/ffrand_allreduce.c).
+ * buf:  ESGD_BUF_DEVICE (sb/rb are device pointers, rb 16-B aligned),
+ *       ESGD_BUF_HOST (sb/rb are host pointers, staged through HBM: the reference's
+ *                      host-memory contract), ESGD_BUF_NONE (control plane only: no data
+ *                      moves; for multi-process tests of the round protocol).
+ * sb == NULL or sb == rb: in place (FFINPLACE).  Buffers are captured at creation and
+ * must stay valid until esgd_schedule_delete (src/colls/ffallreduce.c:113-115).
+ * Creation and deletion are collective, in the same order on every rank. */
+#define ESGD_SCHED_ALLREDUCE 0
+#define ESGD_SCHED_SOLO 1
+#define ESGD_SCHED_MAJORITY 2
+#define ESGD_BUF_DEVICE 0
+#define ESGD_BUF_HOST 1
+#define ESGD_BUF_NONE 2
+
+typedef uint64_t esgd_sched_h;
+
+typedef struct {
+    uint32_t posted, joined, completed, waited; /* round counters of this rank */
+    uint32_t activated;                         /* highest round activated (shared) */
+    int32_t last_activator;                     /* rank that activated it, -1 if none */
+    uint64_t fresh_rounds;                      /* joined after posting them */
+    uint64_t auto_rounds;                       /* joined on a peer's activation */
+    uint64_t activations;                       /* rounds this rank activated */
+} esgd_sched_stats_t;
+
+int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t count,
+                         int dtype, int async, unsigned seed, esgd_sched_h *out);
+/* post: start round `posted+1`.  producer_stream (may be NULL): stream that writes sb;
+ * the snapshot of a round this rank posted waits for the work queued on it so far.
+ * role (may be NULL): 1 activated the round, 0 passive, 2 synchronous round. */
+int esgd_schedule_post(esgd_sched_h h, void *producer_stream, int *role);
+int esgd_schedule_wait(esgd_sched_h h);
+int esgd_schedule_test(esgd_sched_h h, int *flag);
+int esgd_schedule_delete(esgd_sched_h h);
+int esgd_schedule_stats(esgd_sched_h h, esgd_sched_stats_t *out);
+/* per-round log of this rank: round number, fresh (posted before joining), sync,
+ * activator (-1 for synchronous rounds).  Writes up to cap entries, *n = total. */
+int esgd_schedule_log(esgd_sched_h h, uint32_t *rounds, uint8_t *fresh, uint8_t *sync,
+                      int16_t *activator, uint32_t cap, uint32_t *n);
+/* the data-plane stream of a device schedule (consumers of rb may wait on it) */
+int esgd_schedule_stream(esgd_sched_h h, void **stream);
+
 #ifdef __cplusplus
 }
 #endif

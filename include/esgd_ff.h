@@ -1,0 +1,89 @@
+/*
+ * esgd_ff.h — the subset of fflib2's public API that eager-SGD's callers bind,
+ * re-implemented by libesgd.so on MI355X (HIP tree reduction + IPC/xGMI data plane).
+ *
+ * Each declaration names the reference entry point it replaces
+ * (/root/reference/eager-SGD-modules/fflib2/src/ff.h).  Constants keep the reference's
+ * values so that existing callers compile unchanged against include/ff.h.
+ * Differences (documented in INTEGRATION.md):
+ *   - no MPI: ranks are the processes of one node (env RANK / WORLD_SIZE / LOCAL_RANK
+ *     as set by torch.distributed.run, or OMPI_ / PMI_ / SLURM_ equivalents), joined
+ *     through a node-local shared segment named by ESGD_JOB_ID (or
+ *     TORCHELASTIC_RUN_ID + MASTER_PORT);
+ *   - operator FFSUM only (the reference's generic comp also has FFIDENTITY, used
+ *     internally for the move) ; datatypes FFINT32/FFINT64/FFDOUBLE/FFFLOAT + ESGD_FFBF16;
+ *   - FFCOLL_BUFFERS (ffbuffer_h arguments) is not supported;
+ *   - extension option ESGD_FF_DEVICE_BUFFERS: sndbuff/rcvbuff are device pointers.
+ */
+#ifndef ESGD_FF_H
+#define ESGD_FF_H
+
+#include <stdint.h>
+
+#include "esgd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* return codes (src/ff.h:4-10) */
+#define FFCOMPLETED 1
+#define FFSUCCESS 0
+#define FFERROR -1
+#define FFINVALID_ARG -2
+#define FFTOO_MANY_DEPS -3
+#define FFENOMEM -4
+#define FFVERSION -5
+
+/* datatypes (src/ff.h:21-31) */
+#define FFINT32 0
+#define FFINT64 1
+#define FFDOUBLE 2
+#define FFFLOAT 3
+#define ESGD_FFBF16 16   /* extension */
+
+/* operators (src/ff.h:34-40); only FFSUM reduces here */
+#define FFSUM 0
+#define FFPROD 1
+#define FFMAX 2
+#define FFMIN 3
+#define FFIDENTITY 4
+
+/* options used by collective callers (src/ff.h:43-58) */
+#define FFCOLL_BUFFERS (1 << 7)
+#define ESGD_FF_DEVICE_BUFFERS (1 << 20)   /* extension: sndbuff/rcvbuff on the device */
+
+#define FFINPLACE ((void *)0x1)            /* src/ff.h:62 */
+
+typedef int ffdatatype_h;
+typedef int ffoperator_h;
+typedef uint64_t ffschedule_h;
+
+int ffinit(int *argc, char ***argv);   /* src/ff.c:23-86 (MPI_Init + progress thread) */
+int fffinalize(void);                  /* src/ff.c:88- */
+int ffrank(int *rank);                 /* src/ff.h:102 */
+int ffsize(int *size);                 /* src/ff.h:103 */
+
+/* src/colls/ffallreduce.c:74 — every round synchronous */
+int ffallreduce(void *sndbuff, void *rcvbuff, int count, int16_t tag, ffoperator_h ffoperator,
+                ffdatatype_h datatype, int options, ffschedule_h *sched);
+/* src/colls/ffsolo_allreduce.c:20 — solo allreduce with a limiter of `async` */
+int ffsolo_allreduce(void *sndbuff, void *rcvbuff, int count, int16_t tag, ffoperator_h ffoperator,
+                     ffdatatype_h datatype, int options, int async, ffschedule_h *sched);
+/* src/colls/ffrand_allreduce.c:27 — majority allreduce, activator rand_r(&seed) % P */
+int ffrand_allreduce(void *sndbuff, void *rcvbuff, int count, int16_t tag, ffoperator_h ffoperator,
+                     ffdatatype_h datatype, int options, int seed, int async, ffschedule_h *sched);
+
+int ffschedule_start(ffschedule_h sched);              /* src/ffschedule.c (arms receives) */
+int ffschedule_post(ffschedule_h sched);               /* src/ffschedule.c:84-88 */
+int ffschedule_wait(ffschedule_h sched);
+int ffschedule_test(ffschedule_h sched, int *flag);
+int ffschedule_delete(ffschedule_h sched);
+
+/* extension: post with the stream that produced sndbuff (device buffers) */
+int ffschedule_post_stream(ffschedule_h sched, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ESGD_FF_H */

@@ -1,0 +1,196 @@
+"""Multi-process harness: one process per rank, torch.distributed (gloo) for rendezvous
+and result collection, the esgd engine for everything under test.
+
+Worker functions live here (importable by spawned children).  `run(fn, world, **kw)`
+starts `world` ranks on 127.0.0.1 and returns rank 0's result.
+"""
+from __future__ import annotations
+
+import multiprocessing as mp
+import os
+import socket
+import sys
+import time
+import traceback
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "eager-sgd_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _entry(fn_name, rank, world, port, kw, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK="0")
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        out = globals()[fn_name](rank, world, **kw)
+        outs = [None] * world
+        dist.all_gather_object(outs, out)
+        if rank == 0:
+            q.put(("ok", outs))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        q.put(("err", f"rank {rank}: " + traceback.format_exc()))
+
+
+def run(fn_name: str, world: int, timeout: float = 240.0, **kw):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_entry, args=(fn_name, r, world, port, kw, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        status, payload = q.get(timeout=timeout)
+    finally:
+        deadline = time.time() + 30
+        for p in procs:
+            p.join(max(0.1, deadline - time.time()))
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    if status != "ok":
+        raise AssertionError(payload)
+    return payload
+
+
+# --------------------------------------------------------------------------- workers
+
+def _comm():
+    from esgd import comm
+    comm.init()
+    return comm
+
+
+def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0.0,
+              first_poster_rotates=False, barrier_each=False, use_test=False):
+    """Control plane only (ESGD_BUF_NONE): drive `rounds` post/wait cycles and return
+    this rank's per-round log, post roles and stats."""
+    comm = _comm()
+    s = comm.Schedule(kind, None, None, 0, async_=async_, seed=seed, buf=comm.BUF_NONE)
+    roles = []
+    for t in range(1, rounds + 1):
+        if barrier_each:
+            comm.barrier()
+        if first_poster_rotates:
+            if rank == t % world:
+                roles.append(s.post())
+                comm.barrier()
+            else:
+                comm.barrier()
+                time.sleep(0.02)
+                roles.append(s.post())
+        else:
+            if rank == straggler:
+                time.sleep(delay)
+            roles.append(s.post())
+        if use_test:
+            while not s.test():
+                time.sleep(0.0005)
+        else:
+            s.wait()
+    comm.barrier()
+    out = {"log": s.log(), "roles": roles, "stats": s.stats()}
+    s.delete()
+    comm.finalize()
+    return out
+
+
+def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0, buf="device",
+                  in_place=False):
+    """Data plane on the GPU: every rank reduces its splitmix bucket; returns the
+    result bytes' digest per round plus a bit-exactness verdict against the oracle."""
+    import numpy as np
+
+    from esgd import _lib
+    from esgd import device as dev
+    from oracle import ffref
+    comm = _comm()
+    seed = 0x5EEDE56D
+    dt = {"fp32": _lib.FLOAT, "int32": _lib.INT32, "fp64": _lib.DOUBLE, "int64": _lib.INT64,
+          "bf16": _lib.BF16}[dtype_name]
+    verdicts = []
+    if buf == "device":
+        rb = dev.DeviceBuffer(count, dt)
+        sb = None if in_place else dev.DeviceBuffer(count, dt)
+        s = comm.Schedule(kind, sb, rb, count, dtype=dt, buf=comm.BUF_DEVICE)
+    else:
+        npdt = dev.NP_DTYPE[dt]
+        sb_h = None if in_place else np.zeros(count, npdt)
+        rb_h = np.zeros(count, npdt)
+        s = comm.Schedule(kind, sb_h, rb_h, count, dtype=dt, buf=comm.BUF_HOST)
+    for t in range(rounds):
+        xs = []
+        for r in range(world):
+            if dt == _lib.FLOAT:
+                x = ffref.fill_uniform(seed + t, r, count)
+            elif dt == _lib.BF16:
+                x = ffref.f32_to_bf16(ffref.fill_uniform(seed + t, r, count))
+            elif dt in (_lib.INT32, _lib.INT64):
+                x = (np.arange(count) + t + 7 * r).astype(dev.NP_DTYPE[dt])   # allreduce.c:49
+            else:
+                x = ffref.fill_uniform(seed + t, r, count).astype(np.float64) * 1e-3
+            xs.append(x)
+        mine = xs[rank]
+        if buf == "device":
+            (rb if in_place else sb).upload(mine)
+        else:
+            (rb_h if in_place else sb_h)[:] = mine
+        comm.barrier()
+        s.post()
+        s.wait()
+        got = rb.download() if buf == "device" else rb_h.copy()
+        if dt == _lib.BF16:
+            want = ffref.tree_sum_bf16(xs)
+        elif dt in (_lib.INT32, _lib.INT64):
+            want = ffref.allreduce_rd(xs)[rank]
+            assert np.array_equal(want, xs[0].astype(np.int64) * 0 + sum(x.astype(np.int64) for x in xs).astype(want.dtype))
+        else:
+            want = ffref.allreduce_rd(xs)[rank]
+        verdicts.append(bool(np.array_equal(got.view(np.uint8), want.view(np.uint8))))
+        comm.barrier()
+    s.delete()
+    comm.finalize()
+    return verdicts
+
+
+def gpu_partial_semantics(rank, world, kind, rounds, async_=3, seed=6545343, straggler=1,
+                          delay=0.05, count=4096):
+    """eager-SGD semantics with data: rank r writes tag_r(t) = t * 64**r into its send
+    buffer before posting round t (exact in fp32 for P <= 4, t < 64).  The reduced
+    value of a round decodes which posted round each rank's buffer held when that rank
+    joined — checked against the round logs."""
+    import numpy as np
+
+    from esgd import _lib
+    from esgd import device as dev
+    comm = _comm()
+    sb = dev.DeviceBuffer(count, _lib.FLOAT)
+    rb = dev.DeviceBuffer(count, _lib.FLOAT)
+    sb.zero(); dev.synchronize()
+    s = comm.Schedule(kind, sb, rb, count, dtype=_lib.FLOAT, async_=async_, seed=seed,
+                      buf=comm.BUF_DEVICE)
+    results = []
+    for t in range(1, rounds + 1):
+        if rank == straggler:
+            time.sleep(delay)
+        sb.upload(np.full(count, float(t * 64 ** rank), np.float32))
+        s.post()
+        s.wait()
+        v = rb.download()
+        assert np.all(v == v[0]), "non-uniform result"
+        results.append(float(v[0]))
+    comm.barrier()
+    out = {"log": s.log(), "results": results, "stats": s.stats()}
+    s.delete()
+    comm.finalize()
+    return out

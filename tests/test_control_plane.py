@@ -1,0 +1,84 @@
+"""Round protocol of the partial allreduces, multi-process on CPU (gloo rendezvous,
+control plane only: ESGD_BUF_NONE moves no data).
+
+Reference behaviour checked (paths under /root/reference/eager-SGD-modules/fflib2):
+  * limiter cadence — src/colls/ffsolo_limiter.c:4-35 / evaluation/limiter.c: rounds
+    1..async asynchronous, round async+1 synchronous, repeating;
+  * solo activation — the first rank to post an asynchronous round activates it for
+    everyone (src/colls/ffactivation.c:11-106); late ranks join with what they hold;
+  * majority activator — rand_r(&seed) % P with the same seed everywhere
+    (src/colls/ffrand_allreduce.c:83-103), pinned against libc via the oracle;
+  * plain allreduce — every round synchronous, every rank fresh.
+"""
+import pytest
+
+from mp_workers import run
+from oracle import ffref
+
+ALLREDUCE, SOLO, MAJORITY = 0, 1, 2
+pytestmark = pytest.mark.slow
+
+
+def test_allreduce_every_round_sync_and_fresh():
+    outs = run("cp_rounds", 2, kind=ALLREDUCE, rounds=6)
+    for o in outs:
+        assert [e["round"] for e in o["log"]] == list(range(1, 7))
+        assert all(e["sync"] and e["fresh"] for e in o["log"])
+        assert o["roles"] == [2] * 6
+
+
+@pytest.mark.parametrize("async_", [1, 2, 3])
+def test_limiter_cadence(async_):
+    outs = run("cp_rounds", 2, kind=SOLO, rounds=3 * (async_ + 1), async_=async_, barrier_each=True)
+    for o in outs:
+        got = [e["sync"] for e in o["log"]]
+        want = [t % (async_ + 1) == 0 for t in range(1, 3 * (async_ + 1) + 1)]
+        assert got == want
+
+
+def test_solo_first_poster_activates():
+    world, rounds = 3, 8
+    outs = run("cp_rounds", world, kind=SOLO, rounds=rounds, async_=100, first_poster_rotates=True)
+    for r, o in enumerate(outs):
+        for e in o["log"]:
+            t = e["round"]
+            assert e["activator"] == t % world
+            assert e["fresh"] == (r == t % world)   # the others joined on the activation
+        roles = o["roles"]
+        assert [roles[t - 1] for t in range(1, rounds + 1)] == [1 if r == t % world else 0
+                                                                  for t in range(1, rounds + 1)]
+
+
+def test_solo_straggler_bounded_by_limiter():
+    # rank 1 is 0.25 s late every round; rank 0 runs the asynchronous rounds alone and
+    # blocks only at the synchronous one (every 4th) — bounded staleness.
+    async_, rounds = 3, 8
+    outs = run("cp_rounds", 2, kind=SOLO, rounds=rounds, async_=async_, straggler=1, delay=0.25)
+    fast, slow = outs[0]["log"], outs[1]["log"]
+    for e in fast:
+        assert e["fresh"]
+        if not e["sync"]:
+            assert e["activator"] == 0
+    for e in slow:
+        assert e["fresh"] == e["sync"], e   # the straggler is fresh only on sync rounds
+    assert outs[1]["stats"]["auto_rounds"] == rounds - rounds // (async_ + 1)
+
+
+@pytest.mark.parametrize("world,seed", [(2, 6545343), (4, 6545343), (3, 34495645)])
+def test_majority_activator_is_rand_r(world, seed):
+    rounds = 16
+    outs = run("cp_rounds", world, kind=MAJORITY, rounds=rounds, seed=seed, barrier_each=True)
+    want = ffref.activators(seed, world, rounds)
+    for r, o in enumerate(outs):
+        assert [e["activator"] for e in o["log"]] == want
+        assert [o["roles"][t] for t in range(rounds)] == [1 if a == r else 0 for a in want]
+        for e in o["log"]:
+            if e["activator"] == r:
+                assert e["fresh"]
+
+
+def test_test_polling_equivalent_to_wait():
+    outs = run("cp_rounds", 2, kind=SOLO, rounds=6, async_=2, use_test=True)
+    for o in outs:
+        assert [e["round"] for e in o["log"]] == list(range(1, 7))
+        assert o["stats"]["completed"] == 6 and o["stats"]["waited"] == 6

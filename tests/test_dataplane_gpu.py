@@ -1,0 +1,70 @@
+"""Multi-rank data plane on the GPU: P processes (all on device 0 of the test box, one
+per GPU on a full node) run persistent schedules over IPC-mapped peer buffers.
+
+Bar: every rank's receive buffer is bit-identical to the oracle's restatement of
+fflib2's recursive doubling (src/colls/ffallreduce.c:138-171) for the same inputs;
+int32 also matches the known answer of evaluation/allreduce.c:59-63.  Partial
+(solo / majority) rounds are checked through round tags: rank r contributes
+t * 64**r in round t, so the reduced value names the round each rank's buffer held.
+"""
+import pytest
+
+from mp_workers import run
+from oracle import ffref
+
+pytestmark = pytest.mark.gpu
+ALLREDUCE, SOLO, MAJORITY = 0, 1, 2
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("dtype", ["fp32", "int32", "bf16", "fp64", "int64"])
+def test_allreduce_bitwise_device(world, dtype):
+    verdicts = run("gpu_allreduce", world, dtype_name=dtype, count=100003, rounds=2)
+    assert all(all(v) for v in verdicts), verdicts
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_allreduce_ragged_and_tiny(world):
+    for count in (1, 17, 1023, 4099):
+        verdicts = run("gpu_allreduce", world, count=count, rounds=1)
+        assert all(all(v) for v in verdicts), (count, verdicts)
+
+
+@pytest.mark.parametrize("in_place", [False, True])
+def test_allreduce_host_buffers(in_place):
+    # the reference's contract: host buckets in, host result out (staged through HBM)
+    verdicts = run("gpu_allreduce", 2, count=262144, rounds=2, buf="host", in_place=in_place)
+    assert all(all(v) for v in verdicts), verdicts
+
+
+def test_allreduce_in_place_device():
+    verdicts = run("gpu_allreduce", 4, count=65536 * 4 + 5, rounds=2, in_place=True)
+    assert all(all(v) for v in verdicts), verdicts
+
+
+@pytest.mark.parametrize("kind", [SOLO, MAJORITY])
+def test_solo_majority_round_tags(kind):
+    world, rounds, async_ = 2, 9, 3
+    outs = run("gpu_partial_semantics", world, kind=kind, rounds=rounds, async_=async_,
+               straggler=1, delay=0.05)
+    digits = lambda v, r: int(v // 64 ** r) % 64  # noqa: E731
+    fast = outs[0]
+    acts = ffref.activators(6545343, world, rounds)
+    prev = [0] * world
+    for t, v in enumerate(fast["results"], start=1):
+        d = [digits(v, r) for r in range(world)]
+        assert v == sum(d[r] * 64 ** r for r in range(world)), v
+        for r in range(world):
+            assert d[r] <= t and d[r] >= prev[r], (t, d)   # buffers only move forward
+        prev = d
+        if kind == SOLO:
+            assert d[0] == t                                 # the fast rank is always fresh
+            if t % (async_ + 1) == 0:
+                assert d == [t] * world                      # synchronous round: everyone
+        else:
+            assert d[acts[t - 1]] == t                       # the activator is fresh
+    # a rank that joined a round it had posted contributed that round's tag
+    for r, o in enumerate(outs):
+        for e in o["log"]:
+            if e["fresh"] and r == 0:
+                assert digits(fast["results"][e["round"] - 1], r) == e["round"]
