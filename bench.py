@@ -193,6 +193,99 @@ def gate_256(dev, dt, es, k, s, iters=20):
             "frac": round(algo / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+def run_allreduce(args, rank, world):
+    """N > 1: one persistent schedule per rank over a device-resident bucket (config C3:
+    256 MiB fp32, solo-allreduce), in place, all ranks posting every step.  Timed
+    region: barrier + device sync, K x (post, wait), device sync, barrier; the MAX over
+    ranks is the step time."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from esgd import _lib, comm
+    from esgd import device as dev
+    from oracle import ffref
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm.init(rank=rank, world=world)            # job id broadcast over gloo
+    dt = _lib.FLOAT if args.dtype == "fp32" else _lib.BF16
+    es = _lib.dtype_size(dt)
+    count = int(args.bucket_mib * MiB) // es
+    kind = {"solo": comm.SOLO, "majority": comm.MAJORITY, "allreduce": comm.ALLREDUCE}[args.schedule]
+    rb = dev.DeviceBuffer(count, dt)
+    dev.fill_uniform(rb, SEED, rank)
+    dev.synchronize()
+    sched = comm.Schedule(kind, None, rb, count, dtype=dt, async_=32, seed=6545343,
+                          buf=comm.BUF_DEVICE)
+
+    def step():
+        sched.post()
+        sched.wait()
+
+    for _ in range(args.warmup):
+        step()
+    dist.barrier(); comm.barrier(); dev.device_synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    dev.device_synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    wall = float(el.item())
+    t_step = wall / args.steps
+    stats = sched.stats()
+
+    # parity outside the timed region: fresh inputs, one round, slices vs the oracle
+    parity = "skipped"
+    if dt == _lib.FLOAT:
+        dev.fill_uniform(rb, SEED + 1, rank)
+        dev.synchronize()
+        comm.barrier()
+        step()
+        got = rb.download()
+        m = min(count, 1 << 18)
+        ok = True
+        for start in (0, count - m):
+            xs = [ffref.fill_uniform(SEED + 1, r, m, start=start) for r in range(world)]
+            want = ffref.tree_sum(xs)
+            ok &= bool(np.array_equal(got[start:start + m].view(np.uint32), want.view(np.uint32)))
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        parity = "bitwise (head+tail slices, every rank)" if flag.item() else "MISMATCH"
+    sched.delete()
+    comm.finalize()
+
+    S = count * es
+    algbw = S / t_step / 1e9
+    busbw = algbw * 2 * (world - 1) / world
+    t_min = 2 * S / (world * XGMI_LINK_GBS * 1e9)
+    link_in = 2 * (world - 1) / world * S / t_step / 1e9     # bytes each GPU pulls per second
+    line = {
+        "metric": "GB/s grad-bucket reduced (device-resident), solo/majority-allreduce 1-8 GPU",
+        "value": round(world * S * args.steps / wall / 1e9, 2),
+        "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(t_step * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if args.dtype == "fp32" else "bf16 (f32 accumulate)",
+        "data": "synthetic (splitmix64 uniform [-1,1), generated on device)",
+        "config": {"workload": f"C3: {args.schedule}-allreduce of one {args.bucket_mib:g} MiB "
+                               f"{args.dtype} bucket per GPU, in place",
+                   "bucket_bytes": S, "parallelism": f"dp{world} (one rank per GPU)",
+                   "transport": "ipc pull (reduce-scatter tree kernel + all-gather) over xGMI"},
+        "algbw_GBs": round(algbw, 2), "busbw_GBs": round(busbw, 2),
+        "xgmi_frac": round(t_min / t_step, 4),
+        "roofline": {"bound": "xgmi", "achieved": round(link_in, 2),
+                     "peak": XGMI_LINK_GBS * (world - 1), "unit": "GB/s",
+                     "frac": round(link_in / (XGMI_LINK_GBS * (world - 1)), 4), "traffic": None},
+        "rounds": {"fresh": stats["fresh_rounds"], "auto": stats["auto_rounds"],
+                   "activations_rank0": stats["activations"]},
+        "parity": parity,
+    }
+    dist.destroy_process_group()
+    return line
+
+
 def main():
     args = parse()
     if args.bucket_mib is None:
@@ -205,11 +298,14 @@ def main():
 
     import esgd
     from esgd import device as dev
-    esgd.check(esgd.lib().esgd_set_device(local_rank), "esgd_set_device")
+    ndev = esgd.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no HIP device visible")
+    # one rank per GPU; extra ranks wrap around (1-GPU rehearsal of the N>1 path)
+    esgd.check(esgd.lib().esgd_set_device(local_rank % ndev), "esgd_set_device")
 
     if world > 1:
-        from esgd import dataplane
-        res = dataplane.bench_allreduce(args, rank, world, local_rank)
+        res = run_allreduce(args, rank, world)
         if rank == 0:
             print(json.dumps(res))
         return

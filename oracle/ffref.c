@@ -210,12 +210,17 @@ uint64_t ffref_splitmix64(uint64_t x) {
 }
 
 void ffref_fill_uniform_f32(uint64_t seed, int rank, float *out, uint64_t n) {
+    ffref_fill_uniform_f32_at(seed, rank, 0, out, n);
+}
+
+void ffref_fill_uniform_f32_at(uint64_t seed, int rank, uint64_t start, float *out, uint64_t n) {
     uint64_t base = seed ^ ((uint64_t)(uint32_t)rank << 40);
-    for (uint64_t i = 0; i < n; ++i) {
+    for (uint64_t j = 0; j < n; ++j) {
+        uint64_t i = start + j;
         /* top 24 bits -> [0,1) exactly representable, then to [-1, 1) */
         uint64_t h = ffref_splitmix64(base ^ i);
         float u = (float)(h >> 40) * (1.0f / 16777216.0f);
-        out[i] = 2.0f * u - 1.0f;
+        out[j] = 2.0f * u - 1.0f;
     }
 }
 

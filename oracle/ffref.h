@@ -72,6 +72,7 @@ int ffref_rand_r(unsigned int *seed);
  * mapped to [-1, 1).  Same generator runs on the GPU. */
 uint64_t ffref_splitmix64(uint64_t x);
 void ffref_fill_uniform_f32(uint64_t seed, int rank, float *out, uint64_t n);
+void ffref_fill_uniform_f32_at(uint64_t seed, int rank, uint64_t start, float *out, uint64_t n);
 
 /* One reduction step's wall time on this host for the CPU baseline leg:
  * allreduce of P simulated ranks with `threads` (1 => sequential ranks,

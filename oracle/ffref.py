@@ -46,6 +46,7 @@ def lib():
         h.ffref_rand_r.argtypes = [C.POINTER(C.c_uint)]
         h.ffref_rand_r.restype = C.c_int
         h.ffref_fill_uniform_f32.argtypes = [C.c_uint64, i, vp, C.c_uint64]
+        h.ffref_fill_uniform_f32_at.argtypes = [C.c_uint64, i, C.c_uint64, vp, C.c_uint64]
         h.ffref_splitmix64.argtypes = [C.c_uint64]
         h.ffref_splitmix64.restype = C.c_uint64
         h.ffref_f32_to_bf16.argtypes = [C.c_float]
@@ -131,9 +132,9 @@ def activators(seed: int, P: int, n: int):
     return [v % P for v in rand_r_sequence(seed, n)]
 
 
-def fill_uniform(seed: int, rank: int, n: int) -> np.ndarray:
+def fill_uniform(seed: int, rank: int, n: int, start: int = 0) -> np.ndarray:
     out = np.empty(n, dtype=np.float32)
-    lib().ffref_fill_uniform_f32(seed, rank, out.ctypes.data, n)
+    lib().ffref_fill_uniform_f32_at(seed, rank, start, out.ctypes.data, n)
     return out
 
 
