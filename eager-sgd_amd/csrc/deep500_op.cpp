@@ -1,0 +1,174 @@
+// deep500_op.cpp — the eager-SGD gradient operator behind deep500's custom-op C ABI.
+//
+// Restates allreducef (opt_esgd_solo_imagenet_imbalance.py:255-346 and its majority
+// twin) on the esgd engine.  Per op instance and training step:
+//   copy the gradient into the op's persistent send bucket      (:301)
+//   post the partial allreduce, wait for its round              (:304-307)
+//   copy the reduced bucket out, zero the send bucket           (:309-314)
+// Differences, all deliberate:
+//   * each op instance owns its bucket (the reference indexes 161 hard-coded ResNet-50
+//     buckets by call order, :85-248 / :301 — identical under its fixed call order,
+//     and not tied to one model);
+//   * buckets are pinned host memory (host path) or HBM (forward_cuda), and the
+//     schedule is created at the instance's first forward (collective: the training
+//     graph calls ops in the same order on every rank, which the reference relies on
+//     for its 161 creations at :288-293);
+//   * report() returns the bytes reduced (the reference always returns 0, :273-275).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "engine.h"
+#include "esgd_deep500.h"
+#include "esgd_ff.h"
+#include "esgd_internal.h"
+
+using namespace esgd;
+
+namespace {
+
+struct OpConfig {
+    int mode = -1;
+    int async = 32;       // LIMITER, opt_esgd_solo_imagenet_imbalance.py:82
+    unsigned seed = 6545343;   // opt_esgd_majority_imagenet_imbalance.py:252
+};
+
+std::mutex g_op_mu;
+OpConfig g_cfg;
+
+OpConfig current_config() {
+    std::lock_guard<std::mutex> lk(g_op_mu);
+    OpConfig c = g_cfg;
+    if (c.mode < 0) {
+        const char *m = getenv("ESGD_OP_MODE");
+        c.mode = ESGD_OP_SOLO;
+        if (m && !strcmp(m, "majority")) c.mode = ESGD_OP_MAJORITY;
+        if (m && !strcmp(m, "allreduce")) c.mode = ESGD_OP_ALLREDUCE;
+        if (const char *a = getenv("ESGD_OP_ASYNC")) c.async = atoi(a);
+        if (const char *s = getenv("ESGD_OP_SEED")) c.seed = unsigned(strtoul(s, nullptr, 10));
+    }
+    return c;
+}
+
+[[noreturn]] void die(const char *where) {
+    fprintf(stderr, "[esgd] %s failed: %s\n", where, esgd_last_error());
+    std::abort();
+}
+
+struct AllreduceOp {
+    uint64_t len = 0;
+    OpConfig cfg;
+    esgd_sched_h sched = 0;
+    bool device = false;
+    float *sb = nullptr, *rb = nullptr;   // persistent buckets (host pinned or HBM)
+    int64_t bytes = 0;
+
+    void ensure(bool dev) {
+        if (sched) {
+            if (dev != device) {
+                esgd::set_error("op used with both host and device buffers");
+                die("allreducef_forward");
+            }
+            return;
+        }
+        device = dev;
+        const size_t nbytes = size_t(len) * sizeof(float);
+        if (dev) {
+            if (hipMalloc(reinterpret_cast<void **>(&sb), nbytes ? nbytes : 256) != hipSuccess ||
+                hipMalloc(reinterpret_cast<void **>(&rb), nbytes ? nbytes : 256) != hipSuccess ||
+                hipMemset(sb, 0, nbytes) != hipSuccess || hipMemset(rb, 0, nbytes) != hipSuccess) {
+                esgd::set_error("device bucket allocation of %zu bytes", nbytes);
+                die("allreducef_forward_cuda");
+            }
+        } else {
+            if (hipHostMalloc(reinterpret_cast<void **>(&sb), nbytes ? nbytes : 256, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc(reinterpret_cast<void **>(&rb), nbytes ? nbytes : 256, hipHostMallocDefault) != hipSuccess) {
+                esgd::set_error("pinned bucket allocation of %zu bytes", nbytes);
+                die("allreducef_forward");
+            }
+            std::memset(sb, 0, nbytes);   // calloc in the reference (:290-291)
+            std::memset(rb, 0, nbytes);
+        }
+        const int kind = cfg.mode == ESGD_OP_MAJORITY ? ESGD_SCHED_MAJORITY
+                         : cfg.mode == ESGD_OP_ALLREDUCE ? ESGD_SCHED_ALLREDUCE : ESGD_SCHED_SOLO;
+        if (esgd_schedule_create(kind, dev ? ESGD_BUF_DEVICE : ESGD_BUF_HOST, sb, rb, len,
+                                 ESGD_FLOAT, cfg.async, cfg.seed, &sched))
+            die("schedule creation");
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int esgd_op_configure(int mode, int async, unsigned seed) {
+    ESGD_ARG(mode == ESGD_OP_SOLO || mode == ESGD_OP_MAJORITY || mode == ESGD_OP_ALLREDUCE,
+             "esgd_op_configure: bad mode %d", mode);
+    std::lock_guard<std::mutex> lk(g_op_mu);
+    g_cfg.mode = mode;
+    g_cfg.async = async;
+    g_cfg.seed = seed;
+    return ESGD_SUCCESS;
+}
+
+void *create_new_op(esgd_d5_tensor_t *in, int num_inputs, esgd_d5_tensor_t *, int) {
+    if (!in || num_inputs < 1) {
+        esgd::set_error("create_new_op: no input descriptor");
+        return nullptr;
+    }
+    if (!engine_ready() && ffinit(nullptr, nullptr) != FFSUCCESS) die("ffinit");   // :335-339
+    auto *op = new AllreduceOp();
+    uint64_t total = 1;
+    for (int i = 0; i < in[0].dims; ++i) total *= in[0].sizes[i];       // :341-343
+    op->len = total;
+    op->cfg = current_config();
+    return op;
+}
+
+void allreducef_forward(void *handle, const float *input, const float *, float *output) {
+    auto *op = static_cast<AllreduceOp *>(handle);
+    op->ensure(false);
+    const size_t nbytes = size_t(op->len) * sizeof(float);
+    std::memcpy(op->sb, input, nbytes);
+    if (esgd_schedule_post(op->sched, nullptr, nullptr) || esgd_schedule_wait(op->sched))
+        die("allreducef_forward");
+    std::memcpy(output, op->rb, nbytes);
+    std::memset(op->sb, 0, nbytes);
+    op->bytes += int64_t(nbytes);
+}
+
+void allreducef_forward_cuda(void *handle, const float *input, const float *, float *output,
+                             void *stream) {
+    auto *op = static_cast<AllreduceOp *>(handle);
+    op->ensure(true);
+    const size_t nbytes = size_t(op->len) * sizeof(float);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (hipMemcpyAsync(op->sb, input, nbytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
+        die("allreducef_forward_cuda (copy in)");
+    // the snapshot of this round waits for the copy just queued on the caller's stream
+    if (esgd_schedule_post(op->sched, s, nullptr) || esgd_schedule_wait(op->sched))
+        die("allreducef_forward_cuda");
+    if (hipMemcpyAsync(output, op->rb, nbytes, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+        hipMemsetAsync(op->sb, 0, nbytes, s) != hipSuccess)
+        die("allreducef_forward_cuda (copy out)");
+    op->bytes += int64_t(nbytes);
+}
+
+bool is_cuda_supported(void *) { return true; }
+
+int64_t report(void *handle, void *) {
+    return handle ? static_cast<AllreduceOp *>(handle)->bytes : 0;
+}
+
+// The schedule and its buckets stay alive: peers may still activate rounds that read
+// them (the reference never deletes its schedules either).  They go at fffinalize.
+void delete_op(void *handle) {
+    auto *op = static_cast<AllreduceOp *>(handle);
+    if (op && !op->sched) delete op;
+}
+
+}  // extern "C"

@@ -1,0 +1,99 @@
+"""deep500-style custom-operator bridge for the prebuilt eager-SGD gradient op.
+
+The reference compiles the op from a C++ string at run time
+(deep500/lv0/operators/op_compiler.py:57-114 -> CMake -> .so) and loads it with ctypes
+(lv0/operators/operator_interface.py:48-91).  Here the op is part of libesgd.so; this
+module keeps the same handle protocol: descriptors -> create_new_op -> forward ->
+report -> delete_op (include/esgd_deep500.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import lib
+
+TT_FLOAT = 10          # deep500.h:16-34 tensortype_t
+MODES = {"allreduce": 0, "solo": 1, "majority": 2}
+
+
+class tensor_t(C.Structure):
+    """deep500::tensor_t (deep500.h:43-49; utils/tensor_desc.py:6-11)."""
+    _fields_ = [("type", C.c_int), ("order", C.c_int), ("dims", C.c_uint8),
+                ("sizes", C.POINTER(C.c_uint32))]
+
+
+class TensorDesc:
+    def __init__(self, shape: Sequence[int], ttype: int = TT_FLOAT):
+        self._sizes = (C.c_uint32 * max(1, len(shape)))(*[int(s) for s in shape])
+        self.t = tensor_t(ttype, 0, len(shape), self._sizes)
+        self.shape = tuple(int(s) for s in shape)
+
+
+def _bind(h):
+    vp = C.c_void_p
+    h.esgd_op_configure.restype, h.esgd_op_configure.argtypes = C.c_int, [C.c_int, C.c_int, C.c_uint]
+    h.create_new_op.restype = vp
+    h.create_new_op.argtypes = [C.POINTER(tensor_t), C.c_int, C.POINTER(tensor_t), C.c_int]
+    h.allreducef_forward.restype, h.allreducef_forward.argtypes = None, [vp, vp, vp, vp]
+    h.allreducef_forward_cuda.restype = None
+    h.allreducef_forward_cuda.argtypes = [vp, vp, vp, vp, vp]
+    h.is_cuda_supported.restype, h.is_cuda_supported.argtypes = C.c_bool, [vp]
+    h.report.restype, h.report.argtypes = C.c_int64, [vp, vp]
+    h.delete_op.restype, h.delete_op.argtypes = None, [vp]
+
+
+_lib.register_signatures(_bind)
+
+
+def configure(mode: str = "solo", async_: int = 32, seed: int = 6545343):
+    """Mode of the ops created afterwards (solo LIMITER 32 / majority seed 6545343 as
+    in opt_esgd_{solo,majority}_imagenet_imbalance.py)."""
+    _lib.check(lib().esgd_op_configure(MODES[mode], int(async_), int(seed) & 0xFFFFFFFF),
+               "esgd_op_configure")
+
+
+class AllreduceOp:
+    """One allreducef instance (one gradient tensor)."""
+
+    def __init__(self, shape: Sequence[int]):
+        self.inputs = [TensorDesc(shape), TensorDesc(shape)]   # (gradient, unused last)
+        self.outputs = [TensorDesc(shape)]
+        ins = (tensor_t * 2)(self.inputs[0].t, self.inputs[1].t)
+        outs = (tensor_t * 1)(self.outputs[0].t)
+        self.handle = lib().create_new_op(ins, 2, outs, 1)
+        if not self.handle:
+            raise _lib.EsgdError(_lib.ERROR, "create_new_op: " + _lib.last_error())
+        self.numel = int(np.prod(shape)) if len(shape) else 1
+
+    def forward(self, grad: np.ndarray, last: np.ndarray | None = None) -> np.ndarray:
+        """Host path (the reference's CPU-registered kernel)."""
+        g = np.ascontiguousarray(grad, dtype=np.float32)
+        assert g.size == self.numel
+        out = np.empty_like(g)
+        lib().allreducef_forward(self.handle, g.ctypes.data, None, out.ctypes.data)
+        return out
+
+    def forward_cuda(self, grad, out, stream: int | None = None):
+        """Device path: grad / out are device pointers or torch tensors."""
+        from .device import as_ptr
+        lib().allreducef_forward_cuda(self.handle, as_ptr(grad), None, as_ptr(out), stream)
+        return out
+
+    def supports_cuda(self) -> bool:
+        return bool(lib().is_cuda_supported(self.handle))
+
+    def report(self) -> int:
+        return int(lib().report(self.handle, None))
+
+    def close(self):
+        if self.handle:
+            lib().delete_op(self.handle)
+            self.handle = None
+
+
+def custom_op(shape: Sequence[int]) -> AllreduceOp:
+    return AllreduceOp(shape)

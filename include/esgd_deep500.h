@@ -1,0 +1,57 @@
+/*
+ * esgd_deep500.h — the deep500 custom-operator C ABI of the eager-SGD gradient op,
+ * prebuilt in libesgd.so (the reference compiles it at run time from a C++ string,
+ * test-models/tf-models-r1.11/official/utils/opt_esgd_solo_imagenet_imbalance.py:46-347,
+ * against eager-SGD-modules/deep500/deep500/lv0/operators/include/deep500/deep500.h).
+ *
+ * Entry points and the reference symbol each replaces:
+ *   create_new_op      D500_EXPORTED create_new_op (opt_esgd_solo...py:331-346)
+ *   allreducef_forward _op_forward -> allreducef::forward (deep500.h:95-104; :277-318)
+ *                      host buffers, the contract of the CPU-registered TF kernel
+ *                      (deep500/frameworks/tensorflow/custom_operators/tf.py:80)
+ *   allreducef_forward_cuda  device buffers + stream (deep500.h "forward_cuda")
+ *   is_cuda_supported / report / delete_op   tf.tmpl.cpp:20-32
+ * The template-based _op_forward of deep500.h cannot cross a C ABI; a framework bridge
+ * binds allreducef_forward instead.
+ */
+#ifndef ESGD_DEEP500_H
+#define ESGD_DEEP500_H
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* deep500::tensor_t (deep500.h:43-49; ctypes layout utils/tensor_desc.py:6-11) */
+typedef struct {
+    int type;        /* deep500::tensortype_t, TT_FLOAT = 10 */
+    int order;       /* deep500::tensororder_t */
+    uint8_t dims;
+    uint32_t *sizes;
+} esgd_d5_tensor_t;
+
+#define ESGD_OP_SOLO 1       /* opt_esgd_solo_imagenet_imbalance.py (LIMITER 32) */
+#define ESGD_OP_MAJORITY 2   /* opt_esgd_majority_imagenet_imbalance.py (seed 6545343) */
+#define ESGD_OP_ALLREDUCE 0  /* opt_sgd_mpi.py's synchronous baseline */
+
+/* Mode of the ops created afterwards (defaults: env ESGD_OP_MODE=solo|majority|allreduce,
+ * ESGD_OP_ASYNC=32, ESGD_OP_SEED=6545343, ESGD_OP_DEVICE=0|1). */
+int esgd_op_configure(int mode, int async, unsigned seed);
+
+void *create_new_op(esgd_d5_tensor_t *input_descriptors, int num_inputs,
+                    esgd_d5_tensor_t *output_descriptors, int num_outputs);
+/* input: this rank's gradient (already divided by the comm size, :40), last: the unused
+ * false-dependency input, output: the partially reduced gradient. */
+void allreducef_forward(void *handle, const float *input, const float *last, float *output);
+void allreducef_forward_cuda(void *handle, const float *input, const float *last, float *output,
+                             void *stream);
+bool is_cuda_supported(void *handle);
+int64_t report(void *handle, void *data);   /* bytes of gradient reduced so far */
+void delete_op(void *handle);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ESGD_DEEP500_H */

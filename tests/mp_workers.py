@@ -199,3 +199,63 @@ def gpu_partial_semantics(rank, world, kind, rounds, async_=3, seed=6545343, str
     s.delete()
     comm.finalize()
     return out
+
+
+def op_host(rank, world, mode="allreduce", steps=3, count=5000):
+    """deep500 op, host path (the reference's CPU-registered TF kernel contract)."""
+    import numpy as np
+
+    from esgd import deep500
+    from oracle import ffref
+    comm = _comm()
+    deep500.configure(mode, 32, 6545343)
+    op = deep500.AllreduceOp((count // 100, 100) if count % 100 == 0 else (count,))
+    ok = []
+    for t in range(steps):
+        xs = [ffref.fill_uniform(0xABC + t, r, count) for r in range(world)]
+        comm.barrier()          # evaluation/solo_allreduce_correctness.c:84 pattern
+        out = op.forward(xs[rank])
+        ok.append(bool(np.array_equal(out.view(np.uint32), ffref.tree_sum(xs).view(np.uint32))))
+    rep = op.report()
+    comm.barrier()
+    comm.finalize()
+    return {"ok": ok, "report": rep, "cuda": op.supports_cuda()}
+
+
+def optimizer_step(rank, world, mode="allreduce", steps=2):
+    """EagerSGDOptimizer on PyTorch-ROCm: every rank's p.grad after apply_gradients must
+    equal the oracle tree of (grad_r / P) over ranks, bit for bit."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from esgd.optim import EagerSGDOptimizer
+    from oracle import ffref
+    comm = _comm()
+    torch.manual_seed(1234)
+    dev = torch.device("cuda", 0)
+    model = torch.nn.Sequential(torch.nn.Linear(64, 48), torch.nn.ReLU(), torch.nn.Linear(48, 10)).to(dev)
+    opt = EagerSGDOptimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9), world, mode=mode)
+    ok = []
+    for t in range(steps):
+        g = torch.Generator().manual_seed(100 * t + rank)
+        x = torch.randn(32, 64, generator=g).to(dev)
+        y = torch.randint(0, 10, (32,), generator=g).to(dev)
+        opt.zero_grad()
+        loss = torch.nn.functional.cross_entropy(model(x), y)
+        gvs = opt.compute_gradients(loss)
+        local = [(gr.detach().float() / world).cpu().numpy().ravel() for gr, _ in gvs]
+        allg = [None] * world
+        dist.all_gather_object(allg, local)
+        comm.barrier()
+        opt.apply_gradients(gvs)
+        torch.cuda.synchronize()
+        for i, (_, p) in enumerate(gvs):
+            want = ffref.tree_sum([allg[r][i] for r in range(world)])
+            got = p.grad.detach().float().cpu().numpy().ravel()
+            ok.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
+    params = torch.cat([p.detach().float().cpu().ravel() for p in model.parameters()]).numpy()
+    comm.barrier()
+    nbytes = opt.bytes_reduced()
+    comm.finalize()
+    return {"ok": ok, "params_digest": params.tobytes().hex()[:64] + str(params.sum()), "bytes": nbytes}
