@@ -148,6 +148,7 @@ def run_local(args, esgd, dev):
     gate = None
     if not args.no_gate:
         gate = gate_256(dev, dt, es, k, s)
+    e2e = host_e2e(dev, k, count, s) if (dt == _lib.FLOAT and not args.no_gate) else None
     bucket_bytes = count * es
     algo_bytes = (k + 1) * bucket_bytes        # k reads + 1 write per launch
     achieved = algo_bytes / (per_launch_ms * 1e-3) / 1e9
@@ -162,7 +163,53 @@ def run_local(args, esgd, dev):
         "k": k,
         "parity": parity,
         "gate": gate,
+        "host_e2e": e2e,
     }
+
+
+def host_e2e(dev, k, count, s, iters=5):
+    """The reference's contract: buckets start and end in (pinned) host memory.  Per
+    step: k host buckets -> HBM (H2D), tree reduction, result -> host (D2H), one stream.
+    Reported beside the device-resident number, never as `value`."""
+    import ctypes as C
+
+    import numpy as np
+
+    from esgd import _lib
+    from esgd._lib import check, lib
+    nbytes = count * 4
+    hosts = []
+    for _ in range(k + 1):
+        p = C.c_void_p()
+        check(lib().esgd_host_alloc(C.byref(p), nbytes))
+        hosts.append(p.value)
+    for j in range(k):
+        np.frombuffer((C.c_char * nbytes).from_address(hosts[j]), dtype=np.float32)[:] = j
+    bufs = [dev.DeviceBuffer(count) for _ in range(k)]
+    out = dev.DeviceBuffer(count)
+
+    def one():
+        for j in range(k):
+            check(lib().esgd_memcpy_async(bufs[j].ptr, hosts[j], nbytes, 0, s.handle))
+        dev.reduce(_lib.FLOAT, [b.ptr for b in bufs], out, count, stream=s)
+        check(lib().esgd_memcpy_async(hosts[k], out.ptr, nbytes, 1, s.handle))
+        s.synchronize()
+
+    one()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        one()
+    t = (time.perf_counter() - t0) / iters
+    res = np.frombuffer((C.c_char * nbytes).from_address(hosts[k]), dtype=np.float32)
+    ok = bool(np.all(res == float(sum(range(k)))))
+    for p in hosts:
+        lib().esgd_host_free(p)
+    for b in bufs:
+        b.close()
+    out.close()
+    return {"workload": f"{k} pinned host buckets of {nbytes / MiB:g} MiB -> H2D -> tree -> D2H",
+            "ms": round(t * 1e3, 3), "GBs_bucket_bytes": round(k * nbytes / t / 1e9, 2),
+            "pcie_bytes_per_step": (k + 1) * nbytes, "correct": ok}
 
 
 def gate_256(dev, dt, es, k, s, iters=20):
@@ -334,6 +381,8 @@ def main():
     }
     if res.get("gate"):
         line["gate_256MiB"] = res["gate"]
+    if res.get("host_e2e"):
+        line["host_e2e"] = res["host_e2e"]
     traffic = None
     if not args.no_pmc:
         try:
