@@ -1,14 +1,26 @@
 // comm_api.cpp — C ABI of the node communicator and the persistent schedules (esgd.h).
+#include <cstdlib>
 #include <cstring>
+#include <string>
 
 #include "engine.h"
 #include "esgd_internal.h"
 
 namespace esgd {
 Transport *ipc_transport();
-Transport *null_transport();
+Transport *rccl_transport();
+Transport *null_transport(bool ordered);
 hipStream_t sched_stream(Sched &s);
+void rccl_shutdown();
 }  // namespace esgd
+
+static std::string g_transport;   // "" -> env ESGD_TRANSPORT -> "ipc"
+
+static const char *transport_name() {
+    if (!g_transport.empty()) return g_transport.c_str();
+    const char *e = getenv("ESGD_TRANSPORT");
+    return (e && *e) ? e : "ipc";
+}
 
 using namespace esgd;
 
@@ -25,7 +37,22 @@ int esgd_comm_init(const char *job_id, int rank, int world) {
     return engine_init(job_id, rank, world, true);
 }
 
-int esgd_comm_finalize(void) { return engine_finalize(); }
+int esgd_comm_finalize(void) {
+    int rc = engine_finalize();
+    rccl_shutdown();
+    return rc;
+}
+
+int esgd_set_transport(const char *name) {
+    ESGD_ARG(name && (!std::strcmp(name, "ipc") || !std::strcmp(name, "rccl")),
+             "esgd_set_transport: 'ipc' or 'rccl'");
+    g_transport = name;
+    return ESGD_SUCCESS;
+}
+
+int esgd_comm_issue_log(uint32_t *sched, uint32_t *round, uint32_t cap, uint32_t *n) {
+    return engine_issue_log(sched, round, cap, n);
+}
 
 int esgd_comm_rank(int *rank) {
     ESGD_ARG(rank, "esgd_comm_rank: null pointer");
@@ -48,7 +75,9 @@ int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t c
              "esgd_schedule_create: bad buffer kind %d", buf);
     ESGD_ARG(esgd_dtype_size(dtype) > 0, "esgd_schedule_create: unsupported dtype %d", dtype);
     ESGD_ARG(buf == ESGD_BUF_NONE || rb || count == 0, "esgd_schedule_create: null receive buffer");
-    Transport *tp = buf == ESGD_BUF_NONE ? null_transport() : ipc_transport();
+    const bool rccl = !std::strcmp(transport_name(), "rccl");
+    ESGD_ARG(rccl || !std::strcmp(transport_name(), "ipc"), "unknown transport '%s'", transport_name());
+    Transport *tp = buf == ESGD_BUF_NONE ? null_transport(rccl) : rccl ? rccl_transport() : ipc_transport();
     Sched *s = nullptr;
     int rc = sched_create(kind, dtype, count, const_cast<void *>(sb), rb, buf == ESGD_BUF_HOST,
                           async, seed, tp, &s);

@@ -18,6 +18,7 @@
 // it is reachable only through ESGD_BUF_NONE and computes nothing.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -26,6 +27,7 @@
 
 #include "engine.h"
 #include "esgd_internal.h"
+#include "esgd.h"
 
 namespace esgd {
 
@@ -76,21 +78,28 @@ static void ipc_close(void *base) {
     }
 }
 
-struct IpcState {
+// State every GPU transport keeps per schedule: the data-plane stream, the query
+// event, the device receive bucket (the caller's, or an HBM copy of a host bucket), the
+// shard layout and the producer events of posted rounds.
+struct BaseState {
     hipStream_t stream = nullptr;
     hipEvent_t ev = nullptr;
     char *rb_dev = nullptr;
     bool owns_rb = false, reg_sb = false, reg_rb = false;
-    char *peer[kMaxRanks] = {};
-    void *peer_base[kMaxRanks] = {};
     uint64_t off[kMaxRanks] = {}, len[kMaxRanks] = {};   // elements
     std::map<uint32_t, hipEvent_t> producer;
     std::vector<hipEvent_t> spare;
+    virtual ~BaseState() {}
+};
+
+struct IpcState : BaseState {
+    char *peer[kMaxRanks] = {};
+    void *peer_base[kMaxRanks] = {};
 };
 
 // shard j = [off_j, off_j + len_j): equal shards rounded up to 1 KiB so every shard
 // (and the 16-B vectors the kernels move) starts aligned; the last one is ragged.
-static void layout(Sched &s, IpcState &st) {
+static void layout(Sched &s, BaseState &st) {
     const uint64_t align = 1024 / s.esize;
     uint64_t per = (s.count + uint64_t(s.world) - 1) / uint64_t(s.world);
     per = (per + align - 1) / align * align;
@@ -101,38 +110,99 @@ static void layout(Sched &s, IpcState &st) {
     }
 }
 
+static int base_setup(Sched &s, BaseState &st) {
+    if (s.esize == 0) { set_error("schedule: unsupported dtype %d", s.dtype); return ESGD_INVALID_ARG; }
+    if (int rc = require_device()) return rc;
+    const size_t bytes = s.count * s.esize;
+    ESGD_HIP(hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking));
+    ESGD_HIP(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
+    if (s.host_mode) {
+        ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.rb_dev), bytes ? bytes : 256));
+        st.owns_rb = true;
+        // pin the caller's persistent host buckets so the move / copy-out are DMA
+        if (bytes && s.rb && hipHostRegister(s.rb, bytes, hipHostRegisterDefault) == hipSuccess)
+            st.reg_rb = true;
+        if (bytes && s.sb && s.sb != s.rb &&
+            hipHostRegister(s.sb, bytes, hipHostRegisterDefault) == hipSuccess)
+            st.reg_sb = true;
+        (void)hipGetLastError();   // "already registered" is fine
+    } else {
+        if (!s.rb) { set_error("schedule: null receive buffer"); return ESGD_INVALID_ARG; }
+        if (reinterpret_cast<uintptr_t>(s.rb) & 15) {
+            set_error("schedule: device receive buffer must be 16-B aligned");
+            return ESGD_INVALID_ARG;
+        }
+        st.rb_dev = static_cast<char *>(s.rb);
+    }
+    layout(s, st);
+    return ESGD_SUCCESS;
+}
+
+static int base_note_producer(BaseState &st, uint32_t round, void *stream) {
+    hipEvent_t e;
+    if (!st.spare.empty()) { e = st.spare.back(); st.spare.pop_back(); }
+    else ESGD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ESGD_HIP(hipEventRecord(e, static_cast<hipStream_t>(stream)));
+    st.producer[round] = e;
+    return ESGD_SUCCESS;
+}
+
+static int base_snapshot(Sched &s, BaseState &st, uint32_t round, bool fresh) {
+    // gradient producer of this round (posted before the join) must have finished
+    for (auto it = st.producer.begin(); it != st.producer.end();) {
+        if (it->first == round && fresh) ESGD_HIP(hipStreamWaitEvent(st.stream, it->second, 0));
+        if (it->first <= round) { st.spare.push_back(it->second); it = st.producer.erase(it); }
+        else ++it;
+    }
+    const size_t bytes = s.count * s.esize;
+    if (bytes) {
+        if (s.host_mode) {   // the move of ffallreduce.c:126-130, host -> HBM
+            const void *src = s.sb ? s.sb : s.rb;
+            ESGD_HIP(hipMemcpyAsync(st.rb_dev, src, bytes, hipMemcpyHostToDevice, st.stream));
+        } else if (!s.in_place) {
+            ESGD_HIP(hipMemcpyAsync(st.rb_dev, s.sb, bytes, hipMemcpyDeviceToDevice, st.stream));
+        }
+    }
+    ESGD_HIP(hipEventRecord(st.ev, st.stream));
+    return ESGD_SUCCESS;
+}
+
+static int base_finish(Sched &s, BaseState &st) {
+    const size_t bytes = s.count * s.esize;
+    if (s.host_mode && bytes)
+        ESGD_HIP(hipMemcpyAsync(s.rb, st.rb_dev, bytes, hipMemcpyDeviceToHost, st.stream));
+    ESGD_HIP(hipEventRecord(st.ev, st.stream));
+    return ESGD_SUCCESS;
+}
+
+static int base_query(BaseState &st) {
+    hipError_t e = hipEventQuery(st.ev);
+    if (e == hipSuccess) return 1;
+    if (e == hipErrorNotReady) return 0;
+    return hip_fail(e, "hipEventQuery", __FILE__, __LINE__);
+}
+
+static void base_teardown(Sched &s, BaseState &st) {
+    if (st.stream) (void)hipStreamSynchronize(st.stream);
+    if (st.owns_rb) (void)hipFree(st.rb_dev);
+    if (st.reg_rb) (void)hipHostUnregister(s.rb);
+    if (st.reg_sb) (void)hipHostUnregister(s.sb);
+    for (auto &kv : st.producer) (void)hipEventDestroy(kv.second);
+    for (hipEvent_t e : st.spare) (void)hipEventDestroy(e);
+    if (st.ev) (void)hipEventDestroy(st.ev);
+    if (st.stream) (void)hipStreamDestroy(st.stream);
+}
+
 struct IpcTransport final : Transport {
     const char *name() const override { return "ipc"; }
 
     static IpcState &S(Sched &s) { return *static_cast<IpcState *>(s.tstate); }
 
     int setup(Sched &s) override {
-        if (s.esize == 0) { set_error("schedule: unsupported dtype %d", s.dtype); return ESGD_INVALID_ARG; }
-        if (int rc = require_device()) return rc;
         auto *st = new IpcState();
         s.tstate = st;
+        if (int rc = base_setup(s, *st)) return rc;
         const size_t bytes = s.count * s.esize;
-        ESGD_HIP(hipStreamCreateWithFlags(&st->stream, hipStreamNonBlocking));
-        ESGD_HIP(hipEventCreateWithFlags(&st->ev, hipEventDisableTiming));
-        if (s.host_mode) {
-            ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st->rb_dev), bytes ? bytes : 256));
-            st->owns_rb = true;
-            // pin the caller's persistent host buckets so the move / copy-out are DMA
-            if (bytes && s.rb && hipHostRegister(s.rb, bytes, hipHostRegisterDefault) == hipSuccess)
-                st->reg_rb = true;
-            if (bytes && s.sb && s.sb != s.rb &&
-                hipHostRegister(s.sb, bytes, hipHostRegisterDefault) == hipSuccess)
-                st->reg_sb = true;
-            (void)hipGetLastError();   // "already registered" is fine
-        } else {
-            if (!s.rb) { set_error("schedule: null receive buffer"); return ESGD_INVALID_ARG; }
-            if (reinterpret_cast<uintptr_t>(s.rb) & 15) {
-                set_error("schedule: device receive buffer must be 16-B aligned");
-                return ESGD_INVALID_ARG;
-            }
-            st->rb_dev = static_cast<char *>(s.rb);
-        }
-        layout(s, *st);
         st->peer[s.rank] = st->rb_dev;
         if (s.world == 1) return ESGD_SUCCESS;
         // publish this rank's rb, then map every peer's
@@ -168,34 +238,11 @@ struct IpcTransport final : Transport {
     }
 
     int note_producer(Sched &s, uint32_t round, void *stream) override {
-        IpcState &st = S(s);
-        hipEvent_t e;
-        if (!st.spare.empty()) { e = st.spare.back(); st.spare.pop_back(); }
-        else ESGD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        ESGD_HIP(hipEventRecord(e, static_cast<hipStream_t>(stream)));
-        st.producer[round] = e;
-        return ESGD_SUCCESS;
+        return base_note_producer(S(s), round, stream);
     }
 
     int snapshot(Sched &s, uint32_t round, bool fresh) override {
-        IpcState &st = S(s);
-        // gradient producer of this round (posted before the join) must have finished
-        for (auto it = st.producer.begin(); it != st.producer.end();) {
-            if (it->first == round && fresh) ESGD_HIP(hipStreamWaitEvent(st.stream, it->second, 0));
-            if (it->first <= round) { st.spare.push_back(it->second); it = st.producer.erase(it); }
-            else ++it;
-        }
-        const size_t bytes = s.count * s.esize;
-        if (bytes) {
-            if (s.host_mode) {   // the move of ffallreduce.c:126-130, host -> HBM
-                const void *src = s.sb ? s.sb : s.rb;
-                ESGD_HIP(hipMemcpyAsync(st.rb_dev, src, bytes, hipMemcpyHostToDevice, st.stream));
-            } else if (!s.in_place) {
-                ESGD_HIP(hipMemcpyAsync(st.rb_dev, s.sb, bytes, hipMemcpyDeviceToDevice, st.stream));
-            }
-        }
-        ESGD_HIP(hipEventRecord(st.ev, st.stream));
-        return ESGD_SUCCESS;
+        return base_snapshot(s, S(s), round, fresh);
     }
 
     int reduce_scatter(Sched &s) override {
@@ -232,21 +279,9 @@ struct IpcTransport final : Transport {
         return ESGD_SUCCESS;
     }
 
-    int finish(Sched &s) override {
-        IpcState &st = S(s);
-        const size_t bytes = s.count * s.esize;
-        if (s.host_mode && bytes)
-            ESGD_HIP(hipMemcpyAsync(s.rb, st.rb_dev, bytes, hipMemcpyDeviceToHost, st.stream));
-        ESGD_HIP(hipEventRecord(st.ev, st.stream));
-        return ESGD_SUCCESS;
-    }
+    int finish(Sched &s) override { return base_finish(s, S(s)); }
 
-    int query(Sched &s) override {
-        hipError_t e = hipEventQuery(S(s).ev);
-        if (e == hipSuccess) return 1;
-        if (e == hipErrorNotReady) return 0;
-        return hip_fail(e, "hipEventQuery", __FILE__, __LINE__);
-    }
+    int query(Sched &s) override { return base_query(S(s)); }
 
     void teardown(Sched &s) override {
         IpcState *st = static_cast<IpcState *>(s.tstate);
@@ -254,20 +289,17 @@ struct IpcTransport final : Transport {
         if (st->stream) (void)hipStreamSynchronize(st->stream);
         for (int q = 0; q < kMaxRanks; ++q)
             if (st->peer_base[q]) ipc_close(st->peer_base[q]);
-        if (st->owns_rb) (void)hipFree(st->rb_dev);
-        if (st->reg_rb) (void)hipHostUnregister(s.rb);
-        if (st->reg_sb) (void)hipHostUnregister(s.sb);
-        for (auto &kv : st->producer) (void)hipEventDestroy(kv.second);
-        for (hipEvent_t e : st->spare) (void)hipEventDestroy(e);
-        if (st->ev) (void)hipEventDestroy(st->ev);
-        if (st->stream) (void)hipStreamDestroy(st->stream);
+        base_teardown(s, *st);
         delete st;
         s.tstate = nullptr;
     }
 };
 
 struct NullTransport final : Transport {
-    const char *name() const override { return "none"; }
+    explicit NullTransport(bool ord = false) : ordered_(ord) {}
+    bool ordered_;
+    const char *name() const override { return ordered_ ? "none-ordered" : "none"; }
+    bool ordered() const override { return ordered_; }
     int setup(Sched &) override { return ESGD_SUCCESS; }
     int note_producer(Sched &, uint32_t, void *) override { return ESGD_SUCCESS; }
     int snapshot(Sched &, uint32_t, bool) override { return ESGD_SUCCESS; }
@@ -283,14 +315,195 @@ Transport *ipc_transport() {
     return &t;
 }
 
-Transport *null_transport() {
-    static NullTransport t;
-    return &t;
+Transport *null_transport(bool ordered) {
+    static NullTransport plain(false), ord(true);
+    return ordered ? &ord : &plain;
 }
 
+Transport *rccl_transport();
+
 hipStream_t sched_stream(Sched &s) {
-    if (!s.tstate || s.tp != ipc_transport()) return nullptr;
-    return static_cast<IpcState *>(s.tstate)->stream;
+    if (!s.tstate || (s.tp != ipc_transport() && s.tp != rccl_transport())) return nullptr;
+    return static_cast<BaseState *>(s.tstate)->stream;
+}
+
+// ---- RcclTransport: RCCL point-to-point over xGMI + the tree kernel on a side stream --
+//
+// The north-star shape of SURVEY.md §8(e): per round, on ONE process-wide communicator
+// stream, grouped ncclSend/ncclRecv move shard j of this rank's rb to rank j and every
+// peer's copy of shard `rank` into a staging area, chunk by chunk; the schedule's own
+// stream waits for each chunk and folds it with the tree kernel (same order as the
+// reference); a second group all-gathers the reduced shards.  RCCL matches operations
+// by issue order, so rounds are issued in the global ticket order (engine ordered()).
+// RCCL refuses two ranks on one GPU, so this transport only runs with one GPU per rank.
+}  // namespace esgd
+
+#include <rccl/rccl.h>
+
+namespace esgd {
+
+static std::mutex g_nccl_mu;
+static ncclComm_t g_nccl = nullptr;
+static hipStream_t g_cs = nullptr;    // all RCCL operations of this process, in ticket order
+
+static int nccl_fail(ncclResult_t r, const char *what) {
+    set_error("%s: %s", what, ncclGetErrorString(r));
+    return ESGD_ERROR;
+}
+#define ESGD_NCCL(call)                                                       \
+    do {                                                                      \
+        ncclResult_t esgd_r_ = (call);                                        \
+        if (esgd_r_ != ncclSuccess) return nccl_fail(esgd_r_, #call);         \
+    } while (0)
+
+static int nccl_ensure(Sched &s) {
+    std::lock_guard<std::mutex> lk(g_nccl_mu);
+    if (g_nccl) return ESGD_SUCCESS;
+    Segment *seg = engine_segment();
+    ncclUniqueId id;
+    static_assert(sizeof(id) <= sizeof(seg->nccl_id), "nccl id does not fit the segment");
+    if (s.rank == 0) {
+        ESGD_NCCL(ncclGetUniqueId(&id));
+        std::memcpy(seg->nccl_id, &id, sizeof(id));
+    }
+    if (int rc = engine_barrier()) return rc;   // setup runs collectively
+    std::memcpy(&id, seg->nccl_id, sizeof(id));
+    ESGD_NCCL(ncclCommInitRank(&g_nccl, s.world, id, s.rank));
+    ESGD_HIP(hipStreamCreateWithFlags(&g_cs, hipStreamNonBlocking));
+    return ESGD_SUCCESS;
+}
+
+void rccl_shutdown() {
+    std::lock_guard<std::mutex> lk(g_nccl_mu);
+    if (g_cs) { (void)hipStreamSynchronize(g_cs); (void)hipStreamDestroy(g_cs); g_cs = nullptr; }
+    if (g_nccl) { (void)ncclCommDestroy(g_nccl); g_nccl = nullptr; }
+}
+
+struct RcclState : BaseState {
+    char *stage = nullptr;           // P x L elements: every peer's copy of this rank's shard
+    uint64_t L = 0;                  // shard pitch (elements)
+    uint64_t chunk = 0;              // pipeline chunk (elements)
+    hipEvent_t ev_snap = nullptr, ev_red = nullptr;
+    std::vector<hipEvent_t> ev_chunk;
+};
+
+struct RcclTransport final : Transport {
+    const char *name() const override { return "rccl"; }
+    bool ordered() const override { return true; }
+
+    static RcclState &S(Sched &s) { return *static_cast<RcclState *>(s.tstate); }
+
+    int setup(Sched &s) override {
+        auto *st = new RcclState();
+        s.tstate = st;
+        if (int rc = base_setup(s, *st)) return rc;
+        if (int rc = nccl_ensure(s)) return rc;
+        ESGD_HIP(hipEventCreateWithFlags(&st->ev_snap, hipEventDisableTiming));
+        ESGD_HIP(hipEventCreateWithFlags(&st->ev_red, hipEventDisableTiming));
+        st->L = st->len[0];
+        if (s.world > 1 && st->L) {
+            ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st->stage), size_t(s.world) * st->L * s.esize));
+            // ~8 chunks per shard, at least 1 MiB each, 1 KiB aligned
+            const uint64_t align = 1024 / s.esize, minc = (1u << 20) / s.esize;
+            uint64_t c = std::max<uint64_t>(minc, (st->L + 7) / 8);
+            st->chunk = (c + align - 1) / align * align;
+        }
+        return ESGD_SUCCESS;
+    }
+
+    int note_producer(Sched &s, uint32_t round, void *stream) override {
+        return base_note_producer(S(s), round, stream);
+    }
+
+    int snapshot(Sched &s, uint32_t round, bool fresh) override {
+        return base_snapshot(s, S(s), round, fresh);
+    }
+
+    static uint64_t piece(uint64_t len, uint64_t c, uint64_t chunk) {
+        const uint64_t o = c * chunk;
+        return o >= len ? 0 : std::min(chunk, len - o);
+    }
+
+    // The whole round is queued here, in ticket order: RS groups (comm stream) ->
+    // per-chunk tree folds (schedule stream) -> AG group (comm stream).
+    int reduce_scatter(Sched &s) override {
+        RcclState &st = S(s);
+        const int P = s.world, r = s.rank;
+        const size_t es = s.esize;
+        ESGD_HIP(hipEventRecord(st.ev_snap, st.stream));
+        ESGD_HIP(hipStreamWaitEvent(g_cs, st.ev_snap, 0));
+        if (P > 1 && st.L) {
+            const uint64_t nch = (st.L + st.chunk - 1) / st.chunk;
+            while (st.ev_chunk.size() < nch) {
+                hipEvent_t e;
+                ESGD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                st.ev_chunk.push_back(e);
+            }
+            for (uint64_t c = 0; c < nch; ++c) {
+                ESGD_NCCL(ncclGroupStart());
+                for (int j = 0; j < P; ++j) {
+                    if (j == r) continue;
+                    const uint64_t ns = piece(st.len[j], c, st.chunk);
+                    if (ns) ESGD_NCCL(ncclSend(st.rb_dev + (st.off[j] + c * st.chunk) * es, ns * es,
+                                               ncclChar, j, g_nccl, g_cs));
+                    const uint64_t nr = piece(st.len[r], c, st.chunk);
+                    if (nr) ESGD_NCCL(ncclRecv(st.stage + (uint64_t(j) * st.L + c * st.chunk) * es,
+                                               nr * es, ncclChar, j, g_nccl, g_cs));
+                }
+                ESGD_NCCL(ncclGroupEnd());
+                ESGD_HIP(hipEventRecord(st.ev_chunk[c], g_cs));
+                const uint64_t n = piece(st.len[r], c, st.chunk);
+                if (!n) continue;
+                ESGD_HIP(hipStreamWaitEvent(st.stream, st.ev_chunk[c], 0));
+                const void *in[kMaxRanks];
+                char *own = st.rb_dev + (st.off[r] + c * st.chunk) * es;
+                for (int j = 0; j < P; ++j)
+                    in[j] = j == r ? own : st.stage + (uint64_t(j) * st.L + c * st.chunk) * es;
+                if (int rc = esgd_reduce(s.dtype, P, in, own, n, st.stream)) return rc;
+            }
+            ESGD_HIP(hipEventRecord(st.ev_red, st.stream));
+            ESGD_HIP(hipStreamWaitEvent(g_cs, st.ev_red, 0));
+            ESGD_NCCL(ncclGroupStart());
+            for (int j = 0; j < P; ++j) {
+                if (j == r) continue;
+                if (st.len[r]) ESGD_NCCL(ncclSend(st.rb_dev + st.off[r] * es, st.len[r] * es, ncclChar, j,
+                                                  g_nccl, g_cs));
+                if (st.len[j]) ESGD_NCCL(ncclRecv(st.rb_dev + st.off[j] * es, st.len[j] * es, ncclChar, j,
+                                                  g_nccl, g_cs));
+            }
+            ESGD_NCCL(ncclGroupEnd());
+        }
+        ESGD_HIP(hipEventRecord(st.ev, g_cs));
+        return ESGD_SUCCESS;
+    }
+
+    int all_gather(Sched &s) override {   // queued with the reduce-scatter above
+        RcclState &st = S(s);
+        ESGD_HIP(hipEventRecord(st.ev, st.stream));
+        return ESGD_SUCCESS;
+    }
+
+    int finish(Sched &s) override { return base_finish(s, S(s)); }
+    int query(Sched &s) override { return base_query(S(s)); }
+
+    void teardown(Sched &s) override {
+        RcclState *st = static_cast<RcclState *>(s.tstate);
+        if (!st) return;
+        if (g_cs) (void)hipStreamSynchronize(g_cs);
+        if (st->stream) (void)hipStreamSynchronize(st->stream);
+        if (st->stage) (void)hipFree(st->stage);
+        for (hipEvent_t e : st->ev_chunk) (void)hipEventDestroy(e);
+        if (st->ev_snap) (void)hipEventDestroy(st->ev_snap);
+        if (st->ev_red) (void)hipEventDestroy(st->ev_red);
+        base_teardown(s, *st);
+        delete st;
+        s.tstate = nullptr;
+    }
+};
+
+Transport *rccl_transport() {
+    static RcclTransport t;
+    return &t;
 }
 
 }  // namespace esgd

@@ -35,6 +35,9 @@ static int g_next_id = 0;
 static std::thread g_thread;
 static std::atomic<bool> g_running{false};
 static std::atomic<uint32_t> g_wake{0};
+static uint64_t g_cursor = 0;                       // next ticket this rank issues
+static std::mutex g_issue_mu;
+static std::vector<std::pair<uint32_t, uint32_t>> g_issued;
 
 bool engine_ready() { return g_seg != nullptr; }
 int engine_rank() { return g_rank; }
@@ -107,6 +110,11 @@ int engine_finalize() {
     shm_detach(g_seg, nullptr, -1);
     g_seg = nullptr;
     g_next_id = 0;
+    g_cursor = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_issue_mu);
+        g_issued.clear();
+    }
     return rc;
 }
 
@@ -144,6 +152,8 @@ int sched_create(int kind, int dtype, uint64_t count, void *sb, void *rb, bool h
             sh->ready[r].store(0); sh->reduced[r].store(0); sh->done[r].store(0);
             sh->joined[r].store(0); sh->activations[r].store(0);
         }
+        sh->ready_count.store(0);
+        for (int i = 0; i < 256; ++i) sh->act_of[i].store(0);
         sh->gen.fetch_add(1, std::memory_order_acq_rel);
     }
     if (!rc) rc = shm_barrier(g_seg, g_world, g_timeout);
@@ -165,17 +175,29 @@ int sched_create(int kind, int dtype, uint64_t count, void *sb, void *rb, bool h
     return ESGD_SUCCESS;
 }
 
-static void activate_max(SchedShm *sh, uint32_t round, int rank, bool *raised) {
-    uint32_t cur = sh->activated.load(std::memory_order_acquire);
-    *raised = false;
-    while (cur < round) {
-        if (sh->activated.compare_exchange_weak(cur, round, std::memory_order_acq_rel)) {
-            *raised = true;
+// Activate `round` (the activation flood of colls/ffactivation.c): claim the round's
+// slot first (first claimant = activator), then raise the shared counter.
+static void activate(SchedShm *sh, uint32_t round, int rank, bool *won) {
+    std::atomic<uint64_t> &slot = sh->act_of[round % 256];
+    uint64_t cur = slot.load(std::memory_order_acquire);
+    const uint64_t mine = (uint64_t(round) << 32) | uint64_t(rank + 1);
+    *won = false;
+    while ((cur >> 32) < round) {
+        if (slot.compare_exchange_weak(cur, mine, std::memory_order_acq_rel)) {
+            *won = true;
             sh->last_activator.store(rank, std::memory_order_relaxed);
             sh->activations[rank].fetch_add(1, std::memory_order_relaxed);
             break;
         }
     }
+    uint32_t a = sh->activated.load(std::memory_order_acquire);
+    while (a < round && !sh->activated.compare_exchange_weak(a, round, std::memory_order_acq_rel)) {
+    }
+}
+
+static int activator_of(SchedShm *sh, uint32_t round) {
+    const uint64_t v = sh->act_of[round % 256].load(std::memory_order_acquire);
+    return (v >> 32) == round ? int(v & 0xffffffffu) - 1 : -1;
 }
 
 int sched_post(Sched *s, void *producer_stream, int *role) {
@@ -192,11 +214,11 @@ int sched_post(Sched *s, void *producer_stream, int *role) {
             // colls/ffrand_allreduce.c:88 — the same glibc draw on every rank
             const int act = int(unsigned(rand_r(&s->seed)) % unsigned(s->world));
             if (act == s->rank) {
-                bool raised;
-                activate_max(s->sh, t, s->rank, &raised);
+                bool won;
+                activate(s->sh, t, s->rank, &won);
                 s->passive = 0;   // catch-up of :93-96 is implicit in the round counter
                 r = 1;
-                if (raised) ++s->n_activated;
+                if (won) ++s->n_activated;
             } else {
                 ++s->passive;
                 r = 0;
@@ -204,10 +226,10 @@ int sched_post(Sched *s, void *producer_stream, int *role) {
         } else if (round_is_sync(*s, t)) {
             r = 2;
         } else {
-            bool raised;
-            activate_max(s->sh, t, s->rank, &raised);   // first poster activates the round
-            r = raised ? 1 : 0;
-            if (raised) ++s->n_activated;
+            bool won;
+            activate(s->sh, t, s->rank, &won);   // the first poster activates the round
+            r = won ? 1 : 0;
+            if (won) ++s->n_activated;
         }
     }
     g_wake.fetch_add(1, std::memory_order_acq_rel);
@@ -313,7 +335,7 @@ static bool step(Sched &s) {
         if (s.cur_fresh) ++s.n_fresh; else ++s.n_auto;
         if (s.log.size() < 65536)
             s.log.push_back({next, uint8_t(s.cur_fresh), uint8_t(sync),
-                             int16_t(sync ? -1 : sh->last_activator.load())});
+                             int16_t(sync ? -1 : activator_of(sh, next))});
         if (!check(s.tp->snapshot(s, next, s.cur_fresh), "snapshot")) return true;
         enter(ST_SNAPSHOT);
         return true;
@@ -323,9 +345,24 @@ static bool step(Sched &s) {
         if (!check(q, "snapshot")) return true;
         if (!q) return false;
         sh->ready[s.rank].store(s.cur, std::memory_order_release);
+        if (s.tp->ordered()) {
+            enter(ST_WAIT_TICKET);
+            // the rank whose publication completes the round appends it to the ring
+            const uint32_t prev = sh->ready_count.fetch_add(1, std::memory_order_acq_rel);
+            if (prev + 1 == s.cur * uint32_t(s.world)) {
+                const uint64_t tk = g_seg->ticket_next.fetch_add(1, std::memory_order_acq_rel);
+                TicketSlot &slot = g_seg->ring[tk % kRing];
+                slot.sched = uint32_t(s.id);
+                slot.round = s.cur;
+                slot.tag.store(tk + 1, std::memory_order_release);
+            }
+            return true;
+        }
         enter(ST_WAIT_READY);
         return true;
     }
+    case ST_WAIT_TICKET:
+        return timed_out("round never reached its turn in the issue ring") ? true : false;
     case ST_WAIT_READY:
         if (!all_at_least(sh->ready, s.world, s.cur)) return timed_out("peers never published their snapshot");
         if (!check(s.tp->reduce_scatter(s), "reduce-scatter")) return true;
@@ -370,13 +407,55 @@ static bool step(Sched &s) {
     return false;
 }
 
+// Issue ordered rounds strictly in ring order (same sequence on every rank).
+static bool pump_tickets(const std::vector<Sched *> &snap) {
+    if (!g_seg) return false;
+    bool any = false;
+    for (;;) {
+        TicketSlot &slot = g_seg->ring[g_cursor % kRing];
+        if (slot.tag.load(std::memory_order_acquire) != g_cursor + 1) break;
+        Sched *target = nullptr;
+        for (Sched *s : snap)
+            if (uint32_t(s->id) == slot.sched) { target = s; break; }
+        if (!target) break;                      // schedule not registered here yet
+        {
+            std::lock_guard<std::mutex> lk(target->mu);
+            if (target->stage != ST_WAIT_TICKET || target->cur != slot.round) break;
+            int rc = target->tp->reduce_scatter(*target);
+            if (rc < 0) {
+                fail_locked(*target, rc, esgd_last_error());
+            } else {
+                target->stage = ST_RS;
+                target->stage_t0 = now_s();
+            }
+        }
+        {
+            std::lock_guard<std::mutex> lk(g_issue_mu);
+            if (g_issued.size() < 65536) g_issued.emplace_back(slot.sched, slot.round);
+        }
+        ++g_cursor;
+        any = true;
+    }
+    return any;
+}
+
+int engine_issue_log(uint32_t *sched, uint32_t *round, uint32_t cap, uint32_t *n) {
+    std::lock_guard<std::mutex> lk(g_issue_mu);
+    for (uint32_t i = 0; i < g_issued.size() && i < cap; ++i) {
+        if (sched) sched[i] = g_issued[i].first;
+        if (round) round[i] = g_issued[i].second;
+    }
+    if (n) *n = uint32_t(g_issued.size());
+    return ESGD_SUCCESS;
+}
+
 bool engine_progress_once() {
     std::vector<Sched *> snap;
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         snap = g_reg;
     }
-    bool any = false;
+    bool any = pump_tickets(snap);
     for (Sched *s : snap)
         while (step(*s)) any = true;   // run a schedule until it has to wait
     return any;

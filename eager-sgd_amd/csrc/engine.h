@@ -36,6 +36,7 @@ enum Stage {
     ST_IDLE = 0,      // between rounds
     ST_SNAPSHOT,      // move sb -> rb queued
     ST_WAIT_READY,    // waiting for every rank's snapshot
+    ST_WAIT_TICKET,   // ordered transports: waiting for this round's turn in the ring
     ST_RS,            // reduce-scatter queued
     ST_WAIT_REDUCED,  // waiting for every rank's reduced shard
     ST_AG,            // all-gather queued
@@ -50,6 +51,9 @@ struct Sched;
 struct Transport {
     virtual ~Transport() {}
     virtual const char *name() const = 0;
+    // true: collectives must be issued in one global order (RCCL); reduce_scatter() is
+    // then called from the ticket pump in ring order instead of at "all ready".
+    virtual bool ordered() const { return false; }
     virtual int setup(Sched &s) = 0;          // collective: called between barriers
     virtual int note_producer(Sched &s, uint32_t round, void *stream) = 0;
     virtual int snapshot(Sched &s, uint32_t round, bool fresh) = 0;
@@ -119,6 +123,9 @@ int sched_wait(Sched *s);
 int sched_test(Sched *s, int *flag);
 int sched_delete(Sched *s);
 Sched *sched_lookup(uint64_t handle);
+
+// Issue log of ordered transports: (schedule id, round) in the order this rank issued.
+int engine_issue_log(uint32_t *sched, uint32_t *round, uint32_t cap, uint32_t *n);
 
 // One polling pass over all schedules (the progress thread calls it in a loop; tests
 // without a thread may call it directly).  Returns true if anything advanced.

@@ -76,7 +76,7 @@ int ffinit(int *, char ***) {
 
 int fffinalize(void) {
     g_ff_owns_comm = false;
-    return engine_finalize();
+    return esgd_comm_finalize();
 }
 
 int ffrank(int *rank) { return esgd_comm_rank(rank); }

@@ -32,13 +32,26 @@ struct alignas(64) SchedShm {
     std::atomic<uint32_t> gen;            // bumped by each collective (re)creation
     std::atomic<uint32_t> kind;
     std::atomic<uint32_t> activated;      // highest round activated (solo async / majority)
-    std::atomic<int32_t> last_activator;  // rank that activated `activated`
+    std::atomic<int32_t> last_activator;  // diagnostics only (may lag `activated`)
+    // per-round activation record, (round << 32) | (rank + 1), claimed by CAS BEFORE
+    // `activated` is raised: whoever sees activated >= t also sees round t's activator
+    std::atomic<uint64_t> act_of[256];
     std::atomic<uint32_t> ready[kMaxRanks];   // round whose input snapshot rank r has published
     std::atomic<uint32_t> reduced[kMaxRanks]; // round whose phase 1 (reduce-scatter) is done
     std::atomic<uint32_t> done[kMaxRanks];    // round whose phase 2 (all-gather) is done
     std::atomic<uint32_t> joined[kMaxRanks];  // diagnostics: last round rank r joined
     std::atomic<uint32_t> activations[kMaxRanks];  // diagnostics: rounds activated by r
+    std::atomic<uint32_t> ready_count;   // ordered transports: sum of ready publications
     IpcSlot slot[kMaxRanks];
+};
+
+// Global issue order for transports whose collectives must be issued in the same
+// order on every rank (RCCL): the rank that completes a round's readiness appends it.
+constexpr int kRing = 4096;
+struct alignas(16) TicketSlot {
+    std::atomic<uint64_t> tag;   // ticket + 1 once the slot is filled
+    uint32_t sched;
+    uint32_t round;
 };
 
 struct Segment {
@@ -53,6 +66,8 @@ struct Segment {
     uint8_t nccl_id[128];
     std::atomic<int32_t> pid[kMaxRanks];
     std::atomic<int32_t> device[kMaxRanks];
+    std::atomic<uint64_t> ticket_next;
+    TicketSlot ring[kRing];
     SchedShm sched[kMaxSched];
 };
 

@@ -49,6 +49,8 @@ def _bind(h):
         "esgd_schedule_log": (i, [u64, C.POINTER(u32), C.POINTER(C.c_uint8), C.POINTER(C.c_uint8),
                                   C.POINTER(C.c_int16), u32, C.POINTER(u32)]),
         "esgd_schedule_stream": (i, [u64, C.POINTER(vp)]),
+        "esgd_set_transport": (i, [C.c_char_p]),
+        "esgd_comm_issue_log": (i, [C.POINTER(u32), C.POINTER(u32), u32, C.POINTER(u32)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(h, name)
@@ -109,6 +111,21 @@ def world() -> int:
     v = C.c_int()
     check(lib().esgd_comm_size(C.byref(v)))
     return v.value
+
+
+def set_transport(name: str):
+    """Data plane of schedules created afterwards: "ipc" (default) or "rccl"."""
+    check(lib().esgd_set_transport(name.encode()), "esgd_set_transport")
+
+
+def issue_log():
+    """(schedule id, round) in the order this rank issued ordered (rccl) rounds."""
+    n = C.c_uint32()
+    check(lib().esgd_comm_issue_log(None, None, 0, C.byref(n)))
+    cap = n.value
+    a = (C.c_uint32 * max(1, cap))(); b = (C.c_uint32 * max(1, cap))()
+    check(lib().esgd_comm_issue_log(a, b, cap, C.byref(n)))
+    return [(a[i], b[i]) for i in range(min(cap, n.value))]
 
 
 def barrier():

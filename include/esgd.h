@@ -120,6 +120,14 @@ int esgd_comm_rank(int *rank);
 int esgd_comm_size(int *size);
 int esgd_barrier(void);
 
+/* Data plane of schedules created afterwards: "ipc" (default: pull over IPC-mapped peer
+ * HBM, two kernels per round) or "rccl" (grouped ncclSend/ncclRecv + the tree kernel on
+ * a side stream; one GPU per rank).  Env ESGD_TRANSPORT sets the default. */
+int esgd_set_transport(const char *name);
+/* ordered transports (rccl): (schedule id, round) pairs in the order this rank issued
+ * them — identical on every rank by construction (tests). */
+int esgd_comm_issue_log(uint32_t *sched, uint32_t *round, uint32_t cap, uint32_t *n);
+
 /* ---- persistent partial-allreduce schedules ----
  * kind: ESGD_SCHED_ALLREDUCE (every round synchronous, src/colls/ffallreduce.c),
  *       ESGD_SCHED_SOLO (first poster activates; every (async+1)-th round synchronous,

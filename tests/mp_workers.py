@@ -107,7 +107,7 @@ def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0
 
 
 def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0, buf="device",
-                  in_place=False):
+                  in_place=False, transport="ipc"):
     """Data plane on the GPU: every rank reduces its splitmix bucket; returns the
     result bytes' digest per round plus a bit-exactness verdict against the oracle."""
     import numpy as np
@@ -116,6 +116,7 @@ def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0
     from esgd import device as dev
     from oracle import ffref
     comm = _comm()
+    comm.set_transport(transport)
     seed = 0x5EEDE56D
     dt = {"fp32": _lib.FLOAT, "int32": _lib.INT32, "fp64": _lib.DOUBLE, "int64": _lib.INT64,
           "bf16": _lib.BF16}[dtype_name]
@@ -259,3 +260,31 @@ def optimizer_step(rank, world, mode="allreduce", steps=2):
     nbytes = opt.bytes_reduced()
     comm.finalize()
     return {"ok": ok, "params_digest": params.tobytes().hex()[:64] + str(params.sum()), "bytes": nbytes}
+
+
+def cp_ordered(rank, world, nsched=3, rounds=6, seed=7):
+    """Ordered (rccl-style) issue: several schedules posted with per-rank random jitter;
+    every rank must issue the rounds in the same global order (ticket ring)."""
+    import random
+
+    from esgd import comm
+    comm.init()
+    comm.set_transport("rccl")
+    scheds = [comm.Schedule(comm.SOLO if i % 2 else comm.ALLREDUCE, None, None, 0, async_=2,
+                            buf=comm.BUF_NONE) for i in range(nsched)]
+    rng = random.Random(seed * 100 + rank)
+    for t in range(rounds):
+        order = list(range(nsched))
+        rng.shuffle(order)                 # ranks post the buckets in different orders
+        for i in order:
+            time.sleep(rng.random() * 0.003)
+            scheds[i].post()
+        for i in order:
+            scheds[i].wait()
+    comm.barrier()
+    log = comm.issue_log()
+    for s in scheds:
+        s.delete()
+    comm.set_transport("ipc")
+    comm.finalize()
+    return log

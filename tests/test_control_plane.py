@@ -82,3 +82,15 @@ def test_test_polling_equivalent_to_wait():
     for o in outs:
         assert [e["round"] for e in o["log"]] == list(range(1, 7))
         assert o["stats"]["completed"] == 6 and o["stats"]["waited"] == 6
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ordered_transport_same_issue_order_everywhere(world):
+    # RCCL matches operations by issue order: the ticket ring must give every rank the
+    # same (schedule, round) sequence even when ranks post buckets in different orders.
+    logs = run("cp_ordered", world, nsched=4, rounds=5)
+    assert len(logs[0]) == 4 * 5
+    assert all(l == logs[0] for l in logs), logs
+    for sid in range(4):   # rounds of one schedule appear in order
+        rs = [r for s, r in logs[0] if s == sid]
+        assert rs == sorted(rs) == list(range(1, 6))

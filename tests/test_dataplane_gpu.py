@@ -68,3 +68,14 @@ def test_solo_majority_round_tags(kind):
         for e in o["log"]:
             if e["fresh"] and r == 0:
                 assert digits(fast["results"][e["round"] - 1], r) == e["round"]
+
+
+@pytest.mark.parametrize("kind", [ALLREDUCE, SOLO])
+def test_rccl_transport_single_rank(kind):
+    # RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so on a 1-GPU box the
+    # RCCL transport can only run at world size 1: communicator bring-up, ticket ring,
+    # the full round protocol and the copy paths (host and device buckets).
+    for buf in ("device", "host"):
+        verdicts = run("gpu_allreduce", 1, count=300007, rounds=3, kind=kind, buf=buf,
+                       transport="rccl")
+        assert all(all(v) for v in verdicts), (buf, verdicts)
