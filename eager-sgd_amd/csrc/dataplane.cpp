@@ -142,7 +142,9 @@ static int base_note_producer(BaseState &st, uint32_t round, void *stream) {
     hipEvent_t e;
     if (!st.spare.empty()) { e = st.spare.back(); st.spare.pop_back(); }
     else ESGD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    ESGD_HIP(hipEventRecord(e, static_cast<hipStream_t>(stream)));
+    // ESGD_STREAM_NULL names the legacy default stream (records on stream 0)
+    hipStream_t ps = stream == ESGD_STREAM_NULL ? nullptr : static_cast<hipStream_t>(stream);
+    ESGD_HIP(hipEventRecord(e, ps));
     st.producer[round] = e;
     return ESGD_SUCCESS;
 }

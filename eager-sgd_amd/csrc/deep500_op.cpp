@@ -150,7 +150,9 @@ void allreducef_forward_cuda(void *handle, const float *input, const float *, fl
     if (hipMemcpyAsync(op->sb, input, nbytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
         die("allreducef_forward_cuda (copy in)");
     // the snapshot of this round waits for the copy just queued on the caller's stream
-    if (esgd_schedule_post(op->sched, s, nullptr) || esgd_schedule_wait(op->sched))
+    // (the data plane's streams are non-blocking: the NULL stream must be named)
+    if (esgd_schedule_post(op->sched, s ? static_cast<void *>(s) : ESGD_STREAM_NULL, nullptr) ||
+        esgd_schedule_wait(op->sched))
         die("allreducef_forward_cuda");
     if (hipMemcpyAsync(output, op->rb, nbytes, hipMemcpyDeviceToDevice, s) != hipSuccess ||
         hipMemsetAsync(op->sb, 0, nbytes, s) != hipSuccess)

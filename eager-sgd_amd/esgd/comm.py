@@ -158,8 +158,12 @@ class Schedule:
         self.handle = h.value
 
     def post(self, stream=None) -> int:
+        """stream: producer of sb (None = no producer; 0 = the legacy default stream,
+        e.g. torch's default stream, passed on as ESGD_STREAM_NULL)."""
         role = C.c_int()
         s = None if stream is None else (stream.handle if hasattr(stream, "handle") else int(stream))
+        if s == 0:
+            s = 1   # ESGD_STREAM_NULL
         check(lib().esgd_schedule_post(self.handle, s, C.byref(role)), "esgd_schedule_post")
         return role.value
 

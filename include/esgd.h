@@ -160,8 +160,11 @@ typedef struct {
 
 int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t count,
                          int dtype, int async, unsigned seed, esgd_sched_h *out);
-/* post: start round `posted+1`.  producer_stream (may be NULL): stream that writes sb;
- * the snapshot of a round this rank posted waits for the work queued on it so far.
+/* post: start round `posted+1`.  producer_stream: stream that writes sb; the snapshot of
+ * a round this rank posted waits for the work queued on it so far.  NULL = no producer;
+ * ESGD_STREAM_NULL = the legacy default (NULL) stream, e.g. torch's default stream. */
+#define ESGD_STREAM_NULL ((void *)1)
+/*
  * role (may be NULL): 1 activated the round, 0 passive, 2 synchronous round. */
 int esgd_schedule_post(esgd_sched_h h, void *producer_stream, int *role);
 int esgd_schedule_wait(esgd_sched_h h);
