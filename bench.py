@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--no-gate", action="store_true", help="skip the 8 x 256 MiB gate shape")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="N>1: skip the C5 size sweep and the C4 straggler case")
+    ap.add_argument("--transport", choices=["ipc", "rccl"], default=None,
+                    help="N>1 data plane (default: ESGD_TRANSPORT or ipc)")
     ap.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -122,18 +126,23 @@ def run_local(args, esgd, dev):
         dev.reduce(dt, ptrs, out, count, stream=s)
     s.synchronize()
 
-    # HIP event pair around every launch, on the launch stream: kernel time per launch
-    evs = [(dev.Event(), dev.Event()) for _ in range(args.steps)]
+    # HIP event pairs on the launch stream around every 4th launch of the timed region:
+    # the kernel's own duration, without the marker packets slowing every step
+    every = 4
+    evs = [(dev.Event(), dev.Event()) for _ in range(0, args.steps, every)]
     dev.device_synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        evs[i][0].record(s)
-        dev.reduce(dt, ptrs, out, count, stream=s)
-        evs[i][1].record(s)
+        if i % every == 0:
+            evs[i // every][0].record(s)
+            dev.reduce(dt, ptrs, out, count, stream=s)
+            evs[i // every][1].record(s)
+        else:
+            dev.reduce(dt, ptrs, out, count, stream=s)
     s.synchronize()
     dev.device_synchronize()
     wall = time.perf_counter() - t0
-    per_launch_ms = sum(a.elapsed_ms(b) for a, b in evs) / args.steps
+    per_launch_ms = sum(a.elapsed_ms(b) for a, b in evs) / len(evs)
 
     # parity spot-check outside the timed region: first 1 Mi elements vs the oracle
     parity = "skipped"
@@ -240,6 +249,96 @@ def gate_256(dev, dt, es, k, s, iters=20):
             "frac": round(algo / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+def _max_over_ranks(x: float) -> float:
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sweep_c5(comm, dev, world, dt, es, iters=10):
+    """C5: majority-allreduce of one bucket per rank, 64 KiB .. 1 GiB (every 4x), per
+    size the max-over-ranks mean round time of `iters` back-to-back rounds."""
+    out = []
+    for lg in range(16, 31, 2):
+        nbytes = 1 << lg
+        count = nbytes // es
+        buf = dev.DeviceBuffer(count, dt)
+        dev.fill_uniform(buf, SEED, comm.rank())
+        dev.synchronize()
+        sch = comm.Schedule(comm.MAJORITY, None, buf, count, dtype=dt, seed=6545343,
+                            buf=comm.BUF_DEVICE)
+        for _ in range(3):
+            sch.post(); sch.wait()
+        comm.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            sch.post(); sch.wait()
+        t = _max_over_ranks((time.perf_counter() - t0) / iters)
+        sch.delete()
+        buf.close()
+        t_min = 2 * nbytes / (world * XGMI_LINK_GBS * 1e9)
+        out.append({"bytes": nbytes, "us": round(t * 1e6, 1), "algbw_GBs": round(nbytes / t / 1e9, 2),
+                    "busbw_GBs": round(nbytes / t / 1e9 * 2 * (world - 1) / world, 2),
+                    "xgmi_frac": round(t_min / t, 4)})
+    return out
+
+
+def straggler_c4(comm, dev, rank, world, rounds=24):
+    """C4: majority-allreduce of the ResNet-50 fused gradient (25 559 081 fp32,
+    opt_esgd_solo_imagenet_imbalance.py:86-248 summed) with the last rank posting
+    0.2 x T late every round (T = median no-straggler round).  Inputs are 1.0 and
+    zeroed after use, so the result counts the contributors (evaluation/rsgd.c:87,100)."""
+    import ctypes as C
+    import statistics
+
+    import numpy as np
+
+    from esgd import _lib
+    from esgd._lib import check, lib
+    count = 25559081
+    ones = dev.DeviceBuffer(count)
+    ones.upload(np.ones(count, np.float32))
+    sb, rb = dev.DeviceBuffer(count), dev.DeviceBuffer(count)
+    sb.zero(); rb.zero()
+    st = dev.Stream()
+    dev.synchronize()
+    sch = comm.Schedule(comm.MAJORITY, sb, rb, count, dtype=_lib.FLOAT, seed=6545343,
+                        buf=comm.BUF_DEVICE)
+    cell = np.zeros(1, np.float32)
+
+    def one(delay):
+        if delay:
+            time.sleep(delay)
+        check(lib().esgd_memcpy_async(sb.ptr, ones.ptr, count * 4, 2, st.handle))
+        t0 = time.perf_counter()
+        sch.post(st)
+        sch.wait()
+        dt_ = time.perf_counter() - t0
+        check(lib().esgd_memcpy_async(cell.ctypes.data, rb.ptr, 4, 1, st.handle))
+        check(lib().esgd_memset_async(sb.ptr, 0, count * 4, st.handle))
+        st.synchronize()
+        return dt_, float(cell[0])
+
+    base = []
+    for _ in range(rounds // 2):
+        comm.barrier()
+        base.append(one(0.0)[0])
+    T = _max_over_ranks(statistics.median(base))
+    lat, contrib = [], []
+    for _ in range(rounds):
+        comm.barrier()
+        d, c = one(0.2 * T if rank == world - 1 else 0.0)
+        lat.append(d); contrib.append(c)
+    on_time = _max_over_ranks(statistics.median(lat) if rank != world - 1 else 0.0)
+    sch.delete()
+    return {"bucket_fp32": count, "T_no_straggler_ms": round(T * 1e3, 3),
+            "straggler_delay_ms": round(0.2 * T * 1e3, 3),
+            "on_time_ranks_median_ms": round(on_time * 1e3, 3),
+            "mean_contributors": round(float(np.mean(contrib)), 3), "world": world}
+
+
 def run_allreduce(args, rank, world):
     """N > 1: one persistent schedule per rank over a device-resident bucket (config C3:
     256 MiB fp32, solo-allreduce), in place, all ranks posting every step.  Timed
@@ -253,8 +352,11 @@ def run_allreduce(args, rank, world):
     from esgd import device as dev
     from oracle import ffref
 
+    os.environ.setdefault("ESGD_TIMEOUT_S", "120")   # a stuck peer fails the run, not hangs it
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comm.init(rank=rank, world=world)            # job id broadcast over gloo
+    if args.transport:
+        comm.set_transport(args.transport)
     dt = _lib.FLOAT if args.dtype == "fp32" else _lib.BF16
     es = _lib.dtype_size(dt)
     count = int(args.bucket_mib * MiB) // es
@@ -301,6 +403,16 @@ def run_allreduce(args, rank, world):
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         parity = "bitwise (head+tail slices, every rank)" if flag.item() else "MISMATCH"
     sched.delete()
+    rb.close()
+
+    extras = {}
+    if not args.no_extras:
+        for name, fn in (("sweep_c5_majority", lambda: sweep_c5(comm, dev, world, dt, es)),
+                         ("straggler_c4_majority", lambda: straggler_c4(comm, dev, rank, world))):
+            try:
+                extras[name] = fn()
+            except Exception as e:   # keep the headline line; report what failed
+                extras[name + "_error"] = repr(e)[:300]
     comm.finalize()
 
     S = count * es
@@ -319,7 +431,9 @@ def run_allreduce(args, rank, world):
         "config": {"workload": f"C3: {args.schedule}-allreduce of one {args.bucket_mib:g} MiB "
                                f"{args.dtype} bucket per GPU, in place",
                    "bucket_bytes": S, "parallelism": f"dp{world} (one rank per GPU)",
-                   "transport": "ipc pull (reduce-scatter tree kernel + all-gather) over xGMI"},
+                   "transport": ("rccl p2p send/recv + tree kernel on a side stream"
+                                 if (args.transport or os.environ.get("ESGD_TRANSPORT")) == "rccl"
+                                 else "ipc pull (reduce-scatter tree kernel + all-gather) over xGMI")},
         "algbw_GBs": round(algbw, 2), "busbw_GBs": round(busbw, 2),
         "xgmi_frac": round(t_min / t_step, 4),
         "roofline": {"bound": "xgmi", "achieved": round(link_in, 2),
@@ -329,6 +443,7 @@ def run_allreduce(args, rank, world):
                    "activations_rank0": stats["activations"]},
         "parity": parity,
     }
+    line.update(extras)
     dist.destroy_process_group()
     return line
 

@@ -59,6 +59,16 @@ bool round_is_sync(const Sched &s, uint32_t round) {
     }
 }
 
+static std::atomic<int> g_active{0};   // schedules with a round in flight
+
+// A process that exits without fffinalize / esgd_comm_finalize must not die in
+// std::thread's destructor: stop and join the progress thread at static destruction.
+static struct ProgressGuard {
+    ~ProgressGuard() {
+        if (g_running.exchange(false) && g_thread.joinable()) g_thread.join();
+    }
+} g_progress_guard;
+
 static void progress_main() {
     if (g_device >= 0) (void)hipSetDevice(g_device);
     unsigned polls = 0;
@@ -67,6 +77,8 @@ static void progress_main() {
         if (engine_progress_once()) { polls = 0; continue; }
         const uint32_t w = g_wake.load(std::memory_order_acquire);
         if (w != seen) { seen = w; polls = 0; continue; }
+        // a round in flight is latency-critical: spin / yield, never sleep
+        if (g_active.load(std::memory_order_relaxed) > 0 && polls > 1024) polls = 64;
         backoff(polls);
     }
 }
@@ -456,8 +468,12 @@ bool engine_progress_once() {
         snap = g_reg;
     }
     bool any = pump_tickets(snap);
-    for (Sched *s : snap)
+    int active = 0;
+    for (Sched *s : snap) {
         while (step(*s)) any = true;   // run a schedule until it has to wait
+        if (s->stage != ST_IDLE) ++active;
+    }
+    g_active.store(active, std::memory_order_relaxed);
     return any;
 }
 

@@ -170,10 +170,9 @@ __global__ __launch_bounds__(256) void k_tree_sum(InputSet in, void *out, uint64
 // L2 / Infinity Cache.  The descriptor's range check (num_records = bytes of the vector
 // body) turns the ragged last iteration into zero-fill loads and dropped stores, so the
 // loop has no per-element branch (cdna_hip_programming.md §5 item 4c).
-template <class Tr, int K, int U, int LAUX, int SAUX, bool SCALE>
-__global__ __launch_bounds__(256) void k_tree_sum_buf(InputSet in, void *out, uint32_t nvec,
-                                                       uint64_t count, float scale) {
-    constexpr int B = 256;
+template <class Tr, int K, int U, int LAUX, int SAUX, bool SCALE, int B = 256>
+__global__ __launch_bounds__(B) void k_tree_sum_buf(InputSet in, void *out, uint32_t nvec,
+                                                     uint64_t count, float scale) {
     const int bytes = int(nvec * 16u);
     __amdgpu_buffer_rsrc_t rs[K];
 #pragma unroll
@@ -322,9 +321,9 @@ static unsigned grid_for(uint64_t items_per_block_pass, uint64_t items, int bloc
 }
 
 template <typename KernelT>
-static int resident_blocks(KernelT kernel) {
+static int resident_blocks(KernelT kernel, int block = 256) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, 256, 0) != hipSuccess || nb <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, block, 0) != hipSuccess || nb <= 0)
         nb = 4;
     return nb < 8 ? nb : 8;
 }
@@ -339,12 +338,12 @@ static int launch_flat(const InputSet &in, void *out, uint64_t count, float scal
     return ESGD_SUCCESS;
 }
 
-template <class Tr, int K, int U, int LA, int SA, bool SCALE>
+template <class Tr, int K, int U, int LA, int SA, bool SCALE, int B = 256>
 static int launch_buf(const InputSet &in, void *out, uint64_t count, float scale, hipStream_t s) {
     const uint64_t nvec = count / Tr::E;
-    static const int per_cu = resident_blocks(k_tree_sum_buf<Tr, K, U, LA, SA, SCALE>);
-    unsigned grid = grid_for(uint64_t(256) * U, nvec ? nvec : 1, per_cu);
-    hipLaunchKernelGGL((k_tree_sum_buf<Tr, K, U, LA, SA, SCALE>), dim3(grid), dim3(256), 0, s, in,
+    static const int per_cu = resident_blocks(k_tree_sum_buf<Tr, K, U, LA, SA, SCALE, B>, B);
+    unsigned grid = grid_for(uint64_t(B) * U, nvec ? nvec : 1, per_cu);
+    hipLaunchKernelGGL((k_tree_sum_buf<Tr, K, U, LA, SA, SCALE, B>), dim3(grid), dim3(B), 0, s, in,
                        out, uint32_t(nvec), count, scale);
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;
@@ -384,6 +383,12 @@ static int dispatch_u(const InputSet &in, void *out, uint64_t count, float scale
             case ID: return launch_buf<Tr, K, 4, LA, SA, SCALE>(in, out, count, scale, s);
             ESGD_POLICIES(ESGD_CASE)
 #undef ESGD_CASE
+            // block-shape variants of the production policy (sweeps)
+            case 9: return launch_buf<Tr, K, 3, 2, 16, SCALE>(in, out, count, scale, s);
+            case 10: return launch_buf<Tr, K, 2, 2, 16, SCALE, 512>(in, out, count, scale, s);
+            case 11: return launch_buf<Tr, K, 4, 2, 16, SCALE, 512>(in, out, count, scale, s);
+            case 12: return launch_buf<Tr, K, 4, 2, 16, SCALE, 128>(in, out, count, scale, s);
+            case 13: return launch_buf<Tr, K, 2, 2, 16, SCALE, 1024>(in, out, count, scale, s);
             default: break;
             }
         }
@@ -542,7 +547,7 @@ int esgd_set_tuning(const char *key, int value) {
     } else if (!std::strcmp(key, "nt")) {
         g_nt = value ? 1 : 0;
     } else if (!std::strcmp(key, "policy")) {
-        ESGD_ARG(value >= -1 && value <= 8, "policy must be -1..8");
+        ESGD_ARG(value >= -1 && value <= 13, "policy must be -1..13");
         g_policy = value;
     } else {
         set_error("esgd_set_tuning: unknown key '%s'", key);

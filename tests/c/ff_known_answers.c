@@ -1,0 +1,77 @@
+/*
+ * A plain C caller of the fflib2 API (include/ff.h -> libesgd.so), written the way the
+ * reference's evaluation programs use fflib2, with their known answers:
+ *   - ffallreduce of to_reduce[j] = i + j gives (i + j) * size
+ *     (eager-SGD-modules/fflib2/evaluation/allreduce.c:49-63), fresh schedule per i;
+ *   - ffsolo_allreduce / ffrand_allreduce with every rank posting behind a barrier give
+ *     the plain allreduce of the running inputs
+ *     (evaluation/solo_allreduce_correctness.c:76-97, rand_allreduce_correctness.c:78-98).
+ * Ranks come from RANK / WORLD_SIZE / ESGD_JOB_ID (no MPI).  Exit status 0 = passed.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "ff.h"
+
+static int check_int(const int32_t *got, const int32_t *want, int n, const char *what, int it) {
+    for (int j = 0; j < n; ++j)
+        if (got[j] != want[j]) {
+            int rank;
+            ffrank(&rank);
+            fprintf(stderr, "[rank %d] %s iteration %d: element %d = %d, expected %d\n", rank, what, it,
+                    j, got[j], want[j]);
+            return 1;
+        }
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    const int count = argc > 1 ? atoi(argv[1]) : 10007;
+    const int iters = argc > 2 ? atoi(argv[2]) : 4;
+    if (ffinit(&argc, &argv) != FFSUCCESS) { fprintf(stderr, "ffinit: %s\n", esgd_last_error()); return 2; }
+    int rank, size, failed = 0;
+    ffrank(&rank);
+    ffsize(&size);
+    int32_t *to_reduce = calloc(count, sizeof(int32_t));
+    int32_t *reduced = calloc(count, sizeof(int32_t));
+    int32_t *want = calloc(count, sizeof(int32_t));
+
+    /* allreduce.c: a fresh schedule per iteration */
+    int16_t tag = 0;
+    for (int i = 0; i < iters && !failed; ++i) {
+        for (int j = 0; j < count; ++j) { to_reduce[j] = i + j; reduced[j] = 0; want[j] = (i + j) * size; }
+        ffschedule_h ar;
+        if (ffallreduce(to_reduce, reduced, count, tag++, FFSUM, FFINT32, 0, &ar) != FFSUCCESS) {
+            fprintf(stderr, "ffallreduce: %s\n", esgd_last_error());
+            return 2;
+        }
+        ffschedule_post(ar);
+        ffschedule_wait(ar);
+        failed |= check_int(reduced, want, count, "allreduce", i);
+        ffschedule_delete(ar);
+    }
+
+    /* solo / majority correctness: running inputs, every rank posts behind a barrier */
+    for (int kind = 0; kind < 2 && !failed; ++kind) {
+        for (int j = 0; j < count; ++j) to_reduce[j] = 0;
+        ffschedule_h s;
+        int rc = kind == 0 ? ffsolo_allreduce(to_reduce, reduced, count, 0, FFSUM, FFINT32, 0, 20, &s)
+                           : ffrand_allreduce(to_reduce, reduced, count, 0, FFSUM, FFINT32, 0, 34495645, 20, &s);
+        if (rc != FFSUCCESS) { fprintf(stderr, "schedule: %s\n", esgd_last_error()); return 2; }
+        ffschedule_start(s);
+        for (int i = 0; i < iters && !failed; ++i) {
+            for (int j = 0; j < count; ++j) { to_reduce[j]++; want[j] = to_reduce[j] * size; }
+            esgd_barrier();            /* MPI_Barrier in the reference test */
+            ffschedule_post(s);
+            ffschedule_wait(s);
+            esgd_barrier();
+            failed |= check_int(reduced, want, count, kind == 0 ? "solo" : "majority", i);
+        }
+        ffschedule_delete(s);
+    }
+    if (!failed && rank == 0) printf("Correctness check passed! (%d ranks)\n", size);
+    fffinalize();
+    free(to_reduce); free(reduced); free(want);
+    return failed;
+}

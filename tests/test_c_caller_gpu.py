@@ -1,0 +1,35 @@
+"""A C program that only includes ff.h and links libesgd.so (the drop-in boundary),
+run as P processes with launcher-style environment, checking the reference
+evaluation programs' known answers (see tests/c/ff_known_answers.c)."""
+import os
+import subprocess
+import uuid
+
+import pytest
+
+from conftest import LIB, ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def build(tmp_path):
+    exe = str(tmp_path / "ff_known_answers")
+    subprocess.check_call(["gcc", "-O2", "-std=c11", "-I" + os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "c", "ff_known_answers.c"), "-o", exe,
+                           LIB, "-Wl,-rpath," + os.path.dirname(LIB)])
+    return exe
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_c_caller_known_answers(tmp_path, world):
+    exe = build(tmp_path)
+    job = uuid.uuid4().hex
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
+                   ESGD_JOB_ID=job, ESGD_TIMEOUT_S="60")
+        procs.append(subprocess.Popen([exe, "10007", "4"], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate(timeout=180)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    assert "Correctness check passed" in outs[0]
