@@ -22,6 +22,14 @@ static const char *transport_name() {
     return (e && *e) ? e : "ipc";
 }
 
+namespace esgd {
+Transport *default_transport(bool control_only) {
+    const bool rccl = !std::strcmp(transport_name(), "rccl");
+    if (control_only) return null_transport(rccl);
+    return rccl ? rccl_transport() : ipc_transport();
+}
+}  // namespace esgd
+
 using namespace esgd;
 
 static Sched *handle_to_sched(esgd_sched_h h) {
@@ -77,7 +85,7 @@ int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t c
     ESGD_ARG(buf == ESGD_BUF_NONE || rb || count == 0, "esgd_schedule_create: null receive buffer");
     const bool rccl = !std::strcmp(transport_name(), "rccl");
     ESGD_ARG(rccl || !std::strcmp(transport_name(), "ipc"), "unknown transport '%s'", transport_name());
-    Transport *tp = buf == ESGD_BUF_NONE ? null_transport(rccl) : rccl ? rccl_transport() : ipc_transport();
+    Transport *tp = default_transport(buf == ESGD_BUF_NONE);
     Sched *s = nullptr;
     int rc = sched_create(kind, dtype, count, const_cast<void *>(sb), rb, buf == ESGD_BUF_HOST,
                           async, seed, tp, &s);

@@ -85,6 +85,8 @@ struct BaseState {
     hipStream_t stream = nullptr;
     hipEvent_t ev = nullptr;
     char *rb_dev = nullptr;
+    size_t cap = 0;                   // bytes of rb_dev (owned buckets may grow)
+    uint64_t laid_count = ~0ull;      // count the shard layout was computed for
     bool owns_rb = false, reg_sb = false, reg_rb = false;
     uint64_t off[kMaxRanks] = {}, len[kMaxRanks] = {};   // elements
     std::map<uint32_t, hipEvent_t> producer;
@@ -95,11 +97,13 @@ struct BaseState {
 struct IpcState : BaseState {
     char *peer[kMaxRanks] = {};
     void *peer_base[kMaxRanks] = {};
+    uint32_t peer_ver[kMaxRanks] = {};
 };
 
 // shard j = [off_j, off_j + len_j): equal shards rounded up to 1 KiB so every shard
 // (and the 16-B vectors the kernels move) starts aligned; the last one is ragged.
 static void layout(Sched &s, BaseState &st) {
+    st.laid_count = s.count;
     const uint64_t align = 1024 / s.esize;
     uint64_t per = (s.count + uint64_t(s.world) - 1) / uint64_t(s.world);
     per = (per + align - 1) / align * align;
@@ -117,12 +121,14 @@ static int base_setup(Sched &s, BaseState &st) {
     ESGD_HIP(hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking));
     ESGD_HIP(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
     if (s.host_mode) {
-        ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.rb_dev), bytes ? bytes : 256));
+        st.cap = bytes ? bytes : 256;
+        ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.rb_dev), st.cap));
         st.owns_rb = true;
         // pin the caller's persistent host buckets so the move / copy-out are DMA
-        if (bytes && s.rb && hipHostRegister(s.rb, bytes, hipHostRegisterDefault) == hipSuccess)
+        // (not for FFCOLL_BUFFERS: those move every round)
+        if (!s.resolve && bytes && s.rb && hipHostRegister(s.rb, bytes, hipHostRegisterDefault) == hipSuccess)
             st.reg_rb = true;
-        if (bytes && s.sb && s.sb != s.rb &&
+        if (!s.resolve && bytes && s.sb && s.sb != s.rb &&
             hipHostRegister(s.sb, bytes, hipHostRegisterDefault) == hipSuccess)
             st.reg_sb = true;
         (void)hipGetLastError();   // "already registered" is fine
@@ -147,6 +153,25 @@ static int base_note_producer(BaseState &st, uint32_t round, void *stream) {
     ESGD_HIP(hipEventRecord(e, ps));
     st.producer[round] = e;
     return ESGD_SUCCESS;
+}
+
+// FFCOLL_BUFFERS rounds may change the count: re-lay the shards and grow the owned
+// device bucket (ffallreduce_post resizes its temporaries the same way, :42-48).
+// Returns 1 when the device bucket moved (peers must re-map it).
+static int base_refit(Sched &s, BaseState &st) {
+    if (st.laid_count == s.count) return 0;
+    const size_t bytes = s.count * s.esize;
+    int moved = 0;
+    if (bytes > st.cap) {
+        if (!st.owns_rb) { set_error("schedule %d: device bucket cannot grow", s.id); return ESGD_INVALID_ARG; }
+        ESGD_HIP(hipStreamSynchronize(st.stream));
+        ESGD_HIP(hipFree(st.rb_dev));
+        st.cap = bytes;
+        ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.rb_dev), st.cap));
+        moved = 1;
+    }
+    layout(s, st);
+    return moved;
 }
 
 static int base_snapshot(Sched &s, BaseState &st, uint32_t round, bool fresh) {
@@ -200,25 +225,25 @@ struct IpcTransport final : Transport {
 
     static IpcState &S(Sched &s) { return *static_cast<IpcState *>(s.tstate); }
 
-    int setup(Sched &s) override {
-        auto *st = new IpcState();
-        s.tstate = st;
-        if (int rc = base_setup(s, *st)) return rc;
-        const size_t bytes = s.count * s.esize;
-        st->peer[s.rank] = st->rb_dev;
-        if (s.world == 1) return ESGD_SUCCESS;
-        // publish this rank's rb, then map every peer's
+    static int publish(Sched &s, IpcState &st) {
         void *base = nullptr;
         size_t size = 0;
-        ESGD_HIP(hipMemGetAddressRange(&base, &size, st->rb_dev));
+        ESGD_HIP(hipMemGetAddressRange(&base, &size, st.rb_dev));
         hipIpcMemHandle_t h;
         ESGD_HIP(hipIpcGetMemHandle(&h, base));
         IpcSlot &mine = s.sh->slot[s.rank];
         std::memcpy(mine.handle, &h, sizeof(h));
-        mine.offset = uint64_t(st->rb_dev - static_cast<char *>(base));
-        mine.bytes = bytes;
+        mine.offset = uint64_t(st.rb_dev - static_cast<char *>(base));
+        mine.bytes = s.count * s.esize;
         mine.gen.store(s.gen, std::memory_order_release);
-        if (int rc = engine_barrier()) return rc;
+        mine.ver.fetch_add(1, std::memory_order_acq_rel);
+        st.peer[s.rank] = st.rb_dev;
+        return ESGD_SUCCESS;
+    }
+
+    // (re)map every peer whose publication changed since we last mapped it
+    static int map_peers(Sched &s, IpcState &st) {
+        const size_t bytes = s.count * s.esize;
         for (int q = 0; q < s.world; ++q) {
             if (q == s.rank) continue;
             IpcSlot &ps = s.sh->slot[q];
@@ -226,17 +251,33 @@ struct IpcTransport final : Transport {
                 set_error("schedule %d: rank %d did not publish its buffer", s.id, q);
                 return ESGD_ERROR;
             }
+            const uint32_t v = ps.ver.load(std::memory_order_acquire);
+            if (st.peer_base[q] && v == st.peer_ver[q]) continue;
             if (ps.bytes != bytes) {
                 set_error("schedule %d: rank %d has %llu bytes, this rank %zu", s.id, q,
                           (unsigned long long)ps.bytes, bytes);
                 return ESGD_INVALID_ARG;
             }
+            if (st.peer_base[q]) { ipc_close(st.peer_base[q]); st.peer_base[q] = nullptr; }
             void *pb = nullptr;
             if (int rc = ipc_open(q, ps.handle, &pb)) return rc;
-            st->peer_base[q] = pb;
-            st->peer[q] = static_cast<char *>(pb) + ps.offset;
+            st.peer_base[q] = pb;
+            st.peer[q] = static_cast<char *>(pb) + ps.offset;
+            st.peer_ver[q] = v;
         }
         return ESGD_SUCCESS;
+    }
+
+    int setup(Sched &s) override {
+        auto *st = new IpcState();
+        s.tstate = st;
+        if (int rc = base_setup(s, *st)) return rc;
+        st->peer[s.rank] = st->rb_dev;
+        if (s.world == 1) return ESGD_SUCCESS;
+        // publish this rank's rb, then map every peer's
+        if (int rc = publish(s, *st)) return rc;
+        if (int rc = engine_barrier()) return rc;
+        return map_peers(s, *st);
     }
 
     int note_producer(Sched &s, uint32_t round, void *stream) override {
@@ -244,11 +285,20 @@ struct IpcTransport final : Transport {
     }
 
     int snapshot(Sched &s, uint32_t round, bool fresh) override {
-        return base_snapshot(s, S(s), round, fresh);
+        IpcState &st = S(s);
+        const int moved = base_refit(s, st);
+        if (moved < 0) return moved;
+        // size changes (even in place) are re-published before "ready": peers re-map in RS
+        if (s.world > 1 && (moved || s.resolve))
+            if (int rc = publish(s, st)) return rc;
+        st.peer[s.rank] = st.rb_dev;
+        return base_snapshot(s, st, round, fresh);
     }
 
     int reduce_scatter(Sched &s) override {
         IpcState &st = S(s);
+        if (s.world > 1 && s.resolve)
+            if (int rc = map_peers(s, st)) return rc;
         const uint64_t n = st.len[s.rank];
         if (s.world > 1 && n) {
             const void *in[kMaxRanks];
@@ -418,7 +468,19 @@ struct RcclTransport final : Transport {
     }
 
     int snapshot(Sched &s, uint32_t round, bool fresh) override {
-        return base_snapshot(s, S(s), round, fresh);
+        RcclState &st = S(s);
+        const int moved = base_refit(s, st);
+        if (moved < 0) return moved;
+        if (st.laid_count == s.count && st.L != st.len[0]) {   // new layout: resize staging
+            if (st.stage) { ESGD_HIP(hipFree(st.stage)); st.stage = nullptr; }
+            st.L = st.len[0];
+            if (s.world > 1 && st.L)
+                ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.stage), size_t(s.world) * st.L * s.esize));
+            const uint64_t align = 1024 / s.esize, minc = (1u << 20) / s.esize;
+            uint64_t c = std::max<uint64_t>(minc, (st.L + 7) / 8);
+            st.chunk = (c + align - 1) / align * align;
+        }
+        return base_snapshot(s, st, round, fresh);
     }
 
     static uint64_t piece(uint64_t len, uint64_t c, uint64_t chunk) {

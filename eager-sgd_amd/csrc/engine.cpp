@@ -106,6 +106,11 @@ int engine_init(const char *job, int rank, int world, bool start_progress) {
     return ESGD_SUCCESS;
 }
 
+static void free_sched(Sched *s) {
+    if (s->resolve_free && s->resolve_ctx) s->resolve_free(s->resolve_ctx);
+    delete s;
+}
+
 int engine_finalize() {
     if (!g_seg) return ESGD_SUCCESS;
     int rc = shm_barrier(g_seg, g_world, g_timeout);
@@ -117,7 +122,7 @@ int engine_finalize() {
     }
     for (Sched *s : left) {
         if (s->tp) s->tp->teardown(*s);
-        delete s;
+        free_sched(s);
     }
     shm_detach(g_seg, nullptr, -1);
     g_seg = nullptr;
@@ -140,6 +145,13 @@ static void fail_locked(Sched &s, int rc, const char *msg) {
 
 int sched_create(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
                  int async, unsigned seed, Transport *tp, Sched **out) {
+    return sched_create_with(kind, dtype, count, sb, rb, host_mode, async, seed, tp, nullptr,
+                             nullptr, nullptr, out);
+}
+
+int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
+                      int async, unsigned seed, Transport *tp, int (*resolve)(Sched &),
+                      void *ctx, void (*ctx_free)(void *), Sched **out) {
     ESGD_ARG(out, "schedule create: null output");
     ESGD_ARG(kind >= KIND_ALLREDUCE && kind <= KIND_MAJORITY, "schedule create: bad kind %d", kind);
     ESGD_ARG(tp, "schedule create: no transport");
@@ -154,6 +166,9 @@ int sched_create(int kind, int dtype, uint64_t count, void *sb, void *rb, bool h
     s->rank = g_rank; s->world = g_world;
     s->sh = &g_seg->sched[s->id];
     s->tp = tp;
+    s->resolve = resolve;
+    s->resolve_ctx = ctx;
+    s->resolve_free = ctx_free;
     int rc = shm_barrier(g_seg, g_world, g_timeout);
     if (!rc && g_rank == 0) {
         SchedShm *sh = s->sh;
@@ -178,7 +193,11 @@ int sched_create(int kind, int dtype, uint64_t count, void *sb, void *rb, bool h
     if (!rc) rc = tp->setup(*s);   // collective registration (has its own barriers)
     int rc2 = shm_barrier(g_seg, g_world, g_timeout);
     if (!rc) rc = rc2;
-    if (rc) { delete s; return rc; }
+    if (rc) {
+        s->resolve_free = nullptr;   // the caller still owns ctx on failure
+        delete s;
+        return rc;
+    }
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         g_reg.push_back(s);
@@ -219,6 +238,14 @@ int sched_post(Sched *s, void *producer_stream, int *role) {
         std::lock_guard<std::mutex> lk(s->mu);
         if (s->error) { set_error("%s", s->errmsg); return s->error; }
         const uint32_t t = s->posted.load() + 1;
+        if (s->resolve) {
+            // the round about to start must not be in flight with the old buffers
+            if (s->stage != ST_IDLE || s->joined != s->posted.load()) {
+                set_error("schedule %d: FFCOLL_BUFFERS rounds must not overlap", s->id);
+                return ESGD_INVALID_ARG;
+            }
+            if (int rc = s->resolve(*s)) return rc;
+        }
         if (producer_stream)
             if (int rc = s->tp->note_producer(*s, t, producer_stream)) return rc;
         s->posted.store(t, std::memory_order_release);
@@ -293,7 +320,7 @@ int sched_delete(Sched *s) {
     int rc = shm_barrier(g_seg, g_world, g_timeout);
     s->tp->teardown(*s);
     int rc2 = shm_barrier(g_seg, g_world, g_timeout);
-    delete s;
+    free_sched(s);
     return rc ? rc : rc2;
 }
 

@@ -85,6 +85,11 @@ struct Sched {
     // caller buffers (captured at creation, like colls/ffallreduce.c:113-115)
     void *sb = nullptr, *rb = nullptr;
     bool host_mode = false, in_place = false;
+    // FFCOLL_BUFFERS: buffers are re-resolved at every post (colls/ffallreduce.c:20-52
+    // checks type / size and grows the temporaries); returns an esgd status
+    int (*resolve)(Sched &s) = nullptr;
+    void *resolve_ctx = nullptr;
+    void (*resolve_free)(void *ctx) = nullptr;
 
     std::mutex mu;
     std::condition_variable cv;
@@ -118,6 +123,12 @@ double engine_timeout();
 // Schedules (collective create/delete, same order on every rank).
 int sched_create(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
                  int async, unsigned seed, Transport *tp, Sched **out);
+// same, with buffers re-resolved at every post (FFCOLL_BUFFERS); ctx freed by ctx_free
+int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
+                      int async, unsigned seed, Transport *tp, int (*resolve)(Sched &),
+                      void *ctx, void (*ctx_free)(void *), Sched **out);
+// transport chosen by esgd_set_transport / ESGD_TRANSPORT (comm_api.cpp)
+Transport *default_transport(bool control_only);
 int sched_post(Sched *s, void *producer_stream, int *role);
 int sched_wait(Sched *s);
 int sched_test(Sched *s, int *flag);

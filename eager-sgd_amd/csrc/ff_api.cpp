@@ -26,20 +26,67 @@ static int env_int(std::initializer_list<const char *> names, int dflt) {
 
 static bool g_ff_owns_comm = false;
 
+// ---- ffbuffer descriptors (src/ffbuffer.c:10-95 restated) ----
+struct FFBuf {
+    void *ptr = nullptr;
+    uint32_t count = 0;
+    int dtype = -1;
+    bool selfalloc = false;
+};
+
+struct CollBuffers {      // FFCOLL_BUFFERS state of one schedule
+    FFBuf *sb = nullptr;  // nullptr: in place
+    FFBuf *rb = nullptr;
+    int dtype = 0;
+};
+
+static int resolve_coll_buffers(Sched &s) {
+    auto *cb = static_cast<CollBuffers *>(s.resolve_ctx);
+    FFBuf *rb = cb->rb, *sb = cb->sb;
+    // colls/ffallreduce.c:32-40: datatype and size must agree
+    if (rb->dtype != cb->dtype || (sb && (sb->dtype != rb->dtype || sb->count != rb->count))) {
+        set_error("FFCOLL_BUFFERS: datatype / size mismatch between send, receive and schedule");
+        return ESGD_INVALID_ARG;
+    }
+    s.rb = rb->ptr;
+    s.sb = sb ? sb->ptr : nullptr;
+    s.in_place = (sb == nullptr || sb->ptr == rb->ptr);
+    s.count = rb->count;
+    return ESGD_SUCCESS;
+}
+
 static int make_schedule(int kind, void *sndbuff, void *rcvbuff, int count, ffoperator_h op,
                          ffdatatype_h dt, int options, int async, unsigned seed, ffschedule_h *sched) {
     ESGD_ARG(sched, "fflib: null schedule output");
     ESGD_ARG(count >= 0, "fflib: negative count");
     ESGD_ARG(op == FFSUM, "fflib: only FFSUM is reduced by libesgd (operator %d)", op);
-    ESGD_ARG(!(options & FFCOLL_BUFFERS), "fflib: FFCOLL_BUFFERS (ffbuffer_h) is not supported");
+    const bool coll_buffers = (options & FFCOLL_BUFFERS) != 0;
+    ESGD_ARG(!(coll_buffers && (options & ESGD_FF_DEVICE_BUFFERS)),
+             "fflib: FFCOLL_BUFFERS buckets are host buffers");
     ESGD_ARG(dt == FFINT32 || dt == FFINT64 || dt == FFDOUBLE || dt == FFFLOAT || dt == ESGD_FFBF16,
              "fflib: unsupported datatype %d", dt);
     if (!engine_ready()) {
         if (int rc = ffinit(nullptr, nullptr)) return rc;
     }
     const int buf = (options & ESGD_FF_DEVICE_BUFFERS) ? ESGD_BUF_DEVICE : ESGD_BUF_HOST;
-    void *sb = sndbuff == FFINPLACE ? nullptr : sndbuff;
     esgd_sched_h h = 0;
+    if (coll_buffers) {
+        // colls/ffallreduce.c:104-110: the arguments point at ffbuffer_h handles
+        ESGD_ARG(rcvbuff, "fflib: null receive buffer handle");
+        auto *cb = new CollBuffers();
+        cb->rb = reinterpret_cast<FFBuf *>(*static_cast<ffbuffer_h *>(rcvbuff));
+        cb->sb = sndbuff == FFINPLACE ? nullptr : reinterpret_cast<FFBuf *>(*static_cast<ffbuffer_h *>(sndbuff));
+        cb->dtype = dt;
+        Sched *s = nullptr;
+        int rc = sched_create_with(kind, dt, uint64_t(cb->rb->count), cb->sb ? cb->sb->ptr : nullptr,
+                                   cb->rb->ptr, true, async, seed, default_transport(false),
+                                   resolve_coll_buffers, cb,
+                                   [](void *p) { delete static_cast<CollBuffers *>(p); }, &s);
+        if (rc) { delete cb; return rc; }
+        *sched = reinterpret_cast<ffschedule_h>(s);
+        return FFSUCCESS;
+    }
+    void *sb = sndbuff == FFINPLACE ? nullptr : sndbuff;
     int rc = esgd_schedule_create(kind, buf, sb, rcvbuff, uint64_t(count), dt, async, seed, &h);
     if (rc) return rc;
     *sched = h;
@@ -47,6 +94,63 @@ static int make_schedule(int kind, void *sndbuff, void *rcvbuff, int count, ffop
 }
 
 extern "C" {
+
+int ffbuffer_create(void *addr, uint32_t count, ffdatatype_h datatype, int, ffbuffer_h *out) {
+    ESGD_ARG(out, "ffbuffer_create: null output");
+    auto *b = new FFBuf();
+    b->selfalloc = addr == nullptr;
+    if (int rc = ffbuffer_resize(reinterpret_cast<ffbuffer_h>(b), addr, count, datatype)) {
+        delete b;
+        return rc;
+    }
+    *out = reinterpret_cast<ffbuffer_h>(b);
+    return FFSUCCESS;
+}
+
+int ffbuffer_resize(ffbuffer_h h, void *addr, uint32_t new_count, ffdatatype_h dt) {
+    auto *b = reinterpret_cast<FFBuf *>(h);
+    ESGD_ARG(b, "ffbuffer_resize: null handle");
+    const size_t es = esgd_dtype_size(dt), old = b->dtype >= 0 ? esgd_dtype_size(b->dtype) : 0;
+    ESGD_ARG(es > 0, "ffbuffer_resize: unsupported datatype %d", dt);
+    if (!addr) {   // library-owned: grow with realloc (src/ffbuffer.c:79-84)
+        if (!b->ptr || size_t(new_count) * es > size_t(b->count) * old) {
+            void *p = realloc(b->selfalloc ? b->ptr : nullptr, size_t(new_count) * es);
+            if (!p) return FFENOMEM;
+            b->ptr = p;
+            b->selfalloc = true;
+        }
+    } else {
+        if (b->selfalloc) free(b->ptr);
+        b->ptr = addr;
+        b->selfalloc = false;
+    }
+    b->count = new_count;
+    b->dtype = dt;
+    return FFSUCCESS;
+}
+
+int ffbuffer_delete(ffbuffer_h h) {
+    auto *b = reinterpret_cast<FFBuf *>(h);
+    ESGD_ARG(b, "ffbuffer_delete: null handle");
+    if (b->selfalloc) free(b->ptr);
+    delete b;
+    return FFSUCCESS;
+}
+
+int ffbuffer_get_size(ffbuffer_h h, uint32_t *count, ffdatatype_h *datatype) {
+    auto *b = reinterpret_cast<FFBuf *>(h);
+    ESGD_ARG(b && count && datatype, "ffbuffer_get_size: null argument");
+    *count = b->count;
+    *datatype = b->dtype;
+    return FFSUCCESS;
+}
+
+int ffbuffer_get_data(ffbuffer_h h, void **mem) {
+    auto *b = reinterpret_cast<FFBuf *>(h);
+    ESGD_ARG(b && mem, "ffbuffer_get_data: null argument");
+    *mem = b->ptr;
+    return FFSUCCESS;
+}
 
 int ffinit(int *, char ***) {
     if (engine_ready()) return FFSUCCESS;   // already joined (esgd_comm_init / earlier ffinit)

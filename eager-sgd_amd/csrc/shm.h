@@ -26,6 +26,7 @@ struct alignas(64) IpcSlot {
     uint64_t offset;
     uint64_t bytes;
     std::atomic<uint32_t> gen;    // == schedule generation when valid
+    std::atomic<uint32_t> ver;    // bumped at every (re)publication (buffers that grow)
 };
 
 struct alignas(64) SchedShm {

@@ -12,7 +12,7 @@
  *     TORCHELASTIC_RUN_ID + MASTER_PORT);
  *   - operator FFSUM only (the reference's generic comp also has FFIDENTITY, used
  *     internally for the move) ; datatypes FFINT32/FFINT64/FFDOUBLE/FFFLOAT + ESGD_FFBF16;
- *   - FFCOLL_BUFFERS (ffbuffer_h arguments) is not supported;
+ *   - FFCOLL_BUFFERS takes host ffbuffer_h buckets (no FFBUFFER_IDX buffers);
  *   - extension option ESGD_FF_DEVICE_BUFFERS: sndbuff/rcvbuff are device pointers.
  */
 #ifndef ESGD_FF_H
@@ -58,6 +58,18 @@ extern "C" {
 typedef int ffdatatype_h;
 typedef int ffoperator_h;
 typedef uint64_t ffschedule_h;
+typedef uint64_t ffbuffer_h;
+
+/* buffer descriptors (src/ffbuffer.c:10-95): addr NULL = library-allocated (grows on
+ * resize like the reference's realloc).  With FFCOLL_BUFFERS a collective takes
+ * pointers to ffbuffer_h and re-reads address and count at every post, so buckets may
+ * move and change size between rounds (evaluation/allreduce_buffers_*.c); every rank
+ * must use the same count in a round. */
+int ffbuffer_create(void *addr, uint32_t count, ffdatatype_h datatype, int options, ffbuffer_h *buf);
+int ffbuffer_delete(ffbuffer_h buf);
+int ffbuffer_resize(ffbuffer_h buf, void *addr, uint32_t new_count, ffdatatype_h new_datatype);
+int ffbuffer_get_size(ffbuffer_h buf, uint32_t *count, ffdatatype_h *datatype);
+int ffbuffer_get_data(ffbuffer_h buf, void **mem);
 
 int ffinit(int *argc, char ***argv);   /* src/ff.c:23-86 (MPI_Init + progress thread) */
 int fffinalize(void);                  /* src/ff.c:88- */

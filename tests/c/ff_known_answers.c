@@ -5,7 +5,10 @@
  *     (eager-SGD-modules/fflib2/evaluation/allreduce.c:49-63), fresh schedule per i;
  *   - ffsolo_allreduce / ffrand_allreduce with every rank posting behind a barrier give
  *     the plain allreduce of the running inputs
- *     (evaluation/solo_allreduce_correctness.c:76-97, rand_allreduce_correctness.c:78-98).
+ *     (evaluation/solo_allreduce_correctness.c:76-97, rand_allreduce_correctness.c:78-98);
+ *   - FFCOLL_BUFFERS: one schedule, buckets that move and change size every round, one
+ *     user-managed and one library-managed (evaluation/allreduce_buffers_user_managed.c,
+ *     allreduce_buffers_fflib_managed.c), same (i + j) * size answer.
  * Ranks come from RANK / WORLD_SIZE / ESGD_JOB_ID (no MPI).  Exit status 0 = passed.
  */
 #include <stdint.h>
@@ -69,6 +72,39 @@ int main(int argc, char **argv) {
             failed |= check_int(reduced, want, count, kind == 0 ? "solo" : "majority", i);
         }
         ffschedule_delete(s);
+    }
+    /* FFCOLL_BUFFERS: relocating / resizing buckets under one persistent schedule */
+    if (!failed) {
+        const int initial = 1000, max_count = 3 * count;
+        int32_t *sbuf = calloc(initial, sizeof(int32_t));
+        ffbuffer_h sbh, rbh;
+        ffbuffer_create(sbuf, initial, FFINT32, 0, &sbh);     /* user managed */
+        ffbuffer_create(NULL, initial, FFINT32, 0, &rbh);     /* library managed */
+        ffschedule_h s;
+        if (ffallreduce(&sbh, &rbh, initial, 0, FFSUM, FFINT32, FFCOLL_BUFFERS, &s) != FFSUCCESS) {
+            fprintf(stderr, "ffallreduce(FFCOLL_BUFFERS): %s\n", esgd_last_error());
+            return 2;
+        }
+        srand(439634);                  /* same sizes on every rank (the reference's SEED) */
+        for (int i = 0; i < iters + 2 && !failed; ++i) {
+            const int c = (rand() % max_count) + 1;
+            free(sbuf);
+            sbuf = malloc(sizeof(int32_t) * c);
+            ffbuffer_resize(sbh, sbuf, c, FFINT32);
+            ffbuffer_resize(rbh, NULL, c, FFINT32);
+            int32_t *rbuf;
+            ffbuffer_get_data(rbh, (void **)&rbuf);
+            int32_t *w = malloc(sizeof(int32_t) * c);
+            for (int j = 0; j < c; ++j) { sbuf[j] = i + j; rbuf[j] = 0; w[j] = (i + j) * size; }
+            ffschedule_post(s);
+            ffschedule_wait(s);
+            failed |= check_int(rbuf, w, c, "FFCOLL_BUFFERS", i);
+            free(w);
+        }
+        ffschedule_delete(s);
+        ffbuffer_delete(sbh);
+        ffbuffer_delete(rbh);
+        free(sbuf);
     }
     if (!failed && rank == 0) printf("Correctness check passed! (%d ranks)\n", size);
     fffinalize();
