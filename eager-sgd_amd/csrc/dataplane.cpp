@@ -88,6 +88,12 @@ struct BaseState {
     size_t cap = 0;                   // bytes of rb_dev (owned buckets may grow)
     uint64_t laid_count = ~0ull;      // count the shard layout was computed for
     bool owns_rb = false, reg_sb = false, reg_rb = false;
+    // host buckets that could not be pinned (FFCOLL_BUFFERS move every round) go
+    // through this pinned staging buffer: host memcpy + DMA, never an async copy into
+    // pageable memory whose completion an event would not cover
+    char *pin = nullptr;
+    size_t pin_cap = 0;
+    bool copyout_pending = false;
     uint64_t off[kMaxRanks] = {}, len[kMaxRanks] = {};   // elements
     std::map<uint32_t, hipEvent_t> producer;
     std::vector<hipEvent_t> spare;
@@ -174,6 +180,19 @@ static int base_refit(Sched &s, BaseState &st) {
     return moved;
 }
 
+static bool staged(Sched &s, BaseState &st) {
+    return s.host_mode && (s.resolve || !st.reg_rb || (s.sb && s.sb != s.rb && !st.reg_sb));
+}
+
+static int ensure_pin(BaseState &st, size_t bytes) {
+    if (bytes <= st.pin_cap) return ESGD_SUCCESS;
+    if (st.pin) ESGD_HIP(hipHostFree(st.pin));
+    st.pin = nullptr;
+    ESGD_HIP(hipHostMalloc(reinterpret_cast<void **>(&st.pin), bytes, hipHostMallocDefault));
+    st.pin_cap = bytes;
+    return ESGD_SUCCESS;
+}
+
 static int base_snapshot(Sched &s, BaseState &st, uint32_t round, bool fresh) {
     // gradient producer of this round (posted before the join) must have finished
     for (auto it = st.producer.begin(); it != st.producer.end();) {
@@ -185,6 +204,12 @@ static int base_snapshot(Sched &s, BaseState &st, uint32_t round, bool fresh) {
     if (bytes) {
         if (s.host_mode) {   // the move of ffallreduce.c:126-130, host -> HBM
             const void *src = s.sb ? s.sb : s.rb;
+            if (staged(s, st)) {
+                if (int rc = ensure_pin(st, bytes)) return rc;
+                ESGD_HIP(hipStreamSynchronize(st.stream));   // pin is free again
+                std::memcpy(st.pin, src, bytes);
+                src = st.pin;
+            }
             ESGD_HIP(hipMemcpyAsync(st.rb_dev, src, bytes, hipMemcpyHostToDevice, st.stream));
         } else if (!s.in_place) {
             ESGD_HIP(hipMemcpyAsync(st.rb_dev, s.sb, bytes, hipMemcpyDeviceToDevice, st.stream));
@@ -196,9 +221,24 @@ static int base_snapshot(Sched &s, BaseState &st, uint32_t round, bool fresh) {
 
 static int base_finish(Sched &s, BaseState &st) {
     const size_t bytes = s.count * s.esize;
-    if (s.host_mode && bytes)
-        ESGD_HIP(hipMemcpyAsync(s.rb, st.rb_dev, bytes, hipMemcpyDeviceToHost, st.stream));
+    if (s.host_mode && bytes) {
+        if (staged(s, st)) {
+            if (int rc = ensure_pin(st, bytes)) return rc;
+            ESGD_HIP(hipMemcpyAsync(st.pin, st.rb_dev, bytes, hipMemcpyDeviceToHost, st.stream));
+            st.copyout_pending = true;
+        } else {
+            ESGD_HIP(hipMemcpyAsync(s.rb, st.rb_dev, bytes, hipMemcpyDeviceToHost, st.stream));
+        }
+    }
     ESGD_HIP(hipEventRecord(st.ev, st.stream));
+    return ESGD_SUCCESS;
+}
+
+static int base_complete(Sched &s, BaseState &st) {
+    if (st.copyout_pending) {
+        std::memcpy(s.rb, st.pin, s.count * s.esize);
+        st.copyout_pending = false;
+    }
     return ESGD_SUCCESS;
 }
 
@@ -216,6 +256,7 @@ static void base_teardown(Sched &s, BaseState &st) {
     if (st.reg_sb) (void)hipHostUnregister(s.sb);
     for (auto &kv : st.producer) (void)hipEventDestroy(kv.second);
     for (hipEvent_t e : st.spare) (void)hipEventDestroy(e);
+    if (st.pin) (void)hipHostFree(st.pin);
     if (st.ev) (void)hipEventDestroy(st.ev);
     if (st.stream) (void)hipStreamDestroy(st.stream);
 }
@@ -224,6 +265,11 @@ struct IpcTransport final : Transport {
     const char *name() const override { return "ipc"; }
 
     static IpcState &S(Sched &s) { return *static_cast<IpcState *>(s.tstate); }
+
+    // size of this round's bucket, read by peers' size check (no re-map needed)
+    static void publish_size(Sched &s) {
+        s.sh->slot[s.rank].bytes = s.count * s.esize;
+    }
 
     static int publish(Sched &s, IpcState &st) {
         void *base = nullptr;
@@ -252,12 +298,12 @@ struct IpcTransport final : Transport {
                 return ESGD_ERROR;
             }
             const uint32_t v = ps.ver.load(std::memory_order_acquire);
-            if (st.peer_base[q] && v == st.peer_ver[q]) continue;
             if (ps.bytes != bytes) {
                 set_error("schedule %d: rank %d has %llu bytes, this rank %zu", s.id, q,
                           (unsigned long long)ps.bytes, bytes);
                 return ESGD_INVALID_ARG;
             }
+            if (st.peer_base[q] && v == st.peer_ver[q]) continue;   // same allocation
             if (st.peer_base[q]) { ipc_close(st.peer_base[q]); st.peer_base[q] = nullptr; }
             void *pb = nullptr;
             if (int rc = ipc_open(q, ps.handle, &pb)) return rc;
@@ -288,9 +334,11 @@ struct IpcTransport final : Transport {
         IpcState &st = S(s);
         const int moved = base_refit(s, st);
         if (moved < 0) return moved;
-        // size changes (even in place) are re-published before "ready": peers re-map in RS
-        if (s.world > 1 && (moved || s.resolve))
+        // a moved bucket is re-published before "ready" (peers re-map it in RS); a size
+        // change alone only updates the published size
+        if (s.world > 1 && moved)
             if (int rc = publish(s, st)) return rc;
+        if (s.world > 1 && s.resolve) publish_size(s);
         st.peer[s.rank] = st.rb_dev;
         return base_snapshot(s, st, round, fresh);
     }
@@ -334,6 +382,8 @@ struct IpcTransport final : Transport {
     int finish(Sched &s) override { return base_finish(s, S(s)); }
 
     int query(Sched &s) override { return base_query(S(s)); }
+
+    int complete(Sched &s) override { return base_complete(s, S(s)); }
 
     void teardown(Sched &s) override {
         IpcState *st = static_cast<IpcState *>(s.tstate);
@@ -549,6 +599,7 @@ struct RcclTransport final : Transport {
 
     int finish(Sched &s) override { return base_finish(s, S(s)); }
     int query(Sched &s) override { return base_query(S(s)); }
+    int complete(Sched &s) override { return base_complete(s, S(s)); }
 
     void teardown(Sched &s) override {
         RcclState *st = static_cast<RcclState *>(s.tstate);

@@ -437,6 +437,7 @@ static bool step(Sched &s) {
         int q = s.tp->query(s);
         if (!check(q, "copy-out")) return true;
         if (!q) return false;
+        if (!check(s.tp->complete(s), "copy-out")) return true;
         s.completed = s.cur;
         s.stage = ST_IDLE;
         s.cv.notify_all();

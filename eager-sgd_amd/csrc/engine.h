@@ -26,6 +26,7 @@
 #include <mutex>
 #include <vector>
 
+#include "esgd.h"
 #include "shm.h"
 
 namespace esgd {
@@ -61,6 +62,8 @@ struct Transport {
     virtual int all_gather(Sched &s) = 0;
     virtual int finish(Sched &s) = 0;
     virtual int query(Sched &s) = 0;
+    // host-side work once the copy-out has landed (before wait() returns)
+    virtual int complete(Sched &) { return ESGD_SUCCESS; }
     virtual void teardown(Sched &s) = 0;
 };
 
