@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -104,6 +106,7 @@ struct IpcState : BaseState {
     char *peer[kMaxRanks] = {};
     void *peer_base[kMaxRanks] = {};
     uint32_t peer_ver[kMaxRanks] = {};
+    uint8_t peer_handle[kMaxRanks][64] = {};
 };
 
 // shard j = [off_j, off_j + len_j): equal shards rounded up to 1 KiB so every shard
@@ -179,6 +182,15 @@ static int base_refit(Sched &s, BaseState &st) {
     layout(s, st);
     return moved;
 }
+
+static bool debug_on() {
+    static const bool on = getenv("ESGD_DEBUG") && *getenv("ESGD_DEBUG") == '1';
+    return on;
+}
+#define ESGD_TRACE(...)                                                   \
+    do {                                                                  \
+        if (debug_on()) { fprintf(stderr, "[esgd] " __VA_ARGS__); fflush(stderr); } \
+    } while (0)
 
 static bool staged(Sched &s, BaseState &st) {
     return s.host_mode && (s.resolve || !st.reg_rb || (s.sb && s.sb != s.rb && !st.reg_sb));
@@ -303,12 +315,18 @@ struct IpcTransport final : Transport {
                           (unsigned long long)ps.bytes, bytes);
                 return ESGD_INVALID_ARG;
             }
-            if (st.peer_base[q] && v == st.peer_ver[q]) continue;   // same allocation
-            if (st.peer_base[q]) { ipc_close(st.peer_base[q]); st.peer_base[q] = nullptr; }
-            void *pb = nullptr;
-            if (int rc = ipc_open(q, ps.handle, &pb)) return rc;
-            st.peer_base[q] = pb;
-            st.peer[q] = static_cast<char *>(pb) + ps.offset;
+            if (st.peer_base[q] && v == st.peer_ver[q]) continue;   // nothing moved
+            // HIP sub-allocates small buffers from shared chunks: a moved bucket can keep
+            // its chunk (same handle, new offset) -- keep that mapping, never close and
+            // re-open the same handle
+            if (!(st.peer_base[q] && std::memcmp(st.peer_handle[q], ps.handle, 64) == 0)) {
+                void *pb = nullptr;
+                if (int rc = ipc_open(q, ps.handle, &pb)) return rc;   // open new first
+                if (st.peer_base[q]) ipc_close(st.peer_base[q]);
+                st.peer_base[q] = pb;
+                std::memcpy(st.peer_handle[q], ps.handle, 64);
+            }
+            st.peer[q] = static_cast<char *>(st.peer_base[q]) + ps.offset;
             st.peer_ver[q] = v;
         }
         return ESGD_SUCCESS;
@@ -340,6 +358,9 @@ struct IpcTransport final : Transport {
             if (int rc = publish(s, st)) return rc;
         if (s.world > 1 && s.resolve) publish_size(s);
         st.peer[s.rank] = st.rb_dev;
+        ESGD_TRACE("r%d sched %d round %u snapshot count=%llu rb_dev=%p moved=%d sb=%p rb=%p staged=%d\n",
+                   s.rank, s.id, round, (unsigned long long)s.count, (void *)st.rb_dev, moved, s.sb,
+                   s.rb, int(staged(s, st)));
         return base_snapshot(s, st, round, fresh);
     }
 
@@ -347,6 +368,9 @@ struct IpcTransport final : Transport {
         IpcState &st = S(s);
         if (s.world > 1 && s.resolve)
             if (int rc = map_peers(s, st)) return rc;
+        for (int j = 0; j < s.world; ++j)
+            ESGD_TRACE("r%d sched %d RS peer[%d]=%p off=%llu len=%llu\n", s.rank, s.id, j,
+                       (void *)st.peer[j], (unsigned long long)st.off[j], (unsigned long long)st.len[j]);
         const uint64_t n = st.len[s.rank];
         if (s.world > 1 && n) {
             const void *in[kMaxRanks];

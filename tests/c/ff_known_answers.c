@@ -22,8 +22,11 @@ static int check_int(const int32_t *got, const int32_t *want, int n, const char 
         if (got[j] != want[j]) {
             int rank;
             ffrank(&rank);
-            fprintf(stderr, "[rank %d] %s iteration %d: element %d = %d, expected %d\n", rank, what, it,
-                    j, got[j], want[j]);
+            int bad = 0, zero = 0;
+            for (int k = 0; k < n; ++k) { bad += got[k] != want[k]; zero += got[k] == 0; }
+            fprintf(stderr, "[rank %d] %s iteration %d: element %d = %d, expected %d "
+                    "(%d of %d wrong, %d zero; got[1..3] = %d %d %d)\n", rank, what, it, j, got[j],
+                    want[j], bad, n, zero, n > 1 ? got[1] : 0, n > 2 ? got[2] : 0, n > 3 ? got[3] : 0);
             return 1;
         }
     return 0;
@@ -49,8 +52,10 @@ int main(int argc, char **argv) {
             fprintf(stderr, "ffallreduce: %s\n", esgd_last_error());
             return 2;
         }
-        ffschedule_post(ar);
-        ffschedule_wait(ar);
+        if (ffschedule_post(ar) != FFSUCCESS || ffschedule_wait(ar) != FFSUCCESS) {
+            fprintf(stderr, "[rank %d] allreduce: %s\n", rank, esgd_last_error());
+            return 2;
+        }
         failed |= check_int(reduced, want, count, "allreduce", i);
         ffschedule_delete(ar);
     }
@@ -66,8 +71,10 @@ int main(int argc, char **argv) {
         for (int i = 0; i < iters && !failed; ++i) {
             for (int j = 0; j < count; ++j) { to_reduce[j]++; want[j] = to_reduce[j] * size; }
             esgd_barrier();            /* MPI_Barrier in the reference test */
-            ffschedule_post(s);
-            ffschedule_wait(s);
+            if (ffschedule_post(s) != FFSUCCESS || ffschedule_wait(s) != FFSUCCESS) {
+                fprintf(stderr, "[rank %d] schedule: %s\n", rank, esgd_last_error());
+                return 2;
+            }
             esgd_barrier();
             failed |= check_int(reduced, want, count, kind == 0 ? "solo" : "majority", i);
         }
@@ -85,9 +92,12 @@ int main(int argc, char **argv) {
             fprintf(stderr, "ffallreduce(FFCOLL_BUFFERS): %s\n", esgd_last_error());
             return 2;
         }
-        srand(439634);                  /* same sizes on every rank (the reference's SEED) */
+        /* same sizes on every rank: a private LCG seeded like the reference (SEED 439634);
+         * libc rand() is not usable here, the HIP runtime draws from it too */
+        uint32_t lcg = 439634u;
         for (int i = 0; i < iters + 2 && !failed; ++i) {
-            const int c = (rand() % max_count) + 1;
+            lcg = lcg * 1103515245u + 12345u;
+            const int c = (int)((lcg >> 8) % (uint32_t)max_count) + 1;
             free(sbuf);
             sbuf = malloc(sizeof(int32_t) * c);
             ffbuffer_resize(sbh, sbuf, c, FFINT32);
@@ -96,8 +106,12 @@ int main(int argc, char **argv) {
             ffbuffer_get_data(rbh, (void **)&rbuf);
             int32_t *w = malloc(sizeof(int32_t) * c);
             for (int j = 0; j < c; ++j) { sbuf[j] = i + j; rbuf[j] = 0; w[j] = (i + j) * size; }
-            ffschedule_post(s);
-            ffschedule_wait(s);
+            if (ffschedule_post(s) != FFSUCCESS || ffschedule_wait(s) != FFSUCCESS) {
+                fprintf(stderr, "[rank %d] FFCOLL_BUFFERS round %d: %s\n", rank, i, esgd_last_error());
+                failed = 1;
+                free(w);
+                break;
+            }
             failed |= check_int(rbuf, w, c, "FFCOLL_BUFFERS", i);
             free(w);
         }

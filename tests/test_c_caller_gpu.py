@@ -27,7 +27,8 @@ def test_c_caller_known_answers(tmp_path, world):
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
-                   ESGD_JOB_ID=job, ESGD_TIMEOUT_S="60")
+                   ESGD_JOB_ID=job, ESGD_TIMEOUT_S="60",
+                   ESGD_DEBUG=os.environ.get("ESGD_DEBUG", "0"))
         procs.append(subprocess.Popen([exe, "10007", "4"], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))
     outs = [p.communicate(timeout=180)[0] for p in procs]
