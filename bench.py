@@ -352,8 +352,10 @@ def run_allreduce(args, rank, world):
     from esgd import device as dev
     from oracle import ffref
 
+    import datetime
     os.environ.setdefault("ESGD_TIMEOUT_S", "120")   # a stuck peer fails the run, not hangs it
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=180))
     comm.init(rank=rank, world=world)            # job id broadcast over gloo
     if args.transport:
         comm.set_transport(args.transport)
@@ -412,7 +414,10 @@ def run_allreduce(args, rank, world):
             try:
                 extras[name] = fn()
             except Exception as e:   # keep the headline line; report what failed
-                extras[name + "_error"] = repr(e)[:300]
+                import traceback
+                traceback.print_exc()
+                extras[name + "_error"] = f"rank {rank}: " + repr(e)[:300]
+                break                # peers may be inside this extra: do not start another
     comm.finalize()
 
     S = count * es

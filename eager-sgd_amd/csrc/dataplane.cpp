@@ -90,12 +90,16 @@ struct BaseState {
     size_t cap = 0;                   // bytes of rb_dev (owned buckets may grow)
     uint64_t laid_count = ~0ull;      // count the shard layout was computed for
     bool owns_rb = false, reg_sb = false, reg_rb = false;
+    // device buckets the IPC runtime cannot export (carved out of a cached allocation)
+    // are shadowed by an owned bucket: copied in at the snapshot, out at the finish
+    bool shadow = false;
     // host buckets that could not be pinned (FFCOLL_BUFFERS move every round) go
     // through this pinned staging buffer: host memcpy + DMA, never an async copy into
     // pageable memory whose completion an event would not cover
     char *pin = nullptr;
     size_t pin_cap = 0;
     bool copyout_pending = false;
+    std::vector<char *> retired;      // grown-out buckets: peers may still map them
     uint64_t off[kMaxRanks] = {}, len[kMaxRanks] = {};   // elements
     std::map<uint32_t, hipEvent_t> producer;
     std::vector<hipEvent_t> spare;
@@ -123,6 +127,16 @@ static void layout(Sched &s, BaseState &st) {
     }
 }
 
+// Buckets the library owns: whole 2 MiB pages of their own, so the allocation is an
+// exportable one (small hipMallocs can be carved out of a larger cached block).
+static int alloc_bucket(size_t bytes, char **out, size_t *cap) {
+    const size_t gran = size_t(2) << 20;
+    const size_t c = (std::max<size_t>(bytes, 1) + gran - 1) / gran * gran;
+    ESGD_HIP(hipMalloc(reinterpret_cast<void **>(out), c));
+    *cap = c;
+    return ESGD_SUCCESS;
+}
+
 static int base_setup(Sched &s, BaseState &st) {
     if (s.esize == 0) { set_error("schedule: unsupported dtype %d", s.dtype); return ESGD_INVALID_ARG; }
     if (int rc = require_device()) return rc;
@@ -130,8 +144,10 @@ static int base_setup(Sched &s, BaseState &st) {
     ESGD_HIP(hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking));
     ESGD_HIP(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
     if (s.host_mode) {
-        st.cap = bytes ? bytes : 256;
-        ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.rb_dev), st.cap));
+        // FFCOLL_BUFFERS buckets change size: start with head room
+        if (int rc = alloc_bucket(s.resolve ? std::max<size_t>(bytes, size_t(4) << 20) : bytes,
+                                  &st.rb_dev, &st.cap))
+            return rc;
         st.owns_rb = true;
         // pin the caller's persistent host buckets so the move / copy-out are DMA
         // (not for FFCOLL_BUFFERS: those move every round)
@@ -173,10 +189,10 @@ static int base_refit(Sched &s, BaseState &st) {
     int moved = 0;
     if (bytes > st.cap) {
         if (!st.owns_rb) { set_error("schedule %d: device bucket cannot grow", s.id); return ESGD_INVALID_ARG; }
-        ESGD_HIP(hipStreamSynchronize(st.stream));
-        ESGD_HIP(hipFree(st.rb_dev));
-        st.cap = bytes;
-        ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.rb_dev), st.cap));
+        // grow geometrically; the old bucket stays allocated (peers may still have it
+        // mapped: freeing exported memory under an importer breaks later IPC opens)
+        st.retired.push_back(st.rb_dev);
+        if (int rc = alloc_bucket(std::max(bytes, 2 * st.cap), &st.rb_dev, &st.cap)) return rc;
         moved = 1;
     }
     layout(s, st);
@@ -223,8 +239,9 @@ static int base_snapshot(Sched &s, BaseState &st, uint32_t round, bool fresh) {
                 src = st.pin;
             }
             ESGD_HIP(hipMemcpyAsync(st.rb_dev, src, bytes, hipMemcpyHostToDevice, st.stream));
-        } else if (!s.in_place) {
-            ESGD_HIP(hipMemcpyAsync(st.rb_dev, s.sb, bytes, hipMemcpyDeviceToDevice, st.stream));
+        } else if (!s.in_place || st.shadow) {
+            ESGD_HIP(hipMemcpyAsync(st.rb_dev, s.in_place ? s.rb : s.sb, bytes,
+                                    hipMemcpyDeviceToDevice, st.stream));
         }
     }
     ESGD_HIP(hipEventRecord(st.ev, st.stream));
@@ -241,6 +258,8 @@ static int base_finish(Sched &s, BaseState &st) {
         } else {
             ESGD_HIP(hipMemcpyAsync(s.rb, st.rb_dev, bytes, hipMemcpyDeviceToHost, st.stream));
         }
+    } else if (st.shadow && bytes) {
+        ESGD_HIP(hipMemcpyAsync(s.rb, st.rb_dev, bytes, hipMemcpyDeviceToDevice, st.stream));
     }
     ESGD_HIP(hipEventRecord(st.ev, st.stream));
     return ESGD_SUCCESS;
@@ -269,6 +288,7 @@ static void base_teardown(Sched &s, BaseState &st) {
     for (auto &kv : st.producer) (void)hipEventDestroy(kv.second);
     for (hipEvent_t e : st.spare) (void)hipEventDestroy(e);
     if (st.pin) (void)hipHostFree(st.pin);
+    for (char *p : st.retired) (void)hipFree(p);
     if (st.ev) (void)hipEventDestroy(st.ev);
     if (st.stream) (void)hipStreamDestroy(st.stream);
 }
@@ -338,10 +358,22 @@ struct IpcTransport final : Transport {
         if (int rc = base_setup(s, *st)) return rc;
         st->peer[s.rank] = st->rb_dev;
         if (s.world == 1) return ESGD_SUCCESS;
-        // publish this rank's rb, then map every peer's
-        if (int rc = publish(s, *st)) return rc;
-        if (int rc = engine_barrier()) return rc;
-        return map_peers(s, *st);
+        // publish this rank's rb (peers map it in connect())
+        int rc = publish(s, *st);
+        if (rc && !s.host_mode) {
+            ESGD_TRACE("r%d sched %d: bucket %p not exportable (%s), shadowing it\n", s.rank, s.id,
+                       (void *)st->rb_dev, esgd_last_error());
+            (void)hipGetLastError();
+            if ((rc = alloc_bucket(s.count * s.esize, &st->rb_dev, &st->cap))) return rc;
+            st->owns_rb = st->shadow = true;
+            st->peer[s.rank] = st->rb_dev;
+            rc = publish(s, *st);
+        }
+        return rc;
+    }
+
+    int connect(Sched &s) override {
+        return s.world > 1 ? map_peers(s, S(s)) : ESGD_SUCCESS;
     }
 
     int note_producer(Sched &s, uint32_t round, void *stream) override {
@@ -522,7 +554,11 @@ struct RcclTransport final : Transport {
     int setup(Sched &s) override {
         auto *st = new RcclState();
         s.tstate = st;
-        if (int rc = base_setup(s, *st)) return rc;
+        return base_setup(s, *st);
+    }
+
+    int connect(Sched &s) override {
+        RcclState *st = &S(s);
         if (int rc = nccl_ensure(s)) return rc;
         ESGD_HIP(hipEventCreateWithFlags(&st->ev_snap, hipEventDisableTiming));
         ESGD_HIP(hipEventCreateWithFlags(&st->ev_red, hipEventDisableTiming));

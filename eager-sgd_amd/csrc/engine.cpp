@@ -180,6 +180,7 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
             sh->joined[r].store(0); sh->activations[r].store(0);
         }
         sh->ready_count.store(0);
+        sh->setup_err.store(0);
         for (int i = 0; i < 256; ++i) sh->act_of[i].store(0);
         sh->gen.fetch_add(1, std::memory_order_acq_rel);
     }
@@ -190,10 +191,26 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
         rc = ESGD_INVALID_ARG;
     }
     s->gen = s->sh->gen.load();
-    if (!rc) rc = tp->setup(*s);   // collective registration (has its own barriers)
-    int rc2 = shm_barrier(g_seg, g_world, g_timeout);
-    if (!rc) rc = rc2;
+    // Registration is voted: every rank takes part in both barriers whatever happened
+    // locally, and a failure anywhere fails the creation everywhere (no rank is left
+    // waiting on a peer that gave up).
+    auto vote = [&](int r) -> int {
+        if (r) s->sh->setup_err.fetch_add(1, std::memory_order_acq_rel);
+        const int rb = shm_barrier(g_seg, g_world, g_timeout);
+        if (r) return r;
+        if (rb) return rb;
+        if (s->sh->setup_err.load(std::memory_order_acquire)) {
+            set_error("schedule create: another rank failed to register schedule %d", s->id);
+            return ESGD_ERROR;
+        }
+        return ESGD_SUCCESS;
+    };
+    if (!rc) rc = tp->setup(*s);     // local: buffers, streams, publication
+    rc = vote(rc);
+    if (!rc) rc = tp->connect(*s);   // needs every peer's publication
+    rc = vote(rc);
     if (rc) {
+        if (s->tstate) tp->teardown(*s);
         s->resolve_free = nullptr;   // the caller still owns ctx on failure
         delete s;
         return rc;

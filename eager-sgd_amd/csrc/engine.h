@@ -55,7 +55,11 @@ struct Transport {
     // true: collectives must be issued in one global order (RCCL); reduce_scatter() is
     // then called from the ticket pump in ring order instead of at "all ready".
     virtual bool ordered() const { return false; }
-    virtual int setup(Sched &s) = 0;          // collective: called between barriers
+    // creation, in two voted steps: setup() is local (buffers, streams, publishing
+    // this rank's bucket); connect() runs once every rank's setup() succeeded (mapping
+    // peers, communicator bring-up).  A failure in either fails the creation on all ranks.
+    virtual int setup(Sched &s) = 0;
+    virtual int connect(Sched &) { return ESGD_SUCCESS; }
     virtual int note_producer(Sched &s, uint32_t round, void *stream) = 0;
     virtual int snapshot(Sched &s, uint32_t round, bool fresh) = 0;
     virtual int reduce_scatter(Sched &s) = 0;

@@ -43,6 +43,7 @@ struct alignas(64) SchedShm {
     std::atomic<uint32_t> joined[kMaxRanks];  // diagnostics: last round rank r joined
     std::atomic<uint32_t> activations[kMaxRanks];  // diagnostics: rounds activated by r
     std::atomic<uint32_t> ready_count;   // ordered transports: sum of ready publications
+    std::atomic<uint32_t> setup_err;     // ranks whose registration failed (creation vote)
     IpcSlot slot[kMaxRanks];
 };
 
