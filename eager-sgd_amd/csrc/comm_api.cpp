@@ -1,4 +1,5 @@
 // comm_api.cpp — C ABI of the node communicator and the persistent schedules (esgd.h).
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -11,7 +12,6 @@ Transport *ipc_transport();
 Transport *rccl_transport();
 Transport *null_transport(bool ordered);
 hipStream_t sched_stream(Sched &s);
-void rccl_shutdown();
 }  // namespace esgd
 
 static std::string g_transport;   // "" -> env ESGD_TRANSPORT -> "ipc"
@@ -46,9 +46,7 @@ int esgd_comm_init(const char *job_id, int rank, int world) {
 }
 
 int esgd_comm_finalize(void) {
-    int rc = engine_finalize();
-    rccl_shutdown();
-    return rc;
+    return engine_finalize();   // frees the data plane (dataplane_shutdown) too
 }
 
 int esgd_set_transport(const char *name) {
@@ -147,6 +145,17 @@ int esgd_schedule_log(esgd_sched_h h, uint32_t *rounds, uint8_t *fresh, uint8_t 
         if (sync) sync[i] = s->log[i].sync;
         if (activator) activator[i] = s->log[i].activator;
     }
+    if (n) *n = total;
+    return ESGD_SUCCESS;
+}
+
+int esgd_schedule_timeline(esgd_sched_h h, uint64_t *t, uint32_t cap, uint32_t *n) {
+    Sched *s = handle_to_sched(h);
+    if (!s) return ESGD_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(s->mu);
+    const uint32_t total = std::min<uint32_t>(uint32_t(s->tl.size()), s->completed);
+    for (uint32_t i = 0; i < total && i < cap; ++i)
+        for (int k = 0; k < 12; ++k) t[12 * i + k] = s->tl[i][k];
     if (n) *n = total;
     return ESGD_SUCCESS;
 }

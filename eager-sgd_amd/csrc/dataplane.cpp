@@ -80,11 +80,91 @@ static void ipc_close(void *base) {
     }
 }
 
-// State every GPU transport keeps per schedule: the data-plane stream, the query
+// ---- process-wide data-plane resources -----------------------------------------------
+// One round stream per process: every round of every schedule is queued on it in the
+// node's issue order (engine.cpp), so no GPU-side wait of one round can sit in front of
+// a round a peer needs first.  The node segment is registered with the GPU once: the
+// rounds' pairing flags live in it (SchedShm::ready/reduced/done/gpu_err).
+static std::mutex g_dp_mu;
+static hipStream_t g_rs = nullptr;
+static Segment *g_seg_reg = nullptr;
+static char *g_seg_dev = nullptr;
+static long long g_ticks_per_s = 0;
+
+static int round_stream(hipStream_t *out) {
+    std::lock_guard<std::mutex> lk(g_dp_mu);
+    if (!g_rs) ESGD_HIP(hipStreamCreateWithFlags(&g_rs, hipStreamNonBlocking));
+    *out = g_rs;
+    return ESGD_SUCCESS;
+}
+
+static int register_segment() {
+    std::lock_guard<std::mutex> lk(g_dp_mu);
+    Segment *seg = engine_segment();
+    if (g_seg_reg == seg) return ESGD_SUCCESS;
+    ESGD_HIP(hipHostRegister(seg, sizeof(Segment), hipHostRegisterMapped));
+    void *d = nullptr;
+    ESGD_HIP(hipHostGetDevicePointer(&d, seg, 0));
+    int dev = 0, khz = 0;
+    ESGD_HIP(hipGetDevice(&dev));
+    ESGD_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+    g_ticks_per_s = (long long)khz * 1000;
+    g_seg_reg = seg;
+    g_seg_dev = static_cast<char *>(d);
+    return ESGD_SUCCESS;
+}
+
+template <class T>
+static uint32_t *dev_flag(T *host) {
+    return reinterpret_cast<uint32_t *>(g_seg_dev + (reinterpret_cast<char *>(host) -
+                                                     reinterpret_cast<char *>(g_seg_reg)));
+}
+
+int round_sync(uint32_t *flags, int rank, int world, uint32_t value, long long timeout_ticks,
+               uint32_t *err, uint64_t *ts, hipStream_t s);
+
+static bool gpu_trace_on() {
+    static const bool on = getenv("ESGD_GPU_TRACE") && *getenv("ESGD_GPU_TRACE") == '1';
+    return on;
+}
+
+// which = 0 ready, 1 reduced, 2 done
+static int pair_ranks(Sched &s, std::atomic<uint32_t> *flags, int which, uint32_t round, hipStream_t cs) {
+    const long long ticks = (long long)(engine_timeout() * double(g_ticks_per_s));
+    uint64_t *ts = gpu_trace_on() ? reinterpret_cast<uint64_t *>(dev_flag(&s.sh->gpu_ts[s.rank][2 * which]))
+                                  : nullptr;
+    return round_sync(dev_flag(flags), s.rank, s.world, round, ticks, dev_flag(&s.sh->gpu_err[s.rank]), ts, cs);
+}
+
+// ns between the GPU stamps of the last round (ESGD_GPU_TRACE=1), for the timeline
+void gpu_trace_read(Sched &s, uint64_t out[6]) {
+    for (int k = 0; k < 6; ++k) out[k] = 0;
+    if (!gpu_trace_on() || !g_ticks_per_s || s.world < 2) return;
+    volatile uint64_t *t = s.sh->gpu_ts[s.rank];
+    const double ns = 1e9 / double(g_ticks_per_s);
+    // sync1 wait, RS, sync2 wait, AG, sync3 wait, total
+    out[0] = uint64_t(double(t[1] - t[0]) * ns);
+    out[1] = uint64_t(double(t[2] - t[1]) * ns);
+    out[2] = uint64_t(double(t[3] - t[2]) * ns);
+    out[3] = uint64_t(double(t[4] - t[3]) * ns);
+    out[4] = uint64_t(double(t[5] - t[4]) * ns);
+    out[5] = uint64_t(double(t[5] - t[0]) * ns);
+}
+
+void rccl_shutdown();
+
+void dataplane_shutdown() {
+    rccl_shutdown();
+    std::lock_guard<std::mutex> lk(g_dp_mu);
+    if (g_rs) { (void)hipStreamSynchronize(g_rs); (void)hipStreamDestroy(g_rs); g_rs = nullptr; }
+    if (g_seg_reg) { (void)hipHostUnregister(g_seg_reg); g_seg_reg = nullptr; g_seg_dev = nullptr; }
+}
+
+// State every GPU transport keeps per schedule: the round stream, the completion
 // event, the device receive bucket (the caller's, or an HBM copy of a host bucket), the
 // shard layout and the producer events of posted rounds.
 struct BaseState {
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;     // the process's round stream (not owned)
     hipEvent_t ev = nullptr;
     char *rb_dev = nullptr;
     size_t cap = 0;                   // bytes of rb_dev (owned buckets may grow)
@@ -141,7 +221,7 @@ static int base_setup(Sched &s, BaseState &st) {
     if (s.esize == 0) { set_error("schedule: unsupported dtype %d", s.dtype); return ESGD_INVALID_ARG; }
     if (int rc = require_device()) return rc;
     const size_t bytes = s.count * s.esize;
-    ESGD_HIP(hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking));
+    if (int rc = round_stream(&st.stream)) return rc;
     ESGD_HIP(hipEventCreateWithFlags(&st.ev, hipEventDisableTiming));
     if (s.host_mode) {
         // FFCOLL_BUFFERS buckets change size: start with head room
@@ -221,47 +301,52 @@ static int ensure_pin(BaseState &st, size_t bytes) {
     return ESGD_SUCCESS;
 }
 
-static int base_snapshot(Sched &s, BaseState &st, uint32_t round, bool fresh) {
-    // gradient producer of this round (posted before the join) must have finished
+// Join-time host work: the move of an unpinned host bucket into the pinned staging
+// buffer happens now, when the rank joins (the reference's move reads sb at activation,
+// colls/ffallreduce.c:126-130).  The previous round has completed, so the buffer is free.
+static int base_prepare(Sched &s, BaseState &st) {
+    const size_t bytes = s.count * s.esize;
+    if (bytes && staged(s, st)) {
+        if (int rc = ensure_pin(st, bytes)) return rc;
+        std::memcpy(st.pin, s.sb ? s.sb : s.rb, bytes);
+    }
+    return ESGD_SUCCESS;
+}
+
+// queued at launch: the producer of this round (posted before the join) must have
+// finished, then the move sb -> rb (host -> HBM for host buckets)
+static int base_copy_in(Sched &s, BaseState &st, uint32_t round, bool fresh, hipStream_t cs) {
     for (auto it = st.producer.begin(); it != st.producer.end();) {
-        if (it->first == round && fresh) ESGD_HIP(hipStreamWaitEvent(st.stream, it->second, 0));
+        if (it->first == round && fresh) ESGD_HIP(hipStreamWaitEvent(cs, it->second, 0));
         if (it->first <= round) { st.spare.push_back(it->second); it = st.producer.erase(it); }
         else ++it;
     }
     const size_t bytes = s.count * s.esize;
-    if (bytes) {
-        if (s.host_mode) {   // the move of ffallreduce.c:126-130, host -> HBM
-            const void *src = s.sb ? s.sb : s.rb;
-            if (staged(s, st)) {
-                if (int rc = ensure_pin(st, bytes)) return rc;
-                ESGD_HIP(hipStreamSynchronize(st.stream));   // pin is free again
-                std::memcpy(st.pin, src, bytes);
-                src = st.pin;
-            }
-            ESGD_HIP(hipMemcpyAsync(st.rb_dev, src, bytes, hipMemcpyHostToDevice, st.stream));
-        } else if (!s.in_place || st.shadow) {
-            ESGD_HIP(hipMemcpyAsync(st.rb_dev, s.in_place ? s.rb : s.sb, bytes,
-                                    hipMemcpyDeviceToDevice, st.stream));
-        }
+    if (!bytes) return ESGD_SUCCESS;
+    if (s.host_mode) {
+        const void *src = staged(s, st) ? st.pin : (s.sb ? s.sb : s.rb);
+        ESGD_HIP(hipMemcpyAsync(st.rb_dev, src, bytes, hipMemcpyHostToDevice, cs));
+    } else if (!s.in_place || st.shadow) {
+        ESGD_HIP(hipMemcpyAsync(st.rb_dev, s.in_place ? s.rb : s.sb, bytes, hipMemcpyDeviceToDevice, cs));
     }
-    ESGD_HIP(hipEventRecord(st.ev, st.stream));
     return ESGD_SUCCESS;
 }
 
-static int base_finish(Sched &s, BaseState &st) {
+// queued at launch, last: the copy-out and the round's completion event
+static int base_copy_out(Sched &s, BaseState &st, hipStream_t cs) {
     const size_t bytes = s.count * s.esize;
     if (s.host_mode && bytes) {
         if (staged(s, st)) {
             if (int rc = ensure_pin(st, bytes)) return rc;
-            ESGD_HIP(hipMemcpyAsync(st.pin, st.rb_dev, bytes, hipMemcpyDeviceToHost, st.stream));
+            ESGD_HIP(hipMemcpyAsync(st.pin, st.rb_dev, bytes, hipMemcpyDeviceToHost, cs));
             st.copyout_pending = true;
         } else {
-            ESGD_HIP(hipMemcpyAsync(s.rb, st.rb_dev, bytes, hipMemcpyDeviceToHost, st.stream));
+            ESGD_HIP(hipMemcpyAsync(s.rb, st.rb_dev, bytes, hipMemcpyDeviceToHost, cs));
         }
     } else if (st.shadow && bytes) {
-        ESGD_HIP(hipMemcpyAsync(s.rb, st.rb_dev, bytes, hipMemcpyDeviceToDevice, st.stream));
+        ESGD_HIP(hipMemcpyAsync(s.rb, st.rb_dev, bytes, hipMemcpyDeviceToDevice, cs));
     }
-    ESGD_HIP(hipEventRecord(st.ev, st.stream));
+    ESGD_HIP(hipEventRecord(st.ev, cs));
     return ESGD_SUCCESS;
 }
 
@@ -273,11 +358,27 @@ static int base_complete(Sched &s, BaseState &st) {
     return ESGD_SUCCESS;
 }
 
-static int base_query(BaseState &st) {
+static std::string base_diagnose(Sched &s) {
+    std::string m = "(flags ready/reduced/done per rank:";
+    char buf[64];
+    for (int q = 0; q < s.world; ++q) {
+        snprintf(buf, sizeof(buf), " %u/%u/%u", s.sh->ready[q].load(), s.sh->reduced[q].load(),
+                 s.sh->done[q].load());
+        m += buf;
+    }
+    return m + ")";
+}
+
+static int base_query(Sched &s, BaseState &st) {
     hipError_t e = hipEventQuery(st.ev);
-    if (e == hipSuccess) return 1;
     if (e == hipErrorNotReady) return 0;
-    return hip_fail(e, "hipEventQuery", __FILE__, __LINE__);
+    if (e != hipSuccess) return hip_fail(e, "hipEventQuery", __FILE__, __LINE__);
+    if (s.world > 1 && s.sh->gpu_err[s.rank].load(std::memory_order_acquire) == s.cur) {
+        set_error("this rank's GPU waited more than %.0f s for its peers in round %u %s",
+                  engine_timeout(), s.cur, base_diagnose(s).c_str());
+        return ESGD_ERROR;
+    }
+    return 1;
 }
 
 static void base_teardown(Sched &s, BaseState &st) {
@@ -290,7 +391,6 @@ static void base_teardown(Sched &s, BaseState &st) {
     if (st.pin) (void)hipHostFree(st.pin);
     for (char *p : st.retired) (void)hipFree(p);
     if (st.ev) (void)hipEventDestroy(st.ev);
-    if (st.stream) (void)hipStreamDestroy(st.stream);
 }
 
 struct IpcTransport final : Transport {
@@ -358,8 +458,12 @@ struct IpcTransport final : Transport {
         if (int rc = base_setup(s, *st)) return rc;
         st->peer[s.rank] = st->rb_dev;
         if (s.world == 1) return ESGD_SUCCESS;
+        if (int rc = register_segment()) return rc;
         // publish this rank's rb (peers map it in connect())
-        int rc = publish(s, *st);
+        // ESGD_SHADOW=1 shadows every device bucket (caller buckets that are freed and
+        // re-allocated between rounds; also how the tests reach the fallback)
+        static const bool force_shadow = getenv("ESGD_SHADOW") && *getenv("ESGD_SHADOW") == '1';
+        int rc = force_shadow && !s.host_mode ? ESGD_ERROR : publish(s, *st);
         if (rc && !s.host_mode) {
             ESGD_TRACE("r%d sched %d: bucket %p not exportable (%s), shadowing it\n", s.rank, s.id,
                        (void *)st->rb_dev, esgd_last_error());
@@ -380,66 +484,65 @@ struct IpcTransport final : Transport {
         return base_note_producer(S(s), round, stream);
     }
 
-    int snapshot(Sched &s, uint32_t round, bool fresh) override {
+    // join: a moved bucket is re-published before this rank's join counts (peers map it
+    // when they launch the round); a size change alone only updates the published size
+    int prepare(Sched &s, uint32_t round, bool) override {
         IpcState &st = S(s);
         const int moved = base_refit(s, st);
         if (moved < 0) return moved;
-        // a moved bucket is re-published before "ready" (peers re-map it in RS); a size
-        // change alone only updates the published size
         if (s.world > 1 && moved)
             if (int rc = publish(s, st)) return rc;
         if (s.world > 1 && s.resolve) publish_size(s);
         st.peer[s.rank] = st.rb_dev;
-        ESGD_TRACE("r%d sched %d round %u snapshot count=%llu rb_dev=%p moved=%d sb=%p rb=%p staged=%d\n",
-                   s.rank, s.id, round, (unsigned long long)s.count, (void *)st.rb_dev, moved, s.sb,
-                   s.rb, int(staged(s, st)));
-        return base_snapshot(s, st, round, fresh);
+        ESGD_TRACE("r%d sched %d round %u join count=%llu rb_dev=%p moved=%d staged=%d\n", s.rank, s.id,
+                   round, (unsigned long long)s.count, (void *)st.rb_dev, moved, int(staged(s, st)));
+        return base_prepare(s, st);
     }
 
-    int reduce_scatter(Sched &s) override {
+    // The whole round, queued on the round stream:
+    //   move -> [pair: ready] -> reduce-scatter (tree kernel over peer HBM)
+    //        -> [pair: reduced] -> all-gather -> [pair: done] -> copy-out -> event.
+    // The last pairing keeps this rank's shard unchanged until every peer has gathered
+    // it (the caller may overwrite rb once wait() returns).
+    int launch(Sched &s, uint32_t round, bool fresh) override {
         IpcState &st = S(s);
-        if (s.world > 1 && s.resolve)
-            if (int rc = map_peers(s, st)) return rc;
-        for (int j = 0; j < s.world; ++j)
-            ESGD_TRACE("r%d sched %d RS peer[%d]=%p off=%llu len=%llu\n", s.rank, s.id, j,
-                       (void *)st.peer[j], (unsigned long long)st.off[j], (unsigned long long)st.len[j]);
-        const uint64_t n = st.len[s.rank];
-        if (s.world > 1 && n) {
-            const void *in[kMaxRanks];
-            for (int j = 0; j < s.world; ++j) in[j] = st.peer[j] + st.off[s.rank] * s.esize;
-            if (int rc = reduce_remote(s.dtype, s.world, in, st.rb_dev + st.off[s.rank] * s.esize, n,
-                                       1.0f, st.stream))
-                return rc;
-        }
-        ESGD_HIP(hipEventRecord(st.ev, st.stream));
-        return ESGD_SUCCESS;
-    }
-
-    int all_gather(Sched &s) override {
-        IpcState &st = S(s);
+        hipStream_t cs = st.stream;
+        if (int rc = base_copy_in(s, st, round, fresh, cs)) return rc;
         if (s.world > 1) {
+            if (s.resolve)
+                if (int rc = map_peers(s, st)) return rc;
+            if (int rc = pair_ranks(s, s.sh->ready, 0, round, cs)) return rc;
+            const uint64_t n = st.len[s.rank];
+            if (n) {
+                const void *in[kMaxRanks];
+                for (int j = 0; j < s.world; ++j) in[j] = st.peer[j] + st.off[s.rank] * s.esize;
+                if (int rc = reduce_remote(s.dtype, s.world, in, st.rb_dev + st.off[s.rank] * s.esize, n,
+                                           1.0f, cs))
+                    return rc;
+            }
+            if (int rc = pair_ranks(s, s.sh->reduced, 1, round, cs)) return rc;
             const void *src[kMaxRanks];
             void *dst[kMaxRanks];
             uint64_t bytes[kMaxRanks];
-            int n = 0;
+            int m = 0;
             for (int j = 0; j < s.world; ++j) {
                 if (j == s.rank || st.len[j] == 0) continue;
-                src[n] = st.peer[j] + st.off[j] * s.esize;
-                dst[n] = st.rb_dev + st.off[j] * s.esize;
-                bytes[n] = st.len[j] * s.esize;
-                ++n;
+                src[m] = st.peer[j] + st.off[j] * s.esize;
+                dst[m] = st.rb_dev + st.off[j] * s.esize;
+                bytes[m] = st.len[j] * s.esize;
+                ++m;
             }
-            if (int rc = gather_remote(n, src, dst, bytes, st.stream)) return rc;
+            if (int rc = gather_remote(m, src, dst, bytes, cs)) return rc;
+            if (int rc = pair_ranks(s, s.sh->done, 2, round, cs)) return rc;
         }
-        ESGD_HIP(hipEventRecord(st.ev, st.stream));
-        return ESGD_SUCCESS;
+        return base_copy_out(s, st, cs);
     }
 
-    int finish(Sched &s) override { return base_finish(s, S(s)); }
-
-    int query(Sched &s) override { return base_query(S(s)); }
+    int query(Sched &s) override { return base_query(s, S(s)); }
 
     int complete(Sched &s) override { return base_complete(s, S(s)); }
+
+    std::string diagnose(Sched &s) override { return base_diagnose(s); }
 
     void teardown(Sched &s) override {
         IpcState *st = static_cast<IpcState *>(s.tstate);
@@ -455,15 +558,12 @@ struct IpcTransport final : Transport {
 
 struct NullTransport final : Transport {
     explicit NullTransport(bool ord = false) : ordered_(ord) {}
-    bool ordered_;
+    bool ordered_;   // the "rccl" flavour (same protocol; named for the issue-order tests)
     const char *name() const override { return ordered_ ? "none-ordered" : "none"; }
-    bool ordered() const override { return ordered_; }
     int setup(Sched &) override { return ESGD_SUCCESS; }
     int note_producer(Sched &, uint32_t, void *) override { return ESGD_SUCCESS; }
-    int snapshot(Sched &, uint32_t, bool) override { return ESGD_SUCCESS; }
-    int reduce_scatter(Sched &) override { return ESGD_SUCCESS; }
-    int all_gather(Sched &) override { return ESGD_SUCCESS; }
-    int finish(Sched &) override { return ESGD_SUCCESS; }
+    int prepare(Sched &, uint32_t, bool) override { return ESGD_SUCCESS; }
+    int launch(Sched &, uint32_t, bool) override { return ESGD_SUCCESS; }
     int query(Sched &) override { return 1; }
     void teardown(Sched &) override {}
 };
@@ -492,7 +592,8 @@ hipStream_t sched_stream(Sched &s) {
 // peer's copy of shard `rank` into a staging area, chunk by chunk; the schedule's own
 // stream waits for each chunk and folds it with the tree kernel (same order as the
 // reference); a second group all-gathers the reduced shards.  RCCL matches operations
-// by issue order, so rounds are issued in the global ticket order (engine ordered()).
+// by issue order: the engine launches rounds in the node's issue-ring order, on the
+// process's round stream, which is also the communicator stream.
 // RCCL refuses two ranks on one GPU, so this transport only runs with one GPU per rank.
 }  // namespace esgd
 
@@ -502,7 +603,6 @@ namespace esgd {
 
 static std::mutex g_nccl_mu;
 static ncclComm_t g_nccl = nullptr;
-static hipStream_t g_cs = nullptr;    // all RCCL operations of this process, in ticket order
 
 static int nccl_fail(ncclResult_t r, const char *what) {
     set_error("%s: %s", what, ncclGetErrorString(r));
@@ -524,73 +624,66 @@ static int nccl_ensure(Sched &s) {
         ESGD_NCCL(ncclGetUniqueId(&id));
         std::memcpy(seg->nccl_id, &id, sizeof(id));
     }
-    if (int rc = engine_barrier()) return rc;   // setup runs collectively
+    if (int rc = engine_barrier()) return rc;   // connect() runs on every rank
     std::memcpy(&id, seg->nccl_id, sizeof(id));
     ESGD_NCCL(ncclCommInitRank(&g_nccl, s.world, id, s.rank));
-    ESGD_HIP(hipStreamCreateWithFlags(&g_cs, hipStreamNonBlocking));
     return ESGD_SUCCESS;
 }
 
 void rccl_shutdown() {
     std::lock_guard<std::mutex> lk(g_nccl_mu);
-    if (g_cs) { (void)hipStreamSynchronize(g_cs); (void)hipStreamDestroy(g_cs); g_cs = nullptr; }
+    if (g_rs) (void)hipStreamSynchronize(g_rs);
     if (g_nccl) { (void)ncclCommDestroy(g_nccl); g_nccl = nullptr; }
 }
 
 struct RcclState : BaseState {
+    hipStream_t red = nullptr;       // tree folds of arrived chunks
     char *stage = nullptr;           // P x L elements: every peer's copy of this rank's shard
     uint64_t L = 0;                  // shard pitch (elements)
     uint64_t chunk = 0;              // pipeline chunk (elements)
-    hipEvent_t ev_snap = nullptr, ev_red = nullptr;
+    hipEvent_t ev_red = nullptr;
     std::vector<hipEvent_t> ev_chunk;
 };
 
 struct RcclTransport final : Transport {
     const char *name() const override { return "rccl"; }
-    bool ordered() const override { return true; }
 
     static RcclState &S(Sched &s) { return *static_cast<RcclState *>(s.tstate); }
+
+    static int fit_stage(Sched &s, RcclState &st) {
+        if (st.stage && st.L == st.len[0]) return ESGD_SUCCESS;
+        if (st.stage) { ESGD_HIP(hipFree(st.stage)); st.stage = nullptr; }
+        st.L = st.len[0];
+        if (s.world > 1 && st.L)
+            ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.stage), size_t(s.world) * st.L * s.esize));
+        // ~8 chunks per shard, at least 1 MiB each, 1 KiB aligned
+        const uint64_t align = 1024 / s.esize, minc = (1u << 20) / s.esize;
+        const uint64_t c = std::max<uint64_t>(minc, (st.L + 7) / 8);
+        st.chunk = (c + align - 1) / align * align;
+        return ESGD_SUCCESS;
+    }
 
     int setup(Sched &s) override {
         auto *st = new RcclState();
         s.tstate = st;
-        return base_setup(s, *st);
+        if (int rc = base_setup(s, *st)) return rc;
+        ESGD_HIP(hipStreamCreateWithFlags(&st->red, hipStreamNonBlocking));
+        ESGD_HIP(hipEventCreateWithFlags(&st->ev_red, hipEventDisableTiming));
+        return fit_stage(s, *st);
     }
 
-    int connect(Sched &s) override {
-        RcclState *st = &S(s);
-        if (int rc = nccl_ensure(s)) return rc;
-        ESGD_HIP(hipEventCreateWithFlags(&st->ev_snap, hipEventDisableTiming));
-        ESGD_HIP(hipEventCreateWithFlags(&st->ev_red, hipEventDisableTiming));
-        st->L = st->len[0];
-        if (s.world > 1 && st->L) {
-            ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st->stage), size_t(s.world) * st->L * s.esize));
-            // ~8 chunks per shard, at least 1 MiB each, 1 KiB aligned
-            const uint64_t align = 1024 / s.esize, minc = (1u << 20) / s.esize;
-            uint64_t c = std::max<uint64_t>(minc, (st->L + 7) / 8);
-            st->chunk = (c + align - 1) / align * align;
-        }
-        return ESGD_SUCCESS;
-    }
+    int connect(Sched &s) override { return nccl_ensure(s); }
 
     int note_producer(Sched &s, uint32_t round, void *stream) override {
         return base_note_producer(S(s), round, stream);
     }
 
-    int snapshot(Sched &s, uint32_t round, bool fresh) override {
+    int prepare(Sched &s, uint32_t, bool) override {
         RcclState &st = S(s);
         const int moved = base_refit(s, st);
         if (moved < 0) return moved;
-        if (st.laid_count == s.count && st.L != st.len[0]) {   // new layout: resize staging
-            if (st.stage) { ESGD_HIP(hipFree(st.stage)); st.stage = nullptr; }
-            st.L = st.len[0];
-            if (s.world > 1 && st.L)
-                ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.stage), size_t(s.world) * st.L * s.esize));
-            const uint64_t align = 1024 / s.esize, minc = (1u << 20) / s.esize;
-            uint64_t c = std::max<uint64_t>(minc, (st.L + 7) / 8);
-            st.chunk = (c + align - 1) / align * align;
-        }
-        return base_snapshot(s, st, round, fresh);
+        if (int rc = fit_stage(s, st)) return rc;
+        return base_prepare(s, st);
     }
 
     static uint64_t piece(uint64_t len, uint64_t c, uint64_t chunk) {
@@ -598,14 +691,15 @@ struct RcclTransport final : Transport {
         return o >= len ? 0 : std::min(chunk, len - o);
     }
 
-    // The whole round is queued here, in ticket order: RS groups (comm stream) ->
-    // per-chunk tree folds (schedule stream) -> AG group (comm stream).
-    int reduce_scatter(Sched &s) override {
+    // The whole round, in issue order on the round stream: move -> RS groups, each
+    // chunk folded with the tree kernel on the side stream as it lands -> AG group ->
+    // copy-out -> event.
+    int launch(Sched &s, uint32_t round, bool fresh) override {
         RcclState &st = S(s);
+        hipStream_t cs = st.stream;
         const int P = s.world, r = s.rank;
         const size_t es = s.esize;
-        ESGD_HIP(hipEventRecord(st.ev_snap, st.stream));
-        ESGD_HIP(hipStreamWaitEvent(g_cs, st.ev_snap, 0));
+        if (int rc = base_copy_in(s, st, round, fresh, cs)) return rc;
         if (P > 1 && st.L) {
             const uint64_t nch = (st.L + st.chunk - 1) / st.chunk;
             while (st.ev_chunk.size() < nch) {
@@ -619,56 +713,47 @@ struct RcclTransport final : Transport {
                     if (j == r) continue;
                     const uint64_t ns = piece(st.len[j], c, st.chunk);
                     if (ns) ESGD_NCCL(ncclSend(st.rb_dev + (st.off[j] + c * st.chunk) * es, ns * es,
-                                               ncclChar, j, g_nccl, g_cs));
+                                               ncclChar, j, g_nccl, cs));
                     const uint64_t nr = piece(st.len[r], c, st.chunk);
                     if (nr) ESGD_NCCL(ncclRecv(st.stage + (uint64_t(j) * st.L + c * st.chunk) * es,
-                                               nr * es, ncclChar, j, g_nccl, g_cs));
+                                               nr * es, ncclChar, j, g_nccl, cs));
                 }
                 ESGD_NCCL(ncclGroupEnd());
-                ESGD_HIP(hipEventRecord(st.ev_chunk[c], g_cs));
+                ESGD_HIP(hipEventRecord(st.ev_chunk[c], cs));
                 const uint64_t n = piece(st.len[r], c, st.chunk);
                 if (!n) continue;
-                ESGD_HIP(hipStreamWaitEvent(st.stream, st.ev_chunk[c], 0));
+                ESGD_HIP(hipStreamWaitEvent(st.red, st.ev_chunk[c], 0));
                 const void *in[kMaxRanks];
                 char *own = st.rb_dev + (st.off[r] + c * st.chunk) * es;
                 for (int j = 0; j < P; ++j)
                     in[j] = j == r ? own : st.stage + (uint64_t(j) * st.L + c * st.chunk) * es;
-                if (int rc = esgd_reduce(s.dtype, P, in, own, n, st.stream)) return rc;
+                if (int rc = esgd_reduce(s.dtype, P, in, own, n, st.red)) return rc;
             }
-            ESGD_HIP(hipEventRecord(st.ev_red, st.stream));
-            ESGD_HIP(hipStreamWaitEvent(g_cs, st.ev_red, 0));
+            ESGD_HIP(hipEventRecord(st.ev_red, st.red));
+            ESGD_HIP(hipStreamWaitEvent(cs, st.ev_red, 0));
             ESGD_NCCL(ncclGroupStart());
             for (int j = 0; j < P; ++j) {
                 if (j == r) continue;
                 if (st.len[r]) ESGD_NCCL(ncclSend(st.rb_dev + st.off[r] * es, st.len[r] * es, ncclChar, j,
-                                                  g_nccl, g_cs));
+                                                  g_nccl, cs));
                 if (st.len[j]) ESGD_NCCL(ncclRecv(st.rb_dev + st.off[j] * es, st.len[j] * es, ncclChar, j,
-                                                  g_nccl, g_cs));
+                                                  g_nccl, cs));
             }
             ESGD_NCCL(ncclGroupEnd());
         }
-        ESGD_HIP(hipEventRecord(st.ev, g_cs));
-        return ESGD_SUCCESS;
+        return base_copy_out(s, st, cs);
     }
 
-    int all_gather(Sched &s) override {   // queued with the reduce-scatter above
-        RcclState &st = S(s);
-        ESGD_HIP(hipEventRecord(st.ev, st.stream));
-        return ESGD_SUCCESS;
-    }
-
-    int finish(Sched &s) override { return base_finish(s, S(s)); }
-    int query(Sched &s) override { return base_query(S(s)); }
+    int query(Sched &s) override { return base_query(s, S(s)); }
     int complete(Sched &s) override { return base_complete(s, S(s)); }
 
     void teardown(Sched &s) override {
         RcclState *st = static_cast<RcclState *>(s.tstate);
         if (!st) return;
-        if (g_cs) (void)hipStreamSynchronize(g_cs);
         if (st->stream) (void)hipStreamSynchronize(st->stream);
+        if (st->red) { (void)hipStreamSynchronize(st->red); (void)hipStreamDestroy(st->red); }
         if (st->stage) (void)hipFree(st->stage);
         for (hipEvent_t e : st->ev_chunk) (void)hipEventDestroy(e);
-        if (st->ev_snap) (void)hipEventDestroy(st->ev_snap);
         if (st->ev_red) (void)hipEventDestroy(st->ev_red);
         base_teardown(s, *st);
         delete st;

@@ -1,14 +1,15 @@
 // engine.cpp — partial-allreduce schedules, the round protocol and the progress thread.
 //
 // Per schedule and round t, every rank walks the same stages (engine.h: Stage):
-//   join -> snapshot (move sb -> rb)      -> publish ready[r]   = t
-//        -> all ready  -> reduce-scatter  -> publish reduced[r] = t
-//        -> all reduced -> all-gather     -> publish done[r]    = t
-//        -> all done   -> copy-out        -> completed = t, wake wait()
-// "Join" is decided by the activation rules of fflib2 (see engine.h).  The three
-// all-rank conditions are epochs in the node segment; they are what fflib2's matched
-// MPI send/recv pairs guarantee implicitly (src/colls/ffallreduce.c:145-162: a send of
-// rb happens after the previous comp, the comp after the recv).
+//   join (activation rules, prepare: host staging / buffer re-resolution)
+//     -> the last rank to join appends (schedule, t) to the node's issue ring
+//     -> every rank launches the ring's rounds in ring order: the whole round is queued
+//        on the GPU, whose own flag waits pair the ranks (dataplane.cpp)
+//     -> the round's completion event -> copy-out hook -> completed = t, wake wait().
+// "Join" is decided by the activation rules of fflib2 (see engine.h).  The pairing of
+// ranks is what fflib2's matched MPI send/recv pairs guarantee implicitly
+// (src/colls/ffallreduce.c:145-162: a send of rb after the previous comp, the comp after
+// the recv); here it costs no host round trip inside a round.
 #include "engine.h"
 
 #include <hip/hip_runtime.h>
@@ -19,6 +20,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <ctime>
 
 #include "esgd_internal.h"
 
@@ -124,6 +126,7 @@ int engine_finalize() {
         if (s->tp) s->tp->teardown(*s);
         free_sched(s);
     }
+    dataplane_shutdown();
     shm_detach(g_seg, nullptr, -1);
     g_seg = nullptr;
     g_next_id = 0;
@@ -136,6 +139,20 @@ int engine_finalize() {
 }
 
 // ---- schedules -------------------------------------------------------------------
+
+void gpu_trace_read(Sched &s, uint64_t out[6]);   // dataplane.cpp
+
+static uint64_t mono_ns() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+
+void Sched::mark(uint32_t round, int what) {   // caller holds mu
+    if (round == 0 || round > 65536) return;
+    if (tl.size() < round) tl.resize(std::max<size_t>(round, std::min<size_t>(65536, 2 * tl.size())));
+    tl[round - 1][what] = mono_ns();
+}
 
 static void fail_locked(Sched &s, int rc, const char *msg) {
     s.error = rc ? rc : ESGD_ERROR;
@@ -177,6 +194,7 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
         sh->last_activator.store(-1);
         for (int r = 0; r < kMaxRanks; ++r) {
             sh->ready[r].store(0); sh->reduced[r].store(0); sh->done[r].store(0);
+            sh->gpu_err[r].store(0);
             sh->joined[r].store(0); sh->activations[r].store(0);
         }
         sh->ready_count.store(0);
@@ -266,6 +284,7 @@ int sched_post(Sched *s, void *producer_stream, int *role) {
         if (producer_stream)
             if (int rc = s->tp->note_producer(*s, t, producer_stream)) return rc;
         s->posted.store(t, std::memory_order_release);
+        s->mark(t, 0);
         if (s->kind == KIND_MAJORITY) {
             // colls/ffrand_allreduce.c:88 — the same glibc draw on every rank
             const int act = int(unsigned(rand_r(&s->seed)) % unsigned(s->world));
@@ -307,6 +326,7 @@ int sched_wait(Sched *s) {
     }
     if (s->error) { set_error("%s", s->errmsg); return s->error; }
     s->waited = target;
+    s->mark(target, 5);
     return ESGD_SUCCESS;
 }
 
@@ -351,12 +371,6 @@ Sched *sched_lookup(uint64_t handle) {
 
 // ---- the progress step -------------------------------------------------------------
 
-static bool all_at_least(const std::atomic<uint32_t> *v, int world, uint32_t round) {
-    for (int r = 0; r < world; ++r)
-        if (v[r].load(std::memory_order_acquire) < round) return false;
-    return true;
-}
-
 static bool step(Sched &s) {
     std::lock_guard<std::mutex> lk(s.mu);
     if (s.error || !s.live.load()) return false;
@@ -370,13 +384,6 @@ static bool step(Sched &s) {
         }
         return true;
     };
-    auto timed_out = [&](const char *what) {
-        if (now_s() - s.stage_t0 > g_timeout) {
-            fail_locked(s, ESGD_ERROR, what);
-            return true;
-        }
-        return false;
-    };
     switch (s.stage) {
     case ST_IDLE: {
         const uint32_t next = s.joined + 1;
@@ -387,74 +394,50 @@ static bool step(Sched &s) {
         s.cur = next;
         s.cur_fresh = posted >= next;
         s.joined = next;
+        s.mark(next, 1);
         sh->joined[s.rank].store(next, std::memory_order_release);
         if (s.cur_fresh) ++s.n_fresh; else ++s.n_auto;
         if (s.log.size() < 65536)
             s.log.push_back({next, uint8_t(s.cur_fresh), uint8_t(sync),
                              int16_t(sync ? -1 : activator_of(sh, next))});
-        if (!check(s.tp->snapshot(s, next, s.cur_fresh), "snapshot")) return true;
-        enter(ST_SNAPSHOT);
-        return true;
-    }
-    case ST_SNAPSHOT: {
-        int q = s.tp->query(s);
-        if (!check(q, "snapshot")) return true;
-        if (!q) return false;
-        sh->ready[s.rank].store(s.cur, std::memory_order_release);
-        if (s.tp->ordered()) {
-            enter(ST_WAIT_TICKET);
-            // the rank whose publication completes the round appends it to the ring
-            const uint32_t prev = sh->ready_count.fetch_add(1, std::memory_order_acq_rel);
-            if (prev + 1 == s.cur * uint32_t(s.world)) {
-                const uint64_t tk = g_seg->ticket_next.fetch_add(1, std::memory_order_acq_rel);
-                TicketSlot &slot = g_seg->ring[tk % kRing];
-                slot.sched = uint32_t(s.id);
-                slot.round = s.cur;
-                slot.tag.store(tk + 1, std::memory_order_release);
-            }
-            return true;
+        if (!check(s.tp->prepare(s, next, s.cur_fresh), "join")) return true;
+        enter(ST_WAIT_TICKET);
+        // the rank whose join completes the round appends it to the issue ring (every
+        // rank has joined round t-1 of this schedule before any joins round t)
+        const uint32_t prev = sh->ready_count.fetch_add(1, std::memory_order_acq_rel);
+        if (prev + 1 == next * uint32_t(s.world)) {
+            const uint64_t tk = g_seg->ticket_next.fetch_add(1, std::memory_order_acq_rel);
+            TicketSlot &slot = g_seg->ring[tk % kRing];
+            slot.sched = uint32_t(s.id);
+            slot.round = next;
+            slot.tag.store(tk + 1, std::memory_order_release);
         }
-        enter(ST_WAIT_READY);
         return true;
     }
     case ST_WAIT_TICKET:
-        return timed_out("round never reached its turn in the issue ring") ? true : false;
-    case ST_WAIT_READY:
-        if (!all_at_least(sh->ready, s.world, s.cur)) return timed_out("peers never published their snapshot");
-        if (!check(s.tp->reduce_scatter(s), "reduce-scatter")) return true;
-        enter(ST_RS);
-        return true;
-    case ST_RS: {
-        int q = s.tp->query(s);
-        if (!check(q, "reduce-scatter")) return true;
-        if (!q) return false;
-        sh->reduced[s.rank].store(s.cur, std::memory_order_release);
-        enter(ST_WAIT_REDUCED);
-        return true;
-    }
-    case ST_WAIT_REDUCED:
-        if (!all_at_least(sh->reduced, s.world, s.cur)) return timed_out("peers never finished reduce-scatter");
-        if (!check(s.tp->all_gather(s), "all-gather")) return true;
-        enter(ST_AG);
-        return true;
-    case ST_AG: {
-        int q = s.tp->query(s);
-        if (!check(q, "all-gather")) return true;
-        if (!q) return false;
-        sh->done[s.rank].store(s.cur, std::memory_order_release);
-        enter(ST_WAIT_DONE);
-        return true;
-    }
-    case ST_WAIT_DONE:
-        if (!all_at_least(sh->done, s.world, s.cur)) return timed_out("peers never finished all-gather");
-        if (!check(s.tp->finish(s), "copy-out")) return true;
-        enter(ST_FINISH);
-        return true;
-    case ST_FINISH: {
-        int q = s.tp->query(s);
-        if (!check(q, "copy-out")) return true;
-        if (!q) return false;
-        if (!check(s.tp->complete(s), "copy-out")) return true;
+        if (now_s() - s.stage_t0 > g_timeout)
+            fail_locked(s, ESGD_ERROR, "not every rank joined the round (a peer never posted / activated?)");
+        return false;
+    case ST_INFLIGHT: {
+        const int q = s.tp->query(s);
+        if (!check(q, "round")) return true;
+        if (!q) {
+            // the GPU's flag waits give up after the timeout and complete the round with
+            // an error flag; this is the host's backstop
+            if (now_s() - s.stage_t0 > 1.5 * g_timeout + 5) {
+                std::string m = "round did not finish on the GPU " + s.tp->diagnose(s);
+                fail_locked(s, ESGD_ERROR, m.c_str());
+                return true;
+            }
+            return false;
+        }
+        s.mark(s.cur, 4);
+        if (s.cur <= s.tl.size()) {
+            uint64_t g[6];
+            gpu_trace_read(s, g);
+            for (int k = 0; k < 6; ++k) s.tl[s.cur - 1][6 + k] = g[k];
+        }
+        if (!check(s.tp->complete(s), "round")) return true;
         s.completed = s.cur;
         s.stage = ST_IDLE;
         s.cv.notify_all();
@@ -464,7 +447,7 @@ static bool step(Sched &s) {
     return false;
 }
 
-// Issue ordered rounds strictly in ring order (same sequence on every rank).
+// Launch rounds strictly in ring order (the same sequence on every rank).
 static bool pump_tickets(const std::vector<Sched *> &snap) {
     if (!g_seg) return false;
     bool any = false;
@@ -477,13 +460,22 @@ static bool pump_tickets(const std::vector<Sched *> &snap) {
         if (!target) break;                      // schedule not registered here yet
         {
             std::lock_guard<std::mutex> lk(target->mu);
-            if (target->stage != ST_WAIT_TICKET || target->cur != slot.round) break;
-            int rc = target->tp->reduce_scatter(*target);
-            if (rc < 0) {
-                fail_locked(*target, rc, esgd_last_error());
+            if (target->error) {
+                // a failed schedule still consumes its tickets (its peers fail the same
+                // round by timeout); later rounds of other schedules must not stall
+            } else if (target->stage != ST_WAIT_TICKET || target->cur != slot.round) {
+                break;
             } else {
-                target->stage = ST_RS;
-                target->stage_t0 = now_s();
+                target->mark(target->cur, 2);
+                int rc = target->tp->launch(*target, target->cur, target->cur_fresh);
+                target->mark(target->cur, 3);
+                if (rc < 0) {
+                    std::string m = std::string("launch: ") + esgd_last_error();
+                    fail_locked(*target, rc, m.c_str());
+                } else {
+                    target->stage = ST_INFLIGHT;
+                    target->stage_t0 = now_s();
+                }
             }
         }
         {

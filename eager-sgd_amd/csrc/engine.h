@@ -20,10 +20,12 @@
 // counter per schedule in shared memory plays the role of the op versions.
 #pragma once
 
+#include <array>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "esgd.h"
@@ -35,39 +37,34 @@ enum Kind { KIND_ALLREDUCE = 0, KIND_SOLO = 1, KIND_MAJORITY = 2 };
 
 enum Stage {
     ST_IDLE = 0,      // between rounds
-    ST_SNAPSHOT,      // move sb -> rb queued
-    ST_WAIT_READY,    // waiting for every rank's snapshot
-    ST_WAIT_TICKET,   // ordered transports: waiting for this round's turn in the ring
-    ST_RS,            // reduce-scatter queued
-    ST_WAIT_REDUCED,  // waiting for every rank's reduced shard
-    ST_AG,            // all-gather queued
-    ST_WAIT_DONE,     // waiting for every rank's gather (buffers free again)
-    ST_FINISH,        // copy-out queued
+    ST_WAIT_TICKET,   // joined; waiting for this round's turn in the node's issue ring
+    ST_INFLIGHT,      // the whole round is queued on the GPU (or moving nothing)
 };
 
 struct Sched;
 
-// Data movement of one round.  Every step only *queues* work; query() reports whether
-// the last queued step has finished (1), is pending (0) or failed (< 0).
+// Data movement of one round.  A round is joined on the host (activation rules,
+// buffer re-resolution, host staging: prepare()), then queued on the GPU as a whole
+// (launch()), in one node-wide order: every rank launches the rounds of all schedules
+// in the same sequence (the issue ring), so the GPU-side waits of one round can never
+// wait on a round that a peer queued behind another wait.  query() reports whether the
+// launched round has finished (1), is pending (0) or failed (< 0).
 struct Transport {
     virtual ~Transport() {}
     virtual const char *name() const = 0;
-    // true: collectives must be issued in one global order (RCCL); reduce_scatter() is
-    // then called from the ticket pump in ring order instead of at "all ready".
-    virtual bool ordered() const { return false; }
     // creation, in two voted steps: setup() is local (buffers, streams, publishing
     // this rank's bucket); connect() runs once every rank's setup() succeeded (mapping
     // peers, communicator bring-up).  A failure in either fails the creation on all ranks.
     virtual int setup(Sched &s) = 0;
     virtual int connect(Sched &) { return ESGD_SUCCESS; }
     virtual int note_producer(Sched &s, uint32_t round, void *stream) = 0;
-    virtual int snapshot(Sched &s, uint32_t round, bool fresh) = 0;
-    virtual int reduce_scatter(Sched &s) = 0;
-    virtual int all_gather(Sched &s) = 0;
-    virtual int finish(Sched &s) = 0;
+    virtual int prepare(Sched &s, uint32_t round, bool fresh) = 0;
+    virtual int launch(Sched &s, uint32_t round, bool fresh) = 0;
     virtual int query(Sched &s) = 0;
     // host-side work once the copy-out has landed (before wait() returns)
     virtual int complete(Sched &) { return ESGD_SUCCESS; }
+    // why a launched round has not finished (timeouts), "" if unknown
+    virtual std::string diagnose(Sched &) { return std::string(); }
     virtual void teardown(Sched &s) = 0;
 };
 
@@ -111,6 +108,10 @@ struct Sched {
     uint32_t passive = 0;      // majority: passive rounds since the last activation
     uint64_t n_fresh = 0, n_auto = 0, n_activated = 0;
     std::vector<RoundLog> log;
+    // per-round timeline (CLOCK_MONOTONIC ns, comparable across the node's processes):
+    // post, join, launch start, launch queued, completion seen, wait returned
+    std::vector<std::array<uint64_t, 12>> tl;   // [6..11]: GPU spans (ESGD_GPU_TRACE=1)
+    void mark(uint32_t round, int what);
     std::atomic<bool> live{true};
 };
 
@@ -142,11 +143,15 @@ int sched_test(Sched *s, int *flag);
 int sched_delete(Sched *s);
 Sched *sched_lookup(uint64_t handle);
 
-// Issue log of ordered transports: (schedule id, round) in the order this rank issued.
+// Issue log: (schedule id, round) in the order this rank launched rounds.
 int engine_issue_log(uint32_t *sched, uint32_t *round, uint32_t cap, uint32_t *n);
 
 // One polling pass over all schedules (the progress thread calls it in a loop; tests
 // without a thread may call it directly).  Returns true if anything advanced.
 bool engine_progress_once();
+
+// Data-plane resources shared by all schedules of the process (dataplane.cpp): freed at
+// finalize, before the node segment is unmapped.
+void dataplane_shutdown();
 
 }  // namespace esgd

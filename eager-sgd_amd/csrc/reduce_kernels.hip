@@ -490,6 +490,45 @@ int gather_remote(int n, const void *const *src, void *const *dst, const uint64_
     return ESGD_SUCCESS;
 }
 
+// Rank pairing inside a queued round: publish `value` in this rank's flag, then wait
+// until every rank's flag has reached it.  The flags live in host memory shared by the
+// ranks' processes (the registered node segment), written and read at system scope; one
+// lane does it all.  The release fence makes this GPU's earlier writes (the previous
+// kernel's shard) visible before the flag is.  A wait that outlives `timeout` ticks of
+// the constant wall clock records the round in *err and returns, so a missing peer never
+// leaves a wave spinning on the device.
+__global__ void __launch_bounds__(64) k_round_sync(uint32_t *flags, int rank, int world,
+                                                   uint32_t value, long long timeout,
+                                                   uint32_t *err, uint64_t *ts) {
+    if (threadIdx.x != 0) return;
+    if (ts) ts[0] = uint64_t(wall_clock64());
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(&flags[rank], value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const long long t0 = wall_clock64();
+    for (int q = 0; q < world; ++q) {
+        // unsigned distance: rounds are compared modulo 2^32
+        while (int32_t(__hip_atomic_load(&flags[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - value) < 0) {
+            if (wall_clock64() - t0 > timeout) {
+                __hip_atomic_store(err, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (ts) __hip_atomic_store(&ts[1], uint64_t(wall_clock64()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ts (optional): wall-clock stamps of entry and exit (tracing, ESGD_GPU_TRACE=1)
+int round_sync(uint32_t *flags, int rank, int world, uint32_t value, long long timeout_ticks,
+               uint32_t *err, uint64_t *ts, hipStream_t s) {
+    ESGD_ARG(flags && err && world >= 1 && rank >= 0 && rank < world, "round_sync: bad arguments");
+    hipLaunchKernelGGL(k_round_sync, dim3(1), dim3(64), 0, s, flags, rank, world, value,
+                       timeout_ticks, err, ts);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
 }  // namespace esgd
 
 using namespace esgd;

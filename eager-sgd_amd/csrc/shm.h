@@ -37,12 +37,16 @@ struct alignas(64) SchedShm {
     // per-round activation record, (round << 32) | (rank + 1), claimed by CAS BEFORE
     // `activated` is raised: whoever sees activated >= t also sees round t's activator
     std::atomic<uint64_t> act_of[256];
-    std::atomic<uint32_t> ready[kMaxRanks];   // round whose input snapshot rank r has published
-    std::atomic<uint32_t> reduced[kMaxRanks]; // round whose phase 1 (reduce-scatter) is done
-    std::atomic<uint32_t> done[kMaxRanks];    // round whose phase 2 (all-gather) is done
+    // GPU flags (written by the GPUs through the host-registered segment, system scope):
+    alignas(64) std::atomic<uint32_t> ready[kMaxRanks];   // round whose snapshot rank r has made
+    alignas(64) std::atomic<uint32_t> reduced[kMaxRanks]; // round whose reduce-scatter is done
+    alignas(64) std::atomic<uint32_t> done[kMaxRanks];    // round whose all-gather is done
+    alignas(64) std::atomic<uint32_t> gpu_err[kMaxRanks]; // round whose flag wait timed out
+    // ESGD_GPU_TRACE=1: wall-clock (entry, exit) of the three pairings of the last round
+    alignas(64) uint64_t gpu_ts[kMaxRanks][6];
     std::atomic<uint32_t> joined[kMaxRanks];  // diagnostics: last round rank r joined
     std::atomic<uint32_t> activations[kMaxRanks];  // diagnostics: rounds activated by r
-    std::atomic<uint32_t> ready_count;   // ordered transports: sum of ready publications
+    std::atomic<uint32_t> ready_count;   // joins so far, all ranks (issue-ring append)
     std::atomic<uint32_t> setup_err;     // ranks whose registration failed (creation vote)
     IpcSlot slot[kMaxRanks];
 };

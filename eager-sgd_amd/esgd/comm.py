@@ -49,6 +49,7 @@ def _bind(h):
         "esgd_schedule_log": (i, [u64, C.POINTER(u32), C.POINTER(C.c_uint8), C.POINTER(C.c_uint8),
                                   C.POINTER(C.c_int16), u32, C.POINTER(u32)]),
         "esgd_schedule_stream": (i, [u64, C.POINTER(vp)]),
+        "esgd_schedule_timeline": (i, [u64, C.POINTER(u64), u32, C.POINTER(u32)]),
         "esgd_set_transport": (i, [C.c_char_p]),
         "esgd_comm_issue_log": (i, [C.POINTER(u32), C.POINTER(u32), u32, C.POINTER(u32)]),
     }
@@ -189,6 +190,18 @@ class Schedule:
         check(lib().esgd_schedule_log(self.handle, r, f, s, a, cap, C.byref(n)))
         return [{"round": r[i], "fresh": bool(f[i]), "sync": bool(s[i]), "activator": a[i]}
                 for i in range(min(cap, n.value))]
+
+    def timeline(self):
+        """Per completed round (numpy uint64, rounds x 12): CLOCK_MONOTONIC ns of post,
+        join, launch start, launch queued, completion seen, wait returned; then GPU spans
+        in ns (ESGD_GPU_TRACE=1): ready wait, reduce-scatter, reduced wait, all-gather,
+        done wait, total."""
+        n = C.c_uint32()
+        check(lib().esgd_schedule_timeline(self.handle, None, 0, C.byref(n)))
+        out = np.zeros((max(1, n.value), 12), np.uint64)
+        check(lib().esgd_schedule_timeline(self.handle, out.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                           n.value, C.byref(n)))
+        return out[: n.value]
 
     def stream(self) -> int:
         v = C.c_void_p()

@@ -176,7 +176,14 @@ int esgd_schedule_stats(esgd_sched_h h, esgd_sched_stats_t *out);
  * activator (-1 for synchronous rounds).  Writes up to cap entries, *n = total. */
 int esgd_schedule_log(esgd_sched_h h, uint32_t *rounds, uint8_t *fresh, uint8_t *sync,
                       int16_t *activator, uint32_t cap, uint32_t *n);
-/* the data-plane stream of a device schedule (consumers of rb may wait on it) */
+/* per-round timeline of this rank (tracing): 12 values per completed round -- 6
+ * CLOCK_MONOTONIC ns stamps: post, join, launch start, launch queued, completion seen,
+ * wait returned (0 = did not happen, e.g. no post for a round joined on activation);
+ * then, with ESGD_GPU_TRACE=1 and P > 1, 6 GPU spans in ns: wait at the ready pairing,
+ * reduce-scatter, wait at the reduced pairing, all-gather, wait at the done pairing,
+ * first pairing to last.  Writes up to cap rounds (12*cap values), *n = rounds available. */
+int esgd_schedule_timeline(esgd_sched_h h, uint64_t *t, uint32_t cap, uint32_t *n);
+/* the stream rounds run on (consumers of rb may wait on it) */
 int esgd_schedule_stream(esgd_sched_h h, void **stream);
 
 #ifdef __cplusplus

@@ -107,10 +107,14 @@ def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0
 
 
 def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0, buf="device",
-                  in_place=False, transport="ipc"):
+                  in_place=False, transport="ipc", shadow_ranks=()):
     """Data plane on the GPU: every rank reduces its splitmix bucket; returns the
-    result bytes' digest per round plus a bit-exactness verdict against the oracle."""
+    result bytes' digest per round plus a bit-exactness verdict against the oracle.
+    shadow_ranks: ranks whose device buckets go through the owned shadow bucket."""
     import numpy as np
+
+    if rank in shadow_ranks:
+        os.environ["ESGD_SHADOW"] = "1"
 
     from esgd import _lib
     from esgd import device as dev
@@ -288,3 +292,25 @@ def cp_ordered(rank, world, nsched=3, rounds=6, seed=7):
     comm.set_transport("ipc")
     comm.finalize()
     return log
+
+
+def cp_create_failure(rank, world, bad_rank=1):
+    """A creation that fails on one rank fails on every rank (voted registration), and
+    the communicator stays usable: the next creation and its rounds work."""
+    from esgd import comm
+    from esgd._lib import EsgdError
+    comm.init()
+    kind = comm.MAJORITY if rank == bad_rank else comm.SOLO   # creation order mismatch
+    err = None
+    try:
+        comm.Schedule(kind, None, None, 0, async_=2, buf=comm.BUF_NONE)
+    except EsgdError as e:
+        err = str(e)
+    t0 = time.time()
+    s = comm.Schedule(comm.ALLREDUCE, None, None, 0, buf=comm.BUF_NONE)
+    for _ in range(3):
+        s.post()
+        s.wait()
+    s.delete()
+    comm.finalize()
+    return {"err": err, "recovered_s": time.time() - t0}

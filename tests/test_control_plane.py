@@ -94,3 +94,19 @@ def test_ordered_transport_same_issue_order_everywhere(world):
     for sid in range(4):   # rounds of one schedule appear in order
         rs = [r for s, r in logs[0] if s == sid]
         assert rs == sorted(rs) == list(range(1, 6))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_failed_creation_fails_every_rank(world):
+    # registration is voted (engine.cpp sched_create): one rank's failure is every
+    # rank's failure, with no rank left waiting for a peer's publication
+    outs = run("cp_create_failure", world, bad_rank=world - 1)
+    for r, o in enumerate(outs):
+        assert o["err"] is not None, (r, o)
+        if r == world - 1:
+            assert "differs from rank 0" in o["err"]
+        elif r != 0:
+            pass   # either its own mismatch view or the vote's message
+        else:
+            assert "another rank failed" in o["err"]
+        assert o["recovered_s"] < 30

@@ -79,3 +79,11 @@ def test_rccl_transport_single_rank(kind):
         verdicts = run("gpu_allreduce", 1, count=300007, rounds=3, kind=kind, buf=buf,
                        transport="rccl")
         assert all(all(v) for v in verdicts), (buf, verdicts)
+
+
+@pytest.mark.parametrize("in_place", [False, True])
+def test_shadowed_device_buckets(in_place):
+    # a rank whose device bucket cannot be exported reduces through an owned shadow
+    # bucket (copy in at the snapshot, out at the finish); mixed with direct ranks
+    verdicts = run("gpu_allreduce", 3, count=200003, rounds=2, in_place=in_place, shadow_ranks=(1,))
+    assert all(all(v) for v in verdicts), verdicts

@@ -1,6 +1,7 @@
 # One GPU session: parity tests, bench (with PMC traffic), rocprof kernel stats,
 # and a 2-rank rehearsal of the N>1 path on the single GPU.
 set -e
+export ESGD_TIMEOUT_S=60
 O=gpurun_out/$1; mkdir -p $O
 timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
