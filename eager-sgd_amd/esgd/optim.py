@@ -11,6 +11,13 @@ gradient divided by the comm size (:40) through one eager-SGD op instance per te
 and hands the partially reduced gradients to the wrapped optimizer.  The op runs on the
 device (allreducef_forward_cuda): the gradient never leaves HBM, unlike the reference's
 CPU-only TF kernel (deep500/frameworks/tensorflow/custom_operators/tf.py:80).
+
+fuse=True (SURVEY.md §8(f) "bucket fusion"): the reference runs one schedule per tensor,
+161 per ResNet-50 step (opt_esgd_solo_imagenet_imbalance.py:85-248), each a
+host-blocking post/wait.  Fused, the scaled gradients are packed in the same reversed
+order into ONE persistent HBM bucket, reduced by one round and unpacked.  The reduction
+is element-wise, so every element meets the same operands in the same tree order: the
+result is bit-identical to the per-tensor path.
 """
 from __future__ import annotations
 
@@ -21,7 +28,7 @@ from . import deep500
 
 class EagerSGDOptimizer:
     def __init__(self, optimizer, comm_size: int, mode: str = "solo", async_: int = 32,
-                 seed: int = 6545343):
+                 seed: int = 6545343, fuse: bool = False):
         if mode not in deep500.MODES:
             raise ValueError(f"mode must be one of {sorted(deep500.MODES)}")
         if comm_size < 1:
@@ -29,7 +36,9 @@ class EagerSGDOptimizer:
         self.optimizer = optimizer
         self.comm_size = int(comm_size)
         self.mode, self.async_, self.seed = mode, int(async_), int(seed)
+        self.fuse = bool(fuse)
         self._ops = {}          # parameter -> op instance (one bucket per tensor)
+        self._fused = None      # (layout, op, packed bucket, reduced bucket)
         self._configured = False
 
     # -- the reference's two-call protocol ------------------------------------------
@@ -44,20 +53,56 @@ class EagerSGDOptimizer:
             deep500.configure(self.mode, self.async_, self.seed)
             self._configured = True
         stream = torch.cuda.current_stream().cuda_stream
-        for grad, var in reversed(list(grads_and_vars)):
-            if grad is None:          # the reference would still feed None (:35-42); skip
-                continue
-            op = self._ops.get(var)
-            if op is None:
-                op = self._ops[var] = deep500.AllreduceOp(tuple(grad.shape))
-            scaled = (grad.float() / self.comm_size).contiguous()        # :40
-            out = torch.empty_like(scaled)
-            op.forward_cuda(scaled, out, stream)
-            var.grad = out.to(grad.dtype).view_as(grad)
+        gvs = list(grads_and_vars)
+        if self.fuse:
+            self._apply_fused(gvs, stream)
+        else:
+            for grad, var in reversed(gvs):
+                if grad is None:      # the reference would still feed None (:35-42); skip
+                    continue
+                op = self._ops.get(var)
+                if op is None:
+                    op = self._ops[var] = deep500.AllreduceOp(tuple(grad.shape))
+                scaled = (grad.float() / self.comm_size).contiguous()        # :40
+                out = torch.empty_like(scaled)
+                op.forward_cuda(scaled, out, stream)
+                var.grad = out.to(grad.dtype).view_as(grad)
         r = self.optimizer.step()
         if global_step is not None and hasattr(global_step, "add_"):
             global_step.add_(1)
         return r
+
+    def _apply_fused(self, gvs, stream):
+        import torch
+        live = [(g, v) for g, v in reversed(gvs) if g is not None]
+        if not live:
+            return
+        layout = tuple((id(v), g.numel()) for g, v in live)
+        if self._fused is None:
+            total = sum(n for _, n in layout)
+            flat = torch.empty(total, dtype=torch.float32, device=live[0][0].device)
+            # one persistent schedule, created collectively at the first step (the
+            # reference creates its bucket schedules lazily too, :288-298)
+            self._fused = (layout, deep500.AllreduceOp((total,)), flat, torch.empty_like(flat))
+        elif self._fused[0] != layout:
+            raise RuntimeError("EagerSGDOptimizer(fuse=True): the set of gradients changed, "
+                               "but the fused bucket's schedule is persistent")
+        _, op, flat, out = self._fused
+        off = 0
+        for g, _ in live:                                        # pack, scaled as in :40
+            n = g.numel()
+            torch.div(g.reshape(-1).float(), self.comm_size, out=flat[off:off + n])
+            off += n
+        op.forward_cuda(flat, out, stream)
+        off = 0
+        for g, v in live:                                        # unpack into the grads
+            n = g.numel()
+            red = out[off:off + n].view(g.shape)
+            if g.dtype == torch.float32 and g.is_contiguous():
+                g.copy_(red)
+            else:
+                v.grad = red.to(g.dtype).clone()
+            off += n
 
     # -- torch.optim-style convenience ---------------------------------------------
     def step(self, closure=None):
@@ -74,4 +119,7 @@ class EagerSGDOptimizer:
         return self.optimizer.param_groups
 
     def bytes_reduced(self) -> int:
-        return sum(op.report() for op in self._ops.values())
+        n = sum(op.report() for op in self._ops.values())
+        if self._fused is not None:
+            n += self._fused[1].report()
+        return n

@@ -227,7 +227,7 @@ def op_host(rank, world, mode="allreduce", steps=3, count=5000):
     return {"ok": ok, "report": rep, "cuda": op.supports_cuda()}
 
 
-def optimizer_step(rank, world, mode="allreduce", steps=2):
+def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False):
     """EagerSGDOptimizer on PyTorch-ROCm: every rank's p.grad after apply_gradients must
     equal the oracle tree of (grad_r / P) over ranks, bit for bit."""
     import numpy as np
@@ -240,7 +240,8 @@ def optimizer_step(rank, world, mode="allreduce", steps=2):
     torch.manual_seed(1234)
     dev = torch.device("cuda", 0)
     model = torch.nn.Sequential(torch.nn.Linear(64, 48), torch.nn.ReLU(), torch.nn.Linear(48, 10)).to(dev)
-    opt = EagerSGDOptimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9), world, mode=mode)
+    opt = EagerSGDOptimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9), world, mode=mode,
+                            fuse=fuse)
     ok = []
     for t in range(steps):
         g = torch.Generator().manual_seed(100 * t + rank)

@@ -18,9 +18,12 @@ def test_deep500_op_host_path(mode):
             assert all(o["ok"]), o
 
 
+@pytest.mark.parametrize("fuse", [False, True])
 @pytest.mark.parametrize("mode", ["allreduce", "solo"])
-def test_eager_sgd_optimizer(mode):
-    outs = run("optimizer_step", 2, mode=mode, steps=2)
+def test_eager_sgd_optimizer(mode, fuse):
+    # fuse=True packs every gradient into one bucket (one round per step): the same
+    # bits as one round per tensor
+    outs = run("optimizer_step", 2, mode=mode, steps=2, fuse=fuse)
     for o in outs:
         if mode == "allreduce":
             assert all(o["ok"]), o["ok"]
