@@ -257,31 +257,62 @@ def _max_over_ranks(x: float) -> float:
     return float(t.item())
 
 
-def sweep_c5(comm, dev, world, dt, es, iters=10):
-    """C5: majority-allreduce of one bucket per rank, 64 KiB .. 1 GiB (every 4x), per
-    size the max-over-ranks mean round time of `iters` back-to-back rounds."""
+def sweep_c5(comm, dev, world, dt, es):
+    """C5: majority-allreduce of one bucket per rank, 64 KiB .. 1 GiB (every 4x).  Per
+    size: `iters` back-to-back rounds, each timed post -> wait on every rank; a round's
+    time is its max over ranks; reported: the median round and the mean round."""
+    import statistics
+
+    import torch
+    import torch.distributed as dist
     out = []
     for lg in range(16, 31, 2):
         nbytes = 1 << lg
+        iters = 40 if nbytes <= (16 << 20) else (16 if nbytes <= (256 << 20) else 8)
         count = nbytes // es
         buf = dev.DeviceBuffer(count, dt)
         dev.fill_uniform(buf, SEED, comm.rank())
         dev.synchronize()
         sch = comm.Schedule(comm.MAJORITY, None, buf, count, dtype=dt, seed=6545343,
                             buf=comm.BUF_DEVICE)
-        for _ in range(3):
+        for _ in range(5):
             sch.post(); sch.wait()
         comm.barrier()
-        t0 = time.perf_counter()
+        ts = []
         for _ in range(iters):
+            t0 = time.perf_counter()
             sch.post(); sch.wait()
-        t = _max_over_ranks((time.perf_counter() - t0) / iters)
+            ts.append(time.perf_counter() - t0)
+        tt = torch.tensor(ts, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        ts = tt.tolist()
+        t, mean = statistics.median(ts), statistics.fmean(ts)
+        stages = _stages_us(sch.timeline()[-iters:])
         sch.delete()
         buf.close()
         t_min = 2 * nbytes / (world * XGMI_LINK_GBS * 1e9)
-        out.append({"bytes": nbytes, "us": round(t * 1e6, 1), "algbw_GBs": round(nbytes / t / 1e9, 2),
+        out.append({"bytes": nbytes, "us": round(t * 1e6, 1), "mean_us": round(mean * 1e6, 1),
+                    "algbw_GBs": round(nbytes / t / 1e9, 2),
                     "busbw_GBs": round(nbytes / t / 1e9 * 2 * (world - 1) / world, 2),
-                    "xgmi_frac": round(t_min / t, 4)})
+                    "xgmi_frac": round(t_min / t, 4), "rounds": iters,
+                    "rank0_stages_us": stages})
+    return out
+
+
+def _stages_us(tl):
+    """Median per-round host timeline of this rank (esgd_schedule_timeline), in us:
+    post->join, join->launch, launch (host), launched->completion seen, ->wait returned."""
+    import numpy as np
+    tl = tl.astype(np.int64)
+    tl = tl[(tl[:, 0] > 0) & (tl[:, 5] > 0)]
+    if not len(tl):
+        return None
+    names = ["post_join", "join_launch", "launch_host", "gpu_round", "wake"]
+    d = [tl[:, i + 1] - tl[:, i] for i in range(5)]
+    out = {n: round(float(np.median(x)) / 1e3, 1) for n, x in zip(names, d)}
+    if tl[:, 11].any():   # ESGD_GPU_TRACE=1: spans measured on the GPU
+        gn = ["g_wait_ready", "g_rs", "g_wait_reduced", "g_ag", "g_wait_done"]
+        out.update({n: round(float(np.median(tl[:, 6 + i])) / 1e3, 1) for i, n in enumerate(gn)})
     return out
 
 
@@ -386,6 +417,7 @@ def run_allreduce(args, rank, world):
     wall = float(el.item())
     t_step = wall / args.steps
     stats = sched.stats()
+    stages = _stages_us(sched.timeline()[-args.steps:])
 
     # parity outside the timed region: fresh inputs, one round, slices vs the oracle
     parity = "skipped"
@@ -446,6 +478,7 @@ def run_allreduce(args, rank, world):
                      "frac": round(link_in / (XGMI_LINK_GBS * (world - 1)), 4), "traffic": None},
         "rounds": {"fresh": stats["fresh_rounds"], "auto": stats["auto_rounds"],
                    "activations_rank0": stats["activations"]},
+        "rank0_stages_us": stages,
         "parity": parity,
     }
     line.update(extras)

@@ -39,6 +39,16 @@ int gather_remote(int n, const void *const *src, void *const *dst, const uint64_
                   hipStream_t s);
 
 // ---- IPC mapping cache: one hipIpcOpenMemHandle per (peer, allocation) ----
+// Mappings are not closed when the last schedule using them goes: they stay open, idle,
+// until the data plane shuts down.  Measured on MI355X (tools/lat.sh, LAT_NOFREE=1): once
+// a process has closed an IPC mapping, every later kernel that reads peer memory through
+// IPC pays +20..80 us (a 64 KiB round went from 41 us to 138-200 us).
+// An idle mapping is reused only for the same export: the exporter tags each exported
+// allocation with a serial that stays the same only while one of its schedules keeps the
+// allocation published (IpcSlot::serial), so a freed-and-reallocated bucket whose handle
+// bytes happen to repeat is never served from a stale mapping; such a stale idle mapping
+// is closed before the handle is opened again.
+// ESGD_IPC_EAGER_CLOSE=1 restores closing at the last release (A/B runs).
 struct IpcKey {
     int peer;
     uint8_t h[64];
@@ -47,37 +57,82 @@ struct IpcKey {
         return std::memcmp(h, o.h, 64) < 0;
     }
 };
-struct IpcEntry { void *base; int refs; };
+struct IpcEntry { void *base; int refs; uint64_t serial; };
 static std::mutex g_ipc_mu;
 static std::map<IpcKey, IpcEntry> g_ipc;
 
-static int ipc_open(int peer, const uint8_t *h, void **base) {
+static int ipc_open(int peer, const uint8_t *h, uint64_t serial, void **base) {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
     IpcKey k;
     k.peer = peer;
     std::memcpy(k.h, h, 64);
     auto it = g_ipc.find(k);
-    if (it != g_ipc.end()) { ++it->second.refs; *base = it->second.base; return ESGD_SUCCESS; }
+    if (it != g_ipc.end()) {
+        if (it->second.refs > 0 || it->second.serial == serial) {
+            ++it->second.refs;
+            it->second.serial = serial;
+            *base = it->second.base;
+            return ESGD_SUCCESS;
+        }
+        (void)hipIpcCloseMemHandle(it->second.base);   // idle, and a different export
+        g_ipc.erase(it);
+    }
     hipIpcMemHandle_t hh;
     std::memcpy(&hh, h, sizeof(hh));
     void *p = nullptr;
     ESGD_HIP(hipIpcOpenMemHandle(&p, hh, hipIpcMemLazyEnablePeerAccess));
-    g_ipc[k] = {p, 1};
+    g_ipc[k] = {p, 1, serial};
     *base = p;
     return ESGD_SUCCESS;
 }
 
 static void ipc_close(void *base) {
+    static const bool eager = getenv("ESGD_IPC_EAGER_CLOSE") && *getenv("ESGD_IPC_EAGER_CLOSE") == '1';
     std::lock_guard<std::mutex> lk(g_ipc_mu);
     for (auto it = g_ipc.begin(); it != g_ipc.end(); ++it) {
         if (it->second.base == base) {
-            if (--it->second.refs == 0) {
+            if (--it->second.refs == 0 && eager) {
                 (void)hipIpcCloseMemHandle(base);
                 g_ipc.erase(it);
             }
             return;
         }
     }
+}
+
+// Exporter side: allocations this process has published, base -> (serial, schedules
+// publishing it).  A serial is reused only while the allocation stays published.
+struct ExportEntry { uint8_t h[64]; uint64_t serial; int live; };
+static std::map<void *, ExportEntry> g_exports;
+static uint64_t g_export_serial = 0;
+
+static uint64_t export_acquire(void *base, const uint8_t *h) {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    auto it = g_exports.find(base);
+    if (it != g_exports.end() && it->second.live > 0 && std::memcmp(it->second.h, h, 64) == 0) {
+        ++it->second.live;
+        return it->second.serial;
+    }
+    ExportEntry e;
+    std::memcpy(e.h, h, 64);
+    e.serial = ++g_export_serial;
+    e.live = 1;
+    g_exports[base] = e;
+    return e.serial;
+}
+
+static void export_release(void *base) {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    auto it = g_exports.find(base);
+    if (it != g_exports.end() && --it->second.live <= 0) g_exports.erase(it);
+}
+
+// every cached mapping, at data-plane shutdown (after the last round has drained)
+static void ipc_close_all() {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    for (auto &kv : g_ipc) (void)hipIpcCloseMemHandle(kv.second.base);
+    g_ipc.clear();
+    g_exports.clear();
 }
 
 // ---- process-wide data-plane resources -----------------------------------------------
@@ -157,6 +212,7 @@ void dataplane_shutdown() {
     rccl_shutdown();
     std::lock_guard<std::mutex> lk(g_dp_mu);
     if (g_rs) { (void)hipStreamSynchronize(g_rs); (void)hipStreamDestroy(g_rs); g_rs = nullptr; }
+    ipc_close_all();
     if (g_seg_reg) { (void)hipHostUnregister(g_seg_reg); g_seg_reg = nullptr; g_seg_dev = nullptr; }
 }
 
@@ -187,6 +243,7 @@ struct BaseState {
 };
 
 struct IpcState : BaseState {
+    void *pub_base = nullptr;         // allocation this rank published (export_acquire)
     char *peer[kMaxRanks] = {};
     void *peer_base[kMaxRanks] = {};
     uint32_t peer_ver[kMaxRanks] = {};
@@ -411,6 +468,10 @@ struct IpcTransport final : Transport {
         ESGD_HIP(hipIpcGetMemHandle(&h, base));
         IpcSlot &mine = s.sh->slot[s.rank];
         std::memcpy(mine.handle, &h, sizeof(h));
+        const uint64_t serial = export_acquire(base, mine.handle);
+        if (st.pub_base) export_release(st.pub_base);
+        st.pub_base = base;
+        mine.serial = serial;
         mine.offset = uint64_t(st.rb_dev - static_cast<char *>(base));
         mine.bytes = s.count * s.esize;
         mine.gen.store(s.gen, std::memory_order_release);
@@ -441,7 +502,7 @@ struct IpcTransport final : Transport {
             // re-open the same handle
             if (!(st.peer_base[q] && std::memcmp(st.peer_handle[q], ps.handle, 64) == 0)) {
                 void *pb = nullptr;
-                if (int rc = ipc_open(q, ps.handle, &pb)) return rc;   // open new first
+                if (int rc = ipc_open(q, ps.handle, ps.serial, &pb)) return rc;   // open new first
                 if (st.peer_base[q]) ipc_close(st.peer_base[q]);
                 st.peer_base[q] = pb;
                 std::memcpy(st.peer_handle[q], ps.handle, 64);
@@ -550,6 +611,7 @@ struct IpcTransport final : Transport {
         if (st->stream) (void)hipStreamSynchronize(st->stream);
         for (int q = 0; q < kMaxRanks; ++q)
             if (st->peer_base[q]) ipc_close(st->peer_base[q]);
+        if (st->pub_base) export_release(st->pub_base);
         base_teardown(s, *st);
         delete st;
         s.tstate = nullptr;

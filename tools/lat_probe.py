@@ -25,6 +25,7 @@ def main():
     kind = {"allreduce": comm.ALLREDUCE, "solo": comm.SOLO, "majority": comm.MAJORITY}[
         os.environ.get("LAT_KIND", "allreduce")]
     names = ["post->join", "join->launch", "launch(host)", "queued->done", "done->wait", "post->wait"]
+    kept = []
     for nbytes in [int(x) for x in os.environ.get("LAT_SIZES", "65536,4194304,67108864").split(",")]:
         count = nbytes // 4
         buf = dev.DeviceBuffer(count, _lib.FLOAT)
@@ -49,7 +50,17 @@ def main():
             line += " | gpu " + " ".join(f"{n}={m:.1f}" for n, m in zip(
                 ["w_ready", "rs", "w_reduced", "ag", "w_done", "total"], g))
         print(f"[lat] rank {rank} bytes {nbytes}: {line} period={per:.1f}us", flush=True)
-        s.delete()
+        if os.environ.get("LAT_KEEP") == "1":
+            kept.append((s, buf))
+        elif os.environ.get("LAT_NOFREE") == "1":   # delete the schedule, keep the bucket
+            s.delete()
+            kept.append((None, buf))
+        else:
+            s.delete()
+            buf.close()
+    for s, buf in kept:
+        if s is not None:
+            s.delete()
         buf.close()
     comm.finalize()
     dist.destroy_process_group()
