@@ -37,6 +37,21 @@ int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64
                   float scale, hipStream_t s);
 int gather_remote(int n, const void *const *src, void *const *dst, const uint64_t *bytes,
                   hipStream_t s);
+int round_small(int dtype, const void *const *src, void *out, uint64_t n, int nseg,
+                const void *const *gsrc, void *const *gdst, const uint64_t *gbytes,
+                uint32_t *ready, uint32_t *reduced, uint32_t *done, uint32_t *fin, uint32_t *err,
+                uint64_t *ts, uint32_t *counter, int rank, int world, uint32_t value,
+                long long timeout_ticks, hipStream_t s);
+
+// Buckets up to this many bytes run as one launch per round (k_round_small);
+// ESGD_SMALL_ROUND_BYTES overrides (0 = never).
+static uint64_t small_round_bytes() {
+    static const uint64_t v = [] {
+        const char *e = getenv("ESGD_SMALL_ROUND_BYTES");
+        return (e && *e) ? uint64_t(strtoull(e, nullptr, 10)) : (uint64_t(4) << 20);
+    }();
+    return v;
+}
 
 // ---- IPC mapping cache: one hipIpcOpenMemHandle per (peer, allocation) ----
 // Mappings are not closed when the last schedule using them goes: they stay open, idle,
@@ -235,6 +250,7 @@ struct BaseState {
     char *pin = nullptr;
     size_t pin_cap = 0;
     bool copyout_pending = false;
+    bool fin_mode = false;            // the round in flight reports through SchedShm::fin
     std::vector<char *> retired;      // grown-out buckets: peers may still map them
     uint64_t off[kMaxRanks] = {}, len[kMaxRanks] = {};   // elements
     std::map<uint32_t, hipEvent_t> producer;
@@ -244,6 +260,7 @@ struct BaseState {
 
 struct IpcState : BaseState {
     void *pub_base = nullptr;         // allocation this rank published (export_acquire)
+    uint32_t *ctr = nullptr;          // device: k_round_small's two workgroup counters
     char *peer[kMaxRanks] = {};
     void *peer_base[kMaxRanks] = {};
     uint32_t peer_ver[kMaxRanks] = {};
@@ -427,6 +444,15 @@ static std::string base_diagnose(Sched &s) {
 }
 
 static int base_query(Sched &s, BaseState &st) {
+    if (st.fin_mode) {   // a one-launch round: its last workgroup writes fin (no event)
+        if (int32_t(s.sh->fin[s.rank].load(std::memory_order_acquire) - s.cur) >= 0) return 1;
+        if (s.sh->gpu_err[s.rank].load(std::memory_order_acquire) == s.cur) {
+            set_error("this rank's GPU waited more than %.0f s for its peers in round %u %s",
+                      engine_timeout(), s.cur, base_diagnose(s).c_str());
+            return ESGD_ERROR;
+        }
+        return 0;
+    }
     hipError_t e = hipEventQuery(st.ev);
     if (e == hipErrorNotReady) return 0;
     if (e != hipSuccess) return hip_fail(e, "hipEventQuery", __FILE__, __LINE__);
@@ -568,10 +594,20 @@ struct IpcTransport final : Transport {
     int launch(Sched &s, uint32_t round, bool fresh) override {
         IpcState &st = S(s);
         hipStream_t cs = st.stream;
+        st.fin_mode = false;
         if (int rc = base_copy_in(s, st, round, fresh, cs)) return rc;
         if (s.world > 1) {
             if (s.resolve)
                 if (int rc = map_peers(s, st)) return rc;
+            if (s.world <= ESGD_MAX_FANIN && s.count * s.esize <= small_round_bytes()) {
+                if (int rc = launch_small(s, st, round, cs)) return rc;
+                // device buckets: nothing follows the kernel, the host polls its fin flag
+                if (!s.host_mode && !st.shadow) {
+                    st.fin_mode = true;
+                    return ESGD_SUCCESS;
+                }
+                return base_copy_out(s, st, cs);
+            }
             if (int rc = pair_ranks(s, s.sh->ready, 0, round, cs)) return rc;
             const uint64_t n = st.len[s.rank];
             if (n) {
@@ -599,6 +635,33 @@ struct IpcTransport final : Transport {
         return base_copy_out(s, st, cs);
     }
 
+    // the whole round as one k_round_small launch (small buckets)
+    static int launch_small(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) {
+        if (!st.ctr) {   // first one-launch round of this schedule
+            ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.ctr), 256));
+            ESGD_HIP(hipMemsetAsync(st.ctr, 0, 256, cs));
+        }
+        const void *in[kMaxRanks];
+        for (int j = 0; j < s.world; ++j) in[j] = st.peer[j] + st.off[s.rank] * s.esize;
+        const void *src[kMaxRanks];
+        void *dst[kMaxRanks];
+        uint64_t bytes[kMaxRanks];
+        int m = 0;
+        for (int j = 0; j < s.world; ++j) {
+            if (j == s.rank || st.len[j] == 0) continue;
+            src[m] = st.peer[j] + st.off[j] * s.esize;
+            dst[m] = st.rb_dev + st.off[j] * s.esize;
+            bytes[m] = st.len[j] * s.esize;
+            ++m;
+        }
+        const long long ticks = (long long)(engine_timeout() * double(g_ticks_per_s));
+        uint64_t *ts = gpu_trace_on() ? reinterpret_cast<uint64_t *>(dev_flag(&s.sh->gpu_ts[s.rank][0])) : nullptr;
+        return round_small(s.dtype, in, st.rb_dev + st.off[s.rank] * s.esize, st.len[s.rank], m, src, dst,
+                           bytes, dev_flag(s.sh->ready), dev_flag(s.sh->reduced), dev_flag(s.sh->done),
+                           dev_flag(&s.sh->fin[s.rank]), dev_flag(&s.sh->gpu_err[s.rank]), ts, st.ctr,
+                           s.rank, s.world, round, ticks, cs);
+    }
+
     int query(Sched &s) override { return base_query(s, S(s)); }
 
     int complete(Sched &s) override { return base_complete(s, S(s)); }
@@ -612,6 +675,7 @@ struct IpcTransport final : Transport {
         for (int q = 0; q < kMaxRanks; ++q)
             if (st->peer_base[q]) ipc_close(st->peer_base[q]);
         if (st->pub_base) export_release(st->pub_base);
+        if (st->ctr) (void)hipFree(st->ctr);
         base_teardown(s, *st);
         delete st;
         s.tstate = nullptr;

@@ -99,6 +99,7 @@ struct Sched {
     std::condition_variable cv;
     std::atomic<uint32_t> posted{0};
     uint32_t joined = 0, completed = 0, waited = 0;
+    std::atomic<uint32_t> completed_a{0};   // = completed, for wait()'s lock-free spin
     Stage stage = ST_IDLE;
     uint32_t cur = 0;
     bool cur_fresh = false;

@@ -529,6 +529,236 @@ int round_sync(uint32_t *flags, int rank, int world, uint32_t value, long long t
     return ESGD_SUCCESS;
 }
 
+// ---- a whole small round in ONE launch ----
+// For small buckets the round is latency-bound: five launches (three pairings, the
+// reduce-scatter, the all-gather) cost ~15 us of host time and ~4 us of GPU time per
+// kernel boundary (tools/lat.sh).  k_round_small does the same steps inside one kernel of
+// at most kSmallBlocks workgroups:
+//   publish ready -> wait for every rank's ready -> reduce-scatter (tree order) ->
+//   grid count; the last workgroup publishes reduced -> wait for every rank's reduced ->
+//   all-gather -> grid count; the last workgroup publishes done, waits for every rank's
+//   done and writes `fin` (the host polls it instead of an event).
+// Hand-offs: every payload store is system-scope write-through (sc0 sc1) and drained
+// (s_waitcnt vmcnt(0)) before the workgroup counts itself; peer payload is read with
+// system-scope loads after a system-scope acquire.  The grid is far below one workgroup
+// per CU, so every workgroup is resident while others wait on it (several ranks sharing
+// one GPU included); every wait is bounded by the wall-clock timeout, and a timed-out
+// workgroup records the round in *err and leaves.
+constexpr int kSmallBlocks = 64;
+
+struct SmallRoundArgs {
+    const void *src[kMaxSeg];   // phase 1 inputs: shard `rank` of every rank's rb, rank order
+    void *out;                  // phase 1 output: shard `rank` of the local rb
+    uint64_t n;                 // elements of the local shard
+    const void *gsrc[kMaxSeg];  // phase 2: every other rank's shard (peer memory) ...
+    void *gdst[kMaxSeg];        // ... and where it lands in the local rb
+    uint32_t gvec[kMaxSeg];     // 16-B vectors per segment
+    uint32_t gtail[kMaxSeg];    // bytes after the last full vector
+    int nseg;
+    uint32_t *ready, *reduced, *done, *fin, *err;
+    uint64_t *ts;               // optional GPU trace stamps (6)
+    uint32_t *counter;          // device words: [0], [1] arrivals (zero between rounds),
+                                // [2], [3] gates raised to the round by the polling lane
+    int rank, world;
+    uint32_t value;
+    long long timeout;
+};
+
+__device__ __forceinline__ bool spin_all(uint32_t *flags, int world, uint32_t value, long long t0,
+                                         long long timeout) {
+    for (int q = 0; q < world; ++q) {
+        while (int32_t(__hip_atomic_load(&flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - value) < 0) {
+            if (wall_clock64() - t0 > timeout) return false;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return true;
+}
+
+// Only ONE lane of the grid polls the ranks' flags in host memory (`leader`): it then
+// raises `gate` (a device word) to the round, and every workgroup's lane 0 polls that
+// instead -- 64 workgroups polling host memory over PCIe slowed every hand-off ~5x
+// (tools/lat.sh).  The workgroup then acquires at system scope.
+__device__ __forceinline__ bool block_wait(const SmallRoundArgs &a, uint32_t *flags, uint32_t *gate,
+                                           bool leader, long long t0, int *ok) {
+    if (threadIdx.x == 0) {
+        bool good = true;
+        if (leader) {
+            good = spin_all(flags, a.world, a.value, t0, a.timeout);
+            if (good) __hip_atomic_store(gate, a.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            good = spin_all(gate, 1, a.value, t0, a.timeout);
+        }
+        if (good) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        else __hip_atomic_store(a.err, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        *ok = good;
+    }
+    __syncthreads();
+    return *ok != 0;
+}
+
+// every workgroup drains its stores and counts itself; true in the last one to arrive
+__device__ __forceinline__ bool block_count(uint32_t *ctr, int *last) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        *last = old + 1 == gridDim.x;
+        if (*last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    return *last != 0;
+}
+
+// flag publication: release at system scope; the explicit wait keeps the flag behind the
+// write-back (MI355X_MICROARCH.md, compiler hazard)
+__device__ __forceinline__ void publish_flag(uint32_t *flag, uint32_t value) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <class Tr, int K>
+__global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
+    using T = typename Tr::T;
+    using A = typename Tr::A;
+    __shared__ int ok, last;
+    const long long t0 = wall_clock64();
+    const bool lead = threadIdx.x == 0;
+    const bool stamp = a.ts != nullptr && lead;
+    if (lead && blockIdx.x == 0) {   // the snapshot queued before this launch has landed
+        if (stamp) a.ts[0] = uint64_t(t0);
+        __hip_atomic_store(&a.ready[a.rank], a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (!block_wait(a, a.ready, &a.counter[2], blockIdx.x == 0, t0, &ok)) return;
+    if (stamp && blockIdx.x == 0) a.ts[1] = uint64_t(wall_clock64());
+
+    // phase 1: the local shard, folded in tree order from every rank's rb
+    const uint32_t nvec = uint32_t(a.n / Tr::E);
+    const int bytes = int(nvec * 16u);
+    __amdgpu_buffer_rsrc_t rs[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(a.src[j]), (short)0, bytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, bytes, 0x00020000);
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += gridDim.x * 256) {
+        raw16 r[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) r[j] = __builtin_amdgcn_raw_buffer_load_b128(rs[j], i * 16, 0, 17);
+        __builtin_amdgcn_raw_buffer_store_b128(fold16<Tr, K, false>(r, 1.0f), ws, i * 16, 0, 17);
+    }
+    if (blockIdx.x == 0 && uint64_t(nvec) * Tr::E + threadIdx.x < a.n) {
+        const uint64_t e = uint64_t(nvec) * Tr::E + threadIdx.x;
+        A v[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            v[j] = Tr::load(__hip_atomic_load(static_cast<const T *>(a.src[j]) + e, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM));
+        tree_fold<Tr, K>(v);
+        __hip_atomic_store(static_cast<T *>(a.out) + e, Tr::store(v[0]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    const bool last1 = block_count(&a.counter[0], &last);
+    if (last1 && lead) {
+        if (stamp) a.ts[2] = uint64_t(wall_clock64());
+        publish_flag(&a.reduced[a.rank], a.value);
+    }
+    if (!block_wait(a, a.reduced, &a.counter[3], last1, t0, &ok)) return;
+    if (stamp && blockIdx.x == 0) a.ts[3] = uint64_t(wall_clock64());
+
+    // phase 2: every other rank's reduced shard into the local rb
+    for (int sg = 0; sg < a.nseg; ++sg) {
+        const uint32_t gv = a.gvec[sg];
+        if (gv) {
+            __amdgpu_buffer_rsrc_t gs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(a.gsrc[sg]), (short)0,
+                                                                         int(gv * 16u), 0x00020000);
+            __amdgpu_buffer_rsrc_t gd = __builtin_amdgcn_make_buffer_rsrc(a.gdst[sg], (short)0, int(gv * 16u),
+                                                                         0x00020000);
+            for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < gv; i += gridDim.x * 256)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(gs, i * 16, 0, 17),
+                                                       gd, i * 16, 0, 17);
+        }
+        if (blockIdx.x == 0 && threadIdx.x < a.gtail[sg]) {
+            const uint8_t *src = static_cast<const uint8_t *>(a.gsrc[sg]) + size_t(gv) * 16;
+            uint8_t *dst = static_cast<uint8_t *>(a.gdst[sg]) + size_t(gv) * 16;
+            __hip_atomic_store(dst + threadIdx.x,
+                               __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    if (!block_count(&a.counter[1], &last) || !lead) return;
+    // the last workgroup: this rank's shard must stay put until every rank has gathered it
+    if (stamp) a.ts[4] = uint64_t(wall_clock64());
+    publish_flag(&a.done[a.rank], a.value);
+    if (!spin_all(a.done, a.world, a.value, t0, a.timeout)) {
+        __hip_atomic_store(a.err, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    if (stamp) a.ts[5] = uint64_t(wall_clock64());
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stamps land before fin
+    __hip_atomic_store(a.fin, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <class Tr>
+static int launch_small_t(const SmallRoundArgs &a, unsigned grid, hipStream_t s) {
+    switch (a.world) {
+#define ESGD_SMALL_K(KK) \
+    case KK: hipLaunchKernelGGL((k_round_small<Tr, KK>), dim3(grid), dim3(256), 0, s, a); break;
+    ESGD_SMALL_K(2) ESGD_SMALL_K(3) ESGD_SMALL_K(4) ESGD_SMALL_K(5) ESGD_SMALL_K(6) ESGD_SMALL_K(7)
+    ESGD_SMALL_K(8)
+#undef ESGD_SMALL_K
+    default:
+        set_error("small round: %d ranks outside [2, %d]", a.world, ESGD_MAX_FANIN);
+        return ESGD_INVALID_ARG;
+    }
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+// Entry point of the data plane (dataplane.cpp).  The shard layout keeps every shard
+// 1 KiB aligned; segments are checked here.
+int round_small(int dtype, const void *const *src, void *out, uint64_t n, int nseg,
+                const void *const *gsrc, void *const *gdst, const uint64_t *gbytes,
+                uint32_t *ready, uint32_t *reduced, uint32_t *done, uint32_t *fin, uint32_t *err,
+                uint64_t *ts, uint32_t *counter, int rank, int world, uint32_t value,
+                long long timeout_ticks, hipStream_t s) {
+    ESGD_ARG(world >= 2 && world <= ESGD_MAX_FANIN && nseg >= 0 && nseg < kMaxSeg,
+             "small round: world %d, %d segments", world, nseg);
+    const size_t es = esgd_dtype_size(dtype);
+    ESGD_ARG(es > 0, "small round: dtype %d", dtype);
+    SmallRoundArgs a;
+    std::memset(&a, 0, sizeof(a));
+    for (int j = 0; j < world; ++j) a.src[j] = src[j];
+    a.out = out;
+    a.n = n;
+    uint64_t maxv = n * es / 16;
+    for (int i = 0; i < nseg; ++i) {
+        ESGD_ARG(((reinterpret_cast<uintptr_t>(gsrc[i]) | reinterpret_cast<uintptr_t>(gdst[i])) & 15) == 0,
+                 "small round: segment %d not 16-B aligned", i);
+        a.gsrc[i] = gsrc[i];
+        a.gdst[i] = gdst[i];
+        a.gvec[i] = uint32_t(gbytes[i] / 16);
+        a.gtail[i] = uint32_t(gbytes[i] % 16);
+        maxv = std::max<uint64_t>(maxv, a.gvec[i]);
+    }
+    a.nseg = nseg;
+    a.ready = ready; a.reduced = reduced; a.done = done; a.fin = fin; a.err = err;
+    a.ts = ts;
+    a.counter = counter;
+    a.rank = rank; a.world = world; a.value = value; a.timeout = timeout_ticks;
+    const unsigned grid = unsigned(std::min<uint64_t>(kSmallBlocks, std::max<uint64_t>(1, (maxv + 255) / 256)));
+    switch (dtype) {
+    case ESGD_FLOAT: return launch_small_t<F32>(a, grid, s);
+    case ESGD_BF16: return launch_small_t<BF16>(a, grid, s);
+    case ESGD_DOUBLE: return launch_small_t<F64>(a, grid, s);
+    case ESGD_INT32: return launch_small_t<I32>(a, grid, s);
+    case ESGD_INT64: return launch_small_t<I64>(a, grid, s);
+    default: break;
+    }
+    set_error("small round: unsupported dtype %d", dtype);
+    return ESGD_INVALID_ARG;
+}
+
 }  // namespace esgd
 
 using namespace esgd;

@@ -43,6 +43,7 @@ struct alignas(64) SchedShm {
     alignas(64) std::atomic<uint32_t> reduced[kMaxRanks]; // round whose reduce-scatter is done
     alignas(64) std::atomic<uint32_t> done[kMaxRanks];    // round whose all-gather is done
     alignas(64) std::atomic<uint32_t> gpu_err[kMaxRanks]; // round whose flag wait timed out
+    alignas(64) std::atomic<uint32_t> fin[kMaxRanks];     // round a one-launch round finished
     // ESGD_GPU_TRACE=1: wall-clock (entry, exit) of the three pairings of the last round
     alignas(64) uint64_t gpu_ts[kMaxRanks][6];
     std::atomic<uint32_t> joined[kMaxRanks];  // diagnostics: last round rank r joined

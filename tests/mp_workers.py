@@ -107,14 +107,18 @@ def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0
 
 
 def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0, buf="device",
-                  in_place=False, transport="ipc", shadow_ranks=()):
+                  in_place=False, transport="ipc", shadow_ranks=(), small_bytes=None):
     """Data plane on the GPU: every rank reduces its splitmix bucket; returns the
     result bytes' digest per round plus a bit-exactness verdict against the oracle.
-    shadow_ranks: ranks whose device buckets go through the owned shadow bucket."""
+    shadow_ranks: ranks whose device buckets go through the owned shadow bucket.
+    small_bytes: ESGD_SMALL_ROUND_BYTES (buckets up to it run as one launch per round;
+    "0" forces the five-launch path)."""
     import numpy as np
 
     if rank in shadow_ranks:
         os.environ["ESGD_SHADOW"] = "1"
+    if small_bytes is not None:
+        os.environ["ESGD_SMALL_ROUND_BYTES"] = str(small_bytes)
 
     from esgd import _lib
     from esgd import device as dev

@@ -16,17 +16,32 @@ pytestmark = pytest.mark.gpu
 ALLREDUCE, SOLO, MAJORITY = 0, 1, 2
 
 
+SMALL = {"one_launch": None, "five_launch": 0}   # ESGD_SMALL_ROUND_BYTES per round path
+
+
+@pytest.mark.parametrize("path", sorted(SMALL))
 @pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("dtype", ["fp32", "int32", "bf16", "fp64", "int64"])
-def test_allreduce_bitwise_device(world, dtype):
-    verdicts = run("gpu_allreduce", world, dtype_name=dtype, count=100003, rounds=2)
+def test_allreduce_bitwise_device(world, dtype, path):
+    verdicts = run("gpu_allreduce", world, dtype_name=dtype, count=100003, rounds=2,
+                   small_bytes=SMALL[path])
     assert all(all(v) for v in verdicts), verdicts
 
 
+@pytest.mark.parametrize("path", sorted(SMALL))
 @pytest.mark.parametrize("world", [2, 3, 8])
-def test_allreduce_ragged_and_tiny(world):
+def test_allreduce_ragged_and_tiny(world, path):
     for count in (1, 17, 1023, 4099):
-        verdicts = run("gpu_allreduce", world, count=count, rounds=1)
+        verdicts = run("gpu_allreduce", world, count=count, rounds=1, small_bytes=SMALL[path])
+        assert all(all(v) for v in verdicts), (count, verdicts)
+
+
+@pytest.mark.parametrize("world", [2, 5])
+def test_one_launch_rounds_back_to_back(world):
+    # many consecutive one-launch rounds of one schedule (flags, counters and fin reused
+    # every round), at the size limit of the one-launch path and just above it
+    for count, small in ((1 << 20, 4 << 20), ((1 << 20) + 3, 4 << 20)):
+        verdicts = run("gpu_allreduce", world, count=count, rounds=6, small_bytes=small)
         assert all(all(v) for v in verdicts), (count, verdicts)
 
 
