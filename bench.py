@@ -249,6 +249,25 @@ def gate_256(dev, dt, es, k, s, iters=20):
             "frac": round(algo / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+# N > 1: schedules (and their buckets) stay alive until every leg has run, then are
+# deleted together -- persistent, like the reference's.  Deleting one closes the peers'
+# IPC mappings of its bucket, after which every later peer-reading kernel of the process
+# is slower; nothing is closed while a leg is being timed.
+_DEFERRED = []
+
+
+def _defer(sch, *bufs):
+    _DEFERRED.append((sch, bufs))
+
+
+def _delete_deferred():
+    while _DEFERRED:
+        sch, bufs = _DEFERRED.pop(0)
+        sch.delete()
+        for b in bufs:
+            b.close()
+
+
 def _max_over_ranks(x: float) -> float:
     import torch
     import torch.distributed as dist
@@ -288,8 +307,7 @@ def sweep_c5(comm, dev, world, dt, es):
         ts = tt.tolist()
         t, mean = statistics.median(ts), statistics.fmean(ts)
         stages = _stages_us(sch.timeline()[-iters:])
-        sch.delete()
-        buf.close()
+        _defer(sch, buf)
         t_min = 2 * nbytes / (world * XGMI_LINK_GBS * 1e9)
         out.append({"bytes": nbytes, "us": round(t * 1e6, 1), "mean_us": round(mean * 1e6, 1),
                     "algbw_GBs": round(nbytes / t / 1e9, 2),
@@ -297,6 +315,107 @@ def sweep_c5(comm, dev, world, dt, es):
                     "xgmi_frac": round(t_min / t, 4), "rounds": iters,
                     "rank0_stages_us": stages})
     return out
+
+
+def _timed_steps(comm, fn, steps):
+    """Median over `steps` of fn()'s wall time, each step's time the max over ranks."""
+    import statistics
+
+    import torch
+    import torch.distributed as dist
+    ts = []
+    for _ in range(steps):
+        comm.barrier()
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    tt = torch.tensor(ts, dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return statistics.median(tt.tolist())
+
+
+def c4_resnet50_161(comm, dev, rank, world, steps=8):
+    """C4 as the reference runs it: one majority schedule per ResNet-50 gradient tensor
+    (161 buckets, opt_esgd_solo_imagenet_imbalance.py:86-248; tests/golden/
+    resnet50_buckets.json), reduced one after another every step like the op chain of
+    :24-44 -- against the same 25 559 081 fp32 as ONE fused bucket
+    (EagerSGDOptimizer(fuse=True)).  All ranks post every bucket (no straggler)."""
+    with open(os.path.join(ROOT, "tests", "golden", "resnet50_buckets.json")) as f:
+        lengths = json.load(f)["lengths"]
+    total = sum(lengths)
+    bufs = [dev.DeviceBuffer(n) for n in lengths]
+    for b in bufs:
+        dev.fill_uniform(b, SEED, rank)
+    fused = dev.DeviceBuffer(total)
+    dev.fill_uniform(fused, SEED, rank)
+    dev.synchronize()
+    scheds = [comm.Schedule(comm.MAJORITY, None, b, b.count, seed=6545343, buf=comm.BUF_DEVICE)
+              for b in bufs]
+    one = comm.Schedule(comm.MAJORITY, None, fused, total, seed=6545343, buf=comm.BUF_DEVICE)
+
+    def chain():
+        for s in scheds:
+            s.post()
+            s.wait()
+
+    def fused_step():
+        one.post()
+        one.wait()
+
+    for _ in range(2):
+        chain()
+        fused_step()
+    t161 = _timed_steps(comm, chain, steps)
+    t1 = _timed_steps(comm, fused_step, steps)
+    for s, b in zip(scheds, bufs):
+        _defer(s, b)
+    _defer(one, fused)
+    return {"buckets": len(lengths), "fp32_elements": total,
+            "step_ms_161_buckets": round(t161 * 1e3, 3), "step_ms_one_fused_bucket": round(t1 * 1e3, 3),
+            "fused_speedup": round(t161 / t1, 2), "steps": steps}
+
+
+def c3_over_rccl(comm, dev, rank, world, count, steps=20):
+    """C3 (solo-allreduce, 256 MiB per rank) through the RCCL transport: grouped
+    ncclSend/ncclRecv over xGMI, arrived chunks folded by the tree kernel on a side
+    stream.  Needs one GPU per rank (RCCL refuses duplicate GPUs)."""
+    import numpy as np
+
+    import esgd
+    from oracle import ffref
+    if world > esgd.device_count():
+        return {"skipped": "ranks share a GPU; RCCL refuses duplicate GPUs"}
+    comm.set_transport("rccl")
+    try:
+        rb = dev.DeviceBuffer(count)
+        dev.fill_uniform(rb, SEED, rank)
+        dev.synchronize()
+        sch = comm.Schedule(comm.SOLO, None, rb, count, async_=32, seed=6545343, buf=comm.BUF_DEVICE)
+
+        def step():
+            sch.post()
+            sch.wait()
+
+        for _ in range(3):
+            step()
+        t = _timed_steps(comm, step, steps)
+        dev.fill_uniform(rb, SEED + 1, rank)
+        dev.synchronize()
+        comm.barrier()
+        step()
+        m = min(count, 1 << 18)
+        got = rb.download()[:m]
+        want = ffref.tree_sum([ffref.fill_uniform(SEED + 1, r, m) for r in range(world)])
+        ok = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+        sch.delete()
+        rb.close()
+    finally:
+        comm.set_transport("ipc")
+    S = count * 4
+    t_min = 2 * S / (world * XGMI_LINK_GBS * 1e9)
+    return {"bucket_bytes": S, "round_ms_median": round(t * 1e3, 4),
+            "value_GBs": round(world * S / t / 1e9, 2), "algbw_GBs": round(S / t / 1e9, 2),
+            "xgmi_frac": round(t_min / t, 4), "parity_rank_slice": "bitwise" if ok else "MISMATCH"}
 
 
 def _stages_us(tl):
@@ -363,7 +482,7 @@ def straggler_c4(comm, dev, rank, world, rounds=24):
         d, c = one(0.2 * T if rank == world - 1 else 0.0)
         lat.append(d); contrib.append(c)
     on_time = _max_over_ranks(statistics.median(lat) if rank != world - 1 else 0.0)
-    sch.delete()
+    _defer(sch, ones, sb, rb)
     return {"bucket_fp32": count, "T_no_straggler_ms": round(T * 1e3, 3),
             "straggler_delay_ms": round(0.2 * T * 1e3, 3),
             "on_time_ranks_median_ms": round(on_time * 1e3, 3),
@@ -436,13 +555,15 @@ def run_allreduce(args, rank, world):
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         parity = "bitwise (head+tail slices, every rank)" if flag.item() else "MISMATCH"
-    sched.delete()
-    rb.close()
+    _defer(sched, rb)
 
     extras = {}
     if not args.no_extras:
         for name, fn in (("sweep_c5_majority", lambda: sweep_c5(comm, dev, world, dt, es)),
-                         ("straggler_c4_majority", lambda: straggler_c4(comm, dev, rank, world))):
+                         ("straggler_c4_majority", lambda: straggler_c4(comm, dev, rank, world)),
+                         ("c4_resnet50_161_vs_fused", lambda: c4_resnet50_161(comm, dev, rank, world)),
+                         ("sweep_c5_majority_bf16", lambda: sweep_c5(comm, dev, world, _lib.BF16, 2)),
+                         ("c3_rccl_transport", lambda: c3_over_rccl(comm, dev, rank, world, count))):
             try:
                 extras[name] = fn()
             except Exception as e:   # keep the headline line; report what failed
@@ -450,6 +571,8 @@ def run_allreduce(args, rank, world):
                 traceback.print_exc()
                 extras[name + "_error"] = f"rank {rank}: " + repr(e)[:300]
                 break                # peers may be inside this extra: do not start another
+    if not any(k.endswith("_error") for k in extras):
+        _delete_deferred()           # collective; after a failed leg finalize frees them
     comm.finalize()
 
     S = count * es

@@ -54,16 +54,21 @@ static uint64_t small_round_bytes() {
 }
 
 // ---- IPC mapping cache: one hipIpcOpenMemHandle per (peer, allocation) ----
-// Mappings are not closed when the last schedule using them goes: they stay open, idle,
-// until the data plane shuts down.  Measured on MI355X (tools/lat.sh, LAT_NOFREE=1): once
-// a process has closed an IPC mapping, every later kernel that reads peer memory through
-// IPC pays +20..80 us (a 64 KiB round went from 41 us to 138-200 us).
-// An idle mapping is reused only for the same export: the exporter tags each exported
-// allocation with a serial that stays the same only while one of its schedules keeps the
-// allocation published (IpcSlot::serial), so a freed-and-reallocated bucket whose handle
-// bytes happen to repeat is never served from a stale mapping; such a stale idle mapping
-// is closed before the handle is opened again.
-// ESGD_IPC_EAGER_CLOSE=1 restores closing at the last release (A/B runs).
+// A mapping is closed when the last schedule using it is deleted -- before the
+// collective delete returns, so before the exporter can free the bucket.  Keeping
+// mappings open instead (ESGD_IPC_KEEP_OPEN=1) avoids a measured slowdown -- once a
+// process has closed an IPC mapping, every later kernel reading peer memory through IPC
+// paid +20..80 us on MI355X (tools/lat.sh: a 64 KiB round 41 -> 138-200 us) -- but an
+// exporter then frees memory its peers still map, and later peer-reading kernels were
+// seen to fault (bench C5 bf16 sweep after the C4 legs).  Persistent schedules (the
+// reference never deletes its schedules) never close anything.
+// Handle bytes are not unique over time: a new allocation can export exactly the bytes of
+// a freed one (tests/test_dataplane_gpu.py::test_schedule_and_bucket_churn).  The EXPORTER
+// therefore never publishes a handle it published before unless that publication is still
+// live (same allocation, e.g. two buckets carved from one chunk); a handle that repeats
+// after its release is a collision, and the bucket is shadowed by a fresh library-owned
+// bucket instead (checked the same way).  So no importer ever re-opens handle bytes it
+// closed, nor reuses a mapping for a different allocation.
 struct IpcKey {
     int peer;
     uint8_t h[64];
@@ -72,41 +77,36 @@ struct IpcKey {
         return std::memcmp(h, o.h, 64) < 0;
     }
 };
-struct IpcEntry { void *base; int refs; uint64_t serial; };
+struct IpcEntry { void *base; int refs; };
 static std::mutex g_ipc_mu;
 static std::map<IpcKey, IpcEntry> g_ipc;
 
-static int ipc_open(int peer, const uint8_t *h, uint64_t serial, void **base) {
+static int ipc_open(int peer, const uint8_t *h, void **base) {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
     IpcKey k;
     k.peer = peer;
     std::memcpy(k.h, h, 64);
     auto it = g_ipc.find(k);
     if (it != g_ipc.end()) {
-        if (it->second.refs > 0 || it->second.serial == serial) {
-            ++it->second.refs;
-            it->second.serial = serial;
-            *base = it->second.base;
-            return ESGD_SUCCESS;
-        }
-        (void)hipIpcCloseMemHandle(it->second.base);   // idle, and a different export
-        g_ipc.erase(it);
+        ++it->second.refs;
+        *base = it->second.base;
+        return ESGD_SUCCESS;
     }
     hipIpcMemHandle_t hh;
     std::memcpy(&hh, h, sizeof(hh));
     void *p = nullptr;
     ESGD_HIP(hipIpcOpenMemHandle(&p, hh, hipIpcMemLazyEnablePeerAccess));
-    g_ipc[k] = {p, 1, serial};
+    g_ipc[k] = {p, 1};
     *base = p;
     return ESGD_SUCCESS;
 }
 
 static void ipc_close(void *base) {
-    static const bool eager = getenv("ESGD_IPC_EAGER_CLOSE") && *getenv("ESGD_IPC_EAGER_CLOSE") == '1';
+    static const bool keep = getenv("ESGD_IPC_KEEP_OPEN") && *getenv("ESGD_IPC_KEEP_OPEN") == '1';
     std::lock_guard<std::mutex> lk(g_ipc_mu);
     for (auto it = g_ipc.begin(); it != g_ipc.end(); ++it) {
         if (it->second.base == base) {
-            if (--it->second.refs == 0 && eager) {
+            if (--it->second.refs == 0 && !keep) {
                 (void)hipIpcCloseMemHandle(base);
                 g_ipc.erase(it);
             }
@@ -115,31 +115,30 @@ static void ipc_close(void *base) {
     }
 }
 
-// Exporter side: allocations this process has published, base -> (serial, schedules
-// publishing it).  A serial is reused only while the allocation stays published.
-struct ExportEntry { uint8_t h[64]; uint64_t serial; int live; };
-static std::map<void *, ExportEntry> g_exports;
-static uint64_t g_export_serial = 0;
+// Exporter side: every handle this process has published -> schedules publishing it now.
+struct HandleKey {
+    uint8_t h[64];
+    bool operator<(const HandleKey &o) const { return std::memcmp(h, o.h, 64) < 0; }
+};
+static std::map<HandleKey, int> g_published;
+constexpr int kCollide = 1;   // publish(): the handle repeats a released publication
 
-static uint64_t export_acquire(void *base, const uint8_t *h) {
+static int claim_handle(const uint8_t *h) {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
-    auto it = g_exports.find(base);
-    if (it != g_exports.end() && it->second.live > 0 && std::memcmp(it->second.h, h, 64) == 0) {
-        ++it->second.live;
-        return it->second.serial;
-    }
-    ExportEntry e;
-    std::memcpy(e.h, h, 64);
-    e.serial = ++g_export_serial;
-    e.live = 1;
-    g_exports[base] = e;
-    return e.serial;
+    HandleKey k;
+    std::memcpy(k.h, h, 64);
+    auto it = g_published.find(k);
+    if (it != g_published.end() && it->second <= 0) return kCollide;
+    ++g_published[k];
+    return ESGD_SUCCESS;
 }
 
-static void export_release(void *base) {
+static void release_handle(const uint8_t *h) {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
-    auto it = g_exports.find(base);
-    if (it != g_exports.end() && --it->second.live <= 0) g_exports.erase(it);
+    HandleKey k;
+    std::memcpy(k.h, h, 64);
+    auto it = g_published.find(k);
+    if (it != g_published.end()) --it->second;   // stays known: a repeat is a collision
 }
 
 // every cached mapping, at data-plane shutdown (after the last round has drained)
@@ -147,7 +146,7 @@ static void ipc_close_all() {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
     for (auto &kv : g_ipc) (void)hipIpcCloseMemHandle(kv.second.base);
     g_ipc.clear();
-    g_exports.clear();
+    g_published.clear();
 }
 
 // ---- process-wide data-plane resources -----------------------------------------------
@@ -259,7 +258,8 @@ struct BaseState {
 };
 
 struct IpcState : BaseState {
-    void *pub_base = nullptr;         // allocation this rank published (export_acquire)
+    uint8_t pub_h[64] = {};           // handle this rank publishes (claim_handle)
+    bool pub_live = false;
     uint32_t *ctr = nullptr;          // device: k_round_small's two workgroup counters
     char *peer[kMaxRanks] = {};
     void *peer_base[kMaxRanks] = {};
@@ -444,8 +444,20 @@ static std::string base_diagnose(Sched &s) {
 }
 
 static int base_query(Sched &s, BaseState &st) {
-    if (st.fin_mode) {   // a one-launch round: its last workgroup writes fin (no event)
-        if (int32_t(s.sh->fin[s.rank].load(std::memory_order_acquire) - s.cur) >= 0) return 1;
+    if (st.fin_mode) {   // a one-launch round: its last workgroup writes fin
+        if (int32_t(s.sh->fin[s.rank].load(std::memory_order_acquire) - s.cur) >= 0) {
+            // the kernel may still be retiring (not ready is fine); a fault is reported
+            // against this round, not a later one
+            const hipError_t e = hipEventQuery(st.ev);
+            if (e != hipSuccess && e != hipErrorNotReady) {
+                (void)hip_fail(e, "one-launch round", __FILE__, __LINE__);
+                std::string m = esgd_last_error();
+                set_error("%s (schedule %d, %llu elements of dtype %d)", m.c_str(), s.id,
+                          (unsigned long long)s.count, s.dtype);
+                return ESGD_ERROR;
+            }
+            return 1;
+        }
         if (s.sh->gpu_err[s.rank].load(std::memory_order_acquire) == s.cur) {
             set_error("this rank's GPU waited more than %.0f s for its peers in round %u %s",
                       engine_timeout(), s.cur, base_diagnose(s).c_str());
@@ -455,7 +467,13 @@ static int base_query(Sched &s, BaseState &st) {
     }
     hipError_t e = hipEventQuery(st.ev);
     if (e == hipErrorNotReady) return 0;
-    if (e != hipSuccess) return hip_fail(e, "hipEventQuery", __FILE__, __LINE__);
+    if (e != hipSuccess) {
+        (void)hip_fail(e, "hipEventQuery", __FILE__, __LINE__);
+        std::string m = esgd_last_error();
+        set_error("%s (schedule %d, %llu elements of dtype %d)", m.c_str(), s.id,
+                  (unsigned long long)s.count, s.dtype);
+        return ESGD_ERROR;
+    }
     if (s.world > 1 && s.sh->gpu_err[s.rank].load(std::memory_order_acquire) == s.cur) {
         set_error("this rank's GPU waited more than %.0f s for its peers in round %u %s",
                   engine_timeout(), s.cur, base_diagnose(s).c_str());
@@ -486,24 +504,44 @@ struct IpcTransport final : Transport {
         s.sh->slot[s.rank].bytes = s.count * s.esize;
     }
 
+    // Returns kCollide (nothing published) when the handle repeats a released one.
     static int publish(Sched &s, IpcState &st) {
         void *base = nullptr;
         size_t size = 0;
         ESGD_HIP(hipMemGetAddressRange(&base, &size, st.rb_dev));
         hipIpcMemHandle_t h;
         ESGD_HIP(hipIpcGetMemHandle(&h, base));
+        uint8_t hb[64];
+        std::memcpy(hb, &h, 64);
+        if (int rc = claim_handle(hb)) return rc;
+        if (st.pub_live) release_handle(st.pub_h);
+        std::memcpy(st.pub_h, hb, 64);
+        st.pub_live = true;
         IpcSlot &mine = s.sh->slot[s.rank];
-        std::memcpy(mine.handle, &h, sizeof(h));
-        const uint64_t serial = export_acquire(base, mine.handle);
-        if (st.pub_base) export_release(st.pub_base);
-        st.pub_base = base;
-        mine.serial = serial;
+        std::memcpy(mine.handle, hb, 64);
         mine.offset = uint64_t(st.rb_dev - static_cast<char *>(base));
         mine.bytes = s.count * s.esize;
         mine.gen.store(s.gen, std::memory_order_release);
         mine.ver.fetch_add(1, std::memory_order_acq_rel);
         st.peer[s.rank] = st.rb_dev;
         return ESGD_SUCCESS;
+    }
+
+    // publish a library-owned bucket; on a collision allocate another (the colliding one
+    // stays allocated, retired, so its handle cannot come straight back)
+    static int publish_owned(Sched &s, IpcState &st) {
+        int rc = publish(s, st);
+        for (int tries = 0; rc == kCollide && tries < 8; ++tries) {
+            st.retired.push_back(st.rb_dev);
+            if (int e = alloc_bucket(std::max<size_t>(s.count * s.esize, 1), &st.rb_dev, &st.cap)) return e;
+            st.peer[s.rank] = st.rb_dev;
+            rc = publish(s, st);
+        }
+        if (rc == kCollide) {
+            set_error("schedule %d: no exportable bucket with a fresh IPC handle", s.id);
+            return ESGD_ERROR;
+        }
+        return rc;
     }
 
     // (re)map every peer whose publication changed since we last mapped it
@@ -528,7 +566,7 @@ struct IpcTransport final : Transport {
             // re-open the same handle
             if (!(st.peer_base[q] && std::memcmp(st.peer_handle[q], ps.handle, 64) == 0)) {
                 void *pb = nullptr;
-                if (int rc = ipc_open(q, ps.handle, ps.serial, &pb)) return rc;   // open new first
+                if (int rc = ipc_open(q, ps.handle, &pb)) return rc;   // open new first
                 if (st.peer_base[q]) ipc_close(st.peer_base[q]);
                 st.peer_base[q] = pb;
                 std::memcpy(st.peer_handle[q], ps.handle, 64);
@@ -550,15 +588,18 @@ struct IpcTransport final : Transport {
         // ESGD_SHADOW=1 shadows every device bucket (caller buckets that are freed and
         // re-allocated between rounds; also how the tests reach the fallback)
         static const bool force_shadow = getenv("ESGD_SHADOW") && *getenv("ESGD_SHADOW") == '1';
-        int rc = force_shadow && !s.host_mode ? ESGD_ERROR : publish(s, *st);
-        if (rc && !s.host_mode) {
-            ESGD_TRACE("r%d sched %d: bucket %p not exportable (%s), shadowing it\n", s.rank, s.id,
-                       (void *)st->rb_dev, esgd_last_error());
+        if (s.host_mode) return publish_owned(s, *st);
+        int rc = force_shadow ? kCollide : publish(s, *st);
+        if (rc) {
+            // the caller's bucket cannot be exported (carved from a cached allocation), or
+            // its handle repeats a released one: reduce through an owned shadow bucket
+            ESGD_TRACE("r%d sched %d: bucket %p not exported (%s), shadowing it\n", s.rank, s.id,
+                       (void *)st->rb_dev, rc == kCollide ? "handle collision" : esgd_last_error());
             (void)hipGetLastError();
             if ((rc = alloc_bucket(s.count * s.esize, &st->rb_dev, &st->cap))) return rc;
             st->owns_rb = st->shadow = true;
             st->peer[s.rank] = st->rb_dev;
-            rc = publish(s, *st);
+            rc = publish_owned(s, *st);
         }
         return rc;
     }
@@ -578,7 +619,7 @@ struct IpcTransport final : Transport {
         const int moved = base_refit(s, st);
         if (moved < 0) return moved;
         if (s.world > 1 && moved)
-            if (int rc = publish(s, st)) return rc;
+            if (int rc = publish_owned(s, st)) return rc;
         if (s.world > 1 && s.resolve) publish_size(s);
         st.peer[s.rank] = st.rb_dev;
         ESGD_TRACE("r%d sched %d round %u join count=%llu rb_dev=%p moved=%d staged=%d\n", s.rank, s.id,
@@ -602,8 +643,10 @@ struct IpcTransport final : Transport {
             if (s.world <= ESGD_MAX_FANIN && s.count * s.esize <= small_round_bytes()) {
                 if (int rc = launch_small(s, st, round, cs)) return rc;
                 // device buckets: nothing follows the kernel, the host polls its fin flag
+                // (the event only reports faults)
                 if (!s.host_mode && !st.shadow) {
                     st.fin_mode = true;
+                    ESGD_HIP(hipEventRecord(st.ev, cs));
                     return ESGD_SUCCESS;
                 }
                 return base_copy_out(s, st, cs);
@@ -674,7 +717,7 @@ struct IpcTransport final : Transport {
         if (st->stream) (void)hipStreamSynchronize(st->stream);
         for (int q = 0; q < kMaxRanks; ++q)
             if (st->peer_base[q]) ipc_close(st->peer_base[q]);
-        if (st->pub_base) export_release(st->pub_base);
+        if (st->pub_live) release_handle(st->pub_h);
         if (st->ctr) (void)hipFree(st->ctr);
         base_teardown(s, *st);
         delete st;

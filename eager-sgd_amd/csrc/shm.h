@@ -25,7 +25,6 @@ struct alignas(64) IpcSlot {
     uint8_t handle[64];
     uint64_t offset;
     uint64_t bytes;
-    uint64_t serial;              // exporter's tag of this export (IPC mapping reuse)
     std::atomic<uint32_t> gen;    // == schedule generation when valid
     std::atomic<uint32_t> ver;    // bumped at every (re)publication (buffers that grow)
 };

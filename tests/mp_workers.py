@@ -177,6 +177,45 @@ def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0
     return verdicts
 
 
+def gpu_churn(rank, world, plan=(("fp32", 1 << 22), ("fp32", 64), ("fp32", 1001), ("fp32", 64),
+                                  ("bf16", 1 << 23), ("fp32", 1 << 22), ("bf16", 1 << 15)), rounds=2):
+    """Schedules created, run, deleted and their buckets freed one after another (the
+    bench's C5 / C4 sequence in small): later schedules reuse freed addresses and cached
+    sub-allocation chunks, while peers keep their IPC mappings of earlier buckets open.
+    Every round of every schedule must still be bit-exact."""
+    import numpy as np
+
+    from esgd import _lib
+    from esgd import device as dev
+    from oracle import ffref
+    comm = _comm()
+    verdicts = []
+    for i, (dname, count) in enumerate(plan):
+        dt = _lib.FLOAT if dname == "fp32" else _lib.BF16
+        rb = dev.DeviceBuffer(count, dt)
+        s = comm.Schedule(2, None, rb, count, dtype=dt, seed=6545343, buf=comm.BUF_DEVICE)
+        for t in range(rounds):
+            xs = [ffref.fill_uniform(0x5EED + 17 * i + t, r, count) for r in range(world)]
+            if dt == _lib.BF16:
+                xs = [ffref.f32_to_bf16(x) for x in xs]
+                want = ffref.tree_sum_bf16(xs)
+            else:
+                want = ffref.tree_sum(xs)
+            rb.upload(xs[rank])
+            comm.barrier()
+            s.post()     # majority: every rank posts, the drawn activator starts the round
+            s.wait()
+            got = rb.download()
+            bad = np.nonzero(got.view(np.uint8) != want.view(np.uint8))[0]
+            verdicts.append((i, dname, count, t, int(bad.size),
+                             int(bad[0]) if bad.size else -1, int(bad[-1]) if bad.size else -1))
+            comm.barrier()
+        s.delete()
+        rb.close()
+    comm.finalize()
+    return verdicts
+
+
 def gpu_partial_semantics(rank, world, kind, rounds, async_=3, seed=6545343, straggler=1,
                           delay=0.05, count=4096):
     """eager-SGD semantics with data: rank r writes tag_r(t) = t * 64**r into its send

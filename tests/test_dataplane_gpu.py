@@ -57,6 +57,15 @@ def test_allreduce_in_place_device():
     assert all(all(v) for v in verdicts), verdicts
 
 
+def test_schedule_and_bucket_churn():
+    # create / run / delete / free, again and again, mixing sizes, dtypes and tiny
+    # sub-allocated buckets: mappings of freed buckets stay open on the peers
+    verdicts = run("gpu_churn", 2)
+    # (step, dtype, count, round, mismatched bytes, first, last) per rank and round
+    bad = [v for per_rank in verdicts for v in per_rank if v[4]]
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("kind", [SOLO, MAJORITY])
 def test_solo_majority_round_tags(kind):
     world, rounds, async_ = 2, 9, 3
