@@ -222,10 +222,28 @@ void gpu_trace_read(Sched &s, uint64_t out[6]) {
 
 void rccl_shutdown();
 
+// k_round_small's per-schedule device words (two arrival counters, two gates), one
+// allocation for the process: a hipMalloc per schedule, on the round path, is avoided
+// (host-side memory operations were seen to slow later peer-reading kernels).
+static uint32_t *g_ctr_pool = nullptr;
+constexpr int kCtrWords = 16;   // per schedule (64 B)
+
+static int ctr_words(int sched_id, hipStream_t cs, uint32_t **out) {
+    std::lock_guard<std::mutex> lk(g_dp_mu);
+    if (!g_ctr_pool) {
+        const size_t bytes = size_t(kMaxSched) * kCtrWords * sizeof(uint32_t);
+        ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&g_ctr_pool), bytes));
+        ESGD_HIP(hipMemsetAsync(g_ctr_pool, 0, bytes, cs));
+    }
+    *out = g_ctr_pool + size_t(sched_id) * kCtrWords;
+    return ESGD_SUCCESS;
+}
+
 void dataplane_shutdown() {
     rccl_shutdown();
     std::lock_guard<std::mutex> lk(g_dp_mu);
     if (g_rs) { (void)hipStreamSynchronize(g_rs); (void)hipStreamDestroy(g_rs); g_rs = nullptr; }
+    if (g_ctr_pool) { (void)hipFree(g_ctr_pool); g_ctr_pool = nullptr; }
     ipc_close_all();
     if (g_seg_reg) { (void)hipHostUnregister(g_seg_reg); g_seg_reg = nullptr; g_seg_dev = nullptr; }
 }
@@ -260,7 +278,7 @@ struct BaseState {
 struct IpcState : BaseState {
     uint8_t pub_h[64] = {};           // handle this rank publishes (claim_handle)
     bool pub_live = false;
-    uint32_t *ctr = nullptr;          // device: k_round_small's two workgroup counters
+    uint32_t *ctr = nullptr;          // device: k_round_small's counters and gates (pool)
     char *peer[kMaxRanks] = {};
     void *peer_base[kMaxRanks] = {};
     uint32_t peer_ver[kMaxRanks] = {};
@@ -680,10 +698,8 @@ struct IpcTransport final : Transport {
 
     // the whole round as one k_round_small launch (small buckets)
     static int launch_small(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) {
-        if (!st.ctr) {   // first one-launch round of this schedule
-            ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.ctr), 256));
-            ESGD_HIP(hipMemsetAsync(st.ctr, 0, 256, cs));
-        }
+        if (!st.ctr)   // first one-launch round of this schedule
+            if (int rc = ctr_words(s.id, cs, &st.ctr)) return rc;
         const void *in[kMaxRanks];
         for (int j = 0; j < s.world; ++j) in[j] = st.peer[j] + st.off[s.rank] * s.esize;
         const void *src[kMaxRanks];
@@ -718,7 +734,6 @@ struct IpcTransport final : Transport {
         for (int q = 0; q < kMaxRanks; ++q)
             if (st->peer_base[q]) ipc_close(st->peer_base[q]);
         if (st->pub_live) release_handle(st->pub_h);
-        if (st->ctr) (void)hipFree(st->ctr);
         base_teardown(s, *st);
         delete st;
         s.tstate = nullptr;
