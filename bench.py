@@ -557,24 +557,6 @@ def run_allreduce(args, rank, world):
         parity = "bitwise (head+tail slices, every rank)" if flag.item() else "MISMATCH"
     _defer(sched, rb)
 
-    extras = {}
-    if not args.no_extras:
-        for name, fn in (("sweep_c5_majority", lambda: sweep_c5(comm, dev, world, dt, es)),
-                         ("straggler_c4_majority", lambda: straggler_c4(comm, dev, rank, world)),
-                         ("c4_resnet50_161_vs_fused", lambda: c4_resnet50_161(comm, dev, rank, world)),
-                         ("sweep_c5_majority_bf16", lambda: sweep_c5(comm, dev, world, _lib.BF16, 2)),
-                         ("c3_rccl_transport", lambda: c3_over_rccl(comm, dev, rank, world, count))):
-            try:
-                extras[name] = fn()
-            except Exception as e:   # keep the headline line; report what failed
-                import traceback
-                traceback.print_exc()
-                extras[name + "_error"] = f"rank {rank}: " + repr(e)[:300]
-                break                # peers may be inside this extra: do not start another
-    if not any(k.endswith("_error") for k in extras):
-        _delete_deferred()           # collective; after a failed leg finalize frees them
-    comm.finalize()
-
     S = count * es
     algbw = S / t_step / 1e9
     busbw = algbw * 2 * (world - 1) / world
@@ -604,6 +586,49 @@ def run_allreduce(args, rank, world):
         "rank0_stages_us": stages,
         "parity": parity,
     }
+
+    # The extra legs (C5 sweeps, C4, RCCL) run under a watchdog: if one hangs, rank 0
+    # still prints the headline line with the legs finished so far, and every rank leaves.
+    extras = {}
+    if not args.no_extras:
+        import threading
+
+        def give_up(leg):
+            if rank == 0:
+                out = dict(line)
+                out.update(extras)
+                out["extras_timeout"] = leg[0]
+                print(json.dumps(out), flush=True)
+            os._exit(0)
+
+        leg = ["none"]
+        budget = float(os.environ.get("ESGD_BENCH_EXTRAS_S", "420"))
+        dog = threading.Timer(budget, give_up, args=(leg,))
+        dog.daemon = True
+        dog.start()
+        legs = [("sweep_c5_majority", lambda: sweep_c5(comm, dev, world, dt, es)),
+                ("straggler_c4_majority", lambda: straggler_c4(comm, dev, rank, world)),
+                ("c4_resnet50_161_vs_fused", lambda: c4_resnet50_161(comm, dev, rank, world)),
+                ("sweep_c5_majority_bf16", lambda: sweep_c5(comm, dev, world, _lib.BF16, 2))]
+        if os.environ.get("ESGD_BENCH_RCCL", "1") == "1":
+            legs.append(("c3_rccl_transport", lambda: c3_over_rccl(comm, dev, rank, world, count)))
+        for name, fn in legs:
+            leg[0] = name
+            try:
+                extras[name] = fn()
+            except Exception as e:   # keep the headline line; report what failed
+                import traceback
+                traceback.print_exc()
+                extras[name + "_error"] = f"rank {rank}: " + repr(e)[:300]
+                break                # peers may be inside this leg: do not start another
+        leg[0] = "teardown"
+        if not any(k.endswith("_error") for k in extras):
+            _delete_deferred()       # collective; after a failed leg finalize frees them
+        comm.finalize()
+        dog.cancel()
+    else:
+        _delete_deferred()
+        comm.finalize()
     line.update(extras)
     dist.destroy_process_group()
     return line
