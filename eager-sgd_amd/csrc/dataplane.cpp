@@ -43,6 +43,9 @@ int round_small(int dtype, const void *const *src, void *out, uint64_t n, int ns
                 uint64_t *ts, uint32_t *counter, int rank, int world, uint32_t value,
                 long long timeout_ticks, hipStream_t s);
 
+constexpr uint64_t kPiece = uint64_t(1) << 30;   // bytes per input / segment per launch
+constexpr int kMaxSegs = 16;                      // segments per gather launch (kMaxSeg)
+
 // Buckets up to this many bytes run as one launch per round (k_round_small);
 // ESGD_SMALL_ROUND_BYTES overrides (0 = never).
 static uint64_t small_round_bytes() {
@@ -670,27 +673,39 @@ struct IpcTransport final : Transport {
                 return base_copy_out(s, st, cs);
             }
             if (int rc = pair_ranks(s, s.sh->ready, 0, round, cs)) return rc;
+            // Launches move at most kPiece bytes per input / segment (the kernels address
+            // a shard through 32-bit buffer offsets); buckets up to the reference's
+            // 2^31 - 1 elements (ff.h: int count) at any P are cut into pieces.
+            const size_t es = s.esize;
+            const uint64_t piece = kPiece / es;
             const uint64_t n = st.len[s.rank];
-            if (n) {
+            for (uint64_t o = 0; o < n; o += piece) {
+                const uint64_t c = std::min(piece, n - o);
                 const void *in[kMaxRanks];
-                for (int j = 0; j < s.world; ++j) in[j] = st.peer[j] + st.off[s.rank] * s.esize;
-                if (int rc = reduce_remote(s.dtype, s.world, in, st.rb_dev + st.off[s.rank] * s.esize, n,
+                for (int j = 0; j < s.world; ++j) in[j] = st.peer[j] + (st.off[s.rank] + o) * es;
+                if (int rc = reduce_remote(s.dtype, s.world, in, st.rb_dev + (st.off[s.rank] + o) * es, c,
                                            1.0f, cs))
                     return rc;
             }
             if (int rc = pair_ranks(s, s.sh->reduced, 1, round, cs)) return rc;
-            const void *src[kMaxRanks];
-            void *dst[kMaxRanks];
-            uint64_t bytes[kMaxRanks];
+            const void *src[kMaxSegs];
+            void *dst[kMaxSegs];
+            uint64_t bytes[kMaxSegs];
             int m = 0;
             for (int j = 0; j < s.world; ++j) {
-                if (j == s.rank || st.len[j] == 0) continue;
-                src[m] = st.peer[j] + st.off[j] * s.esize;
-                dst[m] = st.rb_dev + st.off[j] * s.esize;
-                bytes[m] = st.len[j] * s.esize;
-                ++m;
+                if (j == s.rank) continue;
+                for (uint64_t o = 0; o < st.len[j]; o += piece) {
+                    src[m] = st.peer[j] + (st.off[j] + o) * es;
+                    dst[m] = st.rb_dev + (st.off[j] + o) * es;
+                    bytes[m] = std::min(piece, st.len[j] - o) * es;
+                    if (++m == kMaxSegs) {
+                        if (int rc = gather_remote(m, src, dst, bytes, cs)) return rc;
+                        m = 0;
+                    }
+                }
             }
-            if (int rc = gather_remote(m, src, dst, bytes, cs)) return rc;
+            if (m)
+                if (int rc = gather_remote(m, src, dst, bytes, cs)) return rc;
             if (int rc = pair_ranks(s, s.sh->done, 2, round, cs)) return rc;
         }
         return base_copy_out(s, st, cs);

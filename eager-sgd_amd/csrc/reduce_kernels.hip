@@ -497,26 +497,42 @@ int gather_remote(int n, const void *const *src, void *const *dst, const uint64_
 // kernel's shard) visible before the flag is.  A wait that outlives `timeout` ticks of
 // the constant wall clock records the round in *err and returns, so a missing peer never
 // leaves a wave spinning on the device.
+// Every rank's flag at once: lane q polls flags[q] (relaxed, system scope) and the wave
+// leaves when all of them reached `value` -- one host-memory round trip per sweep instead
+// of one per rank (8 serial PCIe reads at P = 8).  Called by a whole wave; rounds compare
+// modulo 2^32.  False on timeout.
+__device__ __forceinline__ bool wave_wait_all(uint32_t *flags, int world, uint32_t value, long long t0,
+                                              long long timeout) {
+    const int lane = int(threadIdx.x & 63u);
+    for (;;) {
+        bool mine = true;
+        if (lane < world)
+            mine = int32_t(__hip_atomic_load(&flags[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - value) >= 0;
+        if (__all(mine)) return true;
+        if (wall_clock64() - t0 > timeout) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 __global__ void __launch_bounds__(64) k_round_sync(uint32_t *flags, int rank, int world,
                                                    uint32_t value, long long timeout,
                                                    uint32_t *err, uint64_t *ts) {
-    if (threadIdx.x != 0) return;
-    if (ts) ts[0] = uint64_t(wall_clock64());
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    __hip_atomic_store(&flags[rank], value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    const long long t0 = wall_clock64();
-    for (int q = 0; q < world; ++q) {
-        // unsigned distance: rounds are compared modulo 2^32
-        while (int32_t(__hip_atomic_load(&flags[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - value) < 0) {
-            if (wall_clock64() - t0 > timeout) {
-                __hip_atomic_store(err, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                return;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
+    const bool lead = threadIdx.x == 0;
+    if (lead) {
+        if (ts) ts[0] = uint64_t(wall_clock64());
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // MI355X_MICROARCH.md: compiler hazard
+        __hip_atomic_store(&flags[rank], value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    if (ts) __hip_atomic_store(&ts[1], uint64_t(wall_clock64()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const long long t0 = wall_clock64();
+    if (!wave_wait_all(flags, world, value, t0, timeout)) {
+        if (lead) __hip_atomic_store(err, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    if (lead) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if (ts) __hip_atomic_store(&ts[1], uint64_t(wall_clock64()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ts (optional): wall-clock stamps of entry and exit (tracing, ESGD_GPU_TRACE=1)
@@ -581,17 +597,20 @@ __device__ __forceinline__ bool spin_all(uint32_t *flags, int world, uint32_t va
 // (tools/lat.sh).  The workgroup then acquires at system scope.
 __device__ __forceinline__ bool block_wait(const SmallRoundArgs &a, uint32_t *flags, uint32_t *gate,
                                            bool leader, long long t0, int *ok) {
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {   // the first wave
         bool good = true;
-        if (leader) {
-            good = spin_all(flags, a.world, a.value, t0, a.timeout);
-            if (good) __hip_atomic_store(gate, a.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
+        if (leader) {         // every rank's flag at once, one lane per rank
+            good = wave_wait_all(flags, a.world, a.value, t0, a.timeout);
+            if (good && threadIdx.x == 0)
+                __hip_atomic_store(gate, a.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (threadIdx.x == 0) {
             good = spin_all(gate, 1, a.value, t0, a.timeout);
         }
-        if (good) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        else __hip_atomic_store(a.err, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        *ok = good;
+        if (threadIdx.x == 0) {
+            if (good) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            else __hip_atomic_store(a.err, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            *ok = good;
+        }
     }
     __syncthreads();
     return *ok != 0;
@@ -686,14 +705,18 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    if (!block_count(&a.counter[1], &last) || !lead) return;
-    // the last workgroup: this rank's shard must stay put until every rank has gathered it
-    if (stamp) a.ts[4] = uint64_t(wall_clock64());
-    publish_flag(&a.done[a.rank], a.value);
-    if (!spin_all(a.done, a.world, a.value, t0, a.timeout)) {
-        __hip_atomic_store(a.err, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!block_count(&a.counter[1], &last) || threadIdx.x >= 64) return;
+    // the last workgroup's first wave: this rank's shard must stay put until every rank
+    // has gathered it
+    if (lead) {
+        if (stamp) a.ts[4] = uint64_t(wall_clock64());
+        publish_flag(&a.done[a.rank], a.value);
+    }
+    if (!wave_wait_all(a.done, a.world, a.value, t0, a.timeout)) {
+        if (lead) __hip_atomic_store(a.err, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
+    if (!lead) return;
     if (stamp) a.ts[5] = uint64_t(wall_clock64());
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stamps land before fin
     __hip_atomic_store(a.fin, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

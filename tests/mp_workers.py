@@ -216,6 +216,38 @@ def gpu_churn(rank, world, plan=(("fp32", 1 << 22), ("fp32", 64), ("fp32", 1001)
     return verdicts
 
 
+def gpu_allreduce_max_count(rank, world, count=(1 << 31) - 1, m=1 << 20):
+    """ffallreduce's largest bucket (ff.h: int count = 2^31 - 1 fp32, 8 GiB per rank), in
+    place: shards beyond 2 GiB are moved in pieces.  Inputs are generated on the device;
+    head, shard-seam and tail slices are checked against the oracle on every rank."""
+    import numpy as np
+
+    from esgd import device as dev
+    from esgd._lib import check, lib
+    from oracle import ffref
+    comm = _comm()
+    seed = 0x5EEDCAFE
+    rb = dev.DeviceBuffer(count)
+    dev.fill_uniform(rb, seed, rank)
+    dev.synchronize()
+    s = comm.Schedule(0, None, rb, count, buf=comm.BUF_DEVICE)
+    comm.barrier()
+    s.post()
+    s.wait()
+    verdicts = []
+    for start in (0, count // world - m // 2, count - m):
+        got = np.empty(m, np.float32)
+        check(lib().esgd_memcpy_async(got.ctypes.data, rb.ptr + start * 4, m * 4, 1, None), "d2h")
+        dev.synchronize()
+        want = ffref.tree_sum([ffref.fill_uniform(seed, r, m, start=start) for r in range(world)])
+        verdicts.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
+    comm.barrier()
+    s.delete()
+    rb.close()
+    comm.finalize()
+    return verdicts
+
+
 def gpu_partial_semantics(rank, world, kind, rounds, async_=3, seed=6545343, straggler=1,
                           delay=0.05, count=4096):
     """eager-SGD semantics with data: rank r writes tag_r(t) = t * 64**r into its send

@@ -57,6 +57,12 @@ def test_allreduce_in_place_device():
     assert all(all(v) for v in verdicts), verdicts
 
 
+def test_allreduce_largest_bucket():
+    # 2^31 - 1 fp32 per rank (the reference's int count limit): 4 GiB shards at P = 2
+    verdicts = run("gpu_allreduce_max_count", 2, timeout=400)
+    assert all(all(v) for v in verdicts), verdicts
+
+
 def test_schedule_and_bucket_churn():
     # create / run / delete / free, again and again, mixing sizes, dtypes and tiny
     # sub-allocated buckets: mappings of freed buckets stay open on the peers

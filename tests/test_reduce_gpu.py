@@ -179,6 +179,30 @@ def test_full_size_c2_bitwise():
     bits_equal(got, ffref.tree_sum(xs))
 
 
+def download_slice(buf, start, m):
+    """Elements [start, start + m) of a float32 device buffer."""
+    from esgd._lib import check, lib
+    out = np.empty(m, np.float32)
+    check(lib().esgd_memcpy_async(out.ctypes.data, buf.ptr + start * 4, m * 4, 1, None), "d2h")
+    synchronize()
+    return out
+
+
+def test_reduce_beyond_int32_elements():
+    """Buckets longer than 2^31 elements (8 GiB of fp32: the 64-bit flat path), checked
+    against the oracle on a head, a middle slice across element 2^31, and the ragged tail."""
+    n, k, seed, m = (1 << 31) + 5, 2, 0x5EED0B16, 1 << 20
+    bufs = [DeviceBuffer(n) for _ in range(k)]
+    for r, b in enumerate(bufs):
+        fill_uniform(b, seed, r)
+    out = DeviceBuffer(n)
+    reduce(_lib.FLOAT, [b.ptr for b in bufs], out, n)
+    synchronize()
+    for start in (0, (1 << 31) - m // 2, n - m):
+        want = ffref.tree_sum([ffref.fill_uniform(seed, r, m, start=start) for r in range(k)])
+        bits_equal(download_slice(out, start, m), want)
+
+
 def test_full_size_gate_256mib_bitwise():
     """The 1-GPU gate shape of BASELINE.json: 8 x 256 MiB fp32 buckets, checked in full."""
     n, k, seed = 64 * 1024 * 1024, 8, 0x5EEDE56D
