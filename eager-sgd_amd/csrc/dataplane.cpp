@@ -43,8 +43,19 @@ int round_small(int dtype, const void *const *src, void *out, uint64_t n, int ns
                 uint64_t *ts, uint32_t *counter, int rank, int world, uint32_t value,
                 long long timeout_ticks, hipStream_t s);
 
-constexpr uint64_t kPiece = uint64_t(1) << 30;   // bytes per input / segment per launch
 constexpr int kMaxSegs = 16;                      // segments per gather launch (kMaxSeg)
+
+// Bytes per input / segment of one remote launch (the kernels address a shard through
+// 32-bit buffer offsets): 1 GiB; ESGD_PIECE_BYTES (a multiple of 1 KiB) overrides it so
+// the tests can drive the piecewise path with small buckets.
+static uint64_t piece_bytes() {
+    static const uint64_t v = [] {
+        const char *e = getenv("ESGD_PIECE_BYTES");
+        const uint64_t b = (e && *e) ? uint64_t(strtoull(e, nullptr, 10)) : (uint64_t(1) << 30);
+        return std::max<uint64_t>(1024, std::min<uint64_t>(b, uint64_t(1) << 30) / 1024 * 1024);
+    }();
+    return v;
+}
 
 // Buckets up to this many bytes run as one launch per round (k_round_small);
 // ESGD_SMALL_ROUND_BYTES overrides (0 = never).
@@ -677,7 +688,7 @@ struct IpcTransport final : Transport {
             // a shard through 32-bit buffer offsets); buckets up to the reference's
             // 2^31 - 1 elements (ff.h: int count) at any P are cut into pieces.
             const size_t es = s.esize;
-            const uint64_t piece = kPiece / es;
+            const uint64_t piece = piece_bytes() / es;
             const uint64_t n = st.len[s.rank];
             for (uint64_t o = 0; o < n; o += piece) {
                 const uint64_t c = std::min(piece, n - o);

@@ -107,7 +107,8 @@ def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0
 
 
 def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0, buf="device",
-                  in_place=False, transport="ipc", shadow_ranks=(), small_bytes=None):
+                  in_place=False, transport="ipc", shadow_ranks=(), small_bytes=None,
+                  piece_bytes=None):
     """Data plane on the GPU: every rank reduces its splitmix bucket; returns the
     result bytes' digest per round plus a bit-exactness verdict against the oracle.
     shadow_ranks: ranks whose device buckets go through the owned shadow bucket.
@@ -119,6 +120,8 @@ def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0
         os.environ["ESGD_SHADOW"] = "1"
     if small_bytes is not None:
         os.environ["ESGD_SMALL_ROUND_BYTES"] = str(small_bytes)
+    if piece_bytes is not None:
+        os.environ["ESGD_PIECE_BYTES"] = str(piece_bytes)
 
     from esgd import _lib
     from esgd import device as dev
@@ -212,38 +215,6 @@ def gpu_churn(rank, world, plan=(("fp32", 1 << 22), ("fp32", 64), ("fp32", 1001)
             comm.barrier()
         s.delete()
         rb.close()
-    comm.finalize()
-    return verdicts
-
-
-def gpu_allreduce_max_count(rank, world, count=(1 << 31) - 1, m=1 << 20):
-    """ffallreduce's largest bucket (ff.h: int count = 2^31 - 1 fp32, 8 GiB per rank), in
-    place: shards beyond 2 GiB are moved in pieces.  Inputs are generated on the device;
-    head, shard-seam and tail slices are checked against the oracle on every rank."""
-    import numpy as np
-
-    from esgd import device as dev
-    from esgd._lib import check, lib
-    from oracle import ffref
-    comm = _comm()
-    seed = 0x5EEDCAFE
-    rb = dev.DeviceBuffer(count)
-    dev.fill_uniform(rb, seed, rank)
-    dev.synchronize()
-    s = comm.Schedule(0, None, rb, count, buf=comm.BUF_DEVICE)
-    comm.barrier()
-    s.post()
-    s.wait()
-    verdicts = []
-    for start in (0, count // world - m // 2, count - m):
-        got = np.empty(m, np.float32)
-        check(lib().esgd_memcpy_async(got.ctypes.data, rb.ptr + start * 4, m * 4, 1, None), "d2h")
-        dev.synchronize()
-        want = ffref.tree_sum([ffref.fill_uniform(seed, r, m, start=start) for r in range(world)])
-        verdicts.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
-    comm.barrier()
-    s.delete()
-    rb.close()
     comm.finalize()
     return verdicts
 

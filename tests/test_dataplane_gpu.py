@@ -57,10 +57,14 @@ def test_allreduce_in_place_device():
     assert all(all(v) for v in verdicts), verdicts
 
 
-def test_allreduce_largest_bucket():
-    # 2^31 - 1 fp32 per rank (the reference's int count limit): 4 GiB shards at P = 2
-    verdicts = run("gpu_allreduce_max_count", 2, timeout=400)
-    assert all(all(v) for v in verdicts), verdicts
+@pytest.mark.parametrize("world", [2, 3])
+def test_allreduce_in_pieces(world):
+    # shards are moved in pieces of at most 1 GiB (ff.h's 2^31 - 1 fp32 bucket has 4 GiB
+    # shards at P = 2); 4 KiB pieces drive the same code with a small bucket, ragged last
+    # pieces and more than 16 gather segments included
+    for count in (100003, 65536 * 3 + 1):
+        verdicts = run("gpu_allreduce", world, count=count, rounds=2, small_bytes=0, piece_bytes=4096)
+        assert all(all(v) for v in verdicts), (count, verdicts)
 
 
 def test_schedule_and_bucket_churn():

@@ -198,7 +198,7 @@ def test_reduce_beyond_int32_elements():
     out = DeviceBuffer(n)
     reduce(_lib.FLOAT, [b.ptr for b in bufs], out, n)
     synchronize()
-    for start in (0, (1 << 31) - m // 2, n - m):
+    for start in (0, (1 << 31) - m + 4, n - m):   # the middle slice ends past element 2^31
         want = ffref.tree_sum([ffref.fill_uniform(seed, r, m, start=start) for r in range(k)])
         bits_equal(download_slice(out, start, m), want)
 
