@@ -606,10 +606,12 @@ def run_allreduce(args, rank, world):
         dog = threading.Timer(budget, give_up, args=(leg,))
         dog.daemon = True
         dog.start()
+        # both C5 sweeps first: the C4 legs leave 160+ schedules (and their peer mappings)
+        # alive until the end, and small rounds measured after them were bimodal
         legs = [("sweep_c5_majority", lambda: sweep_c5(comm, dev, world, dt, es)),
+                ("sweep_c5_majority_bf16", lambda: sweep_c5(comm, dev, world, _lib.BF16, 2)),
                 ("straggler_c4_majority", lambda: straggler_c4(comm, dev, rank, world)),
-                ("c4_resnet50_161_vs_fused", lambda: c4_resnet50_161(comm, dev, rank, world)),
-                ("sweep_c5_majority_bf16", lambda: sweep_c5(comm, dev, world, _lib.BF16, 2))]
+                ("c4_resnet50_161_vs_fused", lambda: c4_resnet50_161(comm, dev, rank, world))]
         if os.environ.get("ESGD_BENCH_RCCL", "1") == "1":
             legs.append(("c3_rccl_transport", lambda: c3_over_rccl(comm, dev, rank, world, count)))
         for name, fn in legs:
