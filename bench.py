@@ -452,23 +452,28 @@ def straggler_c4(comm, dev, rank, world, rounds=24):
     ones.upload(np.ones(count, np.float32))
     sb, rb = dev.DeviceBuffer(count), dev.DeviceBuffer(count)
     sb.zero(); rb.zero()
-    st = dev.Stream()
     dev.synchronize()
     sch = comm.Schedule(comm.MAJORITY, sb, rb, count, dtype=_lib.FLOAT, seed=6545343,
                         buf=comm.BUF_DEVICE)
-    cell = np.zeros(1, np.float32)
+    hp = C.c_void_p()   # pinned: a pageable D2H, like an extra stream, slows later rounds
+    check(lib().esgd_host_alloc(C.byref(hp), 64))
+    cell = np.ctypeslib.as_array(C.cast(hp, C.POINTER(C.c_float)), shape=(1,))
 
     def one(delay):
         if delay:
             time.sleep(delay)
-        check(lib().esgd_memcpy_async(sb.ptr, ones.ptr, count * 4, 2, st.handle))
+        # no stream of its own: with ranks sharing the box's one GPU, one more HIP stream
+        # per process made every later round 2-10x slower (tools/chain_probe.py,
+        # CHAIN_STREAMS=1), which the C4 legs after this one would have measured
+        check(lib().esgd_memcpy_async(sb.ptr, ones.ptr, count * 4, 2, None))
+        dev.synchronize()
         t0 = time.perf_counter()
-        sch.post(st)
+        sch.post()
         sch.wait()
         dt_ = time.perf_counter() - t0
-        check(lib().esgd_memcpy_async(cell.ctypes.data, rb.ptr, 4, 1, st.handle))
-        check(lib().esgd_memset_async(sb.ptr, 0, count * 4, st.handle))
-        st.synchronize()
+        check(lib().esgd_memcpy_async(cell.ctypes.data, rb.ptr, 4, 1, None))
+        check(lib().esgd_memset_async(sb.ptr, 0, count * 4, None))
+        dev.synchronize()
         return dt_, float(cell[0])
 
     base = []
@@ -483,6 +488,7 @@ def straggler_c4(comm, dev, rank, world, rounds=24):
         lat.append(d); contrib.append(c)
     on_time = _max_over_ranks(statistics.median(lat) if rank != world - 1 else 0.0)
     _defer(sch, ones, sb, rb)
+    check(lib().esgd_host_free(hp))
     return {"bucket_fp32": count, "T_no_straggler_ms": round(T * 1e3, 3),
             "straggler_delay_ms": round(0.2 * T * 1e3, 3),
             "on_time_ranks_median_ms": round(on_time * 1e3, 3),
@@ -614,6 +620,10 @@ def run_allreduce(args, rank, world):
                 ("c4_resnet50_161_vs_fused", lambda: c4_resnet50_161(comm, dev, rank, world))]
         if os.environ.get("ESGD_BENCH_RCCL", "1") == "1":
             legs.append(("c3_rccl_transport", lambda: c3_over_rccl(comm, dev, rank, world, count)))
+        only = os.environ.get("ESGD_BENCH_LEGS")   # comma-separated subset, in this order
+        if only:
+            pick = only.split(",")
+            legs = sorted((lg for lg in legs if lg[0] in pick), key=lambda lg: pick.index(lg[0]))
         for name, fn in legs:
             leg[0] = name
             try:
