@@ -418,6 +418,45 @@ def c3_over_rccl(comm, dev, rank, world, count, steps=20):
             "xgmi_frac": round(t_min / t, 4), "parity_rank_slice": "bitwise" if ok else "MISMATCH"}
 
 
+def c3_host_buckets(comm, dev, rank, world, count, steps=8):
+    """C3 on the reference's own contract: the bucket lives in host memory (the wrapper's
+    calloc'd buckets, opt_esgd_solo_imagenet_imbalance.py:288-298), so each round is
+    H2D -> reduce-scatter -> all-gather -> D2H.  The caller's array is pinned at schedule
+    creation (hipHostRegister), so both copies are DMA."""
+    import numpy as np
+
+    from esgd._lib import check, lib
+    from oracle import ffref
+    host = np.empty(count, np.float32)
+    sch = comm.Schedule(comm.SOLO, None, host, count, async_=32, seed=6545343, buf=comm.BUF_HOST)
+    src = dev.DeviceBuffer(count)
+
+    def refill(seed):
+        dev.fill_uniform(src, seed, rank)
+        check(lib().esgd_memcpy_async(host.ctypes.data, src.ptr, count * 4, 1, None))
+        dev.synchronize()
+
+    def step():
+        sch.post()
+        sch.wait()
+
+    refill(SEED)
+    for _ in range(2):
+        step()
+    t = _timed_steps(comm, step, steps)
+    refill(SEED + 2)
+    comm.barrier()
+    step()
+    m = min(count, 1 << 18)
+    want = ffref.tree_sum([ffref.fill_uniform(SEED + 2, r, m, start=count - m) for r in range(world)])
+    ok = bool(np.array_equal(host[count - m:].view(np.uint32), want.view(np.uint32)))
+    _defer(sch, src)          # the schedule object keeps `host` alive
+    S = count * 4
+    return {"bucket_bytes": S, "round_ms_median": round(t * 1e3, 3),
+            "value_GBs": round(world * S / t / 1e9, 2), "pcie_bytes_per_rank": 2 * S,
+            "parity_tail_slice": "bitwise" if ok else "MISMATCH"}
+
+
 def _stages_us(tl):
     """Median per-round host timeline of this rank (esgd_schedule_timeline), in us:
     post->join, join->launch, launch (host), launched->completion seen, ->wait returned."""
@@ -617,7 +656,9 @@ def run_allreduce(args, rank, world):
         legs = [("sweep_c5_majority", lambda: sweep_c5(comm, dev, world, dt, es)),
                 ("sweep_c5_majority_bf16", lambda: sweep_c5(comm, dev, world, _lib.BF16, 2)),
                 ("straggler_c4_majority", lambda: straggler_c4(comm, dev, rank, world)),
-                ("c4_resnet50_161_vs_fused", lambda: c4_resnet50_161(comm, dev, rank, world))]
+                ("c4_resnet50_161_vs_fused", lambda: c4_resnet50_161(comm, dev, rank, world)),
+                ("c3_host_buckets", lambda: c3_host_buckets(comm, dev, rank, world,
+                                                                  int(args.bucket_mib * MiB) // 4))]
         if os.environ.get("ESGD_BENCH_RCCL", "1") == "1":
             legs.append(("c3_rccl_transport", lambda: c3_over_rccl(comm, dev, rank, world, count)))
         only = os.environ.get("ESGD_BENCH_LEGS")   # comma-separated subset, in this order
