@@ -181,6 +181,30 @@ static int round_stream(hipStream_t *out) {
     return ESGD_SUCCESS;
 }
 
+// Copy streams of the chunked host-bucket rounds (one per direction, so a chunk's D2H
+// runs while the next chunk's H2D does: PCIe is full duplex).  Created on first use.
+static hipStream_t g_h2d = nullptr, g_d2h = nullptr;
+
+static int copy_streams(hipStream_t *h2d, hipStream_t *d2h) {
+    std::lock_guard<std::mutex> lk(g_dp_mu);
+    if (!g_h2d) ESGD_HIP(hipStreamCreateWithFlags(&g_h2d, hipStreamNonBlocking));
+    if (!g_d2h) ESGD_HIP(hipStreamCreateWithFlags(&g_d2h, hipStreamNonBlocking));
+    *h2d = g_h2d;
+    *d2h = g_d2h;
+    return ESGD_SUCCESS;
+}
+
+// Host buckets of at least two chunks of this many bytes run chunked rounds
+// (ESGD_HOST_CHUNK_BYTES, a multiple of 1 KiB; 0 = never).
+static uint64_t host_chunk_bytes() {
+    static const uint64_t v = [] {
+        const char *e = getenv("ESGD_HOST_CHUNK_BYTES");
+        const uint64_t b = (e && *e) ? uint64_t(strtoull(e, nullptr, 10)) : (uint64_t(16) << 20);
+        return b ? std::max<uint64_t>(16384, b / 1024 * 1024) : 0;
+    }();
+    return v;
+}
+
 static int register_segment() {
     std::lock_guard<std::mutex> lk(g_dp_mu);
     Segment *seg = engine_segment();
@@ -204,19 +228,22 @@ static uint32_t *dev_flag(T *host) {
 }
 
 int round_sync(uint32_t *flags, int rank, int world, uint32_t value, long long timeout_ticks,
-               uint32_t *err, uint64_t *ts, hipStream_t s);
+               uint32_t *err, uint32_t errval, uint64_t *ts, hipStream_t s);
 
 static bool gpu_trace_on() {
     static const bool on = getenv("ESGD_GPU_TRACE") && *getenv("ESGD_GPU_TRACE") == '1';
     return on;
 }
 
-// which = 0 ready, 1 reduced, 2 done
-static int pair_ranks(Sched &s, std::atomic<uint32_t> *flags, int which, uint32_t round, hipStream_t cs) {
+// which = 0 ready, 1 reduced, 2 done; `value` is the round, or the chunk number of a
+// chunked round (a timeout still records the round)
+static int pair_ranks(Sched &s, std::atomic<uint32_t> *flags, int which, uint32_t round, hipStream_t cs,
+                      uint32_t value = 0) {
     const long long ticks = (long long)(engine_timeout() * double(g_ticks_per_s));
     uint64_t *ts = gpu_trace_on() ? reinterpret_cast<uint64_t *>(dev_flag(&s.sh->gpu_ts[s.rank][2 * which]))
                                   : nullptr;
-    return round_sync(dev_flag(flags), s.rank, s.world, round, ticks, dev_flag(&s.sh->gpu_err[s.rank]), ts, cs);
+    return round_sync(dev_flag(flags), s.rank, s.world, value ? value : round, ticks,
+                      dev_flag(&s.sh->gpu_err[s.rank]), round, ts, cs);
 }
 
 // ns between the GPU stamps of the last round (ESGD_GPU_TRACE=1), for the timeline
@@ -257,6 +284,8 @@ void dataplane_shutdown() {
     rccl_shutdown();
     std::lock_guard<std::mutex> lk(g_dp_mu);
     if (g_rs) { (void)hipStreamSynchronize(g_rs); (void)hipStreamDestroy(g_rs); g_rs = nullptr; }
+    for (hipStream_t *c : {&g_h2d, &g_d2h})
+        if (*c) { (void)hipStreamSynchronize(*c); (void)hipStreamDestroy(*c); *c = nullptr; }
     if (g_ctr_pool) { (void)hipFree(g_ctr_pool); g_ctr_pool = nullptr; }
     ipc_close_all();
     if (g_seg_reg) { (void)hipHostUnregister(g_seg_reg); g_seg_reg = nullptr; g_seg_dev = nullptr; }
@@ -293,6 +322,8 @@ struct IpcState : BaseState {
     uint8_t pub_h[64] = {};           // handle this rank publishes (claim_handle)
     bool pub_live = false;
     uint32_t *ctr = nullptr;          // device: k_round_small's counters and gates (pool)
+    std::vector<hipEvent_t> cev;      // chunked host rounds: per chunk H2D / reduced / D2H
+    bool chunked_before = false;
     char *peer[kMaxRanks] = {};
     void *peer_base[kMaxRanks] = {};
     uint32_t peer_ver[kMaxRanks] = {};
@@ -421,12 +452,17 @@ static int base_prepare(Sched &s, BaseState &st) {
 
 // queued at launch: the producer of this round (posted before the join) must have
 // finished, then the move sb -> rb (host -> HBM for host buckets)
-static int base_copy_in(Sched &s, BaseState &st, uint32_t round, bool fresh, hipStream_t cs) {
+static int producer_wait(BaseState &st, uint32_t round, bool fresh, hipStream_t cs) {
     for (auto it = st.producer.begin(); it != st.producer.end();) {
         if (it->first == round && fresh) ESGD_HIP(hipStreamWaitEvent(cs, it->second, 0));
         if (it->first <= round) { st.spare.push_back(it->second); it = st.producer.erase(it); }
         else ++it;
     }
+    return ESGD_SUCCESS;
+}
+
+static int base_copy_in(Sched &s, BaseState &st, uint32_t round, bool fresh, hipStream_t cs) {
+    if (int rc = producer_wait(st, round, fresh, cs)) return rc;
     const size_t bytes = s.count * s.esize;
     if (!bytes) return ESGD_SUCCESS;
     if (s.host_mode) {
@@ -668,6 +704,8 @@ struct IpcTransport final : Transport {
         IpcState &st = S(s);
         hipStream_t cs = st.stream;
         st.fin_mode = false;
+        if (s.host_mode && !s.resolve && host_chunk_bytes() && s.count * s.esize >= 2 * host_chunk_bytes())
+            return launch_chunked(s, st, round, fresh);
         if (int rc = base_copy_in(s, st, round, fresh, cs)) return rc;
         if (s.world > 1) {
             if (s.resolve)
@@ -722,6 +760,86 @@ struct IpcTransport final : Transport {
         return base_copy_out(s, st, cs);
     }
 
+    // Host buckets (the reference's contract) of >= 2 chunks: the round runs chunk by
+    // chunk so that the copies overlap -- chunk c's H2D (copy stream 1) -> on the round
+    // stream [pair: ready] reduce-scatter [pair: reduced] all-gather [pair: done] of
+    // chunk c, each chunk split into P shards like a whole bucket -> chunk c's D2H (copy
+    // stream 2), while chunk c+1 is uploaded.  Pairing values number the chunks,
+    // (round - 1) * C + c + 1, so they keep increasing (C is fixed: the bucket size of a
+    // non-FFCOLL_BUFFERS schedule never changes).  A chunk is overwritten by the next
+    // round's H2D only after this round's D2H of it, which follows its done pairing
+    // (no peer still reads it).  Sums are element-wise, so the result is bit-identical
+    // to the one-piece round.
+    static int launch_chunked(Sched &s, IpcState &st, uint32_t round, bool fresh) {
+        hipStream_t cs = st.stream, hs = nullptr, ds = nullptr;
+        if (int rc = copy_streams(&hs, &ds)) return rc;
+        if (int rc = producer_wait(st, round, fresh, hs)) return rc;
+        const size_t es = s.esize;
+        const uint64_t count = s.count, align = 1024;   // elements: 1 KiB+ aligned chunks
+        const uint64_t want = std::min<uint64_t>(64, (count * es + host_chunk_bytes() - 1) / host_chunk_bytes());
+        uint64_t Q = (count + want - 1) / want;
+        Q = (Q + align - 1) / align * align;
+        const uint32_t C = uint32_t((count + Q - 1) / Q);
+        while (st.cev.size() < 3 * size_t(C)) {
+            hipEvent_t e;
+            ESGD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            st.cev.push_back(e);
+        }
+        const bool stg = staged(s, st);
+        const char *src = stg ? st.pin : static_cast<const char *>(s.sb ? s.sb : s.rb);
+        char *dst = stg ? st.pin : static_cast<char *>(s.rb);
+        const uint64_t salign = 1024 / es;
+        for (uint32_t c = 0; c < C; ++c) {
+            const uint64_t c0 = uint64_t(c) * Q, n = std::min(Q, count - c0);
+            hipEvent_t eh = st.cev[3 * c], er = st.cev[3 * c + 1], ed = st.cev[3 * c + 2];
+            if (st.chunked_before) ESGD_HIP(hipStreamWaitEvent(hs, ed, 0));   // last round's D2H
+            ESGD_HIP(hipMemcpyAsync(st.rb_dev + c0 * es, src + c0 * es, n * es, hipMemcpyHostToDevice, hs));
+            ESGD_HIP(hipEventRecord(eh, hs));
+            ESGD_HIP(hipStreamWaitEvent(cs, eh, 0));
+            if (s.world > 1) {
+                uint64_t per = (n + uint64_t(s.world) - 1) / uint64_t(s.world);
+                per = (per + salign - 1) / salign * salign;
+                uint64_t off[kMaxRanks], len[kMaxRanks];
+                for (int j = 0; j < s.world; ++j) {
+                    const uint64_t o = std::min<uint64_t>(n, per * uint64_t(j));
+                    off[j] = c0 + o;
+                    len[j] = std::min<uint64_t>(per, n - o);
+                }
+                const uint32_t v = (round - 1) * C + c + 1;
+                if (int rc = pair_ranks(s, s.sh->ready, 0, round, cs, v)) return rc;
+                if (len[s.rank]) {
+                    const void *in[kMaxRanks];
+                    for (int j = 0; j < s.world; ++j) in[j] = st.peer[j] + off[s.rank] * es;
+                    if (int rc = reduce_remote(s.dtype, s.world, in, st.rb_dev + off[s.rank] * es, len[s.rank],
+                                               1.0f, cs))
+                        return rc;
+                }
+                if (int rc = pair_ranks(s, s.sh->reduced, 1, round, cs, v)) return rc;
+                const void *gs[kMaxSegs];
+                void *gd[kMaxSegs];
+                uint64_t gb[kMaxSegs];
+                int m = 0;
+                for (int j = 0; j < s.world; ++j) {
+                    if (j == s.rank || !len[j]) continue;
+                    gs[m] = st.peer[j] + off[j] * es;
+                    gd[m] = st.rb_dev + off[j] * es;
+                    gb[m++] = len[j] * es;
+                }
+                if (int rc = gather_remote(m, gs, gd, gb, cs)) return rc;
+                if (int rc = pair_ranks(s, s.sh->done, 2, round, cs, v)) return rc;
+            }
+            ESGD_HIP(hipEventRecord(er, cs));
+            ESGD_HIP(hipStreamWaitEvent(ds, er, 0));
+            ESGD_HIP(hipMemcpyAsync(dst + c0 * es, st.rb_dev + c0 * es, n * es, hipMemcpyDeviceToHost, ds));
+            ESGD_HIP(hipEventRecord(ed, ds));
+        }
+        ESGD_HIP(hipStreamWaitEvent(cs, st.cev[3 * (C - 1) + 2], 0));   // ds is in order
+        st.copyout_pending = stg;
+        st.chunked_before = true;
+        ESGD_HIP(hipEventRecord(st.ev, cs));
+        return ESGD_SUCCESS;
+    }
+
     // the whole round as one k_round_small launch (small buckets)
     static int launch_small(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) {
         if (!st.ctr)   // first one-launch round of this schedule
@@ -757,6 +875,7 @@ struct IpcTransport final : Transport {
         IpcState *st = static_cast<IpcState *>(s.tstate);
         if (!st) return;
         if (st->stream) (void)hipStreamSynchronize(st->stream);
+        for (hipEvent_t e : st->cev) (void)hipEventDestroy(e);
         for (int q = 0; q < kMaxRanks; ++q)
             if (st->peer_base[q]) ipc_close(st->peer_base[q]);
         if (st->pub_live) release_handle(st->pub_h);

@@ -516,7 +516,7 @@ __device__ __forceinline__ bool wave_wait_all(uint32_t *flags, int world, uint32
 
 __global__ void __launch_bounds__(64) k_round_sync(uint32_t *flags, int rank, int world,
                                                    uint32_t value, long long timeout,
-                                                   uint32_t *err, uint64_t *ts) {
+                                                   uint32_t *err, uint32_t errval, uint64_t *ts) {
     const bool lead = threadIdx.x == 0;
     if (lead) {
         if (ts) ts[0] = uint64_t(wall_clock64());
@@ -526,7 +526,7 @@ __global__ void __launch_bounds__(64) k_round_sync(uint32_t *flags, int rank, in
     }
     const long long t0 = wall_clock64();
     if (!wave_wait_all(flags, world, value, t0, timeout)) {
-        if (lead) __hip_atomic_store(err, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lead) __hip_atomic_store(err, errval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
     if (lead) {
@@ -535,12 +535,14 @@ __global__ void __launch_bounds__(64) k_round_sync(uint32_t *flags, int rank, in
     }
 }
 
-// ts (optional): wall-clock stamps of entry and exit (tracing, ESGD_GPU_TRACE=1)
+// ts (optional): wall-clock stamps of entry and exit (tracing, ESGD_GPU_TRACE=1);
+// errval: what a timed-out wait records in *err (the round, also when `value` numbers
+// a chunk of it)
 int round_sync(uint32_t *flags, int rank, int world, uint32_t value, long long timeout_ticks,
-               uint32_t *err, uint64_t *ts, hipStream_t s) {
+               uint32_t *err, uint32_t errval, uint64_t *ts, hipStream_t s) {
     ESGD_ARG(flags && err && world >= 1 && rank >= 0 && rank < world, "round_sync: bad arguments");
     hipLaunchKernelGGL(k_round_sync, dim3(1), dim3(64), 0, s, flags, rank, world, value,
-                       timeout_ticks, err, ts);
+                       timeout_ticks, err, errval, ts);
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;
 }

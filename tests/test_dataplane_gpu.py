@@ -52,6 +52,29 @@ def test_allreduce_host_buffers(in_place):
     assert all(all(v) for v in verdicts), verdicts
 
 
+@pytest.mark.parametrize("in_place", [False, True])
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_allreduce_host_chunked(world, in_place):
+    # host buckets of >= 2 chunks run chunk by chunk (H2D of one chunk beside the D2H of
+    # the previous); 64 KiB chunks: 7 chunks, the last one ragged, 3 rounds back to back
+    verdicts = run("gpu_allreduce", world, count=100003, rounds=3, buf="host", in_place=in_place,
+                   host_chunk=65536)
+    assert all(all(v) for v in verdicts), verdicts
+
+
+@pytest.mark.parametrize("dtype", ["fp64", "bf16", "int32"])
+def test_allreduce_host_chunked_dtypes(dtype):
+    verdicts = run("gpu_allreduce", 2, dtype_name=dtype, count=70001, rounds=2, buf="host",
+                   host_chunk=32768)
+    assert all(all(v) for v in verdicts), verdicts
+
+
+def test_allreduce_host_chunked_default_size():
+    # 36 MB host bucket: three 16 MiB-class chunks at the default chunk size
+    verdicts = run("gpu_allreduce", 2, count=9_000_003, rounds=2, buf="host")
+    assert all(all(v) for v in verdicts), verdicts
+
+
 def test_allreduce_in_place_device():
     verdicts = run("gpu_allreduce", 4, count=65536 * 4 + 5, rounds=2, in_place=True)
     assert all(all(v) for v in verdicts), verdicts
