@@ -771,7 +771,13 @@ int round_small(int dtype, const void *const *src, void *out, uint64_t n, int ns
     a.ts = ts;
     a.counter = counter;
     a.rank = rank; a.world = world; a.value = value; a.timeout = timeout_ticks;
-    const unsigned grid = unsigned(std::min<uint64_t>(kSmallBlocks, std::max<uint64_t>(1, (maxv + 255) / 256)));
+    // ESGD_SMALL_GRID caps the workgroups (default kSmallBlocks); every one must be resident
+    static const uint64_t cap = [] {
+        const char *e = getenv("ESGD_SMALL_GRID");
+        const long v = (e && *e) ? strtol(e, nullptr, 10) : kSmallBlocks;
+        return uint64_t(std::max(1L, std::min(v, 256L)));
+    }();
+    const unsigned grid = unsigned(std::min<uint64_t>(cap, std::max<uint64_t>(1, (maxv + 255) / 256)));
     switch (dtype) {
     case ESGD_FLOAT: return launch_small_t<F32>(a, grid, s);
     case ESGD_BF16: return launch_small_t<BF16>(a, grid, s);
