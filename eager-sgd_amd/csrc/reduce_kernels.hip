@@ -662,11 +662,18 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
     for (int j = 0; j < K; ++j)
         rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(a.src[j]), (short)0, bytes, 0x00020000);
     __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, bytes, 0x00020000);
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += gridDim.x * 256) {
-        raw16 r[K];
+    // U vectors per input per lane in flight (the range check drops the ragged end)
+    constexpr int U = sizeof(T) == 2 ? 2 : 4;
+    for (uint32_t i = blockIdx.x * (256 * U) + threadIdx.x; i < nvec; i += gridDim.x * (256 * U)) {
+        raw16 r[U][K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) r[j] = __builtin_amdgcn_raw_buffer_load_b128(rs[j], i * 16, 0, 17);
-        __builtin_amdgcn_raw_buffer_store_b128(fold16<Tr, K, false>(r, 1.0f), ws, i * 16, 0, 17);
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                r[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs[j], (i + u * 256) * 16, 0, 17);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_raw_buffer_store_b128(fold16<Tr, K, false>(r[u], 1.0f), ws, (i + u * 256) * 16, 0, 17);
     }
     if (blockIdx.x == 0 && uint64_t(nvec) * Tr::E + threadIdx.x < a.n) {
         const uint64_t e = uint64_t(nvec) * Tr::E + threadIdx.x;
@@ -695,9 +702,13 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
                                                                          int(gv * 16u), 0x00020000);
             __amdgpu_buffer_rsrc_t gd = __builtin_amdgcn_make_buffer_rsrc(a.gdst[sg], (short)0, int(gv * 16u),
                                                                          0x00020000);
-            for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < gv; i += gridDim.x * 256)
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(gs, i * 16, 0, 17),
-                                                       gd, i * 16, 0, 17);
+            for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < gv; i += gridDim.x * 1024) {
+                raw16 r[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b128(gs, (i + u * 256) * 16, 0, 17);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(r[u], gd, (i + u * 256) * 16, 0, 17);
+            }
         }
         if (blockIdx.x == 0 && threadIdx.x < a.gtail[sg]) {
             const uint8_t *src = static_cast<const uint8_t *>(a.gsrc[sg]) + size_t(gv) * 16;
@@ -777,7 +788,7 @@ int round_small(int dtype, const void *const *src, void *out, uint64_t n, int ns
         const long v = (e && *e) ? strtol(e, nullptr, 10) : kSmallBlocks;
         return uint64_t(std::max(1L, std::min(v, 256L)));
     }();
-    const unsigned grid = unsigned(std::min<uint64_t>(cap, std::max<uint64_t>(1, (maxv + 255) / 256)));
+    const unsigned grid = unsigned(std::min<uint64_t>(cap, std::max<uint64_t>(1, (maxv + 1023) / 1024)));
     switch (dtype) {
     case ESGD_FLOAT: return launch_small_t<F32>(a, grid, s);
     case ESGD_BF16: return launch_small_t<BF16>(a, grid, s);
