@@ -126,23 +126,21 @@ def run_local(args, esgd, dev):
         dev.reduce(dt, ptrs, out, count, stream=s)
     s.synchronize()
 
-    # HIP event pairs on the launch stream around every 4th launch of the timed region:
-    # the kernel's own duration, without the marker packets slowing every step
-    every = 4
-    evs = [(dev.Event(), dev.Event()) for _ in range(0, args.steps, every)]
+    # One HIP event pair on the launch stream around the whole timed region: the average
+    # launch duration including the dispatch gap between back-to-back launches (a pair
+    # around single launches adds its marker packets' cost to every measured launch:
+    # 96.2 us per launch against rocprof's 92.5 us on one box)
+    ev0, ev1 = dev.Event(), dev.Event()
     dev.device_synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        if i % every == 0:
-            evs[i // every][0].record(s)
-            dev.reduce(dt, ptrs, out, count, stream=s)
-            evs[i // every][1].record(s)
-        else:
-            dev.reduce(dt, ptrs, out, count, stream=s)
+    ev0.record(s)
+    for _ in range(args.steps):
+        dev.reduce(dt, ptrs, out, count, stream=s)
+    ev1.record(s)
     s.synchronize()
     dev.device_synchronize()
     wall = time.perf_counter() - t0
-    per_launch_ms = sum(a.elapsed_ms(b) for a, b in evs) / len(evs)
+    per_launch_ms = ev0.elapsed_ms(ev1) / args.steps
 
     # parity spot-check outside the timed region: first 1 Mi elements vs the oracle
     parity = "skipped"
