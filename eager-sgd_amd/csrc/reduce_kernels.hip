@@ -389,6 +389,10 @@ static int dispatch_u(const InputSet &in, void *out, uint64_t count, float scale
             case 11: return launch_buf<Tr, K, 4, 2, 16, SCALE, 512>(in, out, count, scale, s);
             case 12: return launch_buf<Tr, K, 4, 2, 16, SCALE, 128>(in, out, count, scale, s);
             case 13: return launch_buf<Tr, K, 2, 2, 16, SCALE, 1024>(in, out, count, scale, s);
+            // store policies: nt-only streaming stores, plain stores
+            case 14: return launch_buf<Tr, K, 4, 2, 2, SCALE>(in, out, count, scale, s);
+            case 15: return launch_buf<Tr, K, 4, 2, 0, SCALE>(in, out, count, scale, s);
+            case 16: return launch_buf<Tr, K, 4, 2, 3, SCALE>(in, out, count, scale, s);
             default: break;
             }
         }
@@ -858,7 +862,7 @@ int esgd_set_tuning(const char *key, int value) {
     } else if (!std::strcmp(key, "nt")) {
         g_nt = value ? 1 : 0;
     } else if (!std::strcmp(key, "policy")) {
-        ESGD_ARG(value >= -1 && value <= 13, "policy must be -1..13");
+        ESGD_ARG(value >= -1 && value <= 16, "policy must be -1..16");
         g_policy = value;
     } else {
         set_error("esgd_set_tuning: unknown key '%s'", key);
