@@ -230,6 +230,7 @@ def gate_256(dev, dt, es, k, s, iters=20):
     ptrs = [b.ptr for b in bufs]
     for _ in range(3):
         dev.reduce(dt, ptrs, out, count, stream=s)
+    # per-launch event pairs (each adds its marker packets to the launch it brackets) ...
     ev = [dev.Event() for _ in range(2 * iters)]
     for i in range(iters):
         ev[2 * i].record(s)
@@ -238,13 +239,22 @@ def gate_256(dev, dt, es, k, s, iters=20):
     s.synchronize()
     ts = sorted(ev[2 * i].elapsed_ms(ev[2 * i + 1]) for i in range(iters))
     med = ts[iters // 2]
+    # ... and, like the headline roofline, one pair around `iters` back-to-back launches
+    e0, e1 = dev.Event(), dev.Event()
+    e0.record(s)
+    for _ in range(iters):
+        dev.reduce(dt, ptrs, out, count, stream=s)
+    e1.record(s)
+    s.synchronize()
+    avg = e0.elapsed_ms(e1) / iters
     algo = (k + 1) * count * es
     for b in bufs:
         b.close()
     out.close()
-    return {"workload": f"{k} x 256 MiB -> 1", "kernel_ms_median": round(med, 4),
-            "achieved_GBs": round(algo / (med * 1e-3) / 1e9, 1),
-            "frac": round(algo / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    return {"workload": f"{k} x 256 MiB -> 1", "kernel_ms_avg": round(avg, 4),
+            "kernel_ms_median_per_launch_pairs": round(med, 4),
+            "achieved_GBs": round(algo / (avg * 1e-3) / 1e9, 1),
+            "frac": round(algo / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
 # N > 1: schedules (and their buckets) stay alive until every leg has run, then are
