@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 XGMI_LINK_GBS = 153.0      # per-link figure used by SURVEY.md §8d
+SHARED_GPU = False         # N > 1 with ranks sharing a device (set in run_allreduce)
 SEED = 0x5EEDE56D
 MiB = 1 << 20
 
@@ -55,6 +56,17 @@ def parse():
     return ap.parse_args()
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(k: int, count: int):
     """fflib2's recursive doubling restated (oracle/ffref.c), one pthread per simulated
     rank, on this host: the reference's CPU path for the same k x bucket workload."""
@@ -67,7 +79,22 @@ def cpu_baseline(k: int, count: int):
     return {"value": round(gbs, 3), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"full workload: {k}-rank recursive-doubling allreduce of {count*4/MiB:.0f} MiB "
                       f"fp32 (oracle/ffref.c, 1 pthread/rank, best of {reps}; {t*1e3:.1f} ms each)",
-            "host_cpus": os.cpu_count()}
+            "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
+
+
+def cpu_baseline_c1(P: int = 2, count: int = 262144):
+    """BASELINE.json configs[0] (C1): P ranks reducing one 1 MiB fp32 bucket per step the
+    way the wrapper drives fflib2 -- each rank a main thread (copy-in, post, spin-wait,
+    copy-out, zero) and a progress thread (move + recursive doubling, ff.c:72), i.e. 2
+    cores per rank; value = P x bucket bytes per step / step time."""
+    from oracle import ffref
+    t1, _ = ffref.time_c1(P, count, 20)
+    reps = max(50, min(20000, int(10.0 / max(t1, 1e-5))))
+    t, ok = ffref.time_c1(P, count, reps)
+    return {"value": round(P * count * 4 / t / 1e9, 3), "unit": "GB/s", "cores": 2 * P, "kind": "port",
+            "sample": f"C1: {P} ranks x {count * 4 / MiB:g} MiB fp32, main + progress thread per rank "
+                      f"(oracle/ffref.c ffref_time_c1), best step of {reps}: {t * 1e6:.1f} us",
+            "correct": ok, "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
 
 
 def pmc_traffic(args):
@@ -320,7 +347,7 @@ def sweep_c5(comm, dev, world, dt, es):
         out.append({"bytes": nbytes, "us": round(t * 1e6, 1), "mean_us": round(mean * 1e6, 1),
                     "algbw_GBs": round(nbytes / t / 1e9, 2),
                     "busbw_GBs": round(nbytes / t / 1e9 * 2 * (world - 1) / world, 2),
-                    "xgmi_frac": round(t_min / t, 4), "rounds": iters,
+                    "xgmi_frac": None if SHARED_GPU else round(t_min / t, 4), "rounds": iters,
                     "rank0_stages_us": stages})
     return out
 
@@ -482,11 +509,17 @@ def _stages_us(tl):
     return out
 
 
-def straggler_c4(comm, dev, rank, world, rounds=24):
+def straggler_c4(comm, dev, rank, world, rounds=16, delay_fracs=(0.2, 2.0)):
     """C4: majority-allreduce of the ResNet-50 fused gradient (25 559 081 fp32,
-    opt_esgd_solo_imagenet_imbalance.py:86-248 summed) with the last rank posting
-    0.2 x T late every round (T = median no-straggler round).  Inputs are 1.0 and
-    zeroed after use, so the result counts the contributors (evaluation/rsgd.c:87,100)."""
+    opt_esgd_solo_imagenet_imbalance.py:86-248 summed) with the last rank late every
+    round by f x T (T = median no-straggler round; f = 0.2 is BASELINE.json's "delayed
+    20 %", f = 2 a straggler slower than a whole round).  Gradients are 1.0, zeroed after
+    use (evaluation/rsgd.c:87,100), so a round's result counts its fresh contributors.
+    On-time ranks write theirs before the round's barrier, the straggler f x T after it.
+    Reported per f: the contributor histogram over rounds, how many rounds the straggler
+    activated (rand_r(6545343) % P, ffrand_allreduce.c:88) -- exactly those should take
+    all P -- and the on-time ranks' post -> wait latency."""
+    import collections
     import ctypes as C
     import statistics
 
@@ -502,18 +535,22 @@ def straggler_c4(comm, dev, rank, world, rounds=24):
     dev.synchronize()
     sch = comm.Schedule(comm.MAJORITY, sb, rb, count, dtype=_lib.FLOAT, seed=6545343,
                         buf=comm.BUF_DEVICE)
-    hp = C.c_void_p()   # pinned: a pageable D2H, like an extra stream, slows later rounds
+    hp = C.c_void_p()   # pinned result cell
     check(lib().esgd_host_alloc(C.byref(hp), 64))
     cell = np.ctypeslib.as_array(C.cast(hp, C.POINTER(C.c_float)), shape=(1,))
+    late = rank == world - 1
 
-    def one(delay):
-        if delay:
-            time.sleep(delay)
-        # no stream of its own: with ranks sharing the box's one GPU, one more HIP stream
-        # per process made every later round 2-10x slower (tools/chain_probe.py,
-        # CHAIN_STREAMS=1), which the C4 legs after this one would have measured
+    def fill():
         check(lib().esgd_memcpy_async(sb.ptr, ones.ptr, count * 4, 2, None))
         dev.synchronize()
+
+    def one(delay):
+        if not (late and delay):
+            fill()
+        comm.barrier()
+        if late and delay:
+            time.sleep(delay)
+            fill()
         t0 = time.perf_counter()
         sch.post()
         sch.wait()
@@ -521,25 +558,33 @@ def straggler_c4(comm, dev, rank, world, rounds=24):
         check(lib().esgd_memcpy_async(cell.ctypes.data, rb.ptr, 4, 1, None))
         check(lib().esgd_memset_async(sb.ptr, 0, count * 4, None))
         dev.synchronize()
-        return dt_, float(cell[0])
+        c = float(cell[0])
+        comm.barrier()
+        return dt_, c
 
-    base = []
-    for _ in range(rounds // 2):
-        comm.barrier()
-        base.append(one(0.0)[0])
+    base = [one(0.0)[0] for _ in range(12)]
     T = _max_over_ranks(statistics.median(base))
-    lat, contrib = [], []
-    for _ in range(rounds):
-        comm.barrier()
-        d, c = one(0.2 * T if rank == world - 1 else 0.0)
-        lat.append(d); contrib.append(c)
-    on_time = _max_over_ranks(statistics.median(lat) if rank != world - 1 else 0.0)
+    out = {"bucket_fp32": count, "world": world, "T_no_straggler_ms": round(T * 1e3, 3)}
+    for f in delay_fracs:
+        first = sch.stats()["joined"] + 1
+        lat, contrib = [], []
+        for _ in range(rounds):
+            d, c = one(f * T)
+            lat.append(d); contrib.append(c)
+        log = [e for e in sch.log() if first <= e["round"] < first + rounds]
+        by_straggler = sum(1 for e in log if e["activator"] == world - 1)
+        want = [world if e["activator"] == world - 1 else world - 1 for e in log]
+        on_time = _max_over_ranks(statistics.median(lat) if not late else 0.0)
+        out[f"delay_{f:g}T"] = {
+            "straggler_delay_ms": round(f * T * 1e3, 3),
+            "contributors_histogram": {str(int(k)): v for k, v in sorted(collections.Counter(contrib).items())},
+            "mean_contributors": round(float(np.mean(contrib)), 3),
+            "rounds": rounds, "rounds_activated_by_straggler": by_straggler,
+            "rounds_matching_partial_semantics": int(sum(int(a == b) for a, b in zip(want, contrib))),
+            "on_time_ranks_median_ms": round(on_time * 1e3, 3)}
     _defer(sch, ones, sb, rb)
     check(lib().esgd_host_free(hp))
-    return {"bucket_fp32": count, "T_no_straggler_ms": round(T * 1e3, 3),
-            "straggler_delay_ms": round(0.2 * T * 1e3, 3),
-            "on_time_ranks_median_ms": round(on_time * 1e3, 3),
-            "mean_contributors": round(float(np.mean(contrib)), 3), "world": world}
+    return out
 
 
 def run_allreduce(args, rank, world):
@@ -562,6 +607,16 @@ def run_allreduce(args, rank, world):
     comm.init(rank=rank, world=world)            # job id broadcast over gloo
     if args.transport:
         comm.set_transport(args.transport)
+    # ranks sharing a GPU (a 1-GPU rehearsal of the N > 1 path) move HBM bytes, not xGMI
+    # bytes: no xGMI fraction or roofline can be claimed for them
+    import ctypes as C
+    from esgd._lib import check, lib
+    mydev = C.c_int()
+    check(lib().esgd_get_device(C.byref(mydev)))
+    devs = [None] * world
+    dist.all_gather_object(devs, mydev.value)
+    global SHARED_GPU
+    SHARED_GPU = len(set(devs)) < world
     dt = _lib.FLOAT if args.dtype == "fp32" else _lib.BF16
     es = _lib.dtype_size(dt)
     count = int(args.bucket_mib * MiB) // es
@@ -630,15 +685,18 @@ def run_allreduce(args, rank, world):
                                  if (args.transport or os.environ.get("ESGD_TRANSPORT")) == "rccl"
                                  else "ipc pull (reduce-scatter tree kernel + all-gather) over xGMI")},
         "algbw_GBs": round(algbw, 2), "busbw_GBs": round(busbw, 2),
-        "xgmi_frac": round(t_min / t_step, 4),
-        "roofline": {"bound": "xgmi", "achieved": round(link_in, 2),
-                     "peak": XGMI_LINK_GBS * (world - 1), "unit": "GB/s",
-                     "frac": round(link_in / (XGMI_LINK_GBS * (world - 1)), 4), "traffic": None},
+        "xgmi_frac": None if SHARED_GPU else round(t_min / t_step, 4),
+        "roofline": None if SHARED_GPU else {
+            "bound": "xgmi", "achieved": round(link_in, 2), "peak": XGMI_LINK_GBS * (world - 1),
+            "unit": "GB/s", "frac": round(link_in / (XGMI_LINK_GBS * (world - 1)), 4), "traffic": None},
+        "devices": devs,
         "rounds": {"fresh": stats["fresh_rounds"], "auto": stats["auto_rounds"],
                    "activations_rank0": stats["activations"]},
         "rank0_stages_us": stages,
         "parity": parity,
     }
+    if SHARED_GPU:
+        line["rehearsal"] = "ranks share a GPU (HBM, not xGMI): no xGMI fraction or roofline"
 
     # The extra legs (C5 sweeps, C4, RCCL) run under a watchdog: if one hangs, rank 0
     # still prints the headline line with the legs finished so far, and every rank leaves.
@@ -756,10 +814,13 @@ def main():
         "unit": "GB/s", "frac": round(res["achieved_gbs"] / HBM_PEAK_GBS, 4),
         "traffic": traffic, "algo_bytes_per_launch": res["algo_bytes"],
         "kernel_ms": round(res["kernel_ms"], 5),
+        # the north star's 1-GPU gate: 8 x 256 MiB fp32 buckets, same kernel, same timing
+        "gate_256MiB_frac": res["gate"]["frac"] if res.get("gate") else None,
     }
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(res["k"], res["count"] if args.dtype == "fp32"
                                             else res["count"])
+        line["cpu_baseline_c1"] = cpu_baseline_c1()
     print(json.dumps(line))
 
 

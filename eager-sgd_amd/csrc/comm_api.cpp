@@ -76,6 +76,13 @@ int esgd_barrier(void) { return engine_barrier(); }
 
 int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t count, int dtype,
                          int async, unsigned seed, esgd_sched_h *out) {
+    return esgd_schedule_create_ex(kind, buf, sb, rb, count, dtype, async, seed, 0, out);
+}
+
+int esgd_schedule_create_ex(int kind, int buf, const void *sb, void *rb, uint64_t count, int dtype,
+                            int async, unsigned seed, unsigned flags, esgd_sched_h *out) {
+    ESGD_ARG((flags & ~unsigned(ESGD_SCHED_HOLD | ESGD_SCHED_ZERO_SB)) == 0,
+             "esgd_schedule_create: unknown flags 0x%x", flags);
     ESGD_ARG(out, "esgd_schedule_create: null output");
     ESGD_ARG(buf == ESGD_BUF_DEVICE || buf == ESGD_BUF_HOST || buf == ESGD_BUF_NONE,
              "esgd_schedule_create: bad buffer kind %d", buf);
@@ -86,7 +93,7 @@ int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t c
     Transport *tp = default_transport(buf == ESGD_BUF_NONE);
     Sched *s = nullptr;
     int rc = sched_create(kind, dtype, count, const_cast<void *>(sb), rb, buf == ESGD_BUF_HOST,
-                          async, seed, tp, &s);
+                          async, seed, tp, &s, flags);
     if (rc) return rc;
     *out = reinterpret_cast<esgd_sched_h>(s);
     return ESGD_SUCCESS;
@@ -102,6 +109,18 @@ int esgd_schedule_wait(esgd_sched_h h) {
     Sched *s = handle_to_sched(h);
     if (!s) return ESGD_INVALID_ARG;
     return sched_wait(s);
+}
+
+int esgd_schedule_wait_ex(esgd_sched_h h, int *fresh) {
+    Sched *s = handle_to_sched(h);
+    if (!s) return ESGD_INVALID_ARG;
+    return sched_wait_ex(s, fresh);
+}
+
+int esgd_schedule_release(esgd_sched_h h, void *stream) {
+    Sched *s = handle_to_sched(h);
+    if (!s) return ESGD_INVALID_ARG;
+    return sched_release(s, stream);   // ESGD_STREAM_NULL: the legacy default stream
 }
 
 int esgd_schedule_test(esgd_sched_h h, int *flag) {

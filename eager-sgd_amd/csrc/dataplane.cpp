@@ -37,6 +37,18 @@ int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64
                   float scale, hipStream_t s);
 int gather_remote(int n, const void *const *src, void *const *dst, const uint64_t *bytes,
                   hipStream_t s);
+int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s);
+int cache_flush(hipStream_t s);
+
+// ESGD_FLUSH_L2 (experiment): 1 = flush every XCD's L2 before each round, 2 = after a
+// peer bucket is (re)mapped
+static int flush_mode() {
+    static const int v = [] {
+        const char *e = getenv("ESGD_FLUSH_L2");
+        return (e && *e) ? atoi(e) : 0;
+    }();
+    return v;
+}
 int round_small(int dtype, const void *const *src, void *out, uint64_t n, int nseg,
                 const void *const *gsrc, void *const *gdst, const uint64_t *gbytes,
                 uint32_t *ready, uint32_t *reduced, uint32_t *done, uint32_t *fin, uint32_t *err,
@@ -110,6 +122,15 @@ static int ipc_open(int peer, const uint8_t *h, void **base) {
     std::memcpy(&hh, h, sizeof(hh));
     void *p = nullptr;
     ESGD_HIP(hipIpcOpenMemHandle(&p, hh, hipIpcMemLazyEnablePeerAccess));
+    if (getenv("ESGD_DEBUG") && *getenv("ESGD_DEBUG") == '1') {
+        void *b = nullptr;
+        size_t sz = 0;
+        (void)hipMemGetAddressRange(&b, &sz, p);
+        uint64_t hsh = 1469598103934665603ull;
+        for (int i = 0; i < 64; ++i) hsh = (hsh ^ h[i]) * 1099511628211ull;
+        fprintf(stderr, "[esgd] ipc_open peer %d handle %016llx -> %p (range %p + %zu)\n", peer,
+                (unsigned long long)hsh, p, b, sz);
+    }
     g_ipc[k] = {p, 1};
     *base = p;
     return ESGD_SUCCESS;
@@ -315,6 +336,9 @@ struct BaseState {
     uint64_t off[kMaxRanks] = {}, len[kMaxRanks] = {};   // elements
     std::map<uint32_t, hipEvent_t> producer;
     std::vector<hipEvent_t> spare;
+    // hold mode: the caller's last reads of rb / writes of sb (esgd_schedule_release)
+    hipEvent_t consumer = nullptr;
+    bool consumer_pending = false;
     virtual ~BaseState() {}
 };
 
@@ -324,6 +348,7 @@ struct IpcState : BaseState {
     uint32_t *ctr = nullptr;          // device: k_round_small's counters and gates (pool)
     std::vector<hipEvent_t> cev;      // chunked host rounds: per chunk H2D / reduced / D2H
     bool chunked_before = false;
+    bool need_flush = true;
     char *peer[kMaxRanks] = {};
     void *peer_base[kMaxRanks] = {};
     uint32_t peer_ver[kMaxRanks] = {};
@@ -397,6 +422,24 @@ static int base_note_producer(BaseState &st, uint32_t round, void *stream) {
     return ESGD_SUCCESS;
 }
 
+static int base_note_consumer(BaseState &st, void *stream) {
+    if (!st.consumer) ESGD_HIP(hipEventCreateWithFlags(&st.consumer, hipEventDisableTiming));
+    hipStream_t cs = stream == ESGD_STREAM_NULL ? nullptr : static_cast<hipStream_t>(stream);
+    ESGD_HIP(hipEventRecord(st.consumer, cs));
+    st.consumer_pending = true;
+    return ESGD_SUCCESS;
+}
+
+// queued at launch, before anything touches the buckets: the caller's copy-out of the
+// previous round (and its zeroing of sb) has finished -- fresh round or not
+static int consumer_wait(BaseState &st, hipStream_t cs) {
+    if (st.consumer_pending) {
+        ESGD_HIP(hipStreamWaitEvent(cs, st.consumer, 0));
+        st.consumer_pending = false;
+    }
+    return ESGD_SUCCESS;
+}
+
 // FFCOLL_BUFFERS rounds may change the count: re-lay the shards and grow the owned
 // device bucket (ffallreduce_post resizes its temporaries the same way, :42-48).
 // Returns 1 when the device bucket moved (peers must re-map it).
@@ -462,12 +505,16 @@ static int producer_wait(BaseState &st, uint32_t round, bool fresh, hipStream_t 
 }
 
 static int base_copy_in(Sched &s, BaseState &st, uint32_t round, bool fresh, hipStream_t cs) {
+    if (int rc = consumer_wait(st, cs)) return rc;
     if (int rc = producer_wait(st, round, fresh, cs)) return rc;
     const size_t bytes = s.count * s.esize;
     if (!bytes) return ESGD_SUCCESS;
     if (s.host_mode) {
         const void *src = staged(s, st) ? st.pin : (s.sb ? s.sb : s.rb);
         ESGD_HIP(hipMemcpyAsync(st.rb_dev, src, bytes, hipMemcpyHostToDevice, cs));
+    } else if (s.zero_sb) {
+        // the move and the wrapper's zero-after-use in one pass: rb = sb, sb = 0
+        if (int rc = move_zero(st.rb_dev, s.sb, bytes, cs)) return rc;
     } else if (!s.in_place || st.shadow) {
         ESGD_HIP(hipMemcpyAsync(st.rb_dev, s.in_place ? s.rb : s.sb, bytes, hipMemcpyDeviceToDevice, cs));
     }
@@ -557,6 +604,7 @@ static void base_teardown(Sched &s, BaseState &st) {
     if (st.reg_sb) (void)hipHostUnregister(s.sb);
     for (auto &kv : st.producer) (void)hipEventDestroy(kv.second);
     for (hipEvent_t e : st.spare) (void)hipEventDestroy(e);
+    if (st.consumer) (void)hipEventDestroy(st.consumer);
     if (st.pin) (void)hipHostFree(st.pin);
     for (char *p : st.retired) (void)hipFree(p);
     if (st.ev) (void)hipEventDestroy(st.ev);
@@ -581,6 +629,12 @@ struct IpcTransport final : Transport {
         ESGD_HIP(hipIpcGetMemHandle(&h, base));
         uint8_t hb[64];
         std::memcpy(hb, &h, 64);
+        if (getenv("ESGD_DEBUG") && *getenv("ESGD_DEBUG") == '1') {
+            uint64_t hsh = 1469598103934665603ull;
+            for (int i = 0; i < 64; ++i) hsh = (hsh ^ hb[i]) * 1099511628211ull;
+            fprintf(stderr, "[esgd] r%d publish sched %d rb %p base %p size %zu handle %016llx\n", s.rank, s.id,
+                    (void *)st.rb_dev, base, size, (unsigned long long)hsh);
+        }
         if (int rc = claim_handle(hb)) return rc;
         if (st.pub_live) release_handle(st.pub_h);
         std::memcpy(st.pub_h, hb, 64);
@@ -680,6 +734,8 @@ struct IpcTransport final : Transport {
         return base_note_producer(S(s), round, stream);
     }
 
+    int note_consumer(Sched &s, void *stream) override { return base_note_consumer(S(s), stream); }
+
     // join: a moved bucket is re-published before this rank's join counts (peers map it
     // when they launch the round); a size change alone only updates the published size
     int prepare(Sched &s, uint32_t round, bool) override {
@@ -704,6 +760,10 @@ struct IpcTransport final : Transport {
         IpcState &st = S(s);
         hipStream_t cs = st.stream;
         st.fin_mode = false;
+        if (flush_mode() == 1 || (flush_mode() == 2 && st.need_flush)) {
+            if (int rc = cache_flush(cs)) return rc;
+            st.need_flush = false;
+        }
         if (s.host_mode && !s.resolve && host_chunk_bytes() && s.count * s.esize >= 2 * host_chunk_bytes())
             return launch_chunked(s, st, round, fresh);
         if (int rc = base_copy_in(s, st, round, fresh, cs)) return rc;
@@ -773,6 +833,7 @@ struct IpcTransport final : Transport {
     static int launch_chunked(Sched &s, IpcState &st, uint32_t round, bool fresh) {
         hipStream_t cs = st.stream, hs = nullptr, ds = nullptr;
         if (int rc = copy_streams(&hs, &ds)) return rc;
+        if (int rc = consumer_wait(st, hs)) return rc;
         if (int rc = producer_wait(st, round, fresh, hs)) return rc;
         const size_t es = s.esize;
         const uint64_t count = s.count, align = 1024;   // elements: 1 KiB+ aligned chunks
@@ -1006,6 +1067,8 @@ struct RcclTransport final : Transport {
     int note_producer(Sched &s, uint32_t round, void *stream) override {
         return base_note_producer(S(s), round, stream);
     }
+
+    int note_consumer(Sched &s, void *stream) override { return base_note_consumer(S(s), stream); }
 
     int prepare(Sched &s, uint32_t, bool) override {
         RcclState &st = S(s);

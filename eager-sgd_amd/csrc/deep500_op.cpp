@@ -13,7 +13,17 @@
 //     schedule is created at the instance's first forward (collective: the training
 //     graph calls ops in the same order on every rank, which the reference relies on
 //     for its 161 creations at :288-293);
-//   * report() returns the bytes reduced (the reference always returns 0, :273-275).
+//   * report() returns the bytes reduced (the reference always returns 0, :273-275);
+//   * the schedule holds after each wait (ESGD_SCHED_HOLD) until the copy-out and the
+//     zeroing are queued, so a round a peer activates next cannot overwrite rb under the
+//     copy-out or snapshot a gradient that is about to be dropped -- the reference gets
+//     the same ordering by doing both synchronously right after its wait (:309-314);
+//   * device path: the zeroing is fused into the next snapshot (ESGD_SCHED_ZERO_SB) and
+//     the wrapper's division by the comm size (:40) into the copy-in
+//     (allreducef_forward_cuda_div); a rank whose round was carried by a peer's
+//     activation before its own post drops its late gradient exactly as the reference's
+//     unconditional zeroing does;
+//   * the extension entry points return a status instead of aborting the process.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -95,11 +105,60 @@ struct AllreduceOp {
         }
         const int kind = cfg.mode == ESGD_OP_MAJORITY ? ESGD_SCHED_MAJORITY
                          : cfg.mode == ESGD_OP_ALLREDUCE ? ESGD_SCHED_ALLREDUCE : ESGD_SCHED_SOLO;
-        if (esgd_schedule_create(kind, dev ? ESGD_BUF_DEVICE : ESGD_BUF_HOST, sb, rb, len,
-                                 ESGD_FLOAT, cfg.async, cfg.seed, &sched))
+        const unsigned flags = ESGD_SCHED_HOLD | (dev ? ESGD_SCHED_ZERO_SB : 0u);
+        if (esgd_schedule_create_ex(kind, dev ? ESGD_BUF_DEVICE : ESGD_BUF_HOST, sb, rb, len,
+                                    ESGD_FLOAT, cfg.async, cfg.seed, flags, &sched))
             die("schedule creation");
     }
+
+    // Device round: the gradient is already in sb (queued on s).  post -> wait -> drop a
+    // late gradient -> `out` consumes rb on s -> release.  Returns an esgd status.
+    template <class Out>
+    int device_round(hipStream_t s, Out &&out) {
+        const size_t nbytes = size_t(len) * sizeof(float);
+        // the snapshot of this round waits for the copy-in just queued on the caller's
+        // stream (the data plane's streams are non-blocking: the NULL stream is named)
+        void *ps = s ? static_cast<void *>(s) : ESGD_STREAM_NULL;
+        int fresh = 1;
+        if (int rc = esgd_schedule_post(sched, ps, nullptr)) return rc;
+        if (int rc = esgd_schedule_wait_ex(sched, &fresh)) return rc;
+        // a round carried by a peer's activation before this post did not take the
+        // gradient: drop it (the reference zeroes sb after every wait, :311-314; fresh
+        // rounds had sb zeroed by their snapshot)
+        if (!fresh && hipMemsetAsync(sb, 0, nbytes, s) != hipSuccess) {
+            esgd::set_error("allreducef: zeroing the send bucket failed");
+            return ESGD_ERROR;
+        }
+        if (int rc = out()) return rc;
+        if (int rc = esgd_schedule_release(sched, ps)) return rc;
+        bytes += int64_t(nbytes);
+        return ESGD_SUCCESS;
+    }
 };
+
+constexpr float kNoDivide = 1.0f;
+
+int forward_cuda_impl(AllreduceOp *op, const float *input, float *output, float divisor, hipStream_t s) {
+    ESGD_ARG(op, "allreducef: null handle");
+    op->ensure(true);
+    const size_t nbytes = size_t(op->len) * sizeof(float);
+    const uint64_t n = op->len;
+    if (divisor == kNoDivide) {
+        if (hipMemcpyAsync(op->sb, input, nbytes, hipMemcpyDeviceToDevice, s) != hipSuccess) {
+            esgd::set_error("allreducef: copy-in failed");
+            return ESGD_ERROR;
+        }
+    } else if (int rc = esgd_pack_div(1, &input, &n, op->sb, divisor, s)) {
+        return rc;
+    }
+    return op->device_round(s, [&]() -> int {
+        if (hipMemcpyAsync(output, op->rb, nbytes, hipMemcpyDeviceToDevice, s) != hipSuccess) {
+            esgd::set_error("allreducef: copy-out failed");
+            return ESGD_ERROR;
+        }
+        return ESGD_SUCCESS;
+    });
+}
 
 }  // namespace
 
@@ -138,26 +197,36 @@ void allreducef_forward(void *handle, const float *input, const float *, float *
         die("allreducef_forward");
     std::memcpy(output, op->rb, nbytes);
     std::memset(op->sb, 0, nbytes);
+    if (esgd_schedule_release(op->sched, nullptr)) die("allreducef_forward");
     op->bytes += int64_t(nbytes);
 }
 
 void allreducef_forward_cuda(void *handle, const float *input, const float *, float *output,
                              void *stream) {
-    auto *op = static_cast<AllreduceOp *>(handle);
-    op->ensure(true);
-    const size_t nbytes = size_t(op->len) * sizeof(float);
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    if (hipMemcpyAsync(op->sb, input, nbytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
-        die("allreducef_forward_cuda (copy in)");
-    // the snapshot of this round waits for the copy just queued on the caller's stream
-    // (the data plane's streams are non-blocking: the NULL stream must be named)
-    if (esgd_schedule_post(op->sched, s ? static_cast<void *>(s) : ESGD_STREAM_NULL, nullptr) ||
-        esgd_schedule_wait(op->sched))
+    if (forward_cuda_impl(static_cast<AllreduceOp *>(handle), input, output, kNoDivide,
+                          static_cast<hipStream_t>(stream)))
         die("allreducef_forward_cuda");
-    if (hipMemcpyAsync(output, op->rb, nbytes, hipMemcpyDeviceToDevice, s) != hipSuccess ||
-        hipMemsetAsync(op->sb, 0, nbytes, s) != hipSuccess)
-        die("allreducef_forward_cuda (copy out)");
-    op->bytes += int64_t(nbytes);
+}
+
+int allreducef_forward_cuda_div(void *handle, const float *input, float *output, float divisor,
+                                void *stream) {
+    ESGD_ARG(divisor == divisor && divisor != 0.0f, "allreducef_forward_cuda_div: bad divisor");
+    return forward_cuda_impl(static_cast<AllreduceOp *>(handle), input, output, divisor,
+                             static_cast<hipStream_t>(stream));
+}
+
+int allreducef_forward_cuda_packed(void *handle, int n, const float *const *grads, const uint64_t *counts,
+                                   float *const *outs, float divisor, void *stream) {
+    auto *op = static_cast<AllreduceOp *>(handle);
+    ESGD_ARG(op && n >= 0 && (n == 0 || (grads && counts && outs)), "allreducef_forward_cuda_packed: bad arguments");
+    uint64_t total = 0;
+    for (int i = 0; i < n; ++i) total += counts[i];
+    ESGD_ARG(total == op->len, "allreducef_forward_cuda_packed: %llu elements for a %llu-element op",
+             (unsigned long long)total, (unsigned long long)op->len);
+    op->ensure(true);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int rc = esgd_pack_div(n, grads, counts, op->sb, divisor, s)) return rc;
+    return op->device_round(s, [&]() -> int { return esgd_unpack(n, outs, counts, op->rb, s); });
 }
 
 bool is_cuda_supported(void *) { return true; }

@@ -36,7 +36,7 @@ static std::mutex g_create_mu;
 static int g_next_id = 0;
 static std::thread g_thread;
 static std::atomic<bool> g_running{false};
-static std::atomic<uint32_t> g_wake{0};
+static std::atomic<uint64_t> g_epoch{0};             // progress passes completed
 static uint64_t g_cursor = 0;                       // next ticket this rank issues
 static std::mutex g_issue_mu;
 static std::vector<std::pair<uint32_t, uint32_t>> g_issued;
@@ -71,17 +71,25 @@ static struct ProgressGuard {
     }
 } g_progress_guard;
 
+// Idle, the thread sleeps on the segment's wake word: a peer's activation, an issue-ring
+// append or a local post wakes it at once (the reference's progress thread busy-polls
+// MPI_Testsome instead, ffprogress.c:39-57).  A round in flight is latency-critical: the
+// thread spins / yields then, never sleeps.
 static void progress_main() {
     if (g_device >= 0) (void)hipSetDevice(g_device);
     unsigned polls = 0;
-    uint32_t seen = g_wake.load();
     while (g_running.load(std::memory_order_acquire)) {
+        const uint32_t ws = g_seg->wake_seq.load(std::memory_order_acquire);
         if (engine_progress_once()) { polls = 0; continue; }
-        const uint32_t w = g_wake.load(std::memory_order_acquire);
-        if (w != seen) { seen = w; polls = 0; continue; }
-        // a round in flight is latency-critical: spin / yield, never sleep
-        if (g_active.load(std::memory_order_relaxed) > 0 && polls > 1024) polls = 64;
-        backoff(polls);
+        if (g_seg->wake_seq.load(std::memory_order_acquire) != ws) { polls = 0; continue; }
+        ++polls;
+        if (g_active.load(std::memory_order_relaxed) > 0) {
+            if (polls > 64) sched_yield();
+            continue;
+        }
+        if (polls < 64) continue;
+        if (polls < 256) { sched_yield(); continue; }
+        seg_idle_wait(g_seg, ws, 1000);   // 1 ms backstop
     }
 }
 
@@ -161,14 +169,14 @@ static void fail_locked(Sched &s, int rc, const char *msg) {
 }
 
 int sched_create(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
-                 int async, unsigned seed, Transport *tp, Sched **out) {
+                 int async, unsigned seed, Transport *tp, Sched **out, unsigned flags) {
     return sched_create_with(kind, dtype, count, sb, rb, host_mode, async, seed, tp, nullptr,
-                             nullptr, nullptr, out);
+                             nullptr, nullptr, out, flags);
 }
 
 int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
                       int async, unsigned seed, Transport *tp, int (*resolve)(Sched &),
-                      void *ctx, void (*ctx_free)(void *), Sched **out) {
+                      void *ctx, void (*ctx_free)(void *), Sched **out, unsigned flags) {
     ESGD_ARG(out, "schedule create: null output");
     ESGD_ARG(kind >= KIND_ALLREDUCE && kind <= KIND_MAJORITY, "schedule create: bad kind %d", kind);
     ESGD_ARG(tp, "schedule create: no transport");
@@ -186,6 +194,8 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     s->resolve = resolve;
     s->resolve_ctx = ctx;
     s->resolve_free = ctx_free;
+    s->hold_mode = (flags & ESGD_SCHED_HOLD) != 0;
+    s->zero_sb = (flags & ESGD_SCHED_ZERO_SB) != 0 && !host_mode && !s->in_place;
     int rc = shm_barrier(g_seg, g_world, g_timeout);
     if (!rc && g_rank == 0) {
         SchedShm *sh = s->sh;
@@ -259,6 +269,7 @@ static void activate(SchedShm *sh, uint32_t round, int rank, bool *won) {
     uint32_t a = sh->activated.load(std::memory_order_acquire);
     while (a < round && !sh->activated.compare_exchange_weak(a, round, std::memory_order_acq_rel)) {
     }
+    seg_wake(g_seg);   // the flood: every idle progress thread joins now
 }
 
 static int activator_of(SchedShm *sh, uint32_t round) {
@@ -275,11 +286,13 @@ int sched_post(Sched *s, void *producer_stream, int *role) {
         const uint32_t t = s->posted.load() + 1;
         if (s->resolve) {
             // the round about to start must not be in flight with the old buffers
-            if (s->stage != ST_IDLE || s->joined != s->posted.load()) {
+            if (s->stage != ST_IDLE) {
                 set_error("schedule %d: FFCOLL_BUFFERS rounds must not overlap", s->id);
                 return ESGD_INVALID_ARG;
             }
-            if (int rc = s->resolve(*s)) return rc;
+            // a round a peer activated before this post was joined (and re-resolved) then
+            if (s->joined < t)
+                if (int rc = s->resolve(*s)) return rc;
         }
         if (producer_stream)
             if (int rc = s->tp->note_producer(*s, t, producer_stream)) return rc;
@@ -307,12 +320,14 @@ int sched_post(Sched *s, void *producer_stream, int *role) {
             if (won) ++s->n_activated;
         }
     }
-    g_wake.fetch_add(1, std::memory_order_acq_rel);
+    seg_wake(g_seg);
     if (role) *role = r;
     return ESGD_SUCCESS;
 }
 
-int sched_wait(Sched *s) {
+int sched_wait(Sched *s) { return sched_wait_ex(s, nullptr); }
+
+int sched_wait_ex(Sched *s, int *fresh) {
     ESGD_ARG(s, "schedule wait: null schedule");
     uint32_t target;
     {
@@ -339,6 +354,23 @@ int sched_wait(Sched *s) {
     if (s->error) { set_error("%s", s->errmsg); return s->error; }
     s->waited = target;
     s->mark(target, 5);
+    if (s->hold_mode) s->held = true;
+    if (fresh) *fresh = s->fresh_of[target % 256];
+    return ESGD_SUCCESS;
+}
+
+int sched_release(Sched *s, void *stream) {
+    ESGD_ARG(s, "schedule release: null schedule");
+    {
+        std::lock_guard<std::mutex> lk(s->mu);
+        if (s->error) { set_error("%s", s->errmsg); return s->error; }
+        ESGD_ARG(s->hold_mode, "schedule %d: release() needs a schedule created with ESGD_SCHED_HOLD", s->id);
+        ESGD_ARG(s->held, "schedule %d: nothing to release (no round returned since the last release)", s->id);
+        if (stream)
+            if (int rc = s->tp->note_consumer(*s, stream)) return rc;
+        s->held = false;
+    }
+    seg_wake(g_seg);
     return ESGD_SUCCESS;
 }
 
@@ -346,8 +378,11 @@ int sched_test(Sched *s, int *flag) {
     ESGD_ARG(s && flag, "schedule test: null argument");
     std::lock_guard<std::mutex> lk(s->mu);
     if (s->error) { set_error("%s", s->errmsg); return s->error; }
-    *flag = s->completed >= s->waited + 1;
-    if (*flag) ++s->waited;
+    *flag = !s->held && s->completed >= s->waited + 1;
+    if (*flag) {
+        ++s->waited;
+        if (s->hold_mode) s->held = true;
+    }
     return ESGD_SUCCESS;
 }
 
@@ -365,6 +400,15 @@ int sched_delete(Sched *s) {
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         g_reg.erase(std::remove(g_reg.begin(), g_reg.end(), s), g_reg.end());
+    }
+    // The progress thread may be inside a pass over a registry copy that still holds s:
+    // wait until a pass that began after the erase has finished (two epochs).
+    if (g_running.load(std::memory_order_acquire) && std::this_thread::get_id() != g_thread.get_id()) {
+        const uint64_t e0 = g_epoch.load(std::memory_order_acquire);
+        while (g_epoch.load(std::memory_order_acquire) < e0 + 2 && g_running.load(std::memory_order_acquire)) {
+            seg_wake(g_seg);
+            std::this_thread::yield();
+        }
     }
     int rc = shm_barrier(g_seg, g_world, g_timeout);
     s->tp->teardown(*s);
@@ -398,6 +442,7 @@ static bool step(Sched &s) {
     };
     switch (s.stage) {
     case ST_IDLE: {
+        if (s.held) return false;   // the caller still reads the last round's buckets
         const uint32_t next = s.joined + 1;
         const bool sync = round_is_sync(s, next);
         const uint32_t posted = s.posted.load(std::memory_order_acquire);
@@ -406,6 +451,10 @@ static bool step(Sched &s) {
         s.cur = next;
         s.cur_fresh = posted >= next;
         s.joined = next;
+        s.fresh_of[next % 256] = uint8_t(s.cur_fresh);
+        // FFCOLL_BUFFERS: a round joined on a peer's activation re-resolves the buffers
+        // here (a fresh round did at its post)
+        if (s.resolve && !s.cur_fresh && !check(s.resolve(s), "join")) return true;
         s.mark(next, 1);
         sh->joined[s.rank].store(next, std::memory_order_release);
         if (s.cur_fresh) ++s.n_fresh; else ++s.n_auto;
@@ -423,6 +472,7 @@ static bool step(Sched &s) {
             slot.sched = uint32_t(s.id);
             slot.round = next;
             slot.tag.store(tk + 1, std::memory_order_release);
+            seg_wake(g_seg);
         }
         return true;
     }
@@ -524,6 +574,7 @@ bool engine_progress_once() {
         if (s->stage != ST_IDLE) ++active;
     }
     g_active.store(active, std::memory_order_relaxed);
+    g_epoch.fetch_add(1, std::memory_order_acq_rel);
     return any;
 }
 

@@ -58,6 +58,9 @@ struct Transport {
     virtual int setup(Sched &s) = 0;
     virtual int connect(Sched &) { return ESGD_SUCCESS; }
     virtual int note_producer(Sched &s, uint32_t round, void *stream) = 0;
+    // hold mode: the caller's reads of rb / writes of sb queued on `stream` (after
+    // wait()) must finish before the next round's snapshot touches the buckets
+    virtual int note_consumer(Sched &, void *) { return ESGD_SUCCESS; }
     virtual int prepare(Sched &s, uint32_t round, bool fresh) = 0;
     virtual int launch(Sched &s, uint32_t round, bool fresh) = 0;
     virtual int query(Sched &s) = 0;
@@ -114,6 +117,16 @@ struct Sched {
     std::vector<std::array<uint64_t, 12>> tl;   // [6..11]: GPU spans (ESGD_GPU_TRACE=1)
     void mark(uint32_t round, int what);
     std::atomic<bool> live{true};
+
+    // ESGD_SCHED_HOLD: once wait() has returned a round, the next round is not joined
+    // before release() -- the caller copies rb out (and drops its late send bucket)
+    // before a peer-activated round can overwrite them (opt_esgd_solo...py:309-314 runs
+    // those steps synchronously right after the wait)
+    bool hold_mode = false, held = false;
+    // ESGD_SCHED_ZERO_SB: the snapshot zeroes the send bucket as it reads it (device
+    // buckets): the wrapper's zero-after-use (:311-314) fused into the move
+    bool zero_sb = false;
+    uint8_t fresh_of[256] = {};   // round % 256 -> this rank had posted it before joining
 };
 
 // Round kind / activator rules (pure functions of the schedule parameters).
@@ -131,15 +144,20 @@ double engine_timeout();
 
 // Schedules (collective create/delete, same order on every rank).
 int sched_create(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
-                 int async, unsigned seed, Transport *tp, Sched **out);
+                 int async, unsigned seed, Transport *tp, Sched **out, unsigned flags = 0);
 // same, with buffers re-resolved at every post (FFCOLL_BUFFERS); ctx freed by ctx_free
 int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
                       int async, unsigned seed, Transport *tp, int (*resolve)(Sched &),
-                      void *ctx, void (*ctx_free)(void *), Sched **out);
+                      void *ctx, void (*ctx_free)(void *), Sched **out, unsigned flags = 0);
 // transport chosen by esgd_set_transport / ESGD_TRANSPORT (comm_api.cpp)
 Transport *default_transport(bool control_only);
 int sched_post(Sched *s, void *producer_stream, int *role);
 int sched_wait(Sched *s);
+// wait, and say whether this rank had posted the round it returns before joining it
+int sched_wait_ex(Sched *s, int *fresh);
+// hold mode: the caller is done with the round wait() returned; work it queued on
+// `stream` (may be null) is waited for by the next round's snapshot
+int sched_release(Sched *s, void *stream);
 int sched_test(Sched *s, int *flag);
 int sched_delete(Sched *s);
 Sched *sched_lookup(uint64_t handle);

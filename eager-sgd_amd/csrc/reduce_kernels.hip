@@ -265,6 +265,73 @@ __global__ __launch_bounds__(256) void k_gather(GatherSet g) {
     }
 }
 
+// ---- the snapshot with the zero-after-use fused: dst = src, src = 0 ----
+// The round's move (colls/ffallreduce.c:126-130) and the wrapper's zeroing of the send
+// bucket after the wait (opt_esgd_solo_imagenet_imbalance.py:311-314) in one pass:
+// 1 read + 2 writes instead of 2 reads + 2 writes (+ a memset launch).
+__global__ __launch_bounds__(256) void k_move_zero(raw16 *dst, raw16 *src, uint64_t nvec, uint8_t *dtail,
+                                                    uint8_t *stail, uint32_t ntail) {
+    const uint64_t stride = uint64_t(gridDim.x) * 256 * 4;
+    const raw16 z = {0u, 0u, 0u, 0u};
+    for (uint64_t i = uint64_t(blockIdx.x) * 1024 + threadIdx.x; i < nvec; i += stride) {
+        raw16 r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i + u * 256 < nvec) r[u] = __builtin_nontemporal_load(src + i + u * 256);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i + u * 256 < nvec) {
+                dst[i + u * 256] = r[u];
+                __builtin_nontemporal_store(z, src + i + u * 256);
+            }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < ntail) {
+        dtail[threadIdx.x] = stail[threadIdx.x];
+        stail[threadIdx.x] = 0;
+    }
+}
+
+// unaligned buckets: byte by byte (never on the bench path: rb is 16-B aligned and the
+// op's own buckets are allocation-aligned)
+__global__ __launch_bounds__(256) void k_move_zero_bytes(uint8_t *dst, uint8_t *src, uint64_t n) {
+    const uint64_t stride = uint64_t(gridDim.x) * 256;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride) {
+        dst[i] = src[i];
+        src[i] = 0;
+    }
+}
+
+// ---- bucket packing (fused rounds of many gradient tensors) ----
+// One launch moves up to kPackSeg tensors; block b handles 1024 consecutive elements of
+// the tensor whose tile range holds b.  Elements are fp32; tensor offsets inside the
+// bucket are arbitrary (no vector alignment), so accesses are 4 B, coalesced per wave.
+constexpr int kPackSeg = 48;
+struct PackSet {
+    float *a[kPackSeg];          // pack: sources; unpack: destinations
+    uint64_t off[kPackSeg];      // element offset of tensor i in the bucket
+    uint64_t n[kPackSeg];
+    uint32_t tile0[kPackSeg + 1];
+    int nseg;
+};
+
+template <bool PACK, bool DIV>
+__global__ __launch_bounds__(256) void k_pack(PackSet p, float *bucket, float divisor) {
+    const uint32_t b = blockIdx.x;
+    int i = 0;
+    while (i + 1 < p.nseg && p.tile0[i + 1] <= b) ++i;
+    const uint64_t e0 = uint64_t(b - p.tile0[i]) * 1024;
+    float *t = p.a[i];
+    float *bk = bucket + p.off[i];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint64_t e = e0 + u * 256 + threadIdx.x;
+        if (e < p.n[i]) {
+            if constexpr (PACK) bk[e] = DIV ? __fdiv_rn(t[e], divisor) : t[e];
+            else t[e] = bk[e];
+        }
+    }
+}
+
 // ---- synthetic inputs (same generator as oracle/ffref.c) ----
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -463,7 +530,77 @@ static int reduce_impl(int dtype, int k, const void *const *inputs, void *out, u
     return ESGD_INVALID_ARG;
 }
 
-// ---- internal entry points of the data plane (dataplane_ipc.cpp) ----
+// ---- cache maintenance: write back and invalidate every XCD's L2 ----
+// One workgroup per CU (blocks are dealt round-robin over the XCDs, so every XCD gets
+// some): lane 0 runs a system-scope release + acquire (buffer_wbl2 sc0 sc1 +
+// buffer_inv sc0 sc1), dropping any line of this device's L2s that a reused physical
+// page may still hold.
+__global__ __launch_bounds__(64) void k_cache_flush() {
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+}
+
+int cache_flush(hipStream_t s) {
+    hipLaunchKernelGGL(k_cache_flush, dim3(cu_count()), dim3(64), 0, s);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+// ---- internal entry points of the data plane (dataplane.cpp) ----
+int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s) {
+    if (!bytes) return ESGD_SUCCESS;
+    if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0) {
+        const uint64_t nvec = bytes / 16;
+        const uint32_t ntail = uint32_t(bytes % 16);
+        const unsigned grid = grid_for(1024, nvec ? nvec : 1, 4);
+        hipLaunchKernelGGL(k_move_zero, dim3(grid), dim3(256), 0, s, static_cast<raw16 *>(dst),
+                           static_cast<raw16 *>(src), nvec, static_cast<uint8_t *>(dst) + nvec * 16,
+                           static_cast<uint8_t *>(src) + nvec * 16, ntail);
+    } else {
+        hipLaunchKernelGGL(k_move_zero_bytes, dim3(grid_for(256, bytes, 4)), dim3(256), 0, s,
+                           static_cast<uint8_t *>(dst), static_cast<uint8_t *>(src), bytes);
+    }
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+static int pack_impl(bool pack, int n, float *const *tensors, const uint64_t *count, float *bucket,
+                     float divisor, void *stream) {
+    ESGD_ARG(n >= 0 && n <= 4096, "esgd_pack: %d tensors outside [0, 4096]", n);
+    ESGD_ARG(n == 0 || (tensors && count && bucket), "esgd_pack: null argument");
+    ESGD_ARG(divisor == divisor && divisor != 0.0f, "esgd_pack: divisor must be a non-zero number");
+    if (n == 0) return ESGD_SUCCESS;
+    if (int rc = require_device()) return rc;
+    hipStream_t s = as_stream(stream);
+    uint64_t off = 0;
+    for (int i0 = 0; i0 < n; i0 += kPackSeg) {
+        PackSet p;
+        std::memset(&p, 0, sizeof(p));
+        p.nseg = std::min(kPackSeg, n - i0);
+        uint64_t tiles = 0;
+        for (int j = 0; j < p.nseg; ++j) {
+            const uint64_t c = count[i0 + j];
+            ESGD_ARG(c == 0 || tensors[i0 + j], "esgd_pack: tensor %d is null", i0 + j);
+            p.a[j] = tensors[i0 + j];
+            p.off[j] = off;
+            p.n[j] = c;
+            p.tile0[j] = uint32_t(tiles);
+            tiles += (c + 1023) / 1024;
+            off += c;
+        }
+        ESGD_ARG(tiles < (1ull << 31), "esgd_pack: too many elements in one launch");
+        p.tile0[p.nseg] = uint32_t(tiles);
+        if (!tiles) continue;
+        float *base = bucket;
+        if (pack) {
+            if (divisor == 1.0f) hipLaunchKernelGGL((k_pack<true, false>), dim3(unsigned(tiles)), dim3(256), 0, s, p, base, divisor);
+            else hipLaunchKernelGGL((k_pack<true, true>), dim3(unsigned(tiles)), dim3(256), 0, s, p, base, divisor);
+        } else {
+            hipLaunchKernelGGL((k_pack<false, false>), dim3(unsigned(tiles)), dim3(256), 0, s, p, base, divisor);
+        }
+        ESGD_HIP(hipGetLastError());
+    }
+    return ESGD_SUCCESS;
+}
 int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64_t count,
                   float scale, hipStream_t s) {
     return reduce_impl(dtype, k, inputs, out, count, scale, scale != 1.0f, s, true);
@@ -653,7 +790,8 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
     const bool stamp = a.ts != nullptr && lead;
     if (lead && blockIdx.x == 0) {   // the snapshot queued before this launch has landed
         if (stamp) a.ts[0] = uint64_t(t0);
-        __hip_atomic_store(&a.ready[a.rank], a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // same protocol as k_round_sync: release at system scope, drained, then the flag
+        publish_flag(&a.ready[a.rank], a.value);
     }
     if (!block_wait(a, a.ready, &a.counter[2], blockIdx.x == 0, t0, &ok)) return;
     if (stamp && blockIdx.x == 0) a.ts[1] = uint64_t(wall_clock64());
@@ -827,6 +965,15 @@ int esgd_vsum(int dtype, const void *a, const void *b, void *c, uint64_t count, 
     // the reference's c = a + b (ffop_gcomp_operator.c:13).
     const void *in[2] = {b, a};
     return reduce_impl(dtype, 2, in, c, count, 1.0f, false, stream);
+}
+
+int esgd_pack_div(int n, const float *const *src, const uint64_t *count, float *dst, float divisor,
+                  void *stream) {
+    return pack_impl(true, n, const_cast<float *const *>(src), count, dst, divisor, stream);
+}
+
+int esgd_unpack(int n, float *const *dst, const uint64_t *count, const float *src, void *stream) {
+    return pack_impl(false, n, dst, count, const_cast<float *>(src), 1.0f, stream);
 }
 
 int esgd_fill_uniform_f32(uint64_t seed, int rank, float *out, uint64_t n, void *stream) {

@@ -1,8 +1,12 @@
 // shm.cpp — creation / attachment of the node-local segment and its barrier.
 #include "shm.h"
 
+#include <errno.h>
 #include <fcntl.h>
+#include <linux/futex.h>
 #include <sched.h>
+#include <signal.h>
+#include <sys/syscall.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -27,6 +31,33 @@ void backoff(unsigned &polls) {
     if (polls < 64) return;                      // tight spin: sub-microsecond hand-offs
     if (polls < 2048) { sched_yield(); return; }
     std::this_thread::sleep_for(std::chrono::microseconds(polls < 16384 ? 5 : 50));
+}
+
+// The segment is a MAP_SHARED file mapping, so a (non-private) futex on one of its words
+// works across the node's processes.
+static long futex(std::atomic<uint32_t> *w, int op, uint32_t val, const struct timespec *ts) {
+    return syscall(SYS_futex, reinterpret_cast<uint32_t *>(w), op, val, ts, nullptr, 0);
+}
+
+void seg_wake(Segment *seg) {
+    if (!seg) return;
+    seg->wake_seq.fetch_add(1, std::memory_order_acq_rel);
+    if (seg->sleepers.load(std::memory_order_acquire)) futex(&seg->wake_seq, FUTEX_WAKE, INT32_MAX, nullptr);
+}
+
+void seg_idle_wait(Segment *seg, uint32_t seen, unsigned usec) {
+    seg->sleepers.fetch_add(1, std::memory_order_acq_rel);
+    if (seg->wake_seq.load(std::memory_order_acquire) == seen) {
+        struct timespec ts = {time_t(usec / 1000000u), long(usec % 1000000u) * 1000L};
+        (void)futex(&seg->wake_seq, FUTEX_WAIT, seen, &ts);
+    }
+    seg->sleepers.fetch_sub(1, std::memory_order_acq_rel);
+}
+
+// A segment left behind by a crashed job with the same id: its creator is gone.
+static bool creator_alive(const Segment *seg) {
+    const int32_t pid = seg->pid[0].load();
+    return pid > 0 && (kill(pid, 0) == 0 || errno == EPERM);
 }
 
 static std::string shm_path(const char *job) {
@@ -62,6 +93,7 @@ Segment *shm_attach(const char *job, int rank, int world, double timeout_s) {
         Segment *seg = static_cast<Segment *>(mem);
         seg->world = uint32_t(world);
         seg->bytes = uint32_t(bytes);
+        seg->pid[0].store(int32_t(getpid()));
         std::atomic_thread_fence(std::memory_order_seq_cst);
         seg->magic = kShmMagic;
         if (rename(tmp.c_str(), path.c_str()) != 0) {
@@ -81,7 +113,10 @@ Segment *shm_attach(const char *job, int rank, int world, double timeout_s) {
                     close(fd);
                     if (mem != MAP_FAILED) {
                         Segment *seg = static_cast<Segment *>(mem);
-                        if (seg->magic == kShmMagic && seg->world == uint32_t(world)) break;
+                        // a stale file of an earlier job with this id (its rank 0 died before
+                        // unlinking it) is skipped: rank 0 renames a fresh one over it
+                        if (seg->magic == kShmMagic && seg->world == uint32_t(world) && creator_alive(seg))
+                            break;
                         munmap(mem, bytes);
                         mem = MAP_FAILED;
                     }

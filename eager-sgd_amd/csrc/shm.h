@@ -69,6 +69,10 @@ struct Segment {
     std::atomic<uint32_t> bar_count;
     std::atomic<uint32_t> bar_gen;
     std::atomic<uint32_t> aborted;
+    // idle progress threads sleep on this word (futex); activations, issue-ring appends
+    // and posts bump it, so a peer's activation is seen within a wake-up, not a backoff
+    std::atomic<uint32_t> wake_seq;
+    std::atomic<uint32_t> sleepers;
     std::atomic<uint32_t> nccl_ready;
     uint8_t nccl_id[128];
     std::atomic<int32_t> pid[kMaxRanks];
@@ -86,6 +90,11 @@ void shm_unlink_name(const char *job);
 
 // Sense-reversing barrier over the segment; ESGD_ERROR on timeout or abort.
 int shm_barrier(Segment *seg, int world, double timeout_s);
+
+// Wake every progress thread of the node sleeping in seg_idle_wait (cheap when none is).
+void seg_wake(Segment *seg);
+// Sleep until seg->wake_seq differs from `seen` or `usec` elapsed.
+void seg_idle_wait(Segment *seg, uint32_t seen, unsigned usec);
 
 // Seconds since an arbitrary epoch (steady clock).
 double now_s();

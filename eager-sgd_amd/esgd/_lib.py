@@ -63,6 +63,8 @@ _SIGS = {
     "esgd_reduce_scaled": (_i, [_i, _i, C.POINTER(_vp), _vp, _u64, _f, _vp]),
     "esgd_vsum": (_i, [_i, _vp, _vp, _vp, _u64, _vp]),
     "esgd_fill_uniform_f32": (_i, [_u64, _i, _vp, _u64, _vp]),
+    "esgd_pack_div": (_i, [_i, C.POINTER(_vp), C.POINTER(_u64), _vp, _f, _vp]),
+    "esgd_unpack": (_i, [_i, C.POINTER(_vp), C.POINTER(_u64), _vp, _vp]),
     "esgd_fill_uniform_bf16": (_i, [_u64, _i, _vp, _u64, _vp]),
     "esgd_set_tuning": (_i, [C.c_char_p, _i]),
     "esgd_get_tuning": (_i, [C.c_char_p, C.POINTER(_i)]),

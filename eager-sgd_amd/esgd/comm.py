@@ -23,6 +23,7 @@ from ._lib import check, lib
 
 ALLREDUCE, SOLO, MAJORITY = 0, 1, 2
 BUF_DEVICE, BUF_HOST, BUF_NONE = 0, 1, 2
+HOLD, ZERO_SB = 0x1, 0x2          # esgd_schedule_create_ex flags (esgd.h)
 
 
 class SchedStats(C.Structure):
@@ -41,6 +42,9 @@ def _bind(h):
         "esgd_comm_size": (i, [C.POINTER(i)]),
         "esgd_barrier": (i, []),
         "esgd_schedule_create": (i, [i, i, vp, vp, u64, i, i, C.c_uint, C.POINTER(u64)]),
+        "esgd_schedule_create_ex": (i, [i, i, vp, vp, u64, i, i, C.c_uint, C.c_uint, C.POINTER(u64)]),
+        "esgd_schedule_wait_ex": (i, [u64, C.POINTER(i)]),
+        "esgd_schedule_release": (i, [u64, vp]),
         "esgd_schedule_post": (i, [u64, vp, C.POINTER(i)]),
         "esgd_schedule_wait": (i, [u64]),
         "esgd_schedule_test": (i, [u64, C.POINTER(i)]),
@@ -147,15 +151,15 @@ class Schedule:
     """A persistent schedule (ffallreduce / ffsolo_allreduce / ffrand_allreduce)."""
 
     def __init__(self, kind: int, sb, rb, count: int, dtype: int = _lib.FLOAT,
-                 async_: int = 0, seed: int = 0, buf: int | None = None):
+                 async_: int = 0, seed: int = 0, buf: int | None = None, flags: int = 0):
         if buf is None:
             buf = BUF_HOST if isinstance(rb, np.ndarray) else BUF_NONE if rb is None else BUF_DEVICE
         self.kind, self.buf, self.count, self.dtype = kind, buf, int(count), dtype
         self._keep = (sb, rb)   # host arrays must outlive the schedule
         h = C.c_uint64()
-        check(lib().esgd_schedule_create(kind, buf, _buf_arg(sb, buf), _buf_arg(rb, buf),
-                                         self.count, dtype, int(async_), int(seed) & 0xFFFFFFFF,
-                                         C.byref(h)), "esgd_schedule_create")
+        check(lib().esgd_schedule_create_ex(kind, buf, _buf_arg(sb, buf), _buf_arg(rb, buf),
+                                            self.count, dtype, int(async_), int(seed) & 0xFFFFFFFF,
+                                            int(flags), C.byref(h)), "esgd_schedule_create")
         self.handle = h.value
 
     def post(self, stream=None) -> int:
@@ -168,8 +172,20 @@ class Schedule:
         check(lib().esgd_schedule_post(self.handle, s, C.byref(role)), "esgd_schedule_post")
         return role.value
 
-    def wait(self):
-        check(lib().esgd_schedule_wait(self.handle), "esgd_schedule_wait")
+    def wait(self) -> bool:
+        """Returns whether this rank had posted the round before joining it (False: a
+        peer's activation carried it through with what its send bucket held)."""
+        f = C.c_int()
+        check(lib().esgd_schedule_wait_ex(self.handle, C.byref(f)), "esgd_schedule_wait")
+        return bool(f.value)
+
+    def release(self, stream=None):
+        """HOLD schedules: done with the last round's buckets (work queued on `stream`
+        is waited for by the next round's snapshot; 0 = the legacy default stream)."""
+        s = None if stream is None else (stream.handle if hasattr(stream, "handle") else int(stream))
+        if s == 0:
+            s = 1   # ESGD_STREAM_NULL
+        check(lib().esgd_schedule_release(self.handle, s), "esgd_schedule_release")
 
     def test(self) -> bool:
         f = C.c_int()

@@ -41,6 +41,11 @@ def _bind(h):
     h.allreducef_forward.restype, h.allreducef_forward.argtypes = None, [vp, vp, vp, vp]
     h.allreducef_forward_cuda.restype = None
     h.allreducef_forward_cuda.argtypes = [vp, vp, vp, vp, vp]
+    h.allreducef_forward_cuda_div.restype = C.c_int
+    h.allreducef_forward_cuda_div.argtypes = [vp, vp, vp, C.c_float, vp]
+    h.allreducef_forward_cuda_packed.restype = C.c_int
+    h.allreducef_forward_cuda_packed.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(C.c_uint64),
+                                                 C.POINTER(vp), C.c_float, vp]
     h.is_cuda_supported.restype, h.is_cuda_supported.argtypes = C.c_bool, [vp]
     h.report.restype, h.report.argtypes = C.c_int64, [vp, vp]
     h.delete_op.restype, h.delete_op.argtypes = None, [vp]
@@ -82,6 +87,28 @@ class AllreduceOp:
         from .device import as_ptr
         lib().allreducef_forward_cuda(self.handle, as_ptr(grad), None, as_ptr(out), stream)
         return out
+
+    def forward_cuda_div(self, grad, out, divisor: float, stream: int | None = None):
+        """Device path with the wrapper's grad / comm_size (:40) fused into the copy-in;
+        `out` may be `grad` itself.  Raises EsgdError instead of aborting."""
+        from .device import as_ptr
+        _lib.check(lib().allreducef_forward_cuda_div(self.handle, as_ptr(grad), as_ptr(out),
+                                                     float(divisor), stream),
+                   "allreducef_forward_cuda_div")
+        return out
+
+    def forward_cuda_packed(self, grads, outs, divisor: float = 1.0, stream: int | None = None):
+        """Bucket fusion: the tensors `grads` (fp32, contiguous, sizes summing to this op's
+        size) packed in order, divided, reduced in one round and unpacked into `outs`."""
+        from .device import as_ptr
+        n = len(grads)
+        counts = (C.c_uint64 * max(1, n))(*[int(g.numel()) if hasattr(g, "numel") else int(g.size)
+                                             for g in grads])
+        src = _lib.ptr_array([as_ptr(g) for g in grads])
+        dst = _lib.ptr_array([as_ptr(o) for o in outs])
+        _lib.check(lib().allreducef_forward_cuda_packed(self.handle, n, src, counts, dst, float(divisor),
+                                                        stream), "allreducef_forward_cuda_packed")
+        return outs
 
     def supports_cuda(self) -> bool:
         return bool(lib().is_cuda_supported(self.handle))

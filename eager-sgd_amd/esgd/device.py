@@ -152,6 +152,21 @@ def vsum(dtype: int, a, b, c, count: int, stream=None):
     return check(lib().esgd_vsum(dtype, as_ptr(a), as_ptr(b), as_ptr(c), count, _sh(stream)), "esgd_vsum")
 
 
+def pack_div(srcs, counts, dst, divisor: float = 1.0, stream=None):
+    """dst = concat(src_i / divisor) (esgd_pack_div, fp32)."""
+    n = len(srcs)
+    c = (C.c_uint64 * max(1, n))(*[int(x) for x in counts])
+    return check(lib().esgd_pack_div(n, _lib.ptr_array([as_ptr(x) for x in srcs]), c, as_ptr(dst),
+                                     float(divisor), _sh(stream)), "esgd_pack_div")
+
+
+def unpack(dsts, counts, src, stream=None):
+    n = len(dsts)
+    c = (C.c_uint64 * max(1, n))(*[int(x) for x in counts])
+    return check(lib().esgd_unpack(n, _lib.ptr_array([as_ptr(x) for x in dsts]), c, as_ptr(src),
+                                   _sh(stream)), "esgd_unpack")
+
+
 def fill_uniform(buf: DeviceBuffer, seed: int, rank: int, stream=None):
     if buf.dtype == _lib.FLOAT:
         rc = lib().esgd_fill_uniform_f32(seed, rank, buf.ptr, buf.count, _sh(stream))

@@ -9,8 +9,12 @@ Same protocol: compute_gradients() passes through to the wrapped optimizer's gra
 computation; apply_gradients() walks the (grad, var) list in reverse (:28), feeds every
 gradient divided by the comm size (:40) through one eager-SGD op instance per tensor,
 and hands the partially reduced gradients to the wrapped optimizer.  The op runs on the
-device (allreducef_forward_cuda): the gradient never leaves HBM, unlike the reference's
-CPU-only TF kernel (deep500/frameworks/tensorflow/custom_operators/tf.py:80).
+device (allreducef_forward_cuda_div): the gradient never leaves HBM, unlike the
+reference's CPU-only TF kernel (deep500/frameworks/tensorflow/custom_operators/tf.py:80).
+The division is fused into the op's copy-in (same IEEE fp32 division, same bits) and the
+reduced gradient is written back into p.grad in place: per tensor and step 3 HBM passes
+of the gradient (copy-in with the divide; the move with the zeroing fused; copy-out)
+instead of 5 (divide, copy-in, move, copy-out, memset).
 
 fuse=True (SURVEY.md §8(f) "bucket fusion"): the reference runs one schedule per tensor,
 161 per ResNet-50 step (opt_esgd_solo_imagenet_imbalance.py:85-248), each a
@@ -63,10 +67,11 @@ class EagerSGDOptimizer:
                 op = self._ops.get(var)
                 if op is None:
                     op = self._ops[var] = deep500.AllreduceOp(tuple(grad.shape))
-                scaled = (grad.float() / self.comm_size).contiguous()        # :40
-                out = torch.empty_like(scaled)
-                op.forward_cuda(scaled, out, stream)
-                var.grad = out.to(grad.dtype).view_as(grad)
+                g = grad if (grad.dtype == torch.float32 and grad.is_contiguous()) \
+                    else grad.float().contiguous()
+                op.forward_cuda_div(g, g, self.comm_size, stream)          # :40 fused, in place
+                if g is not grad:
+                    var.grad = g.to(grad.dtype).view_as(grad)
         r = self.optimizer.step()
         if global_step is not None and hasattr(global_step, "add_"):
             global_step.add_(1)
@@ -80,29 +85,21 @@ class EagerSGDOptimizer:
         layout = tuple((id(v), g.numel()) for g, v in live)
         if self._fused is None:
             total = sum(n for _, n in layout)
-            flat = torch.empty(total, dtype=torch.float32, device=live[0][0].device)
-            # one persistent schedule, created collectively at the first step (the
-            # reference creates its bucket schedules lazily too, :288-298)
-            self._fused = (layout, deep500.AllreduceOp((total,)), flat, torch.empty_like(flat))
+            # one persistent schedule over the op's own bucket, created collectively at
+            # the first step (the reference creates its bucket schedules lazily too,
+            # :288-298)
+            self._fused = (layout, deep500.AllreduceOp((total,)))
         elif self._fused[0] != layout:
             raise RuntimeError("EagerSGDOptimizer(fuse=True): the set of gradients changed, "
                                "but the fused bucket's schedule is persistent")
-        _, op, flat, out = self._fused
-        off = 0
-        for g, _ in live:                                        # pack, scaled as in :40
-            n = g.numel()
-            torch.div(g.reshape(-1).float(), self.comm_size, out=flat[off:off + n])
-            off += n
-        op.forward_cuda(flat, out, stream)
-        off = 0
-        for g, v in live:                                        # unpack into the grads
-            n = g.numel()
-            red = out[off:off + n].view(g.shape)
-            if g.dtype == torch.float32 and g.is_contiguous():
-                g.copy_(red)
-            else:
-                v.grad = red.to(g.dtype).clone()
-            off += n
+        _, op = self._fused
+        gs = [g if (g.dtype == torch.float32 and g.is_contiguous()) else g.float().contiguous()
+              for g, _ in live]
+        # pack (divided as in :40) -> one round -> unpack into the same tensors
+        op.forward_cuda_packed(gs, gs, self.comm_size, stream)
+        for g32, (g, v) in zip(gs, live):
+            if g32 is not g:
+                v.grad = g32.to(g.dtype).view_as(g)
 
     # -- torch.optim-style convenience ---------------------------------------------
     def step(self, closure=None):

@@ -94,6 +94,16 @@ int esgd_vsum(int dtype, const void *a, const void *b, void *c, uint64_t count,
 int esgd_reduce_scaled(int dtype, int k, const void *const *inputs, void *out,
                        uint64_t count, float scale, void *stream);
 
+/* Bucket packing for fused rounds (fp32): dst = concat_i(src_i / divisor) in order,
+ * each src_i of count_i elements; divisor == 1 copies.  The division is IEEE fp32
+ * (correctly rounded), the wrapper's grad / comm_size of
+ * opt_esgd_solo_imagenet_imbalance.py:40 fused into the pack.  esgd_unpack is the
+ * inverse copy (dst_i may alias the tensors that were packed).  n <= 4096. */
+int esgd_pack_div(int n, const float *const *src, const uint64_t *count, float *dst,
+                  float divisor, void *stream);
+int esgd_unpack(int n, float *const *dst, const uint64_t *count, const float *src,
+                void *stream);
+
 /* Synthetic gradient generator shared with the oracle: x[i] = 2*u - 1 with
  * u = (splitmix64(seed ^ (rank << 40) ^ i) >> 40) / 2^24  (SURVEY.md §8d). */
 int esgd_fill_uniform_f32(uint64_t seed, int rank, float *out, uint64_t n, void *stream);
@@ -161,6 +171,20 @@ typedef struct {
 
 int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t count,
                          int dtype, int async, unsigned seed, esgd_sched_h *out);
+/* flags (extension, 0 = esgd_schedule_create):
+ *   ESGD_SCHED_HOLD    after wait/test returns a round, this rank joins no further round
+ *                      of the schedule until esgd_schedule_release(): the caller copies
+ *                      rb out and drops a late send bucket first, as the reference
+ *                      wrapper does synchronously right after its wait
+ *                      (opt_esgd_solo_imagenet_imbalance.py:309-314);
+ *   ESGD_SCHED_ZERO_SB the snapshot (move sb -> rb) zeroes sb as it reads it (device
+ *                      buckets, not in place): the wrapper's zero-after-use (:311-314)
+ *                      fused into the move, one HBM pass fewer. */
+#define ESGD_SCHED_HOLD 0x1
+#define ESGD_SCHED_ZERO_SB 0x2
+int esgd_schedule_create_ex(int kind, int buf, const void *sb, void *rb, uint64_t count,
+                            int dtype, int async, unsigned seed, unsigned flags,
+                            esgd_sched_h *out);
 /* post: start round `posted+1`.  producer_stream: stream that writes sb; the snapshot of
  * a round this rank posted waits for the work queued on it so far.  NULL = no producer;
  * ESGD_STREAM_NULL = the legacy default (NULL) stream, e.g. torch's default stream. */
@@ -169,6 +193,14 @@ int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t c
  * role (may be NULL): 1 activated the round, 0 passive, 2 synchronous round. */
 int esgd_schedule_post(esgd_sched_h h, void *producer_stream, int *role);
 int esgd_schedule_wait(esgd_sched_h h);
+/* wait, and report whether this rank had posted the returned round before it joined it
+ * (0: a peer's activation carried this rank through the round with whatever its send
+ * bucket held -- the caller's late gradient did not take part) */
+int esgd_schedule_wait_ex(esgd_sched_h h, int *fresh);
+/* ESGD_SCHED_HOLD schedules: done with the round wait returned.  Work queued on
+ * `stream` so far (copy-out of rb, zeroing sb; NULL = nothing queued) is waited for by
+ * the next round's snapshot on the GPU. */
+int esgd_schedule_release(esgd_sched_h h, void *stream);
 int esgd_schedule_test(esgd_sched_h h, int *flag);
 int esgd_schedule_delete(esgd_sched_h h);
 int esgd_schedule_stats(esgd_sched_h h, esgd_sched_stats_t *out);

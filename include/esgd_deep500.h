@@ -47,6 +47,19 @@ void *create_new_op(esgd_d5_tensor_t *input_descriptors, int num_inputs,
 void allreducef_forward(void *handle, const float *input, const float *last, float *output);
 void allreducef_forward_cuda(void *handle, const float *input, const float *last, float *output,
                              void *stream);
+/* Extensions (device path, return an esgd status instead of aborting):
+ *   allreducef_forward_cuda_div: output = partial allreduce of (input / divisor), the
+ *     wrapper's grad / comm_size (opt_esgd_solo_imagenet_imbalance.py:40) fused into the
+ *     copy-in (IEEE fp32 division, the same bits as dividing first); output may alias input;
+ *   allreducef_forward_cuda_packed: n gradient tensors (counts summing to the op's size)
+ *     packed in order into the op's bucket (divided as above), one round, unpacked into
+ *     outs[i] (may alias grads[i]): the bucket fusion of one round per step instead of
+ *     one per tensor. */
+int allreducef_forward_cuda_div(void *handle, const float *input, float *output, float divisor,
+                                void *stream);
+int allreducef_forward_cuda_packed(void *handle, int n, const float *const *grads,
+                                   const uint64_t *counts, float *const *outs, float divisor,
+                                   void *stream);
 bool is_cuda_supported(void *handle);
 int64_t report(void *handle, void *data);   /* bytes of gradient reduced so far */
 void delete_op(void *handle);

@@ -255,3 +255,97 @@ double ffref_time_allreduce(int P, uint32_t count, int threads, int reps) {
     free(sb); free(rb); free(tmp); free(scratch);
     return best;
 }
+
+/* ---- C1 baseline: P ranks x (main + progress thread), shared-memory "MPI" ---- */
+typedef struct {
+    int P, rank, reps;
+    uint32_t count;
+    float **sb, **rb, **tmp, **in, **out;
+    volatile int *posted, *done;       /* per rank: step numbers */
+    volatile int *ready, *taken;       /* per rank: (step * 64 + round) sequence */
+    pthread_barrier_t *bar;            /* the main threads' MPI_Barrier */
+    volatile int *stop;
+} ffref_c1_arg;
+
+static void ffref_spin_until(volatile int *w, int v) {
+    int polls = 0;
+    while (__atomic_load_n(w, __ATOMIC_ACQUIRE) < v)
+        if (++polls % 5 == 0) sched_yield();    /* ffop.c:156-163 */
+}
+
+static void *ffref_c1_progress(void *p) {
+    ffref_c1_arg *a = (ffref_c1_arg *)p;
+    const int r = a->rank;
+    for (int step = 1; step <= a->reps + 1; ++step) {
+        ffref_spin_until(&a->posted[r], step);
+        ffref_copy(FFREF_FLOAT, a->sb[r], a->rb[r], a->count);      /* move, :126-130 */
+        int round = 0;
+        for (int mask = 1; mask < a->P; mask <<= 1, ++round) {
+            const int dst = r ^ mask, seq = step * 64 + round + 1;
+            __atomic_store_n(&a->ready[r], seq, __ATOMIC_RELEASE);  /* send(rb), :145 */
+            if (dst >= a->P) { __atomic_store_n(&a->taken[r], seq, __ATOMIC_RELEASE); continue; }
+            ffref_spin_until(&a->ready[dst], seq);                   /* recv(tmp), :152 */
+            memcpy(a->tmp[r], a->rb[dst], (size_t)a->count * 4);
+            __atomic_store_n(&a->taken[r], seq, __ATOMIC_RELEASE);
+            ffref_spin_until(&a->taken[dst], seq);                   /* partner has our rb */
+            ffref_vsum(FFREF_FLOAT, a->tmp[r], a->rb[r], a->rb[r], a->count);   /* :155 */
+        }
+        __atomic_store_n(&a->done[r], step, __ATOMIC_RELEASE);
+    }
+    return NULL;
+}
+
+static double ffref_c1_best;
+
+static void *ffref_c1_main(void *p) {
+    ffref_c1_arg *a = (ffref_c1_arg *)p;
+    const int r = a->rank;
+    const size_t bytes = (size_t)a->count * 4;
+    double best = 1e30;
+    for (int step = 1; step <= a->reps + 1; ++step) {
+        pthread_barrier_wait(a->bar);
+        double t0 = ffref_now();
+        memcpy(a->sb[r], a->in[r], bytes);                           /* :301 */
+        __atomic_store_n(&a->posted[r], step, __ATOMIC_RELEASE);     /* post, :304 */
+        ffref_spin_until(&a->done[r], step);                         /* wait, :307 */
+        memcpy(a->out[r], a->rb[r], bytes);                          /* :309 */
+        memset(a->sb[r], 0, bytes);                                  /* :311-314 */
+        double dt = ffref_now() - t0;
+        pthread_barrier_wait(a->bar);
+        if (r == 0 && step > 1 && dt < best) best = dt;
+    }
+    if (r == 0) ffref_c1_best = best;
+    return NULL;
+}
+
+double ffref_time_c1(int P, uint32_t count, int reps, int *ok) {
+    if (P < 1 || P > 64 || reps < 1) return -1.0;
+    const size_t bytes = (size_t)count * 4;
+    float *bufs[5][64];
+    for (int k = 0; k < 5; ++k)
+        for (int r = 0; r < P; ++r) { bufs[k][r] = (float *)malloc(bytes ? bytes : 4); memset(bufs[k][r], 0, bytes); }
+    for (int r = 0; r < P; ++r) ffref_fill_uniform_f32(0x5EEDE56Dull, r, bufs[3][r], count);
+    volatile int posted[64] = {0}, done[64] = {0}, ready[64] = {0}, taken[64] = {0}, stop = 0;
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, (unsigned)P);
+    ffref_c1_arg args[64];
+    pthread_t th[128];
+    for (int r = 0; r < P; ++r) {
+        args[r] = (ffref_c1_arg){P, r, reps, count, bufs[0], bufs[1], bufs[2], bufs[3], bufs[4],
+                                 posted, done, ready, taken, &bar, &stop};
+        pthread_create(&th[2 * r], NULL, ffref_c1_progress, &args[r]);
+        pthread_create(&th[2 * r + 1], NULL, ffref_c1_main, &args[r]);
+    }
+    for (int i = 0; i < 2 * P; ++i) pthread_join(th[i], NULL);
+    pthread_barrier_destroy(&bar);
+    /* every rank's last result vs the tree */
+    float *want = (float *)malloc(bytes ? bytes : 4);
+    ffref_tree_sum(FFREF_FLOAT, P, (const void *const *)bufs[3], want, count);
+    int good = 1;
+    for (int r = 0; r < P; ++r) good &= memcmp(bufs[4][r], want, bytes) == 0;
+    if (ok) *ok = good;
+    free(want);
+    for (int k = 0; k < 5; ++k)
+        for (int r = 0; r < P; ++r) free(bufs[k][r]);
+    return ffref_c1_best;
+}

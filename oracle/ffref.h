@@ -79,6 +79,16 @@ void ffref_fill_uniform_f32_at(uint64_t seed, int rank, uint64_t start, float *o
  * P => one pthread per rank).  Returns seconds per allreduce (best of reps). */
 double ffref_time_allreduce(int P, uint32_t count, int threads, int reps);
 
+/* C1-shaped CPU baseline (BASELINE.json configs[0]): P ranks, each a main thread and a
+ * progress thread (src/ff.c:72), reducing one `count`-element fp32 bucket per step the
+ * way the wrapper drives fflib2 (opt_esgd_solo_imagenet_imbalance.py:301-316): copy the
+ * gradient into the send bucket, post, spin-wait (ffop.c:156-163), copy the result out,
+ * zero the send bucket; the progress thread runs the move and the recursive-doubling
+ * rounds (ffallreduce.c:126-171), exchanging rb through shared memory in place of MPI.
+ * Returns the best per-step seconds over `reps` steps (after one warm-up step); *ok = 1
+ * if every rank's last result equals the oracle tree of the P buckets. */
+double ffref_time_c1(int P, uint32_t count, int reps, int *ok);
+
 #ifdef __cplusplus
 }
 #endif

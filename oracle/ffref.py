@@ -53,6 +53,8 @@ def lib():
         h.ffref_f32_to_bf16.restype = C.c_uint16
         h.ffref_time_allreduce.argtypes = [i, u32, i, i]
         h.ffref_time_allreduce.restype = C.c_double
+        h.ffref_time_c1.argtypes = [i, u32, i, C.POINTER(i)]
+        h.ffref_time_c1.restype = C.c_double
         _lib = h
     return _lib
 
@@ -140,3 +142,11 @@ def fill_uniform(seed: int, rank: int, n: int, start: int = 0) -> np.ndarray:
 
 def time_allreduce(P: int, count: int, threads: int, reps: int) -> float:
     return float(lib().ffref_time_allreduce(P, count, threads, reps))
+
+
+def time_c1(P: int, count: int, reps: int):
+    """(best seconds per step, every rank's result == tree) of the C1-shaped baseline:
+    P ranks x (main + progress thread) (ffref.h: ffref_time_c1)."""
+    ok = C.c_int(0)
+    t = float(lib().ffref_time_c1(P, count, reps, C.byref(ok)))
+    return t, bool(ok.value)

@@ -8,12 +8,16 @@
  *     (evaluation/solo_allreduce_correctness.c:76-97, rand_allreduce_correctness.c:78-98);
  *   - FFCOLL_BUFFERS: one schedule, buckets that move and change size every round, one
  *     user-managed and one library-managed (evaluation/allreduce_buffers_user_managed.c,
- *     allreduce_buffers_fflib_managed.c), same (i + j) * size answer.
+ *     allreduce_buffers_fflib_managed.c), same (i + j) * size answer;
+ *   - FFCOLL_BUFFERS under ffsolo_allreduce with a late rank (posts of rounds a peer
+ *     already ran are accepted).
  * Ranks come from RANK / WORLD_SIZE / ESGD_JOB_ID (no MPI).  Exit status 0 = passed.
  */
+#define _POSIX_C_SOURCE 199309L
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <time.h>
 
 #include "ff.h"
 
@@ -115,6 +119,46 @@ int main(int argc, char **argv) {
             failed |= check_int(rbuf, w, c, "FFCOLL_BUFFERS", i);
             free(w);
         }
+        ffschedule_delete(s);
+        ffbuffer_delete(sbh);
+        ffbuffer_delete(rbh);
+        free(sbuf);
+    }
+    /* FFCOLL_BUFFERS under ffsolo_allreduce with a late rank: peers activate the
+     * asynchronous rounds, the late rank is carried through them and its own post of a
+     * round that already ran must be accepted (the reference takes options =
+     * FFCOLL_BUFFERS for ffsolo_allreduce too, src/colls/ffsolo_allreduce.c:20-95).
+     * Every rank's bucket holds 1 before the barrier, so every round reduces to size. */
+    if (!failed && size > 1) {
+        const int c = count;
+        int32_t *sbuf = malloc(sizeof(int32_t) * c);
+        ffbuffer_h sbh, rbh;
+        ffbuffer_create(sbuf, c, FFINT32, 0, &sbh);
+        ffbuffer_create(NULL, c, FFINT32, 0, &rbh);
+        ffschedule_h s;
+        if (ffsolo_allreduce(&sbh, &rbh, c, 0, FFSUM, FFINT32, FFCOLL_BUFFERS, 3, &s) != FFSUCCESS) {
+            fprintf(stderr, "ffsolo_allreduce(FFCOLL_BUFFERS): %s\n", esgd_last_error());
+            return 2;
+        }
+        int32_t *w = malloc(sizeof(int32_t) * c);
+        for (int j = 0; j < c; ++j) { sbuf[j] = 1; w[j] = size; }
+        for (int i = 0; i < iters + 4 && !failed; ++i) {
+            esgd_barrier();
+            if (rank == size - 1) {
+                struct timespec d = {0, 20 * 1000 * 1000};
+                nanosleep(&d, NULL);
+            }
+            if (ffschedule_post(s) != FFSUCCESS || ffschedule_wait(s) != FFSUCCESS) {
+                fprintf(stderr, "[rank %d] solo FFCOLL_BUFFERS round %d: %s\n", rank, i, esgd_last_error());
+                failed = 1;
+                break;
+            }
+            esgd_barrier();
+            int32_t *rbuf;
+            ffbuffer_get_data(rbh, (void **)&rbuf);
+            failed |= check_int(rbuf, w, c, "solo FFCOLL_BUFFERS", i);
+        }
+        free(w);
         ffschedule_delete(s);
         ffbuffer_delete(sbh);
         ffbuffer_delete(rbh);

@@ -28,8 +28,11 @@ def free_port() -> int:
 def _entry(fn_name, rank, world, port, kw, q):
     try:
         os.environ.setdefault("ESGD_TIMEOUT_S", "60")
+        # one GPU per rank where the box has them (device = rank % device_count, set in
+        # _comm()): on a full node the data plane then crosses xGMI; on a 1-GPU box every
+        # rank shares device 0
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                          WORLD_SIZE=str(world), LOCAL_RANK="0")
+                          WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
         out = globals()[fn_name](rank, world, **kw)
@@ -66,8 +69,19 @@ def run(fn_name: str, world: int, timeout: float = 240.0, **kw):
 
 # --------------------------------------------------------------------------- workers
 
+def local_device(rank=None):
+    """rank % device_count (0 when there is no device)."""
+    import esgd
+    n = esgd.device_count()
+    r = int(os.environ.get("LOCAL_RANK", "0")) if rank is None else rank
+    return r % n if n > 0 else 0
+
+
 def _comm():
+    import esgd
     from esgd import comm
+    if esgd.device_count() > 0:
+        esgd.check(esgd.lib().esgd_set_device(local_device()), "esgd_set_device")
     comm.init()
     return comm
 
@@ -254,8 +268,37 @@ def gpu_partial_semantics(rank, world, kind, rounds, async_=3, seed=6545343, str
     return out
 
 
+LATE_S = 0.03   # how late a delayed rank calls the op (>> one round of these sizes)
+
+
+def late_ranks(mode, world, step, seed=6545343):
+    """Ranks that call the op LATE in `step` so that a partial round's contributor set is
+    deterministic: majority -- the activator (ffrand_allreduce.c:88, rand_r sequence) posts
+    after every other rank has posted, so its round takes every fresh gradient; solo --
+    every rank but 0, so rank 0's post activates the (asynchronous) round and the late
+    ranks are carried through it with a zeroed send bucket (ffactivation.c:11-106, the
+    wrapper's zeroing opt_esgd_solo_imagenet_imbalance.py:311-314)."""
+    from oracle import ffref
+    if mode == "majority":
+        return {ffref.activators(seed, world, step + 1)[step]}
+    if mode == "solo":
+        return set(range(1, world))
+    return set()
+
+
+def expected_inputs(mode, xs):
+    """The per-rank inputs the round reduces under late_ranks' ordering."""
+    import numpy as np
+    if mode == "solo":
+        return [xs[0]] + [np.zeros_like(x) for x in xs[1:]]
+    return xs
+
+
 def op_host(rank, world, mode="allreduce", steps=3, count=5000):
-    """deep500 op, host path (the reference's CPU-registered TF kernel contract)."""
+    """deep500 op, host path (the reference's CPU-registered TF kernel contract).  Step 0
+    creates the schedule (collective, racing the first post); steps >= 1 run in
+    late_ranks' order and are checked bit for bit against the oracle tree of
+    expected_inputs."""
     import numpy as np
 
     from esgd import deep500
@@ -267,26 +310,73 @@ def op_host(rank, world, mode="allreduce", steps=3, count=5000):
     for t in range(steps):
         xs = [ffref.fill_uniform(0xABC + t, r, count) for r in range(world)]
         comm.barrier()          # evaluation/solo_allreduce_correctness.c:84 pattern
+        if t > 0 and rank in late_ranks(mode, world, t):
+            time.sleep(LATE_S)
         out = op.forward(xs[rank])
-        ok.append(bool(np.array_equal(out.view(np.uint32), ffref.tree_sum(xs).view(np.uint32))))
+        if t > 0:
+            want = ffref.tree_sum(expected_inputs(mode, xs))
+            ok.append(bool(np.array_equal(out.view(np.uint32), want.view(np.uint32))))
     rep = op.report()
     comm.barrier()
     comm.finalize()
     return {"ok": ok, "report": rep, "cuda": op.supports_cuda()}
 
 
+def op_device_late(rank, world, async_=3, steps=9, count=100003):
+    """deep500 op, device path, solo, rank > 0 calling late every step.  Asynchronous
+    rounds: rank 0 activates, the late ranks are carried through with a zeroed send
+    bucket, and their late gradient is DROPPED (not carried into the next round): the
+    result is x0 / P.  Synchronous rounds (every async+1-th, ffsolo_limiter.c:4-35): every
+    rank's fresh gradient.  Both on every rank, bit for bit."""
+    import numpy as np
+    import torch
+
+    from esgd import deep500
+    from oracle import ffref
+    comm = _comm()
+    dev = torch.device("cuda", local_device())
+    torch.cuda.set_device(dev)
+    deep500.configure("solo", async_, 6545343)
+    op = deep500.AllreduceOp((count,))
+    stream = torch.cuda.current_stream().cuda_stream
+    ok, fresh = [], []
+    for t in range(steps):
+        xs = [ffref.fill_uniform(0x1A7E + t, r, count) for r in range(world)]
+        g = torch.from_numpy(xs[rank]).to(dev)
+        comm.barrier()
+        if t > 0 and rank > 0:
+            time.sleep(LATE_S)
+        op.forward_cuda_div(g, g, world, stream)
+        got = g.cpu().numpy()
+        rnd = t + 1
+        scaled = [x / np.float32(world) for x in xs]
+        if t == 0:
+            continue
+        sync = rnd % (async_ + 1) == 0
+        want = ffref.tree_sum(scaled if sync else [scaled[0]] + [np.zeros_like(x) for x in scaled[1:]])
+        ok.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
+        fresh.append(sync)
+    comm.barrier()
+    comm.finalize()
+    return {"ok": ok, "sync_rounds": fresh}
+
+
 def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False):
     """EagerSGDOptimizer on PyTorch-ROCm: every rank's p.grad after apply_gradients must
-    equal the oracle tree of (grad_r / P) over ranks, bit for bit."""
+    equal the oracle tree of (grad_r / P) over ranks, bit for bit (allreduce), or over
+    expected_inputs' contributors when the ranks call every op in late_ranks' order
+    (solo / majority; step 0, which creates the schedules collectively, is not checked)."""
     import numpy as np
     import torch
     import torch.distributed as dist
 
+    from esgd import deep500
     from esgd.optim import EagerSGDOptimizer
     from oracle import ffref
     comm = _comm()
     torch.manual_seed(1234)
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", local_device())
+    torch.cuda.set_device(dev)
     model = torch.nn.Sequential(torch.nn.Linear(64, 48), torch.nn.ReLU(), torch.nn.Linear(48, 10)).to(dev)
     opt = EagerSGDOptimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9), world, mode=mode,
                             fuse=fuse)
@@ -302,10 +392,25 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False):
         allg = [None] * world
         dist.all_gather_object(allg, local)
         comm.barrier()
-        opt.apply_gradients(gvs)
+        late = t > 0 and rank in late_ranks(mode, world, t)
+        orig = (deep500.AllreduceOp.forward_cuda_div, deep500.AllreduceOp.forward_cuda_packed)
+        if late:   # every op call of this step comes LATE_S after the peers'
+            def delayed(fn):
+                def f(self, *a, **k):
+                    time.sleep(LATE_S)
+                    return fn(self, *a, **k)
+                return f
+            deep500.AllreduceOp.forward_cuda_div = delayed(orig[0])
+            deep500.AllreduceOp.forward_cuda_packed = delayed(orig[1])
+        try:
+            opt.apply_gradients(gvs)
+        finally:
+            deep500.AllreduceOp.forward_cuda_div, deep500.AllreduceOp.forward_cuda_packed = orig
         torch.cuda.synchronize()
+        if t == 0 and mode != "allreduce":
+            continue
         for i, (_, p) in enumerate(gvs):
-            want = ffref.tree_sum([allg[r][i] for r in range(world)])
+            want = ffref.tree_sum(expected_inputs(mode, [allg[r][i] for r in range(world)]))
             got = p.grad.detach().float().cpu().numpy().ravel()
             ok.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
     params = torch.cat([p.detach().float().cpu().ravel() for p in model.parameters()]).numpy()
@@ -363,3 +468,180 @@ def cp_create_failure(rank, world, bad_rank=1):
     s.delete()
     comm.finalize()
     return {"err": err, "recovered_s": time.time() - t0}
+
+
+def cp_churn_inflight(rank, world, rounds=300, churn=40):
+    """Schedules created and deleted while another schedule's rounds are in flight (a
+    thread posts / waits it back to back): delete must not free a schedule the progress
+    thread is still stepping (engine.cpp: sched_delete waits two progress epochs)."""
+    import threading
+
+    comm = _comm()
+    a = comm.Schedule(comm.ALLREDUCE, None, None, 0, buf=comm.BUF_NONE)
+    errs = []
+
+    def pump():
+        try:
+            for _ in range(rounds):
+                a.post()
+                a.wait()
+        except Exception as e:   # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    th = threading.Thread(target=pump)
+    th.start()
+    for j in range(churn):
+        b = comm.Schedule(comm.SOLO if j % 2 else comm.MAJORITY, None, None, 0, async_=2, seed=7,
+                          buf=comm.BUF_NONE)
+        b.post()
+        b.wait()
+        b.delete()
+    th.join()
+    st = a.stats()
+    a.delete()
+    comm.finalize()
+    return {"errs": errs, "completed": st["completed"]}
+
+
+SEED = 0x5EEDE56D
+
+
+def _download_slice(buf, start, n):
+    """Elements [start, start + n) of a DeviceBuffer, to the host."""
+    import numpy as np
+
+    from esgd import device as dev
+    from esgd._lib import check, lib
+    out = np.empty(n, dtype=dev.NP_DTYPE[buf.dtype])
+    es = out.itemsize
+    check(lib().esgd_memcpy_async(out.ctypes.data, buf.ptr + start * es, n * es, 1, None), "d2h")
+    dev.synchronize()
+    return out
+
+
+def gpu_config(rank, world, kind, counts, dtype_name="fp32", rounds=2, async_=32, seed=6545343,
+               check=65536, transport="ipc", keep=False, detail=False, free=True, env=None):
+    """A BASELINE.json workload: one in-place bucket per rank per size in `counts`, every
+    rank's bucket written BEFORE a barrier and then posted (the pattern of
+    evaluation/{solo,rand}_allreduce_correctness.c:76-97: whichever rank activates, every
+    rank's data is fresh, so solo / majority rounds equal the plain allreduce).  Inputs
+    come from the device generator shared with the oracle; head, middle and tail slices of
+    every rank's result are compared bit for bit with the oracle tree."""
+    import numpy as np
+
+    from esgd import _lib
+    from esgd import device as dev
+    from oracle import ffref
+    os.environ.update(env or {})
+    comm = _comm()
+    comm.set_transport(transport)
+    dt = _lib.FLOAT if dtype_name == "fp32" else _lib.BF16
+    out, kept = [], []
+    for i, count in enumerate(counts):
+        rb = dev.DeviceBuffer(count, dt)
+        s = comm.Schedule(kind, None, rb, count, dtype=dt, async_=async_, seed=seed, buf=comm.BUF_DEVICE)
+        for t in range(rounds):
+            sd = SEED + 7919 * i + t
+            dev.fill_uniform(rb, sd, rank)
+            dev.synchronize()
+            comm.barrier()
+            s.post()
+            s.wait()
+            comm.barrier()
+            m = min(count, check)
+            ok = True
+            for start in sorted({0, (count - m) // 2, count - m}):
+                got = _download_slice(rb, start, m)
+                xs = [ffref.fill_uniform(sd, r, m, start=start) for r in range(world)]
+                if dt == _lib.BF16:
+                    want = ffref.tree_sum_bf16([ffref.f32_to_bf16(x) for x in xs])
+                else:
+                    want = ffref.tree_sum(xs)
+                good = bool(np.array_equal(got.view(np.uint8), want.view(np.uint8)))
+                if not good and detail:
+                    bad = np.nonzero(got.view(np.uint32 if dt == _lib.FLOAT else np.uint16) !=
+                                     want.view(np.uint32 if dt == _lib.FLOAT else np.uint16))[0]
+                    print(f"[r{rank}] count={count} t={t} slice@{start}: {bad.size} bad, first {bad[0] + start} "
+                          f"got {got[bad[0]]} want {want[bad[0]]}; last {bad[-1] + start}", flush=True)
+                ok &= good
+            out.append((count, dtype_name, t, ok))
+        comm.barrier()
+        if keep:
+            kept.append((s, rb))
+        else:
+            s.delete()
+            if free:
+                rb.close()
+            else:
+                kept.append((None, rb))
+    for sch, buf in kept:
+        if sch is not None:
+            sch.delete()
+        buf.close()
+    comm.set_transport("ipc")
+    comm.finalize()
+    return out
+
+
+def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, delay=None):
+    """eager-SGD's partial rounds with a straggler (the last rank), contributor-counted
+    like evaluation/rsgd.c:87,100: every rank's gradient is 1.0, zeroed after use, so a
+    round's result is the number of ranks whose fresh gradient it took.  On-time ranks
+    write theirs before the round's barrier; the straggler writes and posts `delay` after
+    it (default 4x the no-straggler round, at least 20 ms).  Returns this rank's
+    per-round (round, contributors, uniform result) and the round log."""
+    import statistics
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from esgd import _lib
+    from esgd import device as dev
+    from esgd._lib import check, lib
+    comm = _comm()
+    ones = dev.DeviceBuffer(count)
+    ones.upload(np.ones(count, np.float32))
+    sb, rb = dev.DeviceBuffer(count), dev.DeviceBuffer(count)
+    sb.zero(); rb.zero()
+    dev.synchronize()
+    s = comm.Schedule(kind, sb, rb, count, dtype=_lib.FLOAT, async_=async_, seed=seed, buf=comm.BUF_DEVICE)
+    late = world - 1
+
+    def fill():
+        check(lib().esgd_memcpy_async(sb.ptr, ones.ptr, count * 4, 2, None), "d2d")
+        dev.synchronize()
+
+    def one(d):
+        if rank != late or d == 0:
+            fill()
+        comm.barrier()
+        if rank == late and d > 0:
+            time.sleep(d)
+            fill()
+        t0 = time.perf_counter()
+        s.post()
+        s.wait()
+        el = time.perf_counter() - t0
+        sb.zero()
+        dev.synchronize()
+        m = min(count, 4096)
+        head, tail = _download_slice(rb, 0, m), _download_slice(rb, count - m, m)
+        comm.barrier()
+        uniform = bool(np.all(head == head[0]) and np.all(tail == head[0]))
+        return el, float(head[0]), uniform
+
+    warm = [one(0)[0] for _ in range(3)]   # rounds 1..3: everyone on time
+    tt = torch.tensor([statistics.median(warm)], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    T = float(tt.item())
+    d = delay if delay is not None else max(4 * T, 0.02)
+    res = []
+    for t in range(4, 4 + rounds):
+        _, c, u = one(d)
+        res.append((t, c, u))
+    out = {"rounds": res, "log": s.log(), "T_s": T, "delay_s": d}
+    comm.barrier()
+    s.delete()
+    comm.finalize()
+    return out

@@ -26,7 +26,8 @@ def test_c_caller_known_answers(tmp_path, world):
     job = uuid.uuid4().hex
     procs = []
     for r in range(world):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
+        # ffinit picks device LOCAL_RANK % device_count: one GPU per rank on a full node
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    ESGD_JOB_ID=job, ESGD_TIMEOUT_S="60",
                    ESGD_DEBUG=os.environ.get("ESGD_DEBUG", "0"))
         procs.append(subprocess.Popen([exe, "10007", "4"], env=env, stdout=subprocess.PIPE,

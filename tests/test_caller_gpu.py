@@ -1,5 +1,17 @@
 """The drop-in callers on the GPU: the deep500 op ABI (host buckets, the reference's
-contract) and the PyTorch EagerSGDOptimizer (device path), multi-rank on one device."""
+contract; device buckets with the wrapper's division fused) and the PyTorch
+EagerSGDOptimizer, multi-rank (one GPU per rank where the box has them).
+
+Known answers: the plain allreduce equals the oracle tree of every rank's gradient
+(evaluation/allreduce.c:59-63 in fp32 form).  Solo and majority rounds are made
+deterministic by the order in which ranks call the op (mp_workers.late_ranks):
+majority -- the drawn activator (rand_r(6545343) % P, ffrand_allreduce.c:88) calls last,
+so its round takes every fresh gradient (rand_allreduce_correctness.c:78-98's answer);
+solo -- rank 0 calls first and activates, the others are carried through the round with
+a zeroed send bucket, so the round is the oracle tree of (x0, 0, ..., 0) and their late
+gradients are dropped, as the wrapper's zeroing after the wait does
+(opt_esgd_solo_imagenet_imbalance.py:311-314).
+"""
 import pytest
 
 from mp_workers import run
@@ -9,24 +21,30 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("mode", ["allreduce", "solo", "majority"])
 def test_deep500_op_host_path(mode):
-    # with every rank posting behind a barrier, solo / majority rounds see every rank's
-    # fresh gradient (evaluation/{solo,rand}_allreduce_correctness.c known answer)
-    outs = run("op_host", 2, mode=mode, steps=3, count=5000)
+    outs = run("op_host", 2, mode=mode, steps=4, count=5000)
     for o in outs:
-        assert o["cuda"] and o["report"] == 3 * 5000 * 4
-        if mode == "allreduce":
-            assert all(o["ok"]), o
+        assert o["cuda"] and o["report"] == 4 * 5000 * 4
+        assert all(o["ok"]) and len(o["ok"]) == 3, o
+
+
+def test_deep500_op_device_late_gradient_dropped():
+    # solo, async 3: rounds 2, 3 (and 5..7) asynchronous -> x0 / P only; round 4 and 8
+    # synchronous -> every rank.  A late gradient carried into the next round (the race
+    # of the unfused copy-out / zeroing) would break the asynchronous rounds' answer.
+    outs = run("op_device_late", 2, async_=3, steps=9)
+    for o in outs:
+        assert all(o["ok"]), o
+        assert o["sync_rounds"] == [r % 4 == 0 for r in range(2, 10)]
 
 
 @pytest.mark.parametrize("fuse", [False, True])
-@pytest.mark.parametrize("mode", ["allreduce", "solo"])
+@pytest.mark.parametrize("mode", ["allreduce", "solo", "majority"])
 def test_eager_sgd_optimizer(mode, fuse):
     # fuse=True packs every gradient into one bucket (one round per step): the same
     # bits as one round per tensor
-    outs = run("optimizer_step", 2, mode=mode, steps=2, fuse=fuse)
+    outs = run("optimizer_step", 2, mode=mode, steps=3, fuse=fuse)
     for o in outs:
-        if mode == "allreduce":
-            assert all(o["ok"]), o["ok"]
+        assert all(o["ok"]) and o["ok"], o["ok"]
         assert o["bytes"] > 0
     if mode == "allreduce":   # synchronous averaging keeps the replicas identical
         assert outs[0]["params_digest"] == outs[1]["params_digest"]

@@ -110,3 +110,11 @@ def test_failed_creation_fails_every_rank(world):
         else:
             assert "another rank failed" in o["err"]
         assert o["recovered_s"] < 30
+
+
+def test_delete_while_rounds_in_flight():
+    # sched_delete vs a progress pass holding the registry copy
+    outs = run("cp_churn_inflight", 2, rounds=300, churn=40)
+    for o in outs:
+        assert not o["errs"], o
+        assert o["completed"] == 300

@@ -1,5 +1,6 @@
-"""Multi-rank data plane on the GPU: P processes (all on device 0 of the test box, one
-per GPU on a full node) run persistent schedules over IPC-mapped peer buffers.
+"""Multi-rank data plane on the GPU: P processes (device rank % device_count: all on
+device 0 of a 1-GPU box, one per GPU on a full node, where the peer reads cross xGMI)
+run persistent schedules over IPC-mapped peer buffers.
 
 Bar: every rank's receive buffer is bit-identical to the oracle's restatement of
 fflib2's recursive doubling (src/colls/ffallreduce.c:138-171) for the same inputs;
@@ -144,3 +145,95 @@ def test_shadowed_device_buckets(in_place):
     # bucket (copy in at the snapshot, out at the finish); mixed with direct ranks
     verdicts = run("gpu_allreduce", 3, count=200003, rounds=2, in_place=in_place, shadow_ranks=(1,))
     assert all(all(v) for v in verdicts), verdicts
+
+
+# ---- BASELINE.json's workloads (C1, C3, C4, C5) at their full sizes -----------------
+# Every rank writes its bucket before a barrier and posts (the pattern of
+# evaluation/{solo,rand}_allreduce_correctness.c:76-97): solo / majority rounds then
+# equal the plain allreduce, checked bit for bit on head, middle and tail slices of
+# every rank's result (mp_workers.gpu_config).
+
+def _all_ok(outs):
+    bad = [(r, v) for r, per in enumerate(outs) for v in per if not v[3]]
+    assert not bad, bad
+
+
+def test_c1_majority_2_ranks_1mib():
+    # C1: 2-rank majority-allreduce of one 1 MiB fp32 bucket, seed 6545343
+    _all_ok(run("gpu_config", 2, kind=MAJORITY, counts=[262144], rounds=4, seed=6545343))
+
+
+@pytest.mark.timeout(900)
+def test_c3_solo_8_ranks_256mib():
+    # C3: 8-rank solo-allreduce of one 256 MiB fp32 bucket per rank (LIMITER 32)
+    _all_ok(run("gpu_config", 8, kind=SOLO, counts=[64 << 20], rounds=2, async_=32, timeout=420))
+
+
+@pytest.mark.timeout(900)
+def test_c4_majority_8_ranks_resnet50():
+    # C4: 8-rank majority-allreduce of the ResNet-50 fused gradient, 25 559 081 fp32
+    # (opt_esgd_solo_imagenet_imbalance.py:86-248 summed; ragged: not a multiple of 4)
+    _all_ok(run("gpu_config", 8, kind=MAJORITY, counts=[25559081], rounds=3, timeout=420))
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.timeout(900)
+def test_c5_majority_8_ranks_sweep(dtype):
+    # C5: 8-rank majority-allreduce at 64 KiB, 1 MiB, 16 MiB, 256 MiB and 1 GiB buckets
+    es = 4 if dtype == "fp32" else 2
+    counts = [(1 << lg) // es for lg in (16, 20, 24, 28, 30)]
+    _all_ok(run("gpu_config", 8, kind=MAJORITY, counts=counts, dtype_name=dtype, rounds=2,
+                timeout=600))
+
+
+# ---- partial semantics with a straggler ---------------------------
+
+def _check_straggler(outs, world, kind, async_=3, seed=6545343):
+    acts = ffref.activators(seed, world, 64)
+    for r, o in enumerate(outs):
+        assert o["delay_s"] >= 2 * o["T_s"], o
+        for t, c, uniform in o["rounds"]:
+            assert uniform, (r, t)
+            if kind == MAJORITY:
+                want = world if acts[t - 1] == world - 1 else world - 1
+            else:
+                want = world if t % (async_ + 1) == 0 else world - 1
+            assert c == want, (r, t, c, want, acts[t - 1])
+        if kind == MAJORITY:   # the activator of every asynchronous round: libc rand_r
+            for e in o["log"]:
+                assert e["activator"] == acts[e["round"] - 1], e
+
+
+@pytest.mark.parametrize("world,count,rounds", [(4, 1 << 20, 12), (8, 25559081, 8)])
+@pytest.mark.timeout(900)
+def test_majority_straggler_excluded(world, count, rounds):
+    # the last rank is >= 2 T late every round: rounds another rank activates take P - 1
+    # fresh gradients, rounds the straggler activates wait for it and take P
+    outs = run("gpu_straggler", world, kind=MAJORITY, count=count, rounds=rounds, timeout=420)
+    _check_straggler(outs, world, MAJORITY)
+
+
+def test_solo_straggler_excluded():
+    # solo, async 3: asynchronous rounds take P - 1, every 4th (synchronous) round P
+    outs = run("gpu_straggler", 4, kind=SOLO, count=1 << 20, rounds=9, async_=3)
+    _check_straggler(outs, 4, SOLO)
+
+
+# ---- the RCCL transport between ranks on different GPUs ------------------------------
+
+def _devices():
+    import esgd
+    return esgd.device_count()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.timeout(900)
+def test_rccl_transport_multi_gpu(world):
+    # grouped ncclSend/ncclRecv over xGMI + the tree kernel on a side stream; RCCL
+    # refuses two ranks on one GPU, so this runs only where the box has `world` GPUs
+    if _devices() < world:
+        pytest.skip(f"needs {world} GPUs (RCCL refuses ranks sharing a GPU)")
+    for kind in (ALLREDUCE, SOLO, MAJORITY):
+        verdicts = run("gpu_allreduce", world, count=1000003, rounds=2, kind=kind, transport="rccl")
+        assert all(all(v) for v in verdicts), (kind, verdicts)
+    _all_ok(run("gpu_config", world, kind=SOLO, counts=[64 << 20], rounds=2, transport="rccl", timeout=420))
