@@ -79,22 +79,12 @@ static uint64_t small_round_bytes() {
     return v;
 }
 
-// ---- IPC mapping cache: one hipIpcOpenMemHandle per (peer, allocation) ----
-// A mapping is closed when the last schedule using it is deleted -- before the
-// collective delete returns, so before the exporter can free the bucket.  Keeping
-// mappings open instead (ESGD_IPC_KEEP_OPEN=1) avoids a measured slowdown -- once a
-// process has closed an IPC mapping, every later kernel reading peer memory through IPC
-// paid +20..80 us on MI355X (tools/lat.sh: a 64 KiB round 41 -> 138-200 us) -- but an
-// exporter then frees memory its peers still map, and later peer-reading kernels were
-// seen to fault (bench C5 bf16 sweep after the C4 legs).  Persistent schedules (the
-// reference never deletes its schedules) never close anything.
-// Handle bytes are not unique over time: a new allocation can export exactly the bytes of
-// a freed one (tests/test_dataplane_gpu.py::test_schedule_and_bucket_churn).  The EXPORTER
-// therefore never publishes a handle it published before unless that publication is still
-// live (same allocation, e.g. two buckets carved from one chunk); a handle that repeats
-// after its release is a collision, and the bucket is shadowed by a fresh library-owned
-// bucket instead (checked the same way).  So no importer ever re-opens handle bytes it
-// closed, nor reuses a mapping for a different allocation.
+// ---- IPC mapping cache: one hipIpcOpenMemHandle per (peer, arena chunk) ----
+// Every exported bucket lives in an arena chunk that is never freed while the process
+// runs (arena.cpp), so handle bytes never repeat and a mapping, once open, stays valid:
+// mappings are kept until the data plane shuts down, whatever schedules come and go.
+// (Closing mappings and letting exporters free and re-export the memory was the source
+// of round 1's illegal accesses and of wrong sums at 8 ranks; arena.cpp.)
 struct IpcKey {
     int peer;
     uint8_t h[64];
@@ -103,9 +93,8 @@ struct IpcKey {
         return std::memcmp(h, o.h, 64) < 0;
     }
 };
-struct IpcEntry { void *base; int refs; };
 static std::mutex g_ipc_mu;
-static std::map<IpcKey, IpcEntry> g_ipc;
+static std::map<IpcKey, void *> g_ipc;
 
 static int ipc_open(int peer, const uint8_t *h, void **base) {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
@@ -114,74 +103,23 @@ static int ipc_open(int peer, const uint8_t *h, void **base) {
     std::memcpy(k.h, h, 64);
     auto it = g_ipc.find(k);
     if (it != g_ipc.end()) {
-        ++it->second.refs;
-        *base = it->second.base;
+        *base = it->second;
         return ESGD_SUCCESS;
     }
     hipIpcMemHandle_t hh;
     std::memcpy(&hh, h, sizeof(hh));
     void *p = nullptr;
     ESGD_HIP(hipIpcOpenMemHandle(&p, hh, hipIpcMemLazyEnablePeerAccess));
-    if (getenv("ESGD_DEBUG") && *getenv("ESGD_DEBUG") == '1') {
-        void *b = nullptr;
-        size_t sz = 0;
-        (void)hipMemGetAddressRange(&b, &sz, p);
-        uint64_t hsh = 1469598103934665603ull;
-        for (int i = 0; i < 64; ++i) hsh = (hsh ^ h[i]) * 1099511628211ull;
-        fprintf(stderr, "[esgd] ipc_open peer %d handle %016llx -> %p (range %p + %zu)\n", peer,
-                (unsigned long long)hsh, p, b, sz);
-    }
-    g_ipc[k] = {p, 1};
+    g_ipc[k] = p;
     *base = p;
     return ESGD_SUCCESS;
 }
 
-static void ipc_close(void *base) {
-    static const bool keep = getenv("ESGD_IPC_KEEP_OPEN") && *getenv("ESGD_IPC_KEEP_OPEN") == '1';
-    std::lock_guard<std::mutex> lk(g_ipc_mu);
-    for (auto it = g_ipc.begin(); it != g_ipc.end(); ++it) {
-        if (it->second.base == base) {
-            if (--it->second.refs == 0 && !keep) {
-                (void)hipIpcCloseMemHandle(base);
-                g_ipc.erase(it);
-            }
-            return;
-        }
-    }
-}
-
-// Exporter side: every handle this process has published -> schedules publishing it now.
-struct HandleKey {
-    uint8_t h[64];
-    bool operator<(const HandleKey &o) const { return std::memcmp(h, o.h, 64) < 0; }
-};
-static std::map<HandleKey, int> g_published;
-constexpr int kCollide = 1;   // publish(): the handle repeats a released publication
-
-static int claim_handle(const uint8_t *h) {
-    std::lock_guard<std::mutex> lk(g_ipc_mu);
-    HandleKey k;
-    std::memcpy(k.h, h, 64);
-    auto it = g_published.find(k);
-    if (it != g_published.end() && it->second <= 0) return kCollide;
-    ++g_published[k];
-    return ESGD_SUCCESS;
-}
-
-static void release_handle(const uint8_t *h) {
-    std::lock_guard<std::mutex> lk(g_ipc_mu);
-    HandleKey k;
-    std::memcpy(k.h, h, 64);
-    auto it = g_published.find(k);
-    if (it != g_published.end()) --it->second;   // stays known: a repeat is a collision
-}
-
-// every cached mapping, at data-plane shutdown (after the last round has drained)
+// every mapping, at data-plane shutdown (after the last round has drained)
 static void ipc_close_all() {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
-    for (auto &kv : g_ipc) (void)hipIpcCloseMemHandle(kv.second.base);
+    for (auto &kv : g_ipc) (void)hipIpcCloseMemHandle(kv.second);
     g_ipc.clear();
-    g_published.clear();
 }
 
 // ---- process-wide data-plane resources -----------------------------------------------
@@ -309,6 +247,7 @@ void dataplane_shutdown() {
         if (*c) { (void)hipStreamSynchronize(*c); (void)hipStreamDestroy(*c); *c = nullptr; }
     if (g_ctr_pool) { (void)hipFree(g_ctr_pool); g_ctr_pool = nullptr; }
     ipc_close_all();
+    arena_trim();
     if (g_seg_reg) { (void)hipHostUnregister(g_seg_reg); g_seg_reg = nullptr; g_seg_dev = nullptr; }
 }
 
@@ -343,8 +282,6 @@ struct BaseState {
 };
 
 struct IpcState : BaseState {
-    uint8_t pub_h[64] = {};           // handle this rank publishes (claim_handle)
-    bool pub_live = false;
     uint32_t *ctr = nullptr;          // device: k_round_small's counters and gates (pool)
     std::vector<hipEvent_t> cev;      // chunked host rounds: per chunk H2D / reduced / D2H
     bool chunked_before = false;
@@ -369,14 +306,15 @@ static void layout(Sched &s, BaseState &st) {
     }
 }
 
-// Buckets the library owns: whole 2 MiB pages of their own, so the allocation is an
-// exportable one (small hipMallocs can be carved out of a larger cached block).
+// Buckets the library owns come from the IPC arena (exportable, never freed under a peer).
 static int alloc_bucket(size_t bytes, char **out, size_t *cap) {
-    const size_t gran = size_t(2) << 20;
-    const size_t c = (std::max<size_t>(bytes, 1) + gran - 1) / gran * gran;
-    ESGD_HIP(hipMalloc(reinterpret_cast<void **>(out), c));
-    *cap = c;
+    if (int rc = arena_alloc(std::max<size_t>(bytes, 1), reinterpret_cast<void **>(out))) return rc;
+    *cap = std::max<size_t>(bytes, 1);
     return ESGD_SUCCESS;
+}
+
+static void free_bucket(char *p) {
+    if (p && !arena_free(p)) (void)hipFree(p);
 }
 
 static int base_setup(Sched &s, BaseState &st) {
@@ -449,8 +387,7 @@ static int base_refit(Sched &s, BaseState &st) {
     int moved = 0;
     if (bytes > st.cap) {
         if (!st.owns_rb) { set_error("schedule %d: device bucket cannot grow", s.id); return ESGD_INVALID_ARG; }
-        // grow geometrically; the old bucket stays allocated (peers may still have it
-        // mapped: freeing exported memory under an importer breaks later IPC opens)
+        // grow geometrically; the old bucket goes back to the arena at teardown
         st.retired.push_back(st.rb_dev);
         if (int rc = alloc_bucket(std::max(bytes, 2 * st.cap), &st.rb_dev, &st.cap)) return rc;
         moved = 1;
@@ -599,14 +536,14 @@ static int base_query(Sched &s, BaseState &st) {
 
 static void base_teardown(Sched &s, BaseState &st) {
     if (st.stream) (void)hipStreamSynchronize(st.stream);
-    if (st.owns_rb) (void)hipFree(st.rb_dev);
+    if (st.owns_rb) free_bucket(st.rb_dev);
     if (st.reg_rb) (void)hipHostUnregister(s.rb);
     if (st.reg_sb) (void)hipHostUnregister(s.sb);
     for (auto &kv : st.producer) (void)hipEventDestroy(kv.second);
     for (hipEvent_t e : st.spare) (void)hipEventDestroy(e);
     if (st.consumer) (void)hipEventDestroy(st.consumer);
     if (st.pin) (void)hipHostFree(st.pin);
-    for (char *p : st.retired) (void)hipFree(p);
+    for (char *p : st.retired) free_bucket(p);
     if (st.ev) (void)hipEventDestroy(st.ev);
 }
 
@@ -620,50 +557,23 @@ struct IpcTransport final : Transport {
         s.sh->slot[s.rank].bytes = s.count * s.esize;
     }
 
-    // Returns kCollide (nothing published) when the handle repeats a released one.
+    // Publish rb_dev (arena memory: the chunk's handle + the offset); ESGD_INVALID_ARG
+    // when rb_dev is foreign memory, which is never exported.
     static int publish(Sched &s, IpcState &st) {
         void *base = nullptr;
-        size_t size = 0;
-        ESGD_HIP(hipMemGetAddressRange(&base, &size, st.rb_dev));
-        hipIpcMemHandle_t h;
-        ESGD_HIP(hipIpcGetMemHandle(&h, base));
+        uint64_t off = 0;
         uint8_t hb[64];
-        std::memcpy(hb, &h, 64);
-        if (getenv("ESGD_DEBUG") && *getenv("ESGD_DEBUG") == '1') {
-            uint64_t hsh = 1469598103934665603ull;
-            for (int i = 0; i < 64; ++i) hsh = (hsh ^ hb[i]) * 1099511628211ull;
-            fprintf(stderr, "[esgd] r%d publish sched %d rb %p base %p size %zu handle %016llx\n", s.rank, s.id,
-                    (void *)st.rb_dev, base, size, (unsigned long long)hsh);
-        }
-        if (int rc = claim_handle(hb)) return rc;
-        if (st.pub_live) release_handle(st.pub_h);
-        std::memcpy(st.pub_h, hb, 64);
-        st.pub_live = true;
+        if (int rc = arena_export(st.rb_dev, s.count * s.esize, &base, &off, hb)) return rc;
         IpcSlot &mine = s.sh->slot[s.rank];
         std::memcpy(mine.handle, hb, 64);
-        mine.offset = uint64_t(st.rb_dev - static_cast<char *>(base));
+        mine.offset = off;
         mine.bytes = s.count * s.esize;
         mine.gen.store(s.gen, std::memory_order_release);
         mine.ver.fetch_add(1, std::memory_order_acq_rel);
         st.peer[s.rank] = st.rb_dev;
+        ESGD_TRACE("r%d publish sched %d rb %p chunk %p + %llu\n", s.rank, s.id, (void *)st.rb_dev, base,
+                   (unsigned long long)off);
         return ESGD_SUCCESS;
-    }
-
-    // publish a library-owned bucket; on a collision allocate another (the colliding one
-    // stays allocated, retired, so its handle cannot come straight back)
-    static int publish_owned(Sched &s, IpcState &st) {
-        int rc = publish(s, st);
-        for (int tries = 0; rc == kCollide && tries < 8; ++tries) {
-            st.retired.push_back(st.rb_dev);
-            if (int e = alloc_bucket(std::max<size_t>(s.count * s.esize, 1), &st.rb_dev, &st.cap)) return e;
-            st.peer[s.rank] = st.rb_dev;
-            rc = publish(s, st);
-        }
-        if (rc == kCollide) {
-            set_error("schedule %d: no exportable bucket with a fresh IPC handle", s.id);
-            return ESGD_ERROR;
-        }
-        return rc;
     }
 
     // (re)map every peer whose publication changed since we last mapped it
@@ -683,13 +593,11 @@ struct IpcTransport final : Transport {
                 return ESGD_INVALID_ARG;
             }
             if (st.peer_base[q] && v == st.peer_ver[q]) continue;   // nothing moved
-            // HIP sub-allocates small buffers from shared chunks: a moved bucket can keep
-            // its chunk (same handle, new offset) -- keep that mapping, never close and
-            // re-open the same handle
+            // a moved bucket may sit in the same arena chunk (same handle, new offset);
+            // mappings are cached per (peer, chunk) and never closed before shutdown
             if (!(st.peer_base[q] && std::memcmp(st.peer_handle[q], ps.handle, 64) == 0)) {
                 void *pb = nullptr;
-                if (int rc = ipc_open(q, ps.handle, &pb)) return rc;   // open new first
-                if (st.peer_base[q]) ipc_close(st.peer_base[q]);
+                if (int rc = ipc_open(q, ps.handle, &pb)) return rc;
                 st.peer_base[q] = pb;
                 std::memcpy(st.peer_handle[q], ps.handle, 64);
             }
@@ -710,18 +618,17 @@ struct IpcTransport final : Transport {
         // ESGD_SHADOW=1 shadows every device bucket (caller buckets that are freed and
         // re-allocated between rounds; also how the tests reach the fallback)
         static const bool force_shadow = getenv("ESGD_SHADOW") && *getenv("ESGD_SHADOW") == '1';
-        if (s.host_mode) return publish_owned(s, *st);
-        int rc = force_shadow ? kCollide : publish(s, *st);
-        if (rc) {
-            // the caller's bucket cannot be exported (carved from a cached allocation), or
-            // its handle repeats a released one: reduce through an owned shadow bucket
-            ESGD_TRACE("r%d sched %d: bucket %p not exported (%s), shadowing it\n", s.rank, s.id,
-                       (void *)st->rb_dev, rc == kCollide ? "handle collision" : esgd_last_error());
-            (void)hipGetLastError();
+        if (s.host_mode) return publish(s, *st);
+        int rc = force_shadow ? ESGD_INVALID_ARG : publish(s, *st);
+        if (rc == ESGD_INVALID_ARG) {
+            // foreign device memory (torch tensors, plain hipMalloc) is never exported:
+            // reduce through an arena bucket, copied in at the snapshot, out at the finish
+            ESGD_TRACE("r%d sched %d: bucket %p is not arena memory, shadowing it\n", s.rank, s.id,
+                       (void *)st->rb_dev);
             if ((rc = alloc_bucket(s.count * s.esize, &st->rb_dev, &st->cap))) return rc;
             st->owns_rb = st->shadow = true;
             st->peer[s.rank] = st->rb_dev;
-            rc = publish_owned(s, *st);
+            rc = publish(s, *st);
         }
         return rc;
     }
@@ -743,7 +650,7 @@ struct IpcTransport final : Transport {
         const int moved = base_refit(s, st);
         if (moved < 0) return moved;
         if (s.world > 1 && moved)
-            if (int rc = publish_owned(s, st)) return rc;
+            if (int rc = publish(s, st)) return rc;
         if (s.world > 1 && s.resolve) publish_size(s);
         st.peer[s.rank] = st.rb_dev;
         ESGD_TRACE("r%d sched %d round %u join count=%llu rb_dev=%p moved=%d staged=%d\n", s.rank, s.id,
@@ -937,9 +844,6 @@ struct IpcTransport final : Transport {
         if (!st) return;
         if (st->stream) (void)hipStreamSynchronize(st->stream);
         for (hipEvent_t e : st->cev) (void)hipEventDestroy(e);
-        for (int q = 0; q < kMaxRanks; ++q)
-            if (st->peer_base[q]) ipc_close(st->peer_base[q]);
-        if (st->pub_live) release_handle(st->pub_h);
         base_teardown(s, *st);
         delete st;
         s.tstate = nullptr;

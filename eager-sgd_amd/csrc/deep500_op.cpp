@@ -88,8 +88,9 @@ struct AllreduceOp {
         device = dev;
         const size_t nbytes = size_t(len) * sizeof(float);
         if (dev) {
-            if (hipMalloc(reinterpret_cast<void **>(&sb), nbytes ? nbytes : 256) != hipSuccess ||
-                hipMalloc(reinterpret_cast<void **>(&rb), nbytes ? nbytes : 256) != hipSuccess ||
+            // arena buckets: exported to the peers as they are (no shadow copies)
+            if (esgd::arena_alloc(nbytes ? nbytes : 256, reinterpret_cast<void **>(&sb)) ||
+                esgd::arena_alloc(nbytes ? nbytes : 256, reinterpret_cast<void **>(&rb)) ||
                 hipMemset(sb, 0, nbytes) != hipSuccess || hipMemset(rb, 0, nbytes) != hipSuccess) {
                 esgd::set_error("device bucket allocation of %zu bytes", nbytes);
                 die("allreducef_forward_cuda");

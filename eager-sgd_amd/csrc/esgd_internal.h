@@ -26,6 +26,12 @@ int require_device();
 
 inline hipStream_t as_stream(void *s) { return s ? static_cast<hipStream_t>(s) : default_stream(); }
 
+// Device memory that peers may map (arena.cpp): never given back while it may be mapped.
+int arena_alloc(size_t bytes, void **out);
+bool arena_free(void *p);
+int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_t handle[64]);
+void arena_trim();
+
 }  // namespace esgd
 
 #define ESGD_HIP(call)                                                          \

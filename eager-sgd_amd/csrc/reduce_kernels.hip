@@ -237,7 +237,7 @@ struct GatherSet {
     uint32_t tail[kMaxSeg];   // bytes after the last full 16-B vector
 };
 
-template <int U>
+template <int U, int LAUX = 19>
 __global__ __launch_bounds__(256) void k_gather(GatherSet g) {
     constexpr int B = 256;
     const int seg = blockIdx.y;
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void k_gather(GatherSet g) {
             raw16 r[U];
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                r[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (i + u * B) * 16, 0, 19);
+                r[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (i + u * B) * 16, 0, LAUX);
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 __builtin_amdgcn_raw_buffer_store_b128(r[u], ws, (i + u * B) * 16, 0, 16);
@@ -358,6 +358,16 @@ __global__ void k_fill_uniform_bf16(uint64_t base, uint16_t *out, uint64_t n) {
 }
 
 // ---- launch configuration ----
+// ESGD_REMOTE_POLICY (experiment): load aux of the peer-reading kernels (default 19 =
+// sc0 sc1 nt; 2 = nt; 3 = sc0 nt)
+static int remote_policy() {
+    static const int v = [] {
+        const char *e = getenv("ESGD_REMOTE_POLICY");
+        return (e && *e) ? atoi(e) : 19;
+    }();
+    return v;
+}
+
 static int g_unroll = 0;   // 0 -> default (4 x 16 B per input per lane)
 static int g_grid = 0;     // 0 -> auto: 8 blocks of 256 per CU, grid-stride
 static int g_nt = -1;      // flat path only: -1/1 -> nt loads/stores
@@ -440,6 +450,8 @@ static int dispatch_u(const InputSet &in, void *out, uint64_t count, float scale
             set_error("remote reduce: shard must be 16-B aligned and < 2 GiB");
             return ESGD_INVALID_ARG;
         }
+        if (remote_policy() == 2) return launch_buf<Tr, K, UD, 2, 16, SCALE>(in, out, count, scale, s);
+        if (remote_policy() == 3) return launch_buf<Tr, K, UD, 3, 16, SCALE>(in, out, count, scale, s);
         return launch_buf<Tr, K, UD, 19, 16, SCALE>(in, out, count, scale, s);
     }
     if (!aligned) return launch_scalar<Tr, K, SCALE>(in, out, count, scale, s);
@@ -626,7 +638,9 @@ int gather_remote(int n, const void *const *src, void *const *dst, const uint64_
     unsigned gx = grid_for(256 * 4, maxvec ? maxvec : 1, 8);
     unsigned per_seg = std::max(1u, (unsigned(cu_count()) * 4 + n - 1) / unsigned(n));
     if (gx > per_seg) gx = per_seg;
-    hipLaunchKernelGGL(k_gather<4>, dim3(gx, n), dim3(256), 0, s, g);
+    if (remote_policy() == 2) hipLaunchKernelGGL((k_gather<4, 2>), dim3(gx, n), dim3(256), 0, s, g);
+    else if (remote_policy() == 3) hipLaunchKernelGGL((k_gather<4, 3>), dim3(gx, n), dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((k_gather<4, 19>), dim3(gx, n), dim3(256), 0, s, g);
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;
 }

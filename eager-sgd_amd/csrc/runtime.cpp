@@ -101,15 +101,16 @@ int esgd_device_arch(int dev, char *name, size_t len) {
     return ESGD_SUCCESS;
 }
 
+// Buckets come from the IPC arena (arena.cpp): a freed bucket is recycled in this
+// process, never handed back to the driver while peers may map it.
 int esgd_malloc(void **ptr, size_t bytes) {
     ESGD_ARG(ptr, "esgd_malloc: null pointer");
-    if (int rc = require_device()) return rc;
-    ESGD_HIP(hipMalloc(ptr, bytes ? bytes : 256));
-    return ESGD_SUCCESS;
+    return arena_alloc(bytes ? bytes : 256, ptr);
 }
 
 int esgd_free(void *ptr) {
     if (!ptr) return ESGD_SUCCESS;
+    if (arena_free(ptr)) return ESGD_SUCCESS;
     ESGD_HIP(hipFree(ptr));
     return ESGD_SUCCESS;
 }

@@ -520,7 +520,8 @@ def _download_slice(buf, start, n):
 
 
 def gpu_config(rank, world, kind, counts, dtype_name="fp32", rounds=2, async_=32, seed=6545343,
-               check=65536, transport="ipc", keep=False, detail=False, free=True, env=None):
+               check=65536, transport="ipc", keep=False, detail=False, free=True, env=None,
+               alloc_ahead=False):
     """A BASELINE.json workload: one in-place bucket per rank per size in `counts`, every
     rank's bucket written BEFORE a barrier and then posted (the pattern of
     evaluation/{solo,rand}_allreduce_correctness.c:76-97: whichever rank activates, every
@@ -537,10 +538,12 @@ def gpu_config(rank, world, kind, counts, dtype_name="fp32", rounds=2, async_=32
     comm.set_transport(transport)
     dt = _lib.FLOAT if dtype_name == "fp32" else _lib.BF16
     out, kept = [], []
+    nxt = None
     for i, count in enumerate(counts):
-        rb = dev.DeviceBuffer(count, dt)
+        rb = nxt if nxt is not None else dev.DeviceBuffer(count, dt)
+        nxt = None
         s = comm.Schedule(kind, None, rb, count, dtype=dt, async_=async_, seed=seed, buf=comm.BUF_DEVICE)
-        for t in range(rounds):
+        for t in range(rounds[i] if isinstance(rounds, (list, tuple)) else rounds):
             sd = SEED + 7919 * i + t
             dev.fill_uniform(rb, sd, rank)
             dev.synchronize()
@@ -570,6 +573,8 @@ def gpu_config(rank, world, kind, counts, dtype_name="fp32", rounds=2, async_=32
             kept.append((s, rb))
         else:
             s.delete()
+            if alloc_ahead and i + 1 < len(counts):
+                nxt = dev.DeviceBuffer(counts[i + 1], dt)
             if free:
                 rb.close()
             else:

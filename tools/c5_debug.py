@@ -1,4 +1,4 @@
-"""Scratch: reproduce the C5 mismatch after schedule churn with details."""
+"""Scratch: the C5 churn pattern (buckets freed and re-allocated between schedules)."""
 import os
 import sys
 
@@ -9,5 +9,11 @@ MAJ = 2
 
 if __name__ == "__main__":
     sizes = [(1 << lg) // 4 for lg in (24, 28)]
-    outs = run("gpu_config", 8, kind=MAJ, counts=sizes, rounds=1, timeout=300, detail=True)
-    print("free", "->", [[v[3] for v in per] for per in outs], flush=True)
+    for name, kw in [("base", {}), ("norounds_first", {"rounds": [0, 2]}),
+                     ("p4_norounds", {"rounds": [0, 2], "world": 4}),
+                     ("torch_like_shadow", {"env": {"ESGD_SHADOW": "1"}})]:
+        kw.setdefault("counts", sizes)
+        kw.setdefault("rounds", 2)
+        world = kw.pop("world", 8)
+        outs = run("gpu_config", world, kind=MAJ, timeout=300, **kw)
+        print(name, "->", [[v[3] for v in per] for per in outs], flush=True)

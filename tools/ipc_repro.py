@@ -13,11 +13,19 @@ class Handle(C.Structure):
     _fields_ = [("reserved", C.c_char * 64)]
 
 
-def worker(rank, world, sizes, free=True, kernel=False):
+def worker(rank, world, sizes, free=True, kernel=False, read_first=True, hostreg=False, engine=False):
     import torch.distributed as dist
     import esgd
     from esgd import device as dev
     hip = C.CDLL("libamdhip64.so")
+    hip.hipSetDevice(0)
+    if engine:   # the esgd node communicator: registered segment + progress thread
+        from esgd import comm
+        comm.init()
+        s0 = comm.Schedule(0, None, dev.DeviceBuffer(4096), 4096, buf=comm.BUF_DEVICE)
+    if hostreg:
+        hb = (C.c_char * (1 << 20))()
+        assert hip.hipHostRegister(hb, C.c_size_t(1 << 20), 2) == 0
     loc = dev.DeviceBuffer(max(sizes) // 4)
     vp = C.c_void_p
     hip.hipSetDevice(0)
@@ -45,6 +53,8 @@ def worker(rank, world, sizes, free=True, kernel=False):
             assert rc == 0, rc
             maps.append(m)
             want = (q * 16 + si + 1) & 0xFF
+            if si == 0 and not read_first:
+                continue
             for off in (0, size // 2, size - 4096):
                 buf = (C.c_uint8 * 4096)()
                 if kernel:   # the whole peer buffer read through the mapping by the tree kernel
@@ -74,12 +84,14 @@ mp_workers.ipc_worker = worker
 
 if __name__ == "__main__":
     MiB = 1 << 20
-    for world in (8,):
-        for free, kernel in ((True, True), (False, True)):
-            res = mp_workers.run("ipc_worker", world, sizes=[16 * MiB, 256 * MiB, 16 * MiB, 1024 * MiB], free=free,
-                                 kernel=kernel, timeout=300)
+    for name, kw in [("noread", dict(read_first=False)), ("hostreg", dict(read_first=False, hostreg=True)),
+                     ("engine", dict(read_first=False, engine=True))]:
+        if True:
+            world = 8
+            res = mp_workers.run("ipc_worker", world, sizes=[16 * MiB, 256 * MiB], free=True, kernel=True,
+                                 timeout=300, **kw)
             nbad = [[len(b) for _, b in per] for per in res]
-            print(f"world {world} free {free} kernel {kernel}: mismatches per size {nbad}", flush=True)
+            print(f"world {world} {name}: mismatches per size {nbad}", flush=True)
             for r, per in enumerate(res):
                 for size, b in per:
                     if b:
