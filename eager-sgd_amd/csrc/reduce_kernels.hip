@@ -207,6 +207,74 @@ __global__ __launch_bounds__(B) void k_tree_sum_buf(InputSet in, void *out, uint
     }
 }
 
+// LDS-DMA body (experiment, tuning policies 17-20): every wave streams chunks of 64
+// 16-B columns; the K inputs of a chunk arrive by `buffer_load_dwordx4 ... lds` straight
+// into the wave's own LDS ring (no VGPR destination), NB - 1 chunks ahead, and are folded
+// from LDS.  Each wave only reads what it loaded itself, so a counted vmcnt is the only
+// synchronisation (loads retire in order; a store in between only makes the wait stricter).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    // gfx9 encoding: vmcnt[3:0] | expcnt[6:4] = 7 | lgkmcnt[11:8] = 15 | vmcnt[5:4] << 14
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// K LDS-DMA loads of this lane's 16-B column `col` into the wave's ring stage (past the
+// end of a bucket the descriptor's range check loads zeros)
+typedef __attribute__((address_space(3))) char lds_char;
+
+template <int K, int LAUX>
+__device__ __forceinline__ void lds_issue(__amdgpu_buffer_rsrc_t (&rs)[K], lds_char *stage, uint32_t col) {
+#if defined(__HIP_DEVICE_COMPILE__)   // the LDS-DMA builtin exists for the device target only
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs[j], (__attribute__((address_space(3))) void *)(stage + j * 1024),
+                                                 16, col * 16, 0, 0, LAUX);
+#endif
+}
+
+template <class Tr, int K, int W, int NB, int LAUX, bool SCALE>
+__global__ __launch_bounds__(W * 64) void k_tree_sum_lds(InputSet in, void *out, uint32_t nvec, uint64_t count,
+                                                         float scale) {
+    __shared__ raw16 ring[W][NB][K][64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int bytes = int(nvec * 16u);
+    __amdgpu_buffer_rsrc_t rs[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(in.p[j]), (short)0, bytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, bytes, 0x00020000);
+    const uint32_t nchunk = (nvec + 63) / 64;
+    const uint32_t c0 = blockIdx.x * W + w, step = gridDim.x * W;
+    // the wave's ring in LDS address space (stage st at byte st * K * 1 KiB)
+    lds_char *mine = (lds_char *)(&ring[w][0][0][0]);
+#pragma unroll
+    for (int p = 0; p < NB - 1; ++p) lds_issue<K, LAUX>(rs, mine + p * K * 1024, (c0 + p * step) * 64 + lane);
+    int st = 0;
+    for (uint32_t c = c0; c < nchunk; c += step) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the stage refilled next was read
+        lds_issue<K, LAUX>(rs, mine + ((st + NB - 1) % NB) * K * 1024, (c + (NB - 1) * step) * 64 + lane);
+        wait_vmcnt<K * (NB - 1)>();                            // chunk c has landed
+        raw16 r[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) r[j] = ring[w][st][j][lane];
+        __builtin_amdgcn_raw_buffer_store_b128(fold16<Tr, K, SCALE>(r, scale), ws, (c * 64 + lane) * 16, 0, 16);
+        st = (st + 1) % NB;
+    }
+    using T = typename Tr::T;
+    using A = typename Tr::A;
+    const uint64_t tail0 = uint64_t(nvec) * Tr::E;
+    if (blockIdx.x == 0 && tail0 + threadIdx.x < count) {
+        const uint64_t e = tail0 + threadIdx.x;
+        A v[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) v[j] = Tr::load(static_cast<const T *>(in.p[j])[e]);
+        tree_fold<Tr, K>(v);
+        if constexpr (SCALE) v[0] = v[0] * scale;
+        static_cast<T *>(out)[e] = Tr::store(v[0]);
+    }
+}
+
 // Fallback for pointers that are not 16-B aligned: one element per lane.
 template <class Tr, int K, bool SCALE>
 __global__ __launch_bounds__(256) void k_tree_sum_scalar(InputSet in, void *out, uint64_t count,
@@ -426,6 +494,17 @@ static int launch_buf(const InputSet &in, void *out, uint64_t count, float scale
     return ESGD_SUCCESS;
 }
 
+template <class Tr, int K, int W, int NB, int LA, bool SCALE>
+static int launch_lds(const InputSet &in, void *out, uint64_t count, float scale, hipStream_t s) {
+    const uint64_t nvec = count / Tr::E;
+    static const int per_cu = resident_blocks(k_tree_sum_lds<Tr, K, W, NB, LA, SCALE>, W * 64);
+    unsigned grid = grid_for(uint64_t(W) * 64, (nvec + 63) / 64 * 64 ? (nvec + 63) / 64 * 64 : 1, per_cu);
+    hipLaunchKernelGGL((k_tree_sum_lds<Tr, K, W, NB, LA, SCALE>), dim3(grid), dim3(W * 64), 0, s, in, out,
+                       uint32_t(nvec), count, scale);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
 // alternative {load aux, store aux} pairs kept for sweeps (tools/sweep_reduce.py)
 #define ESGD_POLICIES(X) X(1, 2, 16) X(2, 2, 17) X(3, 2, 18) X(4, 2, 19) X(5, 0, 16) X(6, 3, 16) X(7, 18, 16) X(8, 16, 16)
 
@@ -472,6 +551,11 @@ static int dispatch_u(const InputSet &in, void *out, uint64_t count, float scale
             case 14: return launch_buf<Tr, K, 4, 2, 2, SCALE>(in, out, count, scale, s);
             case 15: return launch_buf<Tr, K, 4, 2, 0, SCALE>(in, out, count, scale, s);
             case 16: return launch_buf<Tr, K, 4, 2, 3, SCALE>(in, out, count, scale, s);
+            // LDS-DMA ring variants: (waves per block, ring depth)
+            case 17: return launch_lds<Tr, K, 4, 2, 2, SCALE>(in, out, count, scale, s);
+            case 18: return launch_lds<Tr, K, 2, 4, 2, SCALE>(in, out, count, scale, s);
+            case 19: return launch_lds<Tr, K, 1, 8, 2, SCALE>(in, out, count, scale, s);
+            case 20: return launch_lds<Tr, K, 2, 3, 2, SCALE>(in, out, count, scale, s);
             default: break;
             }
         }
@@ -1023,7 +1107,7 @@ int esgd_set_tuning(const char *key, int value) {
     } else if (!std::strcmp(key, "nt")) {
         g_nt = value ? 1 : 0;
     } else if (!std::strcmp(key, "policy")) {
-        ESGD_ARG(value >= -1 && value <= 16, "policy must be -1..16");
+        ESGD_ARG(value >= -1 && value <= 20, "policy must be -1..20");
         g_policy = value;
     } else {
         set_error("esgd_set_tuning: unknown key '%s'", key);

@@ -54,6 +54,25 @@ variants = list(itertools.product([int(x) for x in a.unrolls.split(",")],
                                   [int(x) for x in a.nts.split(",")],
                                   [int(x) for x in a.grids.split(",")],
                                   [int(x) for x in a.policies.split(",")]))
+# every variant's output must be the production variant's, bit for bit
+import numpy as np  # noqa: E402
+dev.set_tuning("policy", -1); dev.set_tuning("unroll", 0); dev.set_tuning("grid", 0); dev.set_tuning("nt", 1)
+dev.reduce(dt, ptrs, out, count, stream=s)
+s.synchronize()
+ref = out.download() if not a.stagger else None
+bad = {}
+for v in variants:
+    u, nt, g, pol = v
+    dev.set_tuning("unroll", u); dev.set_tuning("nt", nt); dev.set_tuning("grid", g)
+    dev.set_tuning("policy", pol)
+    if ref is not None:
+        out.zero(stream=s)
+        dev.reduce(dt, ptrs, out, count, stream=s)
+        s.synchronize()
+        got = out.download()
+        nbad = int(np.count_nonzero(got.view(np.uint8) != ref.view(np.uint8)))
+        if nbad:
+            bad[v] = nbad
 ev = [dev.Event() for _ in range(2 * a.iters)]
 times = {v: [] for v in variants}
 for rnd in range(a.rounds):
@@ -73,7 +92,7 @@ algo = (a.k + 1) * count * es
 rows = []
 for v, t in times.items():
     med, mn = statistics.median(t), min(t)
-    rows.append({"unroll": v[0], "nt": v[1], "grid": v[2], "policy": v[3],
+    rows.append({"unroll": v[0], "nt": v[1], "grid": v[2], "policy": v[3], "bad_bytes": bad.get(v, 0),
                  "median_us": round(med * 1e3, 2),
                  "min_us": round(mn * 1e3, 2), "median_GBs": round(algo / (med * 1e-3) / 1e9, 1),
                  "frac_of_8TBs": round(algo / (med * 1e-3) / 8e12, 4)})
