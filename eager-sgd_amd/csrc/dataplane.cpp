@@ -38,17 +38,8 @@ int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64
 int gather_remote(int n, const void *const *src, void *const *dst, const uint64_t *bytes,
                   hipStream_t s);
 int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s);
-int cache_flush(hipStream_t s);
+int peer_acquire(hipStream_t s);
 
-// ESGD_FLUSH_L2 (experiment): 1 = flush every XCD's L2 before each round, 2 = after a
-// peer bucket is (re)mapped
-static int flush_mode() {
-    static const int v = [] {
-        const char *e = getenv("ESGD_FLUSH_L2");
-        return (e && *e) ? atoi(e) : 0;
-    }();
-    return v;
-}
 int round_small(int dtype, const void *const *src, void *out, uint64_t n, int nseg,
                 const void *const *gsrc, void *const *gdst, const uint64_t *gbytes,
                 uint32_t *ready, uint32_t *reduced, uint32_t *done, uint32_t *fin, uint32_t *err,
@@ -201,8 +192,11 @@ static int pair_ranks(Sched &s, std::atomic<uint32_t> *flags, int which, uint32_
     const long long ticks = (long long)(engine_timeout() * double(g_ticks_per_s));
     uint64_t *ts = gpu_trace_on() ? reinterpret_cast<uint64_t *>(dev_flag(&s.sh->gpu_ts[s.rank][2 * which]))
                                   : nullptr;
-    return round_sync(dev_flag(flags), s.rank, s.world, value ? value : round, ticks,
-                      dev_flag(&s.sh->gpu_err[s.rank]), round, ts, cs);
+    if (int rc = round_sync(dev_flag(flags), s.rank, s.world, value ? value : round, ticks,
+                            dev_flag(&s.sh->gpu_err[s.rank]), round, ts, cs))
+        return rc;
+    // the ready and reduced pairings are followed by a phase that reads peer buckets
+    return which < 2 ? peer_acquire(cs) : ESGD_SUCCESS;
 }
 
 // ns between the GPU stamps of the last round (ESGD_GPU_TRACE=1), for the timeline
@@ -285,7 +279,6 @@ struct IpcState : BaseState {
     uint32_t *ctr = nullptr;          // device: k_round_small's counters and gates (pool)
     std::vector<hipEvent_t> cev;      // chunked host rounds: per chunk H2D / reduced / D2H
     bool chunked_before = false;
-    bool need_flush = true;
     char *peer[kMaxRanks] = {};
     void *peer_base[kMaxRanks] = {};
     uint32_t peer_ver[kMaxRanks] = {};
@@ -667,10 +660,6 @@ struct IpcTransport final : Transport {
         IpcState &st = S(s);
         hipStream_t cs = st.stream;
         st.fin_mode = false;
-        if (flush_mode() == 1 || (flush_mode() == 2 && st.need_flush)) {
-            if (int rc = cache_flush(cs)) return rc;
-            st.need_flush = false;
-        }
         if (s.host_mode && !s.resolve && host_chunk_bytes() && s.count * s.esize >= 2 * host_chunk_bytes())
             return launch_chunked(s, st, round, fresh);
         if (int rc = base_copy_in(s, st, round, fresh, cs)) return rc;

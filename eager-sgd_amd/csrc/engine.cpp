@@ -284,15 +284,16 @@ int sched_post(Sched *s, void *producer_stream, int *role) {
         std::lock_guard<std::mutex> lk(s->mu);
         if (s->error) { set_error("%s", s->errmsg); return s->error; }
         const uint32_t t = s->posted.load() + 1;
-        if (s->resolve) {
-            // the round about to start must not be in flight with the old buffers
+        // FFCOLL_BUFFERS: the buffers of round t are resolved at its post -- unless a peer's
+        // activation already carried this rank into round t (re-resolved at that join,
+        // possibly still in flight: nothing to do).  A round not yet joined must not start
+        // while an earlier one is in flight with the old buffers.
+        if (s->resolve && s->joined < t) {
             if (s->stage != ST_IDLE) {
                 set_error("schedule %d: FFCOLL_BUFFERS rounds must not overlap", s->id);
                 return ESGD_INVALID_ARG;
             }
-            // a round a peer activated before this post was joined (and re-resolved) then
-            if (s->joined < t)
-                if (int rc = s->resolve(*s)) return rc;
+            if (int rc = s->resolve(*s)) return rc;
         }
         if (producer_stream)
             if (int rc = s->tp->note_producer(*s, t, producer_stream)) return rc;

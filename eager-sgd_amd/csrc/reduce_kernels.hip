@@ -305,7 +305,7 @@ struct GatherSet {
     uint32_t tail[kMaxSeg];   // bytes after the last full 16-B vector
 };
 
-template <int U, int LAUX = 19>
+template <int U>
 __global__ __launch_bounds__(256) void k_gather(GatherSet g) {
     constexpr int B = 256;
     const int seg = blockIdx.y;
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(256) void k_gather(GatherSet g) {
             raw16 r[U];
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                r[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (i + u * B) * 16, 0, LAUX);
+                r[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (i + u * B) * 16, 0, 19);
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 __builtin_amdgcn_raw_buffer_store_b128(r[u], ws, (i + u * B) * 16, 0, 16);
@@ -426,16 +426,6 @@ __global__ void k_fill_uniform_bf16(uint64_t base, uint16_t *out, uint64_t n) {
 }
 
 // ---- launch configuration ----
-// ESGD_REMOTE_POLICY (experiment): load aux of the peer-reading kernels (default 19 =
-// sc0 sc1 nt; 2 = nt; 3 = sc0 nt)
-static int remote_policy() {
-    static const int v = [] {
-        const char *e = getenv("ESGD_REMOTE_POLICY");
-        return (e && *e) ? atoi(e) : 19;
-    }();
-    return v;
-}
-
 static int g_unroll = 0;   // 0 -> default (4 x 16 B per input per lane)
 static int g_grid = 0;     // 0 -> auto: 8 blocks of 256 per CU, grid-stride
 static int g_nt = -1;      // flat path only: -1/1 -> nt loads/stores
@@ -529,8 +519,6 @@ static int dispatch_u(const InputSet &in, void *out, uint64_t count, float scale
             set_error("remote reduce: shard must be 16-B aligned and < 2 GiB");
             return ESGD_INVALID_ARG;
         }
-        if (remote_policy() == 2) return launch_buf<Tr, K, UD, 2, 16, SCALE>(in, out, count, scale, s);
-        if (remote_policy() == 3) return launch_buf<Tr, K, UD, 3, 16, SCALE>(in, out, count, scale, s);
         return launch_buf<Tr, K, UD, 19, 16, SCALE>(in, out, count, scale, s);
     }
     if (!aligned) return launch_scalar<Tr, K, SCALE>(in, out, count, scale, s);
@@ -626,21 +614,6 @@ static int reduce_impl(int dtype, int k, const void *const *inputs, void *out, u
     return ESGD_INVALID_ARG;
 }
 
-// ---- cache maintenance: write back and invalidate every XCD's L2 ----
-// One workgroup per CU (blocks are dealt round-robin over the XCDs, so every XCD gets
-// some): lane 0 runs a system-scope release + acquire (buffer_wbl2 sc0 sc1 +
-// buffer_inv sc0 sc1), dropping any line of this device's L2s that a reused physical
-// page may still hold.
-__global__ __launch_bounds__(64) void k_cache_flush() {
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
-}
-
-int cache_flush(hipStream_t s) {
-    hipLaunchKernelGGL(k_cache_flush, dim3(cu_count()), dim3(64), 0, s);
-    ESGD_HIP(hipGetLastError());
-    return ESGD_SUCCESS;
-}
-
 // ---- internal entry points of the data plane (dataplane.cpp) ----
 int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s) {
     if (!bytes) return ESGD_SUCCESS;
@@ -722,9 +695,7 @@ int gather_remote(int n, const void *const *src, void *const *dst, const uint64_
     unsigned gx = grid_for(256 * 4, maxvec ? maxvec : 1, 8);
     unsigned per_seg = std::max(1u, (unsigned(cu_count()) * 4 + n - 1) / unsigned(n));
     if (gx > per_seg) gx = per_seg;
-    if (remote_policy() == 2) hipLaunchKernelGGL((k_gather<4, 2>), dim3(gx, n), dim3(256), 0, s, g);
-    else if (remote_policy() == 3) hipLaunchKernelGGL((k_gather<4, 3>), dim3(gx, n), dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((k_gather<4, 19>), dim3(gx, n), dim3(256), 0, s, g);
+    hipLaunchKernelGGL((k_gather<4>), dim3(gx, n), dim3(256), 0, s, g);
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;
 }
@@ -772,6 +743,21 @@ __global__ void __launch_bounds__(64) k_round_sync(uint32_t *flags, int rank, in
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         if (ts) __hip_atomic_store(&ts[1], uint64_t(wall_clock64()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+// Peer buckets are coarse-grained memory of other processes (other GPUs on a node).
+// After a pairing and before the phase that reads peers, every XCD's L2 (and the L1 of
+// every CU used) drops whatever lines of them it may still hold from an earlier round:
+// one workgroup per CU (dealt round-robin over the XCDs) runs a system-scope acquire
+// (buffer_inv sc0 sc1).  The dispatch's own acquire scope is not relied on for this.
+__global__ __launch_bounds__(64) void k_peer_acquire() {
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+int peer_acquire(hipStream_t s) {
+    hipLaunchKernelGGL(k_peer_acquire, dim3(cu_count()), dim3(64), 0, s);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
 }
 
 // ts (optional): wall-clock stamps of entry and exit (tracing, ESGD_GPU_TRACE=1);
