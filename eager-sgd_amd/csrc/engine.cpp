@@ -233,10 +233,19 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
         }
         return ESGD_SUCCESS;
     };
+    static const bool dbg = getenv("ESGD_DEBUG") && *getenv("ESGD_DEBUG") == '1';
+    const double c0 = now_s();
     if (!rc) rc = tp->setup(*s);     // local: buffers, streams, publication
+    const double c1 = now_s();
     rc = vote(rc);
+    const double c2 = now_s();
     if (!rc) rc = tp->connect(*s);   // needs every peer's publication
+    const double c3 = now_s();
     rc = vote(rc);
+    if (dbg)
+        fprintf(stderr, "[esgd] r%d create sched %d (%llu x %d B): setup %.1f ms, vote %.1f ms, connect %.1f ms, "
+                "vote %.1f ms\n", g_rank, s->id, (unsigned long long)count, int(s->esize), (c1 - c0) * 1e3,
+                (c2 - c1) * 1e3, (c3 - c2) * 1e3, (now_s() - c3) * 1e3);
     if (rc) {
         if (s->tstate) tp->teardown(*s);
         s->resolve_free = nullptr;   // the caller still owns ctx on failure

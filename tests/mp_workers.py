@@ -650,3 +650,64 @@ def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, dela
     s.delete()
     comm.finalize()
     return out
+
+
+def cp_stale_segment(rank, world, job):
+    """A segment file left behind under this job id by a crashed run (its creator is
+    dead) must not be joined: ranks > 0 wait for rank 0's fresh one (shm.cpp)."""
+    comm = _comm_job(job)
+    s = comm.Schedule(comm.ALLREDUCE, None, None, 0, buf=comm.BUF_NONE)
+    for _ in range(3):
+        s.post()
+        s.wait()
+    s.delete()
+    comm.finalize()
+    return True
+
+
+def _comm_job(job):
+    from esgd import comm
+    comm.init(job_id=job)
+    return comm
+
+
+def gpu_big(rank, world, count, rounds=1):
+    """One bucket of `count` fp32 per rank (up to ff.h's 2^31 - 1): creation, a round and
+    head / tail slices checked; returns the wall time of each step."""
+    import numpy as np
+
+    from esgd import device as dev
+    from oracle import ffref
+    comm = _comm()
+    t = {}
+    t0 = time.perf_counter()
+    rb = dev.DeviceBuffer(count)
+    dev.fill_uniform(rb, SEED, rank)
+    dev.synchronize()
+    t["alloc_fill_s"] = time.perf_counter() - t0
+    comm.barrier()
+    t0 = time.perf_counter()
+    s = comm.Schedule(comm.ALLREDUCE, None, rb, count, buf=comm.BUF_DEVICE)
+    t["create_s"] = time.perf_counter() - t0
+    ok = True
+    for i in range(rounds):
+        if i:   # in place: fresh inputs every round
+            dev.fill_uniform(rb, SEED + i, rank)
+            dev.synchronize()
+        comm.barrier()
+        t0 = time.perf_counter()
+        s.post()
+        s.wait()
+        t.setdefault("round_s", []).append(time.perf_counter() - t0)
+        m = 1 << 16
+        for start in (0, count // 2, count - m):
+            got = _download_slice(rb, start, m)
+            want = ffref.tree_sum([ffref.fill_uniform(SEED + i, r, m, start=start) for r in range(world)])
+            ok &= bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+    t["ok"] = ok
+    comm.barrier()
+    t0 = time.perf_counter()
+    s.delete()
+    t["delete_s"] = time.perf_counter() - t0
+    comm.finalize()
+    return t

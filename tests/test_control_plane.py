@@ -10,6 +10,8 @@ Reference behaviour checked (paths under /root/reference/eager-SGD-modules/fflib
     (src/colls/ffrand_allreduce.c:83-103), pinned against libc via the oracle;
   * plain allreduce — every round synchronous, every rank fresh.
 """
+import os
+
 import pytest
 
 from mp_workers import run
@@ -118,3 +120,37 @@ def test_delete_while_rounds_in_flight():
     for o in outs:
         assert not o["errs"], o
         assert o["completed"] == 300
+
+
+def test_stale_segment_of_a_dead_job_is_not_joined():
+    # a crashed run's /dev/shm/esgd-<job> (same job id) holds old barrier
+    # counts; ranks > 0 must not attach to it.  Make a real one: a rank 0 of a 2-rank job
+    # that is killed while it waits for its peer in the init barrier (the file is
+    # published, never unlinked).
+    import signal
+    import subprocess
+    import sys
+    import time
+    import uuid
+
+    from conftest import PKG
+    job = "stale-" + uuid.uuid4().hex[:12]
+    path = "/dev/shm/esgd-" + job
+    code = ("import sys; sys.path.insert(0, %r); from esgd import comm; "
+            "comm.init(job_id=%r, rank=0, world=2)") % (PKG, job)
+    p = subprocess.Popen([sys.executable, "-c", code], env=dict(os.environ, ESGD_TIMEOUT_S="120"))
+    try:
+        t0 = time.time()
+        while not os.path.exists(path) and time.time() - t0 < 60:
+            time.sleep(0.05)
+        assert os.path.exists(path), "rank 0 never published its segment"
+    finally:
+        p.send_signal(signal.SIGKILL)
+        p.wait()
+    assert os.path.exists(path)          # the crash left it behind
+    try:
+        outs = run("cp_stale_segment", 2, job=job, timeout=120)
+        assert outs == [True, True]
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)

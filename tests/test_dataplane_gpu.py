@@ -237,3 +237,13 @@ def test_rccl_transport_multi_gpu(world):
         verdicts = run("gpu_allreduce", world, count=1000003, rounds=2, kind=kind, transport="rccl")
         assert all(all(v) for v in verdicts), (kind, verdicts)
     _all_ok(run("gpu_config", world, kind=SOLO, counts=[64 << 20], rounds=2, transport="rccl", timeout=420))
+
+
+@pytest.mark.timeout(600)
+def test_largest_ff_bucket_2_ranks():
+    # ff.h's int count: 2^31 - 1 fp32 = 8 GiB per rank, two ranks (16 GiB exported over
+    # IPC from the arena), shards moved in 1 GiB pieces; round 1 never finished creating it
+    outs = run("gpu_big", 2, count=(1 << 31) - 1, rounds=2, timeout=600)
+    for o in outs:
+        assert o["ok"], o
+        assert o["create_s"] < 30, o
