@@ -89,11 +89,11 @@ def cpu_baseline_c1(P: int = 2, count: int = 262144):
     cores per rank; value = P x bucket bytes per step / step time."""
     from oracle import ffref
     t1, _ = ffref.time_c1(P, count, 20)
-    reps = max(50, min(20000, int(10.0 / max(t1, 1e-5))))
+    reps = max(50, min(20000, int(10.0 / max(t1, 1e-5))))   # ~10 s of steps
     t, ok = ffref.time_c1(P, count, reps)
     return {"value": round(P * count * 4 / t / 1e9, 3), "unit": "GB/s", "cores": 2 * P, "kind": "port",
             "sample": f"C1: {P} ranks x {count * 4 / MiB:g} MiB fp32, main + progress thread per rank "
-                      f"(oracle/ffref.c ffref_time_c1), best step of {reps}: {t * 1e6:.1f} us",
+                      f"(oracle/ffref.c ffref_time_c1), median step of {reps}: {t * 1e6:.1f} us",
             "correct": ok, "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
 
 

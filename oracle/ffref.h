@@ -85,7 +85,7 @@ double ffref_time_allreduce(int P, uint32_t count, int threads, int reps);
  * gradient into the send bucket, post, spin-wait (ffop.c:156-163), copy the result out,
  * zero the send bucket; the progress thread runs the move and the recursive-doubling
  * rounds (ffallreduce.c:126-171), exchanging rb through shared memory in place of MPI.
- * Returns the best per-step seconds over `reps` steps (after one warm-up step); *ok = 1
+ * Returns the median per-step seconds over `reps` steps (after one warm-up step); *ok = 1
  * if every rank's last result equals the oracle tree of the P buckets. */
 double ffref_time_c1(int P, uint32_t count, int reps, int *ok);
 
