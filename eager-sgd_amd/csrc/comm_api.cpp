@@ -30,6 +30,28 @@ Transport *default_transport(bool control_only) {
 }
 }  // namespace esgd
 
+namespace esgd {
+int create_schedule(int kind, int buf, const void *sb, void *rb, uint64_t count, int dtype, int async,
+                    unsigned seed, unsigned flags, int tag, uint64_t *out) {
+    ESGD_ARG(out, "esgd_schedule_create: null output");
+    ESGD_ARG((flags & ~unsigned(ESGD_SCHED_HOLD | ESGD_SCHED_ZERO_SB)) == 0,
+             "esgd_schedule_create: unknown flags 0x%x", flags);
+    ESGD_ARG(buf == ESGD_BUF_DEVICE || buf == ESGD_BUF_HOST || buf == ESGD_BUF_NONE,
+             "esgd_schedule_create: bad buffer kind %d", buf);
+    ESGD_ARG(esgd_dtype_size(dtype) > 0, "esgd_schedule_create: unsupported dtype %d", dtype);
+    ESGD_ARG(buf == ESGD_BUF_NONE || rb || count == 0, "esgd_schedule_create: null receive buffer");
+    const bool rccl = !std::strcmp(transport_name(), "rccl");
+    ESGD_ARG(rccl || !std::strcmp(transport_name(), "ipc"), "unknown transport '%s'", transport_name());
+    Transport *tp = default_transport(buf == ESGD_BUF_NONE);
+    Sched *s = nullptr;
+    int rc = sched_create(kind, dtype, count, const_cast<void *>(sb), rb, buf == ESGD_BUF_HOST,
+                          async, seed, tp, &s, flags, tag);
+    if (rc) return rc;
+    *out = reinterpret_cast<uint64_t>(s);
+    return ESGD_SUCCESS;
+}
+}  // namespace esgd
+
 using namespace esgd;
 
 static Sched *handle_to_sched(esgd_sched_h h) {
@@ -81,22 +103,7 @@ int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t c
 
 int esgd_schedule_create_ex(int kind, int buf, const void *sb, void *rb, uint64_t count, int dtype,
                             int async, unsigned seed, unsigned flags, esgd_sched_h *out) {
-    ESGD_ARG((flags & ~unsigned(ESGD_SCHED_HOLD | ESGD_SCHED_ZERO_SB)) == 0,
-             "esgd_schedule_create: unknown flags 0x%x", flags);
-    ESGD_ARG(out, "esgd_schedule_create: null output");
-    ESGD_ARG(buf == ESGD_BUF_DEVICE || buf == ESGD_BUF_HOST || buf == ESGD_BUF_NONE,
-             "esgd_schedule_create: bad buffer kind %d", buf);
-    ESGD_ARG(esgd_dtype_size(dtype) > 0, "esgd_schedule_create: unsupported dtype %d", dtype);
-    ESGD_ARG(buf == ESGD_BUF_NONE || rb || count == 0, "esgd_schedule_create: null receive buffer");
-    const bool rccl = !std::strcmp(transport_name(), "rccl");
-    ESGD_ARG(rccl || !std::strcmp(transport_name(), "ipc"), "unknown transport '%s'", transport_name());
-    Transport *tp = default_transport(buf == ESGD_BUF_NONE);
-    Sched *s = nullptr;
-    int rc = sched_create(kind, dtype, count, const_cast<void *>(sb), rb, buf == ESGD_BUF_HOST,
-                          async, seed, tp, &s, flags);
-    if (rc) return rc;
-    *out = reinterpret_cast<esgd_sched_h>(s);
-    return ESGD_SUCCESS;
+    return esgd::create_schedule(kind, buf, sb, rb, count, dtype, async, seed, flags, esgd::kNoTag, out);
 }
 
 int esgd_schedule_post(esgd_sched_h h, void *producer_stream, int *role) {

@@ -169,14 +169,14 @@ static void fail_locked(Sched &s, int rc, const char *msg) {
 }
 
 int sched_create(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
-                 int async, unsigned seed, Transport *tp, Sched **out, unsigned flags) {
+                 int async, unsigned seed, Transport *tp, Sched **out, unsigned flags, int tag) {
     return sched_create_with(kind, dtype, count, sb, rb, host_mode, async, seed, tp, nullptr,
-                             nullptr, nullptr, out, flags);
+                             nullptr, nullptr, out, flags, tag);
 }
 
 int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
                       int async, unsigned seed, Transport *tp, int (*resolve)(Sched &),
-                      void *ctx, void (*ctx_free)(void *), Sched **out, unsigned flags) {
+                      void *ctx, void (*ctx_free)(void *), Sched **out, unsigned flags, int tag) {
     ESGD_ARG(out, "schedule create: null output");
     ESGD_ARG(kind >= KIND_ALLREDUCE && kind <= KIND_MAJORITY, "schedule create: bad kind %d", kind);
     ESGD_ARG(tp, "schedule create: no transport");
@@ -196,32 +196,16 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     s->resolve_free = ctx_free;
     s->hold_mode = (flags & ESGD_SCHED_HOLD) != 0;
     s->zero_sb = (flags & ESGD_SCHED_ZERO_SB) != 0 && !host_mode && !s->in_place;
-    int rc = shm_barrier(g_seg, g_world, g_timeout);
-    if (!rc && g_rank == 0) {
-        SchedShm *sh = s->sh;
-        sh->kind.store(uint32_t(kind));
-        sh->activated.store(0);
-        sh->last_activator.store(-1);
-        for (int r = 0; r < kMaxRanks; ++r) {
-            sh->ready[r].store(0); sh->reduced[r].store(0); sh->done[r].store(0);
-            sh->gpu_err[r].store(0); sh->fin[r].store(0);
-            sh->joined[r].store(0); sh->activations[r].store(0);
-        }
-        sh->ready_count.store(0);
-        sh->setup_err.store(0);
-        for (int i = 0; i < 256; ++i) sh->act_of[i].store(0);
-        sh->gen.fetch_add(1, std::memory_order_acq_rel);
-    }
-    if (!rc) rc = shm_barrier(g_seg, g_world, g_timeout);
-    if (!rc && s->sh->kind.load() != uint32_t(kind)) {
-        set_error("schedule create: rank %d kind %d differs from rank 0's %u (creation order must match)",
-                  g_rank, kind, s->sh->kind.load());
-        rc = ESGD_INVALID_ARG;
-    }
-    s->gen = s->sh->gen.load();
-    // Registration is voted: every rank takes part in both barriers whatever happened
-    // locally, and a failure anywhere fails the creation everywhere (no rank is left
-    // waiting on a peer that gave up).
+    // Schedule ids are never reused within a job and the segment starts zeroed, so the
+    // shared state of this id needs no reset (no barrier before setup).  Creation is two
+    // voted steps: setup (local: buckets, streams, publication) -> barrier -> every rank
+    // checks every rank's signature (kind, dtype, tag: creation order must match) and
+    // failures -> connect (mapping peers) -> barrier -> failures.  A failure anywhere
+    // fails the creation everywhere; no rank is left waiting on a peer that gave up.
+    s->gen = 1;   // IpcSlot::gen == 1: published for this id
+    const uint64_t sig = (uint64_t(uint32_t(kind)) << 40) | (uint64_t(uint32_t(dtype) & 0xff) << 32) |
+                         (tag == kNoTag ? 0 : (0x10000u | uint16_t(tag)));
+    int rc = ESGD_SUCCESS;
     auto vote = [&](int r) -> int {
         if (r) s->sh->setup_err.fetch_add(1, std::memory_order_acq_rel);
         const int rb = shm_barrier(g_seg, g_world, g_timeout);
@@ -235,9 +219,20 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     };
     static const bool dbg = getenv("ESGD_DEBUG") && *getenv("ESGD_DEBUG") == '1';
     const double c0 = now_s();
+    s->sh->sig[g_rank].store(sig, std::memory_order_release);
     if (!rc) rc = tp->setup(*s);     // local: buffers, streams, publication
     const double c1 = now_s();
     rc = vote(rc);
+    for (int q = 0; !rc && q < g_world; ++q) {
+        const uint64_t o = s->sh->sig[q].load(std::memory_order_acquire);
+        if (o != sig) {
+            set_error("schedule create: rank %d created (kind %d, dtype %d, tag %d), rank %d (kind %d, "
+                      "dtype %d, tag %d): creation order must match", g_rank, kind, dtype,
+                      tag == kNoTag ? -1 : tag, q, int(o >> 40), int((o >> 32) & 0xff),
+                      (o & 0x10000) ? int(int16_t(o & 0xffff)) : -1);
+            rc = ESGD_INVALID_ARG;   // every rank sees the same signatures: all fail
+        }
+    }
     const double c2 = now_s();
     if (!rc) rc = tp->connect(*s);   // needs every peer's publication
     const double c3 = now_s();
@@ -420,11 +415,12 @@ int sched_delete(Sched *s) {
             std::this_thread::yield();
         }
     }
-    int rc = shm_barrier(g_seg, g_world, g_timeout);
+    // Local, like ffschedule_delete: every peer finished reading this rank's buckets for
+    // the rounds it joined (the done pairing), and the buckets go back to the IPC arena,
+    // which never unmaps them under a peer (arena.cpp).
     s->tp->teardown(*s);
-    int rc2 = shm_barrier(g_seg, g_world, g_timeout);
     free_sched(s);
-    return rc ? rc : rc2;
+    return ESGD_SUCCESS;
 }
 
 Sched *sched_lookup(uint64_t handle) {

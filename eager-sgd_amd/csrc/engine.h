@@ -35,6 +35,11 @@ namespace esgd {
 
 enum Kind { KIND_ALLREDUCE = 0, KIND_SOLO = 1, KIND_MAJORITY = 2 };
 
+// Schedule creation from the C ABIs (comm_api.cpp): transport by esgd_set_transport /
+// ESGD_TRANSPORT; tag as ff.h passes it (or kNoTag).
+int create_schedule(int kind, int buf, const void *sb, void *rb, uint64_t count, int dtype, int async,
+                    unsigned seed, unsigned flags, int tag, uint64_t *out);
+
 enum Stage {
     ST_IDLE = 0,      // between rounds
     ST_WAIT_TICKET,   // joined; waiting for this round's turn in the node's issue ring
@@ -142,13 +147,16 @@ Segment *engine_segment();
 int engine_barrier();
 double engine_timeout();
 
-// Schedules (collective create/delete, same order on every rank).
+// Schedules: creation is collective, in the same order on every rank (checked: kind,
+// dtype and, through ff.h, the tag must match); deletion is local.
+constexpr int kNoTag = INT32_MIN;   // creation without a tag to check
 int sched_create(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
-                 int async, unsigned seed, Transport *tp, Sched **out, unsigned flags = 0);
+                 int async, unsigned seed, Transport *tp, Sched **out, unsigned flags = 0, int tag = kNoTag);
 // same, with buffers re-resolved at every post (FFCOLL_BUFFERS); ctx freed by ctx_free
 int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, bool host_mode,
                       int async, unsigned seed, Transport *tp, int (*resolve)(Sched &),
-                      void *ctx, void (*ctx_free)(void *), Sched **out, unsigned flags = 0);
+                      void *ctx, void (*ctx_free)(void *), Sched **out, unsigned flags = 0,
+                      int tag = kNoTag);
 // transport chosen by esgd_set_transport / ESGD_TRANSPORT (comm_api.cpp)
 Transport *default_transport(bool control_only);
 int sched_post(Sched *s, void *producer_stream, int *role);

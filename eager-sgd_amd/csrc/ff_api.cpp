@@ -55,7 +55,7 @@ static int resolve_coll_buffers(Sched &s) {
     return ESGD_SUCCESS;
 }
 
-static int make_schedule(int kind, void *sndbuff, void *rcvbuff, int count, ffoperator_h op,
+static int make_schedule(int kind, void *sndbuff, void *rcvbuff, int count, int16_t tag, ffoperator_h op,
                          ffdatatype_h dt, int options, int async, unsigned seed, ffschedule_h *sched) {
     ESGD_ARG(sched, "fflib: null schedule output");
     ESGD_ARG(count >= 0, "fflib: negative count");
@@ -81,13 +81,15 @@ static int make_schedule(int kind, void *sndbuff, void *rcvbuff, int count, ffop
         int rc = sched_create_with(kind, dt, uint64_t(cb->rb->count), cb->sb ? cb->sb->ptr : nullptr,
                                    cb->rb->ptr, true, async, seed, default_transport(false),
                                    resolve_coll_buffers, cb,
-                                   [](void *p) { delete static_cast<CollBuffers *>(p); }, &s);
+                                   [](void *p) { delete static_cast<CollBuffers *>(p); }, &s, 0, tag);
         if (rc) { delete cb; return rc; }
         *sched = reinterpret_cast<ffschedule_h>(s);
         return FFSUCCESS;
     }
     void *sb = sndbuff == FFINPLACE ? nullptr : sndbuff;
-    int rc = esgd_schedule_create(kind, buf, sb, rcvbuff, uint64_t(count), dt, async, seed, &h);
+    // the tag is checked across ranks at creation (schedules match by creation order;
+    // the reference matches MPI messages by tag, src/components/mpi/ffop_mpi_send.c:30)
+    int rc = create_schedule(kind, buf, sb, rcvbuff, uint64_t(count), dt, async, seed, 0, tag, &h);
     if (rc) return rc;
     *sched = h;
     return FFSUCCESS;
@@ -186,19 +188,19 @@ int fffinalize(void) {
 int ffrank(int *rank) { return esgd_comm_rank(rank); }
 int ffsize(int *size) { return esgd_comm_size(size); }
 
-int ffallreduce(void *sndbuff, void *rcvbuff, int count, int16_t, ffoperator_h op,
+int ffallreduce(void *sndbuff, void *rcvbuff, int count, int16_t tag, ffoperator_h op,
                 ffdatatype_h datatype, int options, ffschedule_h *sched) {
-    return make_schedule(KIND_ALLREDUCE, sndbuff, rcvbuff, count, op, datatype, options, 0, 0, sched);
+    return make_schedule(KIND_ALLREDUCE, sndbuff, rcvbuff, count, tag, op, datatype, options, 0, 0, sched);
 }
 
-int ffsolo_allreduce(void *sndbuff, void *rcvbuff, int count, int16_t, ffoperator_h op,
+int ffsolo_allreduce(void *sndbuff, void *rcvbuff, int count, int16_t tag, ffoperator_h op,
                      ffdatatype_h datatype, int options, int async, ffschedule_h *sched) {
-    return make_schedule(KIND_SOLO, sndbuff, rcvbuff, count, op, datatype, options, async, 0, sched);
+    return make_schedule(KIND_SOLO, sndbuff, rcvbuff, count, tag, op, datatype, options, async, 0, sched);
 }
 
-int ffrand_allreduce(void *sndbuff, void *rcvbuff, int count, int16_t, ffoperator_h op,
+int ffrand_allreduce(void *sndbuff, void *rcvbuff, int count, int16_t tag, ffoperator_h op,
                      ffdatatype_h datatype, int options, int seed, int async, ffschedule_h *sched) {
-    return make_schedule(KIND_MAJORITY, sndbuff, rcvbuff, count, op, datatype, options, async,
+    return make_schedule(KIND_MAJORITY, sndbuff, rcvbuff, count, tag, op, datatype, options, async,
                          unsigned(seed), sched);
 }
 

@@ -25,13 +25,11 @@ struct alignas(64) IpcSlot {
     uint8_t handle[64];
     uint64_t offset;
     uint64_t bytes;
-    std::atomic<uint32_t> gen;    // == schedule generation when valid
+    std::atomic<uint32_t> gen;    // 1 once this rank published its bucket for this id
     std::atomic<uint32_t> ver;    // bumped at every (re)publication (buffers that grow)
 };
 
 struct alignas(64) SchedShm {
-    std::atomic<uint32_t> gen;            // bumped by each collective (re)creation
-    std::atomic<uint32_t> kind;
     std::atomic<uint32_t> activated;      // highest round activated (solo async / majority)
     std::atomic<int32_t> last_activator;  // diagnostics only (may lag `activated`)
     // per-round activation record, (round << 32) | (rank + 1), claimed by CAS BEFORE
@@ -49,6 +47,7 @@ struct alignas(64) SchedShm {
     std::atomic<uint32_t> activations[kMaxRanks];  // diagnostics: rounds activated by r
     std::atomic<uint32_t> ready_count;   // joins so far, all ranks (issue-ring append)
     std::atomic<uint32_t> setup_err;     // ranks whose registration failed (creation vote)
+    std::atomic<uint64_t> sig[kMaxRanks];   // creation signature of rank r: kind, dtype, tag
     IpcSlot slot[kMaxRanks];
 };
 

@@ -150,7 +150,8 @@ int esgd_comm_issue_log(uint32_t *sched, uint32_t *round, uint32_t cap, uint32_t
  *                      moves; for multi-process tests of the round protocol).
  * sb == NULL or sb == rb: in place (FFINPLACE).  Buffers are captured at creation and
  * must stay valid until esgd_schedule_delete (src/colls/ffallreduce.c:113-115).
- * Creation and deletion are collective, in the same order on every rank. */
+ * Creation is collective, in the same order on every rank (kind and dtype are checked
+ * across ranks); deletion is local, like ffschedule_delete. */
 #define ESGD_SCHED_ALLREDUCE 0
 #define ESGD_SCHED_SOLO 1
 #define ESGD_SCHED_MAJORITY 2

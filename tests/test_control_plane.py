@@ -102,15 +102,13 @@ def test_ordered_transport_same_issue_order_everywhere(world):
 def test_failed_creation_fails_every_rank(world):
     # registration is voted (engine.cpp sched_create): one rank's failure is every
     # rank's failure, with no rank left waiting for a peer's publication
+    # the last rank creates a MAJORITY schedule where the others create a SOLO one: every
+    # rank sees every rank's creation signature after the vote and fails the same way
     outs = run("cp_create_failure", world, bad_rank=world - 1)
     for r, o in enumerate(outs):
         assert o["err"] is not None, (r, o)
-        if r == world - 1:
-            assert "differs from rank 0" in o["err"]
-        elif r != 0:
-            pass   # either its own mismatch view or the vote's message
-        else:
-            assert "another rank failed" in o["err"]
+        assert "creation order must match" in o["err"], o["err"]
+        assert "kind 2" in o["err"] and "kind 1" in o["err"], o["err"]
         assert o["recovered_s"] < 30
 
 
