@@ -38,7 +38,6 @@ int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64
 int gather_remote(int n, const void *const *src, void *const *dst, const uint64_t *bytes,
                   hipStream_t s);
 int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s);
-int peer_acquire(hipStream_t s);
 
 int round_small(int dtype, const void *const *src, void *out, uint64_t n, int nseg,
                 const void *const *gsrc, void *const *gdst, const uint64_t *gbytes,
@@ -178,12 +177,14 @@ static uint32_t *dev_flag(T *host) {
 }
 
 int round_sync(uint32_t *flags, int rank, int world, uint32_t value, long long timeout_ticks,
-               uint32_t *err, uint32_t errval, uint64_t *ts, hipStream_t s);
+               uint32_t *err, uint32_t errval, uint64_t *ts, uint32_t *gate, hipStream_t s);
 
 static bool gpu_trace_on() {
     static const bool on = getenv("ESGD_GPU_TRACE") && *getenv("ESGD_GPU_TRACE") == '1';
     return on;
 }
+
+static int ctr_words(int sched_id, hipStream_t cs, uint32_t **out);
 
 // which = 0 ready, 1 reduced, 2 done; `value` is the round, or the chunk number of a
 // chunked round (a timeout still records the round)
@@ -192,11 +193,17 @@ static int pair_ranks(Sched &s, std::atomic<uint32_t> *flags, int which, uint32_
     const long long ticks = (long long)(engine_timeout() * double(g_ticks_per_s));
     uint64_t *ts = gpu_trace_on() ? reinterpret_cast<uint64_t *>(dev_flag(&s.sh->gpu_ts[s.rank][2 * which]))
                                   : nullptr;
-    if (int rc = round_sync(dev_flag(flags), s.rank, s.world, value ? value : round, ticks,
-                            dev_flag(&s.sh->gpu_err[s.rank]), round, ts, cs))
-        return rc;
-    // the ready and reduced pairings are followed by a phase that reads peer buckets
-    return which < 2 ? peer_acquire(cs) : ESGD_SUCCESS;
+    // the ready and reduced pairings are followed by a phase that reads peer buckets:
+    // their launch also drops stale peer lines from every XCD's caches (gate words 4, 5
+    // of the schedule's device counters)
+    uint32_t *gate = nullptr;
+    if (which < 2) {
+        uint32_t *ctr = nullptr;
+        if (int rc = ctr_words(s.id, cs, &ctr)) return rc;
+        gate = ctr + 4 + which;
+    }
+    return round_sync(dev_flag(flags), s.rank, s.world, value ? value : round, ticks,
+                      dev_flag(&s.sh->gpu_err[s.rank]), round, ts, gate, cs);
 }
 
 // ns between the GPU stamps of the last round (ESGD_GPU_TRACE=1), for the timeline
@@ -216,7 +223,8 @@ void gpu_trace_read(Sched &s, uint64_t out[6]) {
 
 void rccl_shutdown();
 
-// k_round_small's per-schedule device words (two arrival counters, two gates), one
+// Per-schedule device words -- k_round_small's two arrival counters and two gates
+// ([0..3]) and the five-launch round's cache-maintenance gates ([4], [5]) -- one
 // allocation for the process: a hipMalloc per schedule, on the round path, is avoided
 // (host-side memory operations were seen to slow later peer-reading kernels).
 static uint32_t *g_ctr_pool = nullptr;

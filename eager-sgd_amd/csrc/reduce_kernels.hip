@@ -724,10 +724,31 @@ __device__ __forceinline__ bool wave_wait_all(uint32_t *flags, int world, uint32
     }
 }
 
+//
+// Peer buckets are coarse-grained memory of other processes (other GPUs on a node).  When
+// the phase after this pairing reads peers (`gate` != nullptr), every XCD's L2 (and the
+// L1 of every CU used) must first drop whatever lines of them it may still hold from an
+// earlier round: the launch then has one workgroup per CU (dealt round-robin over the
+// XCDs); workgroup 0 runs the pairing and raises the device word `gate` to `value`, the
+// others wait for it and run a system-scope acquire (buffer_inv sc0 sc1).  The dispatch's
+// own acquire scope is not relied on for this.  A timed-out pairing still raises the gate
+// (the error flag fails the round), so no workgroup is left waiting.
 __global__ void __launch_bounds__(64) k_round_sync(uint32_t *flags, int rank, int world,
                                                    uint32_t value, long long timeout,
-                                                   uint32_t *err, uint32_t errval, uint64_t *ts) {
+                                                   uint32_t *err, uint32_t errval, uint64_t *ts,
+                                                   uint32_t *gate) {
     const bool lead = threadIdx.x == 0;
+    if (blockIdx.x != 0) {   // cache maintenance only
+        if (lead) {
+            const long long t0 = wall_clock64();
+            while (int32_t(__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - value) < 0) {
+                if (wall_clock64() - t0 > timeout) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        }
+        return;
+    }
     if (lead) {
         if (ts) ts[0] = uint64_t(wall_clock64());
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -735,39 +756,22 @@ __global__ void __launch_bounds__(64) k_round_sync(uint32_t *flags, int rank, in
         __hip_atomic_store(&flags[rank], value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     const long long t0 = wall_clock64();
-    if (!wave_wait_all(flags, world, value, t0, timeout)) {
-        if (lead) __hip_atomic_store(err, errval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return;
-    }
-    if (lead) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        if (ts) __hip_atomic_store(&ts[1], uint64_t(wall_clock64()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
-// Peer buckets are coarse-grained memory of other processes (other GPUs on a node).
-// After a pairing and before the phase that reads peers, every XCD's L2 (and the L1 of
-// every CU used) drops whatever lines of them it may still hold from an earlier round:
-// one workgroup per CU (dealt round-robin over the XCDs) runs a system-scope acquire
-// (buffer_inv sc0 sc1).  The dispatch's own acquire scope is not relied on for this.
-__global__ __launch_bounds__(64) void k_peer_acquire() {
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-}
-
-int peer_acquire(hipStream_t s) {
-    hipLaunchKernelGGL(k_peer_acquire, dim3(cu_count()), dim3(64), 0, s);
-    ESGD_HIP(hipGetLastError());
-    return ESGD_SUCCESS;
+    const bool ok = wave_wait_all(flags, world, value, t0, timeout);
+    if (!lead) return;
+    if (!ok) __hip_atomic_store(err, errval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (gate) __hip_atomic_store(gate, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ok && ts) __hip_atomic_store(&ts[1], uint64_t(wall_clock64()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ts (optional): wall-clock stamps of entry and exit (tracing, ESGD_GPU_TRACE=1);
 // errval: what a timed-out wait records in *err (the round, also when `value` numbers
 // a chunk of it)
 int round_sync(uint32_t *flags, int rank, int world, uint32_t value, long long timeout_ticks,
-               uint32_t *err, uint32_t errval, uint64_t *ts, hipStream_t s) {
+               uint32_t *err, uint32_t errval, uint64_t *ts, uint32_t *gate, hipStream_t s) {
     ESGD_ARG(flags && err && world >= 1 && rank >= 0 && rank < world, "round_sync: bad arguments");
-    hipLaunchKernelGGL(k_round_sync, dim3(1), dim3(64), 0, s, flags, rank, world, value,
-                       timeout_ticks, err, errval, ts);
+    hipLaunchKernelGGL(k_round_sync, dim3(gate ? unsigned(cu_count()) : 1u), dim3(64), 0, s, flags, rank, world,
+                       value, timeout_ticks, err, errval, ts, gate);
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;
 }
