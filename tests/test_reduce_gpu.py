@@ -150,7 +150,9 @@ def test_fill_uniform_bitwise():
 @pytest.mark.parametrize("policy,unroll,nt,grid", [
     (-1, 0, 1, 0), (-1, 2, 1, 7), (-1, 4, 1, 1), (0, 1, 0, 0), (0, 2, 1, 0), (0, 4, 0, 7),
     (1, 0, 1, 0), (3, 0, 1, 5), (5, 0, 1, 0), (8, 0, 1, 3), (9, 0, 1, 0), (10, 0, 1, 0),
-    (11, 0, 1, 3), (12, 0, 1, 0), (13, 0, 1, 0)])
+    (11, 0, 1, 3), (12, 0, 1, 0), (13, 0, 1, 0), (14, 0, 1, 0), (16, 0, 1, 0),
+    # LDS-DMA ring variants (sweep only): (waves, depth) 4/2, 2/4, 1/8, 2/3
+    (17, 0, 1, 0), (18, 0, 1, 3), (19, 0, 1, 0), (20, 0, 1, 5)])
 @pytest.mark.parametrize("k", [2, 8])
 def test_tuning_variants_identical(policy, unroll, nt, grid, k):
     xs = rand_input(np.float32, k, 300007, seed=3)
