@@ -337,6 +337,7 @@ int sched_wait_ex(Sched *s, int *fresh) {
     uint32_t target;
     {
         std::lock_guard<std::mutex> lk(s->mu);
+        ESGD_ARG(!s->held, "schedule %d: release() the round wait() returned before waiting for the next", s->id);
         target = s->waited + 1;
     }
     // a round about to complete is seen ~5 us sooner by spinning than through the
@@ -383,7 +384,8 @@ int sched_test(Sched *s, int *flag) {
     ESGD_ARG(s && flag, "schedule test: null argument");
     std::lock_guard<std::mutex> lk(s->mu);
     if (s->error) { set_error("%s", s->errmsg); return s->error; }
-    *flag = !s->held && s->completed >= s->waited + 1;
+    ESGD_ARG(!s->held, "schedule %d: release() the round test() returned before testing for the next", s->id);
+    *flag = s->completed >= s->waited + 1;
     if (*flag) {
         ++s->waited;
         if (s->hold_mode) s->held = true;
