@@ -711,3 +711,38 @@ def gpu_big(rank, world, count, rounds=1):
     t["delete_s"] = time.perf_counter() - t0
     comm.finalize()
     return t
+
+
+def cp_hold(rank, world, hold_s=0.3):
+    """ESGD_SCHED_HOLD on the control plane: after wait() a rank joins no further round
+    of the schedule until release(); waiting again before releasing is an error."""
+    from esgd._lib import EsgdError
+    comm = _comm()
+    s = comm.Schedule(comm.SOLO, None, None, 0, async_=100, buf=comm.BUF_NONE, flags=comm.HOLD)
+    out = {}
+    s.post()
+    s.wait()
+    try:
+        s.wait()
+        out["double_wait"] = "no error"
+    except EsgdError as e:
+        out["double_wait"] = str(e)
+    comm.barrier()
+    if rank == 1:
+        time.sleep(hold_s)       # rank 0's round 2 cannot complete before this release
+        s.release()
+        s.post()
+        s.wait()
+        s.release()
+    else:
+        s.release()
+        t0 = time.time()
+        s.post()                 # activates round 2 (solo, asynchronous)
+        s.wait()
+        out["round2_s"] = time.time() - t0
+        s.release()
+    comm.barrier()
+    out["log"] = s.log()
+    s.delete()
+    comm.finalize()
+    return out

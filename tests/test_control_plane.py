@@ -152,3 +152,11 @@ def test_stale_segment_of_a_dead_job_is_not_joined():
     finally:
         if os.path.exists(path):
             os.unlink(path)
+
+
+def test_hold_until_release():
+    outs = run("cp_hold", 2, hold_s=0.3)
+    for o in outs:
+        assert "release() the round" in o["double_wait"], o
+    assert outs[0]["round2_s"] >= 0.25, outs[0]      # rank 1 joined only after its release
+    assert [e["round"] for e in outs[1]["log"]] == [1, 2]
