@@ -26,7 +26,7 @@ OBJS      := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.hip.o,$(HIP_SRCS)) \
              $(patsubst $(CSRC)/%.cpp,$(BUILD)/%.cpp.o,$(CPP_SRCS))
 HDRS      := $(wildcard include/*.h) $(wildcard $(CSRC)/*.h)
 
-.PHONY: all lib oracle clean
+.PHONY: all lib oracle clean tsan
 all: lib oracle
 
 lib: $(OUTLIB)
@@ -51,3 +51,25 @@ oracle/libffref.so: oracle/ffref.c oracle/ffref.h
 
 clean:
 	rm -rf $(BUILD) $(OUTLIB) oracle/libffref.so
+
+# ---- ThreadSanitizer build of the host side (CPU control-plane tests only) ----
+# make tsan -> build/tsan/libesgd.so; run e.g.
+#   LD_PRELOAD=$(TSAN_RT) ESGD_LIB=build/tsan/libesgd.so TSAN_OPTIONS=report_signal_unsafe=0 \
+#   python -m pytest tests/test_control_plane.py -m "not gpu"
+TSAN_RT   := $(ROCM)/lib/llvm/lib/clang/22/lib/linux/libclang_rt.tsan-x86_64.so
+TSAN_DIR  := build/tsan
+TSAN_OBJS := $(patsubst $(CSRC)/%.hip,$(TSAN_DIR)/%.hip.o,$(HIP_SRCS)) \
+             $(patsubst $(CSRC)/%.cpp,$(TSAN_DIR)/%.cpp.o,$(CPP_SRCS))
+
+tsan: $(TSAN_DIR)/libesgd.so
+
+$(TSAN_DIR)/%.hip.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(TSAN_DIR)
+	$(HIPCC) $(HIPFLAGS) -O1 -g -Xarch_host -fsanitize=thread -c $< -o $@
+
+$(TSAN_DIR)/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(TSAN_DIR)
+	$(HIPCC) $(CXXFLAGS) -O1 -g -fsanitize=thread -x c++ -c $< -o $@
+
+$(TSAN_DIR)/libesgd.so: $(TSAN_OBJS) $(CSRC)/exports.map
+	$(HIPCC) --offload-arch=$(ARCH) $(TSAN_OBJS) $(LDFLAGS) $(TSAN_RT) -Wl,-rpath,$(dir $(TSAN_RT)) -o $@
