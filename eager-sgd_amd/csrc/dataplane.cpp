@@ -25,6 +25,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "engine.h"
@@ -39,9 +40,9 @@ int gather_remote(int n, const void *const *src, void *const *dst, const uint64_
                   hipStream_t s);
 int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s);
 
-int round_small(int dtype, const void *const *src, void *out, uint64_t n, int nseg,
+int round_small(int dtype, const void *const *src, void *out, void *pub, uint64_t n, int nseg,
                 const void *const *gsrc, void *const *gdst, const uint64_t *gbytes,
-                uint32_t *ready, uint32_t *reduced, uint32_t *done, uint32_t *fin, uint32_t *err,
+                uint32_t *ready, uint32_t *reduced, uint32_t *fin, uint32_t *err,
                 uint64_t *ts, uint32_t *counter, int rank, int world, uint32_t value,
                 long long timeout_ticks, hipStream_t s);
 
@@ -283,14 +284,32 @@ struct BaseState {
     virtual ~BaseState() {}
 };
 
+// A mapped peer publication (IpcSlot): where it is in this process and which version.
+struct PeerMap {
+    char *ptr = nullptr;
+    void *base = nullptr;
+    uint32_t ver = 0;
+    uint8_t handle[64] = {};
+};
+
 struct IpcState : BaseState {
     uint32_t *ctr = nullptr;          // device: k_round_small's counters and gates (pool)
     std::vector<hipEvent_t> cev;      // chunked host rounds: per chunk H2D / reduced / D2H
     bool chunked_before = false;
-    char *peer[kMaxRanks] = {};
-    void *peer_base[kMaxRanks] = {};
-    uint32_t peer_ver[kMaxRanks] = {};
-    uint8_t peer_handle[kMaxRanks][64] = {};
+    // this rank's published shard (one-launch rounds): phase 1 writes the reduced shard
+    // here as well as into rb, peers all-gather from it.  rb is then read by peers only in
+    // phase 1, and pub is rewritten only after the next round's ready pairing, so the
+    // round needs no third ("done") pairing.  Arena memory, L elements (the largest
+    // shard).  k_round_small's last workgroup ends the round with SchedShm::fin = round;
+    // teardown returns pub to the arena only once every peer's fin has reached pub_round
+    // (deletion is local).  Five-launch rounds keep the done pairing and gather from rb:
+    // the second store of the shard costs more there (+15-28 % at 256 MiB - 1 GiB,
+    // profiles/r02/README.md) than the pairing's few microseconds.
+    char *pub = nullptr;
+    size_t pub_cap = 0;
+    uint32_t pub_round = 0;
+    char *peer[kMaxRanks] = {};       // every rank's rb (own included)
+    PeerMap rbmap[kMaxRanks], pubmap[kMaxRanks];
 };
 
 // shard j = [off_j, off_j + len_j): equal shards rounded up to 1 KiB so every shard
@@ -560,50 +579,84 @@ struct IpcTransport final : Transport {
 
     // Publish rb_dev (arena memory: the chunk's handle + the offset); ESGD_INVALID_ARG
     // when rb_dev is foreign memory, which is never exported.
-    static int publish(Sched &s, IpcState &st) {
+    // Publish an arena buffer in this rank's slot (the chunk's handle + the offset);
+    // ESGD_INVALID_ARG when `p` is foreign memory, which is never exported.
+    static int publish_buf(Sched &s, IpcSlot &mine, char *p, size_t bytes, const char *what) {
         void *base = nullptr;
         uint64_t off = 0;
         uint8_t hb[64];
-        if (int rc = arena_export(st.rb_dev, s.count * s.esize, &base, &off, hb)) return rc;
-        IpcSlot &mine = s.sh->slot[s.rank];
+        if (int rc = arena_export(p, bytes, &base, &off, hb)) return rc;
         std::memcpy(mine.handle, hb, 64);
         mine.offset = off;
-        mine.bytes = s.count * s.esize;
+        mine.bytes = bytes;
         mine.gen.store(s.gen, std::memory_order_release);
         mine.ver.fetch_add(1, std::memory_order_acq_rel);
-        st.peer[s.rank] = st.rb_dev;
-        ESGD_TRACE("r%d publish sched %d rb %p chunk %p + %llu\n", s.rank, s.id, (void *)st.rb_dev, base,
+        ESGD_TRACE("r%d publish sched %d %s %p chunk %p + %llu\n", s.rank, s.id, what, (void *)p, base,
                    (unsigned long long)off);
         return ESGD_SUCCESS;
     }
 
-    // (re)map every peer whose publication changed since we last mapped it
+    static int publish(Sched &s, IpcState &st) {
+        st.peer[s.rank] = st.rb_dev;
+        return publish_buf(s, s.sh->slot[s.rank], st.rb_dev, s.count * s.esize, "rb");
+    }
+
+    // rounds of this size run as one k_round_small launch
+    static bool one_launch(const Sched &s) {
+        return s.world > 1 && s.world <= ESGD_MAX_FANIN && s.count * s.esize <= small_round_bytes();
+    }
+
+    // the published shard (one-launch rounds only): grown and re-published when the
+    // largest shard outgrows it
+    static int publish_pub(Sched &s, IpcState &st) {
+        if (!one_launch(s)) return ESGD_SUCCESS;
+        const size_t need = std::max<size_t>(st.len[0] * s.esize, 16);
+        if (st.pub && need <= st.pub_cap) return ESGD_SUCCESS;
+        if (st.pub) st.retired.push_back(st.pub);   // peers may still map it: back at teardown
+        if (int rc = alloc_bucket(need, &st.pub, &st.pub_cap)) return rc;
+        return publish_buf(s, s.sh->pub[s.rank], st.pub, st.pub_cap, "pub");
+    }
+
+    // (re)map one peer publication if it changed since we last mapped it
+    static int map_slot(Sched &s, int q, IpcSlot &ps, PeerMap &m, const char *what) {
+        if (ps.gen.load(std::memory_order_acquire) != s.gen) {
+            set_error("schedule %d: rank %d did not publish its %s", s.id, q, what);
+            return ESGD_ERROR;
+        }
+        const uint32_t v = ps.ver.load(std::memory_order_acquire);
+        if (m.base && v == m.ver) return ESGD_SUCCESS;   // nothing moved
+        // a moved buffer may sit in the same arena chunk (same handle, new offset);
+        // mappings are cached per (peer, chunk) and never closed before shutdown
+        if (!(m.base && std::memcmp(m.handle, ps.handle, 64) == 0)) {
+            void *pb = nullptr;
+            if (int rc = ipc_open(q, ps.handle, &pb)) return rc;
+            m.base = pb;
+            std::memcpy(m.handle, ps.handle, 64);
+        }
+        m.ptr = static_cast<char *>(m.base) + ps.offset;
+        m.ver = v;
+        return ESGD_SUCCESS;
+    }
+
+    // (re)map every peer's rb and published shard
     static int map_peers(Sched &s, IpcState &st) {
         const size_t bytes = s.count * s.esize;
         for (int q = 0; q < s.world; ++q) {
             if (q == s.rank) continue;
             IpcSlot &ps = s.sh->slot[q];
-            if (ps.gen.load(std::memory_order_acquire) != s.gen) {
-                set_error("schedule %d: rank %d did not publish its buffer", s.id, q);
-                return ESGD_ERROR;
-            }
-            const uint32_t v = ps.ver.load(std::memory_order_acquire);
+            if (int rc = map_slot(s, q, ps, st.rbmap[q], "bucket")) return rc;
             if (ps.bytes != bytes) {
                 set_error("schedule %d: rank %d has %llu bytes, this rank %zu", s.id, q,
                           (unsigned long long)ps.bytes, bytes);
                 return ESGD_INVALID_ARG;
             }
-            if (st.peer_base[q] && v == st.peer_ver[q]) continue;   // nothing moved
-            // a moved bucket may sit in the same arena chunk (same handle, new offset);
-            // mappings are cached per (peer, chunk) and never closed before shutdown
-            if (!(st.peer_base[q] && std::memcmp(st.peer_handle[q], ps.handle, 64) == 0)) {
-                void *pb = nullptr;
-                if (int rc = ipc_open(q, ps.handle, &pb)) return rc;
-                st.peer_base[q] = pb;
-                std::memcpy(st.peer_handle[q], ps.handle, 64);
+            st.peer[q] = st.rbmap[q].ptr;
+            if (!one_launch(s)) continue;   // every rank has this size (checked above)
+            if (int rc = map_slot(s, q, s.sh->pub[q], st.pubmap[q], "published shard")) return rc;
+            if (s.sh->pub[q].bytes < st.len[q] * s.esize) {
+                set_error("schedule %d: rank %d's published shard is too small", s.id, q);
+                return ESGD_ERROR;
             }
-            st.peer[q] = static_cast<char *>(st.peer_base[q]) + ps.offset;
-            st.peer_ver[q] = v;
         }
         return ESGD_SUCCESS;
     }
@@ -619,6 +672,7 @@ struct IpcTransport final : Transport {
         // ESGD_SHADOW=1 shadows every device bucket (caller buckets that are freed and
         // re-allocated between rounds; also how the tests reach the fallback)
         static const bool force_shadow = getenv("ESGD_SHADOW") && *getenv("ESGD_SHADOW") == '1';
+        if (int rc = publish_pub(s, *st)) return rc;
         if (s.host_mode) return publish(s, *st);
         int rc = force_shadow ? ESGD_INVALID_ARG : publish(s, *st);
         if (rc == ESGD_INVALID_ARG) {
@@ -652,7 +706,10 @@ struct IpcTransport final : Transport {
         if (moved < 0) return moved;
         if (s.world > 1 && moved)
             if (int rc = publish(s, st)) return rc;
-        if (s.world > 1 && s.resolve) publish_size(s);
+        if (s.world > 1 && s.resolve) {
+            publish_size(s);
+            if (int rc = publish_pub(s, st)) return rc;   // larger shards need a larger pub
+        }
         st.peer[s.rank] = st.rb_dev;
         ESGD_TRACE("r%d sched %d round %u join count=%llu rb_dev=%p moved=%d staged=%d\n", s.rank, s.id,
                    round, (unsigned long long)s.count, (void *)st.rb_dev, moved, int(staged(s, st)));
@@ -663,7 +720,9 @@ struct IpcTransport final : Transport {
     //   move -> [pair: ready] -> reduce-scatter (tree kernel over peer HBM)
     //        -> [pair: reduced] -> all-gather -> [pair: done] -> copy-out -> event.
     // The last pairing keeps this rank's shard unchanged until every peer has gathered
-    // it (the caller may overwrite rb once wait() returns).
+    // it (the caller may overwrite rb once wait() returns).  Buckets up to
+    // small_round_bytes() run as one k_round_small launch instead (launch_small: two
+    // pairings, the gather reads the published shards).
     int launch(Sched &s, uint32_t round, bool fresh) override {
         IpcState &st = S(s);
         hipStream_t cs = st.stream;
@@ -674,7 +733,7 @@ struct IpcTransport final : Transport {
         if (s.world > 1) {
             if (s.resolve)
                 if (int rc = map_peers(s, st)) return rc;
-            if (s.world <= ESGD_MAX_FANIN && s.count * s.esize <= small_round_bytes()) {
+            if (one_launch(s)) {
                 if (int rc = launch_small(s, st, round, cs)) return rc;
                 // device buckets: nothing follows the kernel, the host polls its fin flag
                 // (the event only reports faults)
@@ -809,6 +868,7 @@ struct IpcTransport final : Transport {
     static int launch_small(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) {
         if (!st.ctr)   // first one-launch round of this schedule
             if (int rc = ctr_words(s.id, cs, &st.ctr)) return rc;
+        st.pub_round = round;
         const void *in[kMaxRanks];
         for (int j = 0; j < s.world; ++j) in[j] = st.peer[j] + st.off[s.rank] * s.esize;
         const void *src[kMaxRanks];
@@ -817,15 +877,15 @@ struct IpcTransport final : Transport {
         int m = 0;
         for (int j = 0; j < s.world; ++j) {
             if (j == s.rank || st.len[j] == 0) continue;
-            src[m] = st.peer[j] + st.off[j] * s.esize;
+            src[m] = st.pubmap[j].ptr;   // peer j's published shard j
             dst[m] = st.rb_dev + st.off[j] * s.esize;
             bytes[m] = st.len[j] * s.esize;
             ++m;
         }
         const long long ticks = (long long)(engine_timeout() * double(g_ticks_per_s));
         uint64_t *ts = gpu_trace_on() ? reinterpret_cast<uint64_t *>(dev_flag(&s.sh->gpu_ts[s.rank][0])) : nullptr;
-        return round_small(s.dtype, in, st.rb_dev + st.off[s.rank] * s.esize, st.len[s.rank], m, src, dst,
-                           bytes, dev_flag(s.sh->ready), dev_flag(s.sh->reduced), dev_flag(s.sh->done),
+        return round_small(s.dtype, in, st.rb_dev + st.off[s.rank] * s.esize, st.pub, st.len[s.rank], m, src,
+                           dst, bytes, dev_flag(s.sh->ready), dev_flag(s.sh->reduced),
                            dev_flag(&s.sh->fin[s.rank]), dev_flag(&s.sh->gpu_err[s.rank]), ts, st.ctr,
                            s.rank, s.world, round, ticks, cs);
     }
@@ -836,11 +896,31 @@ struct IpcTransport final : Transport {
 
     std::string diagnose(Sched &s) override { return base_diagnose(s); }
 
+    // Deletion is local: peers may still be gathering this rank's published shard of the
+    // last round (they passed the same `reduced` pairing; their gather is queued right
+    // behind it).  pub goes back to the arena once every peer's fin shows that round;
+    // if a peer never gets there (it failed), pub is kept out of the arena instead.
     void teardown(Sched &s) override {
         IpcState *st = static_cast<IpcState *>(s.tstate);
         if (!st) return;
         if (st->stream) (void)hipStreamSynchronize(st->stream);
         for (hipEvent_t e : st->cev) (void)hipEventDestroy(e);
+        bool pub_free = true;
+        if (st->pub && st->pub_round && s.world > 1) {
+            const double t0 = now_s(), limit = std::min(engine_timeout(), 10.0);
+            for (int q = 0; q < s.world && pub_free; ++q) {
+                if (q == s.rank) continue;
+                while (int32_t(s.sh->fin[q].load(std::memory_order_acquire) - st->pub_round) < 0) {
+                    if (now_s() - t0 > limit) { pub_free = false; break; }
+                    std::this_thread::yield();
+                }
+            }
+            if (!pub_free)
+                ESGD_TRACE("r%d sched %d: a peer never finished round %u, its published shard is kept\n",
+                           s.rank, s.id, st->pub_round);
+        }
+        if (st->pub && pub_free) free_bucket(st->pub);
+        if (!pub_free) st->retired.clear();   // earlier pubs too: a peer may be stuck on any
         base_teardown(s, *st);
         delete st;
         s.tstate = nullptr;

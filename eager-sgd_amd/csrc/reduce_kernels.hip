@@ -781,10 +781,10 @@ int round_sync(uint32_t *flags, int rank, int world, uint32_t value, long long t
 // reduce-scatter, the all-gather) cost ~15 us of host time and ~4 us of GPU time per
 // kernel boundary (tools/lat.sh).  k_round_small does the same steps inside one kernel of
 // at most kSmallBlocks workgroups:
-//   publish ready -> wait for every rank's ready -> reduce-scatter (tree order) ->
-//   grid count; the last workgroup publishes reduced -> wait for every rank's reduced ->
-//   all-gather -> grid count; the last workgroup publishes done, waits for every rank's
-//   done and writes `fin` (the host polls it instead of an event).
+//   publish ready -> wait for every rank's ready -> reduce-scatter (tree order) into rb
+//   and the published shard -> grid count; the last workgroup publishes reduced -> wait
+//   for every rank's reduced -> all-gather from the peers' published shards -> grid
+//   count; the last workgroup writes `fin` (the host polls it instead of an event).
 // Hand-offs: every payload store is system-scope write-through (sc0 sc1) and drained
 // (s_waitcnt vmcnt(0)) before the workgroup counts itself; peer payload is read with
 // system-scope loads after a system-scope acquire.  The grid is far below one workgroup
@@ -795,14 +795,15 @@ constexpr int kSmallBlocks = 64;
 
 struct SmallRoundArgs {
     const void *src[kMaxSeg];   // phase 1 inputs: shard `rank` of every rank's rb, rank order
-    void *out;                  // phase 1 output: shard `rank` of the local rb
+    void *out;                  // phase 1 output: shard `rank` of the local rb ...
+    void *pub;                  // ... and of this rank's published shard (peers gather it)
     uint64_t n;                 // elements of the local shard
-    const void *gsrc[kMaxSeg];  // phase 2: every other rank's shard (peer memory) ...
+    const void *gsrc[kMaxSeg];  // phase 2: every other rank's published shard (peer memory) ...
     void *gdst[kMaxSeg];        // ... and where it lands in the local rb
     uint32_t gvec[kMaxSeg];     // 16-B vectors per segment
     uint32_t gtail[kMaxSeg];    // bytes after the last full vector
     int nseg;
-    uint32_t *ready, *reduced, *done, *fin, *err;
+    uint32_t *ready, *reduced, *fin, *err;
     uint64_t *ts;               // optional GPU trace stamps (6)
     uint32_t *counter;          // device words: [0], [1] arrivals (zero between rounds),
                                 // [2], [3] gates raised to the round by the polling lane
@@ -892,6 +893,7 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
     for (int j = 0; j < K; ++j)
         rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(a.src[j]), (short)0, bytes, 0x00020000);
     __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, bytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t wp = __builtin_amdgcn_make_buffer_rsrc(a.pub, (short)0, bytes, 0x00020000);
     // U vectors per input per lane in flight (the range check drops the ragged end)
     constexpr int U = sizeof(T) == 2 ? 2 : 4;
     for (uint32_t i = blockIdx.x * (256 * U) + threadIdx.x; i < nvec; i += gridDim.x * (256 * U)) {
@@ -902,8 +904,11 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
             for (int j = 0; j < K; ++j)
                 r[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs[j], (i + u * 256) * 16, 0, 17);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            __builtin_amdgcn_raw_buffer_store_b128(fold16<Tr, K, false>(r[u], 1.0f), ws, (i + u * 256) * 16, 0, 17);
+        for (int u = 0; u < U; ++u) {
+            const raw16 o = fold16<Tr, K, false>(r[u], 1.0f);
+            __builtin_amdgcn_raw_buffer_store_b128(o, ws, (i + u * 256) * 16, 0, 17);
+            __builtin_amdgcn_raw_buffer_store_b128(o, wp, (i + u * 256) * 16, 0, 17);
+        }
     }
     if (blockIdx.x == 0 && uint64_t(nvec) * Tr::E + threadIdx.x < a.n) {
         const uint64_t e = uint64_t(nvec) * Tr::E + threadIdx.x;
@@ -914,6 +919,8 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
                                               __HIP_MEMORY_SCOPE_SYSTEM));
         tree_fold<Tr, K>(v);
         __hip_atomic_store(static_cast<T *>(a.out) + e, Tr::store(v[0]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(static_cast<T *>(a.pub) + e, Tr::store(v[0]), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
     const bool last1 = block_count(&a.counter[0], &last);
@@ -948,19 +955,11 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    if (!block_count(&a.counter[1], &last) || threadIdx.x >= 64) return;
-    // the last workgroup's first wave: this rank's shard must stay put until every rank
-    // has gathered it
-    if (lead) {
-        if (stamp) a.ts[4] = uint64_t(wall_clock64());
-        publish_flag(&a.done[a.rank], a.value);
-    }
-    if (!wave_wait_all(a.done, a.world, a.value, t0, a.timeout)) {
-        if (lead) __hip_atomic_store(a.err, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return;
-    }
-    if (!lead) return;
-    if (stamp) a.ts[5] = uint64_t(wall_clock64());
+    // No third pairing: peers gather from `pub`, which this rank rewrites only in the
+    // next round's phase 1 -- after that round's ready pairing, i.e. after every peer's
+    // kernel of this round has finished -- and rb itself is read by peers only in phase 1.
+    if (!block_count(&a.counter[1], &last) || !lead) return;
+    if (stamp) a.ts[4] = a.ts[5] = uint64_t(wall_clock64());
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stamps land before fin
     __hip_atomic_store(a.fin, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -983,9 +982,9 @@ static int launch_small_t(const SmallRoundArgs &a, unsigned grid, hipStream_t s)
 
 // Entry point of the data plane (dataplane.cpp).  The shard layout keeps every shard
 // 1 KiB aligned; segments are checked here.
-int round_small(int dtype, const void *const *src, void *out, uint64_t n, int nseg,
+int round_small(int dtype, const void *const *src, void *out, void *pub, uint64_t n, int nseg,
                 const void *const *gsrc, void *const *gdst, const uint64_t *gbytes,
-                uint32_t *ready, uint32_t *reduced, uint32_t *done, uint32_t *fin, uint32_t *err,
+                uint32_t *ready, uint32_t *reduced, uint32_t *fin, uint32_t *err,
                 uint64_t *ts, uint32_t *counter, int rank, int world, uint32_t value,
                 long long timeout_ticks, hipStream_t s) {
     ESGD_ARG(world >= 2 && world <= ESGD_MAX_FANIN && nseg >= 0 && nseg < kMaxSeg,
@@ -995,7 +994,11 @@ int round_small(int dtype, const void *const *src, void *out, uint64_t n, int ns
     SmallRoundArgs a;
     std::memset(&a, 0, sizeof(a));
     for (int j = 0; j < world; ++j) a.src[j] = src[j];
+    // an empty shard may start anywhere (count 1 at P = 2: shard 1 at element 1)
+    ESGD_ARG(n == 0 || ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(pub)) & 15) == 0,
+             "small round: shard not 16-B aligned");
     a.out = out;
+    a.pub = pub;
     a.n = n;
     uint64_t maxv = n * es / 16;
     for (int i = 0; i < nseg; ++i) {
@@ -1008,7 +1011,7 @@ int round_small(int dtype, const void *const *src, void *out, uint64_t n, int ns
         maxv = std::max<uint64_t>(maxv, a.gvec[i]);
     }
     a.nseg = nseg;
-    a.ready = ready; a.reduced = reduced; a.done = done; a.fin = fin; a.err = err;
+    a.ready = ready; a.reduced = reduced; a.fin = fin; a.err = err;
     a.ts = ts;
     a.counter = counter;
     a.rank = rank; a.world = world; a.value = value; a.timeout = timeout_ticks;

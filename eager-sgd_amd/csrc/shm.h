@@ -38,7 +38,7 @@ struct alignas(64) SchedShm {
     // GPU flags (written by the GPUs through the host-registered segment, system scope):
     alignas(64) std::atomic<uint32_t> ready[kMaxRanks];   // round whose snapshot rank r has made
     alignas(64) std::atomic<uint32_t> reduced[kMaxRanks]; // round whose reduce-scatter is done
-    alignas(64) std::atomic<uint32_t> done[kMaxRanks];    // round whose all-gather is done
+    alignas(64) std::atomic<uint32_t> done[kMaxRanks];    // chunk whose all-gather is done (chunked host rounds)
     alignas(64) std::atomic<uint32_t> gpu_err[kMaxRanks]; // round whose flag wait timed out
     alignas(64) std::atomic<uint32_t> fin[kMaxRanks];     // round a one-launch round finished
     // ESGD_GPU_TRACE=1: wall-clock (entry, exit) of the three pairings of the last round
@@ -48,7 +48,8 @@ struct alignas(64) SchedShm {
     std::atomic<uint32_t> ready_count;   // joins so far, all ranks (issue-ring append)
     std::atomic<uint32_t> setup_err;     // ranks whose registration failed (creation vote)
     std::atomic<uint64_t> sig[kMaxRanks];   // creation signature of rank r: kind, dtype, tag
-    IpcSlot slot[kMaxRanks];
+    IpcSlot slot[kMaxRanks];   // rank r's receive bucket (peers read shard q of it in phase 1)
+    IpcSlot pub[kMaxRanks];    // rank r's reduced shard, published for the all-gather
 };
 
 // Global issue order for transports whose collectives must be issued in the same
