@@ -316,8 +316,9 @@ def _max_over_ranks(x: float) -> float:
 
 def sweep_c5(comm, dev, world, dt, es):
     """C5: majority-allreduce of one bucket per rank, 64 KiB .. 1 GiB (every 2x).  Per
-    size: `iters` back-to-back rounds, each timed post -> wait on every rank; a round's
-    time is its max over ranks; reported: the median round and the mean round."""
+    size: 20 warm-up rounds, then 50 back-to-back rounds, each timed
+    post -> wait on every rank; a round's time is its max over ranks; reported: the
+    median round and the mean round."""
     import statistics
 
     import torch
@@ -325,14 +326,14 @@ def sweep_c5(comm, dev, world, dt, es):
     out = []
     for lg in range(16, 31):   # the 15 sizes of SURVEY.md §8(d), 64 KiB .. 1 GiB
         nbytes = 1 << lg
-        iters = 50 if nbytes <= (16 << 20) else (20 if nbytes <= (256 << 20) else 10)
+        iters = 50
         count = nbytes // es
         buf = dev.DeviceBuffer(count, dt)
         dev.fill_uniform(buf, SEED, comm.rank())
         dev.synchronize()
         sch = comm.Schedule(comm.MAJORITY, None, buf, count, dtype=dt, seed=6545343,
                             buf=comm.BUF_DEVICE)
-        for _ in range(5):
+        for _ in range(20):
             sch.post(); sch.wait()
         comm.barrier()
         ts = []

@@ -61,7 +61,7 @@ bool round_is_sync(const Sched &s, uint32_t round) {
     }
 }
 
-static std::atomic<int> g_active{0};   // schedules with a round in flight
+static std::atomic<int> g_active{0};   // schedules with a round in flight or a post pending
 
 // A process that exits without fffinalize / esgd_comm_finalize must not die in
 // std::thread's destructor: stop and join the progress thread at static destruction.
@@ -437,7 +437,7 @@ Sched *sched_lookup(uint64_t handle) {
 
 static bool step(Sched &s) {
     std::lock_guard<std::mutex> lk(s.mu);
-    if (s.error || !s.live.load()) return false;
+    if (s.error || !s.live.load()) { s.awaiting = false; return false; }
     SchedShm *sh = s.sh;
     auto enter = [&](Stage st) { s.stage = st; s.stage_t0 = now_s(); };
     auto check = [&](int rc, const char *what) {
@@ -450,12 +450,16 @@ static bool step(Sched &s) {
     };
     switch (s.stage) {
     case ST_IDLE: {
+        s.awaiting = false;
         if (s.held) return false;   // the caller still reads the last round's buckets
         const uint32_t next = s.joined + 1;
         const bool sync = round_is_sync(s, next);
         const uint32_t posted = s.posted.load(std::memory_order_acquire);
         const bool go = sync ? posted >= next : sh->activated.load(std::memory_order_acquire) >= next;
-        if (!go) return false;
+        if (!go) {
+            s.awaiting = posted >= next;
+            return false;
+        }
         s.cur = next;
         s.cur_fresh = posted >= next;
         s.joined = next;
@@ -579,7 +583,10 @@ bool engine_progress_once() {
     int active = 0;
     for (Sched *s : snap) {
         while (step(*s)) any = true;   // run a schedule until it has to wait
-        if (s->stage != ST_IDLE) ++active;
+        // in flight, or posted and waiting for its activation (majority: the drawn
+        // activator's post; solo: a sync round's last poster): the join is imminent and
+        // its latency adds to the round, so the thread keeps polling instead of sleeping
+        if (s->stage != ST_IDLE || s->awaiting) ++active;
     }
     g_active.store(active, std::memory_order_relaxed);
     g_epoch.fetch_add(1, std::memory_order_acq_rel);
