@@ -42,7 +42,7 @@ int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s);
 
 int round_small(int dtype, const void *const *src, void *out, void *pub, uint64_t n, int nseg,
                 const void *const *gsrc, void *const *gdst, const uint64_t *gbytes,
-                uint32_t *ready, uint32_t *reduced, uint32_t *fin, uint32_t *err,
+                const PairFlags &ready, const PairFlags &reduced, uint32_t *fin, uint32_t *err,
                 uint64_t *ts, uint32_t *counter, int rank, int world, uint32_t value,
                 long long timeout_ticks, hipStream_t s);
 
@@ -177,8 +177,85 @@ static uint32_t *dev_flag(T *host) {
                                                      reinterpret_cast<char *>(g_seg_reg)));
 }
 
-int round_sync(uint32_t *flags, int rank, int world, uint32_t value, long long timeout_ticks,
+int round_sync(const PairFlags &f, int world, uint32_t value, long long timeout_ticks,
                uint32_t *err, uint32_t errval, uint64_t *ts, uint32_t *gate, hipStream_t s);
+
+// ---- device pairing flags (ESGD_DEVICE_FLAGS=1, opt-in) ----
+// Each rank owns a page of uncached HBM (hipDeviceMallocUncached: loads and stores go to
+// memory, no cache holds a flag) with one word per (schedule, pairing, peer); a rank
+// publishes a round by storing it in its word of EVERY rank's page (peers' pages are
+// IPC-mapped, stores cross xGMI) and polls its own page -- no PCIe round trip to host
+// memory.  Opt-in: cross-GPU visibility of these stores has only been exercised with the
+// ranks sharing one GPU.  The page, like every exported buffer, is never
+// freed while the process runs; it is zeroed for every new job.
+static int device_flags_mode() {   // 0 host flags, 1 uncached HBM, 2 fine-grained HBM
+    static const int m = getenv("ESGD_DEVICE_FLAGS") ? atoi(getenv("ESGD_DEVICE_FLAGS")) : 0;
+    return m;
+}
+static bool device_flags() { return device_flags_mode() > 0; }
+constexpr size_t kPageWords = size_t(kMaxSched) * 3 * kMaxRanks;
+static uint32_t *g_page = nullptr;                 // this rank's page
+static Segment *g_page_seg = nullptr;              // the job it was published for
+static uint32_t *g_peer_page[kMaxRanks] = {};      // every rank's page (own included)
+static bool g_pages_mapped = false;
+
+static int flags_publish(int rank) {
+    std::lock_guard<std::mutex> lk(g_dp_mu);
+    Segment *seg = engine_segment();
+    if (g_page_seg == seg) return ESGD_SUCCESS;
+    if (!g_page)
+        ESGD_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&g_page), kPageWords * sizeof(uint32_t),
+                                       device_flags_mode() == 2 ? hipDeviceMallocFinegrained
+                                                                : hipDeviceMallocUncached));
+    ESGD_HIP(hipMemset(g_page, 0, kPageWords * sizeof(uint32_t)));
+    ESGD_HIP(hipDeviceSynchronize());
+    hipIpcMemHandle_t h;
+    ESGD_HIP(hipIpcGetMemHandle(&h, g_page));
+    IpcSlot &mine = seg->flagpage[rank];
+    std::memcpy(mine.handle, &h, 64);
+    mine.offset = 0;
+    mine.bytes = kPageWords * sizeof(uint32_t);
+    mine.gen.store(1, std::memory_order_release);
+    g_page_seg = seg;
+    g_pages_mapped = false;
+    return ESGD_SUCCESS;
+}
+
+// after the creation vote: every peer has published its page
+static int flags_connect(int rank, int world) {
+    std::lock_guard<std::mutex> lk(g_dp_mu);
+    if (g_pages_mapped) return ESGD_SUCCESS;
+    Segment *seg = engine_segment();
+    for (int q = 0; q < world; ++q) {
+        if (q == rank) { g_peer_page[q] = g_page; continue; }
+        if (seg->flagpage[q].gen.load(std::memory_order_acquire) != 1) {
+            set_error("device flags: rank %d did not publish its flag page (ESGD_DEVICE_FLAGS must be "
+                      "set on every rank)", q);
+            return ESGD_ERROR;
+        }
+        void *p = nullptr;
+        if (int rc = ipc_open(q, seg->flagpage[q].handle, &p)) return rc;
+        g_peer_page[q] = static_cast<uint32_t *>(p);
+    }
+    g_pages_mapped = true;
+    return ESGD_SUCCESS;
+}
+
+// the flags of pairing `which` (0 ready, 1 reduced, 2 done) of schedule s
+static PairFlags pair_flags(Sched &s, std::atomic<uint32_t> *host, int which) {
+    PairFlags f{};
+    if (device_flags()) {
+        const size_t base = (size_t(s.id) * 3 + size_t(which)) * kMaxRanks;
+        f.mine = g_page + base;
+        for (int q = 0; q < s.world; ++q) f.dst[q] = g_peer_page[q] + base + s.rank;
+        f.ndst = s.world;
+    } else {
+        f.mine = dev_flag(host);
+        f.dst[0] = dev_flag(&host[s.rank]);
+        f.ndst = 1;
+    }
+    return f;
+}
 
 static bool gpu_trace_on() {
     static const bool on = getenv("ESGD_GPU_TRACE") && *getenv("ESGD_GPU_TRACE") == '1';
@@ -203,7 +280,7 @@ static int pair_ranks(Sched &s, std::atomic<uint32_t> *flags, int which, uint32_
         if (int rc = ctr_words(s.id, cs, &ctr)) return rc;
         gate = ctr + 4 + which;
     }
-    return round_sync(dev_flag(flags), s.rank, s.world, value ? value : round, ticks,
+    return round_sync(pair_flags(s, flags, which), s.world, value ? value : round, ticks,
                       dev_flag(&s.sh->gpu_err[s.rank]), round, ts, gate, cs);
 }
 
@@ -250,6 +327,9 @@ void dataplane_shutdown() {
         if (*c) { (void)hipStreamSynchronize(*c); (void)hipStreamDestroy(*c); *c = nullptr; }
     if (g_ctr_pool) { (void)hipFree(g_ctr_pool); g_ctr_pool = nullptr; }
     ipc_close_all();
+    for (auto &p : g_peer_page) p = nullptr;   // g_page itself stays (exported memory)
+    g_pages_mapped = false;
+    g_page_seg = nullptr;
     arena_trim();
     if (g_seg_reg) { (void)hipHostUnregister(g_seg_reg); g_seg_reg = nullptr; g_seg_dev = nullptr; }
 }
@@ -505,6 +585,7 @@ static int base_complete(Sched &s, BaseState &st) {
 }
 
 static std::string base_diagnose(Sched &s) {
+    if (device_flags()) return "(pairing flags in device memory, ESGD_DEVICE_FLAGS=1)";
     std::string m = "(flags ready/reduced/done per rank:";
     char buf[64];
     for (int q = 0; q < s.world; ++q) {
@@ -668,6 +749,8 @@ struct IpcTransport final : Transport {
         st->peer[s.rank] = st->rb_dev;
         if (s.world == 1) return ESGD_SUCCESS;
         if (int rc = register_segment()) return rc;
+        if (device_flags())
+            if (int rc = flags_publish(s.rank)) return rc;
         // publish this rank's rb (peers map it in connect())
         // ESGD_SHADOW=1 shadows every device bucket (caller buckets that are freed and
         // re-allocated between rounds; also how the tests reach the fallback)
@@ -689,7 +772,10 @@ struct IpcTransport final : Transport {
     }
 
     int connect(Sched &s) override {
-        return s.world > 1 ? map_peers(s, S(s)) : ESGD_SUCCESS;
+        if (s.world == 1) return ESGD_SUCCESS;
+        if (device_flags())
+            if (int rc = flags_connect(s.rank, s.world)) return rc;
+        return map_peers(s, S(s));
     }
 
     int note_producer(Sched &s, uint32_t round, void *stream) override {
@@ -885,7 +971,7 @@ struct IpcTransport final : Transport {
         const long long ticks = (long long)(engine_timeout() * double(g_ticks_per_s));
         uint64_t *ts = gpu_trace_on() ? reinterpret_cast<uint64_t *>(dev_flag(&s.sh->gpu_ts[s.rank][0])) : nullptr;
         return round_small(s.dtype, in, st.rb_dev + st.off[s.rank] * s.esize, st.pub, st.len[s.rank], m, src,
-                           dst, bytes, dev_flag(s.sh->ready), dev_flag(s.sh->reduced),
+                           dst, bytes, pair_flags(s, s.sh->ready, 0), pair_flags(s, s.sh->reduced, 1),
                            dev_flag(&s.sh->fin[s.rank]), dev_flag(&s.sh->gpu_err[s.rank]), ts, st.ctr,
                            s.rank, s.world, round, ticks, cs);
     }

@@ -27,6 +27,19 @@ int require_device();
 inline hipStream_t as_stream(void *s) { return s ? static_cast<hipStream_t>(s) : default_stream(); }
 
 // Device memory that peers may map (arena.cpp): never given back while it may be mapped.
+// Where the flags of one rank pairing live (data plane -> round kernels).  A rank
+// publishes a round by storing it at dst[0..ndst-1] and waits until mine[0..world-1] have
+// all reached it.  Host flags (default): one shared array in the node segment, so dst is
+// this rank's own word and mine the array.  Device flags (ESGD_DEVICE_FLAGS=1): every
+// rank owns a page of uncached HBM holding one word per peer; dst is this rank's word in
+// every rank's page (peers' pages mapped over IPC), mine this rank's own words.
+constexpr int kPairMax = 16;   // = kMaxRanks
+struct PairFlags {
+    uint32_t *mine;
+    uint32_t *dst[kPairMax];
+    int ndst;
+};
+
 int arena_alloc(size_t bytes, void **out);
 bool arena_free(void *p);
 int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_t handle[64]);

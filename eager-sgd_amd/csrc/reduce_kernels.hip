@@ -711,17 +711,27 @@ int gather_remote(int n, const void *const *src, void *const *dst, const uint64_
 // leaves when all of them reached `value` -- one host-memory round trip per sweep instead
 // of one per rank (8 serial PCIe reads at P = 8).  Called by a whole wave; rounds compare
 // modulo 2^32.  False on timeout.
-__device__ __forceinline__ bool wave_wait_all(uint32_t *flags, int world, uint32_t value, long long t0,
+__device__ __forceinline__ bool wave_wait_all(const uint32_t *flags, int world, uint32_t value, long long t0,
                                               long long timeout) {
     const int lane = int(threadIdx.x & 63u);
     for (;;) {
         bool mine = true;
         if (lane < world)
-            mine = int32_t(__hip_atomic_load(&flags[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - value) >= 0;
+            mine = int32_t(__hip_atomic_load(const_cast<uint32_t *>(&flags[lane]), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM) - value) >= 0;
         if (__all(mine)) return true;
         if (wall_clock64() - t0 > timeout) return false;
         __builtin_amdgcn_s_sleep(1);
     }
+}
+
+// Publication: release at system scope, drained (MI355X_MICROARCH.md: the explicit wait
+// keeps the flag behind the write-back), then the value in every destination word -- one
+// word in host memory, or this rank's word in every rank's device flag page.  Lane 0.
+__device__ __forceinline__ void publish_flags(const PairFlags &f, uint32_t value) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int q = 0; q < f.ndst; ++q) __hip_atomic_store(f.dst[q], value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 //
@@ -733,7 +743,7 @@ __device__ __forceinline__ bool wave_wait_all(uint32_t *flags, int world, uint32
 // others wait for it and run a system-scope acquire (buffer_inv sc0 sc1).  The dispatch's
 // own acquire scope is not relied on for this.  A timed-out pairing still raises the gate
 // (the error flag fails the round), so no workgroup is left waiting.
-__global__ void __launch_bounds__(64) k_round_sync(uint32_t *flags, int rank, int world,
+__global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world,
                                                    uint32_t value, long long timeout,
                                                    uint32_t *err, uint32_t errval, uint64_t *ts,
                                                    uint32_t *gate) {
@@ -751,12 +761,10 @@ __global__ void __launch_bounds__(64) k_round_sync(uint32_t *flags, int rank, in
     }
     if (lead) {
         if (ts) ts[0] = uint64_t(wall_clock64());
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // MI355X_MICROARCH.md: compiler hazard
-        __hip_atomic_store(&flags[rank], value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        publish_flags(f, value);
     }
     const long long t0 = wall_clock64();
-    const bool ok = wave_wait_all(flags, world, value, t0, timeout);
+    const bool ok = wave_wait_all(f.mine, world, value, t0, timeout);
     if (!lead) return;
     if (!ok) __hip_atomic_store(err, errval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -767,10 +775,11 @@ __global__ void __launch_bounds__(64) k_round_sync(uint32_t *flags, int rank, in
 // ts (optional): wall-clock stamps of entry and exit (tracing, ESGD_GPU_TRACE=1);
 // errval: what a timed-out wait records in *err (the round, also when `value` numbers
 // a chunk of it)
-int round_sync(uint32_t *flags, int rank, int world, uint32_t value, long long timeout_ticks,
+int round_sync(const PairFlags &f, int world, uint32_t value, long long timeout_ticks,
                uint32_t *err, uint32_t errval, uint64_t *ts, uint32_t *gate, hipStream_t s) {
-    ESGD_ARG(flags && err && world >= 1 && rank >= 0 && rank < world, "round_sync: bad arguments");
-    hipLaunchKernelGGL(k_round_sync, dim3(gate ? unsigned(cu_count()) : 1u), dim3(64), 0, s, flags, rank, world,
+    ESGD_ARG(f.mine && err && world >= 1 && world <= kPairMax && f.ndst >= 1 && f.ndst <= kPairMax,
+             "round_sync: bad arguments");
+    hipLaunchKernelGGL(k_round_sync, dim3(gate ? unsigned(cu_count()) : 1u), dim3(64), 0, s, f, world,
                        value, timeout_ticks, err, errval, ts, gate);
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;
@@ -803,7 +812,8 @@ struct SmallRoundArgs {
     uint32_t gvec[kMaxSeg];     // 16-B vectors per segment
     uint32_t gtail[kMaxSeg];    // bytes after the last full vector
     int nseg;
-    uint32_t *ready, *reduced, *fin, *err;
+    PairFlags ready, reduced;
+    uint32_t *fin, *err;
     uint64_t *ts;               // optional GPU trace stamps (6)
     uint32_t *counter;          // device words: [0], [1] arrivals (zero between rounds),
                                 // [2], [3] gates raised to the round by the polling lane
@@ -827,7 +837,7 @@ __device__ __forceinline__ bool spin_all(uint32_t *flags, int world, uint32_t va
 // raises `gate` (a device word) to the round, and every workgroup's lane 0 polls that
 // instead -- 64 workgroups polling host memory over PCIe slowed every hand-off ~5x
 // (tools/lat.sh).  The workgroup then acquires at system scope.
-__device__ __forceinline__ bool block_wait(const SmallRoundArgs &a, uint32_t *flags, uint32_t *gate,
+__device__ __forceinline__ bool block_wait(const SmallRoundArgs &a, const uint32_t *flags, uint32_t *gate,
                                            bool leader, long long t0, int *ok) {
     if (threadIdx.x < 64) {   // the first wave
         bool good = true;
@@ -861,14 +871,6 @@ __device__ __forceinline__ bool block_count(uint32_t *ctr, int *last) {
     return *last != 0;
 }
 
-// flag publication: release at system scope; the explicit wait keeps the flag behind the
-// write-back (MI355X_MICROARCH.md, compiler hazard)
-__device__ __forceinline__ void publish_flag(uint32_t *flag, uint32_t value) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 template <class Tr, int K>
 __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
     using T = typename Tr::T;
@@ -880,9 +882,9 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
     if (lead && blockIdx.x == 0) {   // the snapshot queued before this launch has landed
         if (stamp) a.ts[0] = uint64_t(t0);
         // same protocol as k_round_sync: release at system scope, drained, then the flag
-        publish_flag(&a.ready[a.rank], a.value);
+        publish_flags(a.ready, a.value);
     }
-    if (!block_wait(a, a.ready, &a.counter[2], blockIdx.x == 0, t0, &ok)) return;
+    if (!block_wait(a, a.ready.mine, &a.counter[2], blockIdx.x == 0, t0, &ok)) return;
     if (stamp && blockIdx.x == 0) a.ts[1] = uint64_t(wall_clock64());
 
     // phase 1: the local shard, folded in tree order from every rank's rb
@@ -926,9 +928,9 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
     const bool last1 = block_count(&a.counter[0], &last);
     if (last1 && lead) {
         if (stamp) a.ts[2] = uint64_t(wall_clock64());
-        publish_flag(&a.reduced[a.rank], a.value);
+        publish_flags(a.reduced, a.value);
     }
-    if (!block_wait(a, a.reduced, &a.counter[3], last1, t0, &ok)) return;
+    if (!block_wait(a, a.reduced.mine, &a.counter[3], last1, t0, &ok)) return;
     if (stamp && blockIdx.x == 0) a.ts[3] = uint64_t(wall_clock64());
 
     // phase 2: every other rank's reduced shard into the local rb
@@ -984,7 +986,7 @@ static int launch_small_t(const SmallRoundArgs &a, unsigned grid, hipStream_t s)
 // 1 KiB aligned; segments are checked here.
 int round_small(int dtype, const void *const *src, void *out, void *pub, uint64_t n, int nseg,
                 const void *const *gsrc, void *const *gdst, const uint64_t *gbytes,
-                uint32_t *ready, uint32_t *reduced, uint32_t *fin, uint32_t *err,
+                const PairFlags &ready, const PairFlags &reduced, uint32_t *fin, uint32_t *err,
                 uint64_t *ts, uint32_t *counter, int rank, int world, uint32_t value,
                 long long timeout_ticks, hipStream_t s) {
     ESGD_ARG(world >= 2 && world <= ESGD_MAX_FANIN && nseg >= 0 && nseg < kMaxSeg,

@@ -78,6 +78,8 @@ struct Segment {
     std::atomic<int32_t> pid[kMaxRanks];
     std::atomic<int32_t> device[kMaxRanks];
     std::atomic<uint64_t> ticket_next;
+    // ESGD_DEVICE_FLAGS=1: rank r's pairing-flag page (uncached HBM, dataplane.cpp)
+    IpcSlot flagpage[kMaxRanks];
     TicketSlot ring[kRing];
     SchedShm sched[kMaxSched];
 };
