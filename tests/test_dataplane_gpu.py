@@ -37,6 +37,18 @@ def test_allreduce_ragged_and_tiny(world, path):
         assert all(all(v) for v in verdicts), (count, verdicts)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("world", [2, 3])
+def test_device_pairing_flags(world, mode):
+    # ESGD_DEVICE_FLAGS (opt-in): pairing flags in uncached (1) / fine-grained (2) HBM pages,
+    # every kind of round: one launch, five launches, chunked host buckets, majority
+    for kw in (dict(count=4099, small_bytes=4 << 20), dict(count=300007, small_bytes=0),
+               dict(count=(32 << 20) // 4 + 5, buf="host", host_chunk=16 << 20),
+               dict(count=65536, kind=2)):
+        verdicts = run("gpu_allreduce", world, rounds=3, device_flags=mode, **kw)
+        assert all(all(v) for v in verdicts), (kw, verdicts)
+
+
 @pytest.mark.parametrize("world", [2, 5])
 def test_one_launch_rounds_back_to_back(world):
     # many consecutive one-launch rounds of one schedule (flags, counters and fin reused
