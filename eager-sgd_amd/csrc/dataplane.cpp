@@ -207,8 +207,9 @@ static int flags_publish(int rank) {
         ESGD_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&g_page), kPageWords * sizeof(uint32_t),
                                        device_flags_mode() == 2 ? hipDeviceMallocFinegrained
                                                                 : hipDeviceMallocUncached));
-    ESGD_HIP(hipMemset(g_page, 0, kPageWords * sizeof(uint32_t)));
-    ESGD_HIP(hipDeviceSynchronize());
+    // the null stream: rounds run on non-blocking streams, nothing in flight is waited for
+    ESGD_HIP(hipMemsetAsync(g_page, 0, kPageWords * sizeof(uint32_t), nullptr));
+    ESGD_HIP(hipStreamSynchronize(nullptr));
     hipIpcMemHandle_t h;
     ESGD_HIP(hipIpcGetMemHandle(&h, g_page));
     IpcSlot &mine = seg->flagpage[rank];
