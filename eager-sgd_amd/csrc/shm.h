@@ -38,10 +38,11 @@ struct alignas(64) SchedShm {
     // GPU flags (written by the GPUs through the host-registered segment, system scope):
     alignas(64) std::atomic<uint32_t> ready[kMaxRanks];   // round whose snapshot rank r has made
     alignas(64) std::atomic<uint32_t> reduced[kMaxRanks]; // round whose reduce-scatter is done
-    alignas(64) std::atomic<uint32_t> done[kMaxRanks];    // chunk whose all-gather is done (chunked host rounds)
+    alignas(64) std::atomic<uint32_t> done[kMaxRanks];    // round (chunk, chunked host rounds) whose all-gather
+                                                          // is done; one-launch rounds have no done pairing
     alignas(64) std::atomic<uint32_t> gpu_err[kMaxRanks]; // round whose flag wait timed out
     alignas(64) std::atomic<uint32_t> fin[kMaxRanks];     // round a one-launch round finished
-    // ESGD_GPU_TRACE=1: wall-clock (entry, exit) of the three pairings of the last round
+    // ESGD_GPU_TRACE=1: wall-clock (entry, exit) of the pairings of the last round
     alignas(64) uint64_t gpu_ts[kMaxRanks][6];
     std::atomic<uint32_t> joined[kMaxRanks];  // diagnostics: last round rank r joined
     std::atomic<uint32_t> activations[kMaxRanks];  // diagnostics: rounds activated by r
