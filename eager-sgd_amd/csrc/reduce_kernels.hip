@@ -931,7 +931,9 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
         publish_flags(a.reduced, a.value);
     }
     if (!block_wait(a, a.reduced.mine, &a.counter[3], last1, t0, &ok)) return;
-    if (stamp && blockIdx.x == 0) a.ts[3] = uint64_t(wall_clock64());
+    // the all-gather span is stamped by ONE workgroup (the last to finish): the wall
+    // clocks of different XCDs are not aligned to the microsecond
+    const uint64_t t_gather = stamp ? uint64_t(wall_clock64()) : 0;
 
     // phase 2: every other rank's reduced shard into the local rb
     for (int sg = 0; sg < a.nseg; ++sg) {
@@ -961,7 +963,10 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
     // next round's phase 1 -- after that round's ready pairing, i.e. after every peer's
     // kernel of this round has finished -- and rb itself is read by peers only in phase 1.
     if (!block_count(&a.counter[1], &last) || !lead) return;
-    if (stamp) a.ts[4] = a.ts[5] = uint64_t(wall_clock64());
+    if (stamp) {
+        a.ts[3] = t_gather;
+        a.ts[4] = a.ts[5] = uint64_t(wall_clock64());
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stamps land before fin
     __hip_atomic_store(a.fin, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
