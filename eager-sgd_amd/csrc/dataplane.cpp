@@ -178,7 +178,7 @@ static uint32_t *dev_flag(T *host) {
 }
 
 int round_sync(const PairFlags &f, int world, uint32_t value, long long timeout_ticks,
-               uint32_t *err, uint32_t errval, uint64_t *ts, uint32_t *gate, hipStream_t s);
+               uint32_t *err, uint32_t errval, uint64_t *ts, uint32_t *gate, uint32_t *fin, hipStream_t s);
 
 // ---- device pairing flags (ESGD_DEVICE_FLAGS=1, opt-in) ----
 // Each rank owns a page of uncached HBM (hipDeviceMallocUncached: loads and stores go to
@@ -267,8 +267,9 @@ static int ctr_words(int sched_id, hipStream_t cs, uint32_t **out);
 
 // which = 0 ready, 1 reduced, 2 done; `value` is the round, or the chunk number of a
 // chunked round (a timeout still records the round)
+// fin: the pairing is the round's last kernel and stores the round there when it is done
 static int pair_ranks(Sched &s, std::atomic<uint32_t> *flags, int which, uint32_t round, hipStream_t cs,
-                      uint32_t value = 0) {
+                      uint32_t value = 0, std::atomic<uint32_t> *fin = nullptr) {
     const long long ticks = (long long)(engine_timeout() * double(g_ticks_per_s));
     uint64_t *ts = gpu_trace_on() ? reinterpret_cast<uint64_t *>(dev_flag(&s.sh->gpu_ts[s.rank][2 * which]))
                                   : nullptr;
@@ -282,7 +283,7 @@ static int pair_ranks(Sched &s, std::atomic<uint32_t> *flags, int which, uint32_
         gate = ctr + 4 + which;
     }
     return round_sync(pair_flags(s, flags, which), s.world, value ? value : round, ticks,
-                      dev_flag(&s.sh->gpu_err[s.rank]), round, ts, gate, cs);
+                      dev_flag(&s.sh->gpu_err[s.rank]), round, ts, gate, fin ? dev_flag(fin) : nullptr, cs);
 }
 
 // ns between the GPU stamps of the last round (ESGD_GPU_TRACE=1), for the timeline
@@ -865,7 +866,16 @@ struct IpcTransport final : Transport {
             }
             if (m)
                 if (int rc = gather_remote(m, src, dst, bytes, cs)) return rc;
-            if (int rc = pair_ranks(s, s.sh->done, 2, round, cs)) return rc;
+            // device buckets: the done pairing ends the round and reports it in fin, which
+            // the host polls (as for one-launch rounds; the event only reports faults)
+            const bool last = !s.host_mode && !st.shadow;
+            if (int rc = pair_ranks(s, s.sh->done, 2, round, cs, 0, last ? &s.sh->fin[s.rank] : nullptr))
+                return rc;
+            if (last) {
+                st.fin_mode = true;
+                ESGD_HIP(hipEventRecord(st.ev, cs));
+                return ESGD_SUCCESS;
+            }
         }
         return base_copy_out(s, st, cs);
     }

@@ -746,7 +746,7 @@ __device__ __forceinline__ void publish_flags(const PairFlags &f, uint32_t value
 __global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world,
                                                    uint32_t value, long long timeout,
                                                    uint32_t *err, uint32_t errval, uint64_t *ts,
-                                                   uint32_t *gate) {
+                                                   uint32_t *gate, uint32_t *fin) {
     const bool lead = threadIdx.x == 0;
     if (blockIdx.x != 0) {   // cache maintenance only
         if (lead) {
@@ -770,17 +770,22 @@ __global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world,
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     if (gate) __hip_atomic_store(gate, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ok && ts) __hip_atomic_store(&ts[1], uint64_t(wall_clock64()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // the round's last kernel reports completion itself (the host polls fin, not an event)
+    if (ok && fin) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(fin, errval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ts (optional): wall-clock stamps of entry and exit (tracing, ESGD_GPU_TRACE=1);
 // errval: what a timed-out wait records in *err (the round, also when `value` numbers
 // a chunk of it)
 int round_sync(const PairFlags &f, int world, uint32_t value, long long timeout_ticks,
-               uint32_t *err, uint32_t errval, uint64_t *ts, uint32_t *gate, hipStream_t s) {
+               uint32_t *err, uint32_t errval, uint64_t *ts, uint32_t *gate, uint32_t *fin, hipStream_t s) {
     ESGD_ARG(f.mine && err && world >= 1 && world <= kPairMax && f.ndst >= 1 && f.ndst <= kPairMax,
              "round_sync: bad arguments");
     hipLaunchKernelGGL(k_round_sync, dim3(gate ? unsigned(cu_count()) : 1u), dim3(64), 0, s, f, world,
-                       value, timeout_ticks, err, errval, ts, gate);
+                       value, timeout_ticks, err, errval, ts, gate, fin);
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;
 }
