@@ -457,6 +457,45 @@ def c3_over_rccl(comm, dev, rank, world, count, steps=20):
             "xgmi_frac": round(t_min / t, 4), "parity_rank_slice": "bitwise" if ok else "MISMATCH"}
 
 
+def c1_host_majority(comm, dev, rank, world, count=262144, warmup=20, iters=50):
+    """BASELINE's C1 shape on the GPU path and the reference's contract: majority-allreduce
+    of a 1 MiB fp32 HOST bucket (calloc'd in the wrapper, opt_esgd_majority...py:288-298;
+    pinned here at creation), seed 6545343 (:252), every rank posting every round: each
+    round is H2D -> one-launch round -> D2H.  Timed post -> wait, max over ranks, median
+    of `iters` rounds; the CPU restatement of the same shape is `cpu_baseline_c1`."""
+    import statistics
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from oracle import ffref
+    host = np.zeros(count, np.float32)
+    sch = comm.Schedule(comm.MAJORITY, None, host, count, seed=6545343, buf=comm.BUF_HOST)
+    x = ffref.fill_uniform(SEED, rank, count)
+    for _ in range(warmup):
+        host[:] = x
+        sch.post(); sch.wait()
+    ts = []
+    for _ in range(iters):
+        host[:] = x
+        comm.barrier()
+        t0 = time.perf_counter()
+        sch.post(); sch.wait()
+        ts.append(time.perf_counter() - t0)
+    tt = torch.tensor(ts, dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t = statistics.median(tt.tolist())
+    want = ffref.tree_sum([ffref.fill_uniform(SEED, r, count) for r in range(world)])
+    ok = bool(np.array_equal(host.view(np.uint32), want.view(np.uint32)))
+    stages = _stages_us(sch.timeline()[-iters:])
+    _defer(sch)
+    S = count * 4
+    return {"bucket_bytes": S, "round_us_median": round(t * 1e6, 1),
+            "value_GBs": round(world * S / t / 1e9, 3), "rounds": iters,
+            "parity": "bitwise" if ok else "MISMATCH", "rank0_stages_us": stages}
+
+
 def c3_host_buckets(comm, dev, rank, world, count, steps=8):
     """C3 on the reference's own contract: the bucket lives in host memory (the wrapper's
     calloc'd buckets, opt_esgd_solo_imagenet_imbalance.py:288-298), so each round is
@@ -725,6 +764,7 @@ def run_allreduce(args, rank, world):
         # alive until the end, and small rounds measured after them were bimodal
         legs = [("sweep_c5_majority", lambda: sweep_c5(comm, dev, world, dt, es)),
                 ("sweep_c5_majority_bf16", lambda: sweep_c5(comm, dev, world, _lib.BF16, 2)),
+                ("c1_host_majority", lambda: c1_host_majority(comm, dev, rank, world)),
                 ("straggler_c4_majority", lambda: straggler_c4(comm, dev, rank, world)),
                 ("c4_resnet50_161_vs_fused", lambda: c4_resnet50_161(comm, dev, rank, world)),
                 ("c3_host_buckets", lambda: c3_host_buckets(comm, dev, rank, world,

@@ -39,6 +39,7 @@ int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64
 int gather_remote(int n, const void *const *src, void *const *dst, const uint64_t *bytes,
                   hipStream_t s);
 int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s);
+int store_fin(uint32_t *fin, uint32_t value, hipStream_t s);
 
 int round_small(int dtype, const void *const *src, void *out, void *pub, uint64_t n, int nseg,
                 const void *const *gsrc, void *const *gdst, const uint64_t *gbytes,
@@ -175,6 +176,16 @@ template <class T>
 static uint32_t *dev_flag(T *host) {
     return reinterpret_cast<uint32_t *>(g_seg_dev + (reinterpret_cast<char *>(host) -
                                                      reinterpret_cast<char *>(g_seg_reg)));
+}
+
+// the device address of pinned host memory (nullptr: not mapped, use DMA copies)
+static void *host_view(void *host) {
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return d;
 }
 
 int round_sync(const PairFlags &f, int world, uint32_t value, long long timeout_ticks,
@@ -353,6 +364,9 @@ struct BaseState {
     // through this pinned staging buffer: host memcpy + DMA, never an async copy into
     // pageable memory whose completion an event would not cover
     char *pin = nullptr;
+    // device views of the pinned host buffers (registered caller buckets, the staging
+    // buffer): small host rounds move through them by kernel (host_move)
+    char *view_sb = nullptr, *view_rb = nullptr, *view_pin = nullptr;
     size_t pin_cap = 0;
     bool copyout_pending = false;
     bool fin_mode = false;            // the round in flight reports through SchedShm::fin
@@ -433,11 +447,15 @@ static int base_setup(Sched &s, BaseState &st) {
         st.owns_rb = true;
         // pin the caller's persistent host buckets so the move / copy-out are DMA
         // (not for FFCOLL_BUFFERS: those move every round)
-        if (!s.resolve && bytes && s.rb && hipHostRegister(s.rb, bytes, hipHostRegisterDefault) == hipSuccess)
+        if (!s.resolve && bytes && s.rb && hipHostRegister(s.rb, bytes, hipHostRegisterMapped) == hipSuccess) {
             st.reg_rb = true;
+            st.view_rb = static_cast<char *>(host_view(s.rb));
+        }
         if (!s.resolve && bytes && s.sb && s.sb != s.rb &&
-            hipHostRegister(s.sb, bytes, hipHostRegisterDefault) == hipSuccess)
+            hipHostRegister(s.sb, bytes, hipHostRegisterMapped) == hipSuccess) {
             st.reg_sb = true;
+            st.view_sb = static_cast<char *>(host_view(s.sb));
+        }
         (void)hipGetLastError();   // "already registered" is fine
     } else {
         if (!s.rb) { set_error("schedule: null receive buffer"); return ESGD_INVALID_ARG; }
@@ -507,6 +525,31 @@ static bool debug_on() {
         if (debug_on()) { fprintf(stderr, "[esgd] " __VA_ARGS__); fflush(stderr); } \
     } while (0)
 
+// Host buckets up to this many bytes move between host memory and HBM by kernel: the
+// round's stream reads / writes the pinned bucket directly over PCIe (16-B system-scope
+// loads, all in flight at once) instead of a DMA copy, whose fixed cost dominates small
+// buckets (C1, 1 MiB: DESIGN.md §7).  ESGD_HOST_KERNEL_COPY_BYTES overrides (0 = never).
+static uint64_t host_kernel_copy_bytes() {
+    static const uint64_t v = [] {
+        const char *e = getenv("ESGD_HOST_KERNEL_COPY_BYTES");
+        return (e && *e) ? uint64_t(strtoull(e, nullptr, 10)) : (uint64_t(4) << 20);
+    }();
+    return v;
+}
+
+// dst <- src, one of them pinned host memory with device view `view` (or nullptr)
+static int host_move(void *dst, const void *src, const void *view, bool h2d, size_t bytes, hipStream_t cs) {
+    const void *ks = h2d ? view : src;
+    void *kd = h2d ? dst : const_cast<void *>(view);
+    if (view && bytes <= host_kernel_copy_bytes() &&
+        ((reinterpret_cast<uintptr_t>(ks) | reinterpret_cast<uintptr_t>(kd)) & 15) == 0) {
+        const uint64_t b = bytes;
+        return gather_remote(1, &ks, &kd, &b, cs);
+    }
+    ESGD_HIP(hipMemcpyAsync(dst, src, bytes, h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, cs));
+    return ESGD_SUCCESS;
+}
+
 static bool staged(Sched &s, BaseState &st) {
     return s.host_mode && (s.resolve || !st.reg_rb || (s.sb && s.sb != s.rb && !st.reg_sb));
 }
@@ -515,8 +558,9 @@ static int ensure_pin(BaseState &st, size_t bytes) {
     if (bytes <= st.pin_cap) return ESGD_SUCCESS;
     if (st.pin) ESGD_HIP(hipHostFree(st.pin));
     st.pin = nullptr;
-    ESGD_HIP(hipHostMalloc(reinterpret_cast<void **>(&st.pin), bytes, hipHostMallocDefault));
+    ESGD_HIP(hipHostMalloc(reinterpret_cast<void **>(&st.pin), bytes, hipHostMallocMapped));
     st.pin_cap = bytes;
+    st.view_pin = static_cast<char *>(host_view(st.pin));
     return ESGD_SUCCESS;
 }
 
@@ -549,8 +593,10 @@ static int base_copy_in(Sched &s, BaseState &st, uint32_t round, bool fresh, hip
     const size_t bytes = s.count * s.esize;
     if (!bytes) return ESGD_SUCCESS;
     if (s.host_mode) {
-        const void *src = staged(s, st) ? st.pin : (s.sb ? s.sb : s.rb);
-        ESGD_HIP(hipMemcpyAsync(st.rb_dev, src, bytes, hipMemcpyHostToDevice, cs));
+        const bool stg = staged(s, st);
+        const void *src = stg ? st.pin : (s.sb ? s.sb : s.rb);
+        const void *view = stg ? st.view_pin : (s.sb ? st.view_sb : st.view_rb);
+        if (int rc = host_move(st.rb_dev, src, view, true, bytes, cs)) return rc;
     } else if (s.zero_sb) {
         // the move and the wrapper's zero-after-use in one pass: rb = sb, sb = 0
         if (int rc = move_zero(st.rb_dev, s.sb, bytes, cs)) return rc;
@@ -561,21 +607,32 @@ static int base_copy_in(Sched &s, BaseState &st, uint32_t round, bool fresh, hip
 }
 
 // queued at launch, last: the copy-out and the round's completion event
+// The end of every queued round: a one-lane kernel stores the round in the rank's fin
+// word (polled by the progress thread) behind everything queued before it; the event
+// after it only reports faults.  Without the registered node segment (a world of one
+// that never needed it) completion is the event's.
+static int finish_round(Sched &s, BaseState &st, hipStream_t cs) {
+    st.fin_mode = g_seg_reg != nullptr && g_seg_reg == engine_segment();
+    if (st.fin_mode)
+        if (int rc = store_fin(dev_flag(&s.sh->fin[s.rank]), s.cur, cs)) return rc;
+    ESGD_HIP(hipEventRecord(st.ev, cs));
+    return ESGD_SUCCESS;
+}
+
 static int base_copy_out(Sched &s, BaseState &st, hipStream_t cs) {
     const size_t bytes = s.count * s.esize;
     if (s.host_mode && bytes) {
         if (staged(s, st)) {
             if (int rc = ensure_pin(st, bytes)) return rc;
-            ESGD_HIP(hipMemcpyAsync(st.pin, st.rb_dev, bytes, hipMemcpyDeviceToHost, cs));
+            if (int rc = host_move(st.pin, st.rb_dev, st.view_pin, false, bytes, cs)) return rc;
             st.copyout_pending = true;
         } else {
-            ESGD_HIP(hipMemcpyAsync(s.rb, st.rb_dev, bytes, hipMemcpyDeviceToHost, cs));
+            if (int rc = host_move(s.rb, st.rb_dev, st.view_rb, false, bytes, cs)) return rc;
         }
     } else if (st.shadow && bytes) {
         ESGD_HIP(hipMemcpyAsync(s.rb, st.rb_dev, bytes, hipMemcpyDeviceToDevice, cs));
     }
-    ESGD_HIP(hipEventRecord(st.ev, cs));
-    return ESGD_SUCCESS;
+    return finish_round(s, st, cs);
 }
 
 static int base_complete(Sched &s, BaseState &st) {
@@ -599,7 +656,7 @@ static std::string base_diagnose(Sched &s) {
 }
 
 static int base_query(Sched &s, BaseState &st) {
-    if (st.fin_mode) {   // a one-launch round: its last workgroup writes fin
+    if (st.fin_mode) {   // the round's last kernel writes fin (finish_round, k_round_small, done pairing)
         if (int32_t(s.sh->fin[s.rank].load(std::memory_order_acquire) - s.cur) >= 0) {
             // the kernel may still be retiring (not ready is fine); a fault is reported
             // against this round, not a later one
@@ -957,8 +1014,7 @@ struct IpcTransport final : Transport {
         ESGD_HIP(hipStreamWaitEvent(cs, st.cev[3 * (C - 1) + 2], 0));   // ds is in order
         st.copyout_pending = stg;
         st.chunked_before = true;
-        ESGD_HIP(hipEventRecord(st.ev, cs));
-        return ESGD_SUCCESS;
+        return finish_round(s, st, cs);
     }
 
     // the whole round as one k_round_small launch (small buckets)
@@ -983,7 +1039,8 @@ struct IpcTransport final : Transport {
         uint64_t *ts = gpu_trace_on() ? reinterpret_cast<uint64_t *>(dev_flag(&s.sh->gpu_ts[s.rank][0])) : nullptr;
         return round_small(s.dtype, in, st.rb_dev + st.off[s.rank] * s.esize, st.pub, st.len[s.rank], m, src,
                            dst, bytes, pair_flags(s, s.sh->ready, 0), pair_flags(s, s.sh->reduced, 1),
-                           dev_flag(&s.sh->fin[s.rank]), dev_flag(&s.sh->gpu_err[s.rank]), ts, st.ctr,
+                           (s.host_mode || st.shadow) ? nullptr : dev_flag(&s.sh->fin[s.rank]),
+                           dev_flag(&s.sh->gpu_err[s.rank]), ts, st.ctr,
                            s.rank, s.world, round, ticks, cs);
     }
 

@@ -614,7 +614,20 @@ static int reduce_impl(int dtype, int k, const void *const *inputs, void *out, u
     return ESGD_INVALID_ARG;
 }
 
+// A round's completion word, stored by the GPU once everything queued before it on the
+// stream is done (copy-outs included): the host polls it instead of an event, whose
+// completion reaches the host several microseconds later.
+__global__ void __launch_bounds__(64) k_store_fin(uint32_t *fin, uint32_t value) {
+    if (threadIdx.x == 0) __hip_atomic_store(fin, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---- internal entry points of the data plane (dataplane.cpp) ----
+int store_fin(uint32_t *fin, uint32_t value, hipStream_t s) {
+    hipLaunchKernelGGL(k_store_fin, dim3(1), dim3(64), 0, s, fin, value);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
 int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s) {
     if (!bytes) return ESGD_SUCCESS;
     if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0) {
@@ -973,7 +986,8 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
         a.ts[4] = a.ts[5] = uint64_t(wall_clock64());
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the stamps land before fin
-    __hip_atomic_store(a.fin, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // no fin when a copy-out follows on the stream (its own finish reports the round)
+    if (a.fin) __hip_atomic_store(a.fin, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <class Tr>
