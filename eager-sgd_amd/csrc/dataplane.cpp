@@ -445,8 +445,9 @@ static int base_setup(Sched &s, BaseState &st) {
                                   &st.rb_dev, &st.cap))
             return rc;
         st.owns_rb = true;
-        // pin the caller's persistent host buckets so the move / copy-out are DMA
-        // (not for FFCOLL_BUFFERS: those move every round)
+        // pin (and map) the caller's persistent host buckets so the move / copy-out go
+        // straight between them and HBM: DMA, or by kernel through the device view for
+        // small buckets (host_move); not for FFCOLL_BUFFERS, whose buffers move every round
         if (!s.resolve && bytes && s.rb && hipHostRegister(s.rb, bytes, hipHostRegisterMapped) == hipSuccess) {
             st.reg_rb = true;
             st.view_rb = static_cast<char *>(host_view(s.rb));
