@@ -953,22 +953,32 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
     // clocks of different XCDs are not aligned to the microsecond
     const uint64_t t_gather = stamp ? uint64_t(wall_clock64()) : 0;
 
-    // phase 2: every other rank's reduced shard into the local rb
-    for (int sg = 0; sg < a.nseg; ++sg) {
-        const uint32_t gv = a.gvec[sg];
-        if (gv) {
+    // phase 2: every other rank's reduced shard into the local rb.
+    // The segments' 1024-vector chunks are dealt over the grid as ONE list, so every
+    // workgroup has work whatever the segment sizes (segment by segment, only
+    // gvec / 1024 workgroups were busy at a time -- half the grid at P = 2).
+    {
+        uint32_t total = 0;
+        for (int sg = 0; sg < a.nseg; ++sg) total += (a.gvec[sg] + 1023u) / 1024u;
+        int sg = 0;
+        uint32_t base = 0;   // first chunk index of segment sg
+        for (uint32_t c = blockIdx.x; c < total; c += gridDim.x) {
+            while (c >= base + (a.gvec[sg] + 1023u) / 1024u) base += (a.gvec[sg++] + 1023u) / 1024u;
+            const uint32_t gv = a.gvec[sg];
             __amdgpu_buffer_rsrc_t gs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(a.gsrc[sg]), (short)0,
                                                                          int(gv * 16u), 0x00020000);
             __amdgpu_buffer_rsrc_t gd = __builtin_amdgcn_make_buffer_rsrc(a.gdst[sg], (short)0, int(gv * 16u),
                                                                          0x00020000);
-            for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < gv; i += gridDim.x * 1024) {
-                raw16 r[4];
+            const uint32_t i = (c - base) * 1024u + threadIdx.x;
+            raw16 r[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b128(gs, (i + u * 256) * 16, 0, 17);
+            for (int u = 0; u < 4; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b128(gs, (i + u * 256) * 16, 0, 17);
 #pragma unroll
-                for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(r[u], gd, (i + u * 256) * 16, 0, 17);
-            }
+            for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(r[u], gd, (i + u * 256) * 16, 0, 17);
         }
+    }
+    for (int sg = 0; sg < a.nseg; ++sg) {   // ragged tails (bytes after the last vector)
+        const uint32_t gv = a.gvec[sg];
         if (blockIdx.x == 0 && threadIdx.x < a.gtail[sg]) {
             const uint8_t *src = static_cast<const uint8_t *>(a.gsrc[sg]) + size_t(gv) * 16;
             uint8_t *dst = static_cast<uint8_t *>(a.gdst[sg]) + size_t(gv) * 16;
