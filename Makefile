@@ -16,7 +16,7 @@ HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off \
              -Iinclude -I$(CSRC) -Wall -Wno-unused-result -D__HIP_PLATFORM_AMD__
 CXXFLAGS  := -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -I$(CSRC) \
              -I$(ROCM)/include -D__HIP_PLATFORM_AMD__ -Wall
-LDFLAGS   := -shared -L$(ROCM)/lib -lamdhip64 -lrccl -lpthread -lrt \
+LDFLAGS   := -shared -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -lpthread -lrt \
              -Wl,--no-undefined -Wl,-soname,libesgd.so \
              -Wl,--version-script=$(CSRC)/exports.map
 

@@ -13,6 +13,7 @@
 #include "engine.h"
 
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -59,6 +60,15 @@ bool round_is_sync(const Sched &s, uint32_t round) {
     case KIND_MAJORITY: return false;
     default: return true;
     }
+}
+
+// ESGD_ROCTX=1: roctx ranges for rocprofv3 --marker-trace (SURVEY.md §5 "tracing"): one
+// range per round from join to completion ("esgd s<id> r<round>"), one per launch and one
+// per blocking wait; the kernels of a round appear in the kernel trace by name
+// (k_round_small, k_round_sync, k_tree_sum_buf, k_gather).
+static bool roctx_on() {
+    static const bool on = getenv("ESGD_ROCTX") && *getenv("ESGD_ROCTX") == '1';
+    return on;
 }
 
 static std::atomic<int> g_active{0};   // schedules with a round in flight or a post pending
@@ -163,6 +173,7 @@ void Sched::mark(uint32_t round, int what) {   // caller holds mu
 }
 
 static void fail_locked(Sched &s, int rc, const char *msg) {
+    if (s.roctx_round) { roctxRangeStop(s.roctx_round); s.roctx_round = 0; }
     s.error = rc ? rc : ESGD_ERROR;
     snprintf(s.errmsg, sizeof(s.errmsg), "schedule %d round %u: %s", s.id, s.cur, msg);
     s.cv.notify_all();
@@ -347,6 +358,7 @@ int sched_wait_ex(Sched *s, int *fresh) {
         return ((e && *e) ? atof(e) : 200.0) * 1e-6;
     }();
     const double t0 = now_s();
+    if (roctx_on()) roctxRangePushA("esgd wait");
     while (int32_t(s->completed_a.load(std::memory_order_acquire) - target) < 0 && now_s() - t0 < spin_s)
         std::this_thread::yield();
     std::unique_lock<std::mutex> lk(s->mu);
@@ -357,6 +369,7 @@ int sched_wait_ex(Sched *s, int *fresh) {
             break;
         }
     }
+    if (roctx_on()) roctxRangePop();
     if (s->error) { set_error("%s", s->errmsg); return s->error; }
     s->waited = target;
     s->mark(target, 5);
@@ -474,6 +487,11 @@ static bool step(Sched &s) {
             s.log.push_back({next, uint8_t(s.cur_fresh), uint8_t(sync),
                              int16_t(sync ? -1 : activator_of(sh, next))});
         if (!check(s.tp->prepare(s, next, s.cur_fresh), "join")) return true;
+        if (roctx_on()) {
+            char name[64];
+            snprintf(name, sizeof(name), "esgd s%d r%u%s", s.id, next, s.cur_fresh ? "" : " (auto)");
+            s.roctx_round = roctxRangeStartA(name);
+        }
         enter(ST_WAIT_TICKET);
         // the rank whose join completes the round appends it to the issue ring (every
         // rank has joined round t-1 of this schedule before any joins round t)
@@ -512,6 +530,7 @@ static bool step(Sched &s) {
             for (int k = 0; k < 6; ++k) s.tl[s.cur - 1][6 + k] = g[k];
         }
         if (!check(s.tp->complete(s), "round")) return true;
+        if (s.roctx_round) { roctxRangeStop(s.roctx_round); s.roctx_round = 0; }
         s.completed = s.cur;
         s.completed_a.store(s.cur, std::memory_order_release);
         s.stage = ST_IDLE;
@@ -542,7 +561,9 @@ static bool pump_tickets(const std::vector<Sched *> &snap) {
                 break;
             } else {
                 target->mark(target->cur, 2);
+                if (roctx_on()) roctxRangePushA("esgd launch");
                 int rc = target->tp->launch(*target, target->cur, target->cur_fresh);
+                if (roctx_on()) roctxRangePop();
                 target->mark(target->cur, 3);
                 if (rc < 0) {
                     std::string m = std::string("launch: ") + esgd_last_error();
