@@ -496,6 +496,37 @@ def c1_host_majority(comm, dev, rank, world, count=262144, warmup=20, iters=50):
             "parity": "bitwise" if ok else "MISMATCH", "rank0_stages_us": stages}
 
 
+def small_round_after_idle(comm, dev, rank, world, count=16384, iters=30, idle_s=0.002):
+    """A 64 KiB majority round after every rank has been idle for `idle_s` (the training
+    pattern: buckets are posted once per backward pass, the progress threads sleep in
+    between), post -> wait, max over ranks, median.  Compare with C5's back-to-back
+    64 KiB round: the difference is the cost of waking up."""
+    import statistics
+
+    import torch
+    import torch.distributed as dist
+    buf = dev.DeviceBuffer(count)
+    dev.fill_uniform(buf, SEED, rank)
+    dev.synchronize()
+    sch = comm.Schedule(comm.MAJORITY, None, buf, count, seed=6545343, buf=comm.BUF_DEVICE)
+    for _ in range(5):
+        sch.post(); sch.wait()
+    ts = []
+    for _ in range(iters):
+        comm.barrier()
+        time.sleep(idle_s)
+        t0 = time.perf_counter()
+        sch.post(); sch.wait()
+        ts.append(time.perf_counter() - t0)
+    tt = torch.tensor(ts, dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    stages = _stages_us(sch.timeline()[-iters:])
+    _defer(sch, buf)
+    return {"bucket_bytes": count * 4, "idle_ms": idle_s * 1e3,
+            "us": round(statistics.median(tt.tolist()) * 1e6, 1), "rounds": iters,
+            "rank0_stages_us": stages}
+
+
 def c3_host_buckets(comm, dev, rank, world, count, steps=8):
     """C3 on the reference's own contract: the bucket lives in host memory (the wrapper's
     calloc'd buckets, opt_esgd_solo_imagenet_imbalance.py:288-298), so each round is
@@ -765,6 +796,7 @@ def run_allreduce(args, rank, world):
         legs = [("sweep_c5_majority", lambda: sweep_c5(comm, dev, world, dt, es)),
                 ("sweep_c5_majority_bf16", lambda: sweep_c5(comm, dev, world, _lib.BF16, 2)),
                 ("c1_host_majority", lambda: c1_host_majority(comm, dev, rank, world)),
+                ("small_round_after_idle", lambda: small_round_after_idle(comm, dev, rank, world)),
                 ("straggler_c4_majority", lambda: straggler_c4(comm, dev, rank, world)),
                 ("c4_resnet50_161_vs_fused", lambda: c4_resnet50_161(comm, dev, rank, world)),
                 ("c3_host_buckets", lambda: c3_host_buckets(comm, dev, rank, world,
