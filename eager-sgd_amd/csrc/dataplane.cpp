@@ -49,13 +49,15 @@ int round_small(int dtype, const void *const *src, void *out, void *pub, uint64_
 
 constexpr int kMaxSegs = 16;                      // segments per gather launch (kMaxSeg)
 
-// Bytes per input / segment of one remote launch (the kernels address a shard through
-// 32-bit buffer offsets): 1 GiB; ESGD_PIECE_BYTES (a multiple of 1 KiB) overrides it so
-// the tests can drive the piecewise path with small buckets.
+// Bytes per input / segment of one remote launch: 64 MiB, the local tree kernel's window
+// (reduce_kernels.hip kWindowBytes; in the shared-GPU rehearsal 64 MiB pieces took C5's
+// 256 MiB - 1 GiB rounds 2-7 % faster than 1 GiB ones), at most 1 GiB (the kernels
+// address a shard through 32-bit buffer offsets).  ESGD_PIECE_BYTES (a multiple of
+// 1 KiB) overrides it; the tests drive the piecewise path with small pieces.
 static uint64_t piece_bytes() {
     static const uint64_t v = [] {
         const char *e = getenv("ESGD_PIECE_BYTES");
-        const uint64_t b = (e && *e) ? uint64_t(strtoull(e, nullptr, 10)) : (uint64_t(1) << 30);
+        const uint64_t b = (e && *e) ? uint64_t(strtoull(e, nullptr, 10)) : (uint64_t(64) << 20);
         return std::max<uint64_t>(1024, std::min<uint64_t>(b, uint64_t(1) << 30) / 1024 * 1024);
     }();
     return v;

@@ -191,8 +191,9 @@ def download_slice(buf, start, m):
 
 
 def test_reduce_beyond_int32_elements():
-    """Buckets longer than 2^31 elements (8 GiB of fp32: the 64-bit flat path), checked
-    against the oracle on a head, a middle slice across element 2^31, and the ragged tail."""
+    """Buckets longer than 2^31 elements (8 GiB of fp32: 128 windowed launches, each inside
+    the buffer descriptors' 32-bit range), checked against the oracle on a head, a middle
+    slice across element 2^31, and the ragged tail."""
     n, k, seed, m = (1 << 31) + 5, 2, 0x5EED0B16, 1 << 20
     bufs = [DeviceBuffer(n) for _ in range(k)]
     for r, b in enumerate(bufs):
