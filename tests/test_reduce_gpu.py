@@ -220,3 +220,35 @@ def test_full_size_gate_256mib_bitwise():
     del bufs
     xs = [ffref.fill_uniform(seed, r, n) for r in range(k)]
     bits_equal(got, ffref.tree_sum(xs))
+
+
+def _download(buf, start, m, np_dtype):
+    from esgd._lib import check, lib
+    out = np.empty(m, np_dtype)
+    es = out.itemsize
+    check(lib().esgd_memcpy_async(out.ctypes.data, buf.ptr + start * es, m * es, 1, None), "d2h")
+    synchronize()
+    return out
+
+
+@pytest.mark.parametrize("dtype,n", [(_lib.FLOAT, 25 * (1 << 20) + 3), (_lib.BF16, 56 * (1 << 20) + 5)])
+def test_windowed_buckets_ragged(dtype, n):
+    """Buckets above 96 MiB run as 64 MiB windows (launch_windows): 8 inputs of 100 MiB fp32
+    / 112 MiB bf16 with a ragged count, checked at the head, across the first window
+    boundary and at the tail."""
+    k, seed, m = 8, 0x5EED0B17, 1 << 16
+    bf = dtype == _lib.BF16
+    bufs = [DeviceBuffer(n, dtype) for _ in range(k)]
+    for r, b in enumerate(bufs):
+        fill_uniform(b, seed, r)
+    out = DeviceBuffer(n, dtype)
+    reduce(dtype, [b.ptr for b in bufs], out, n)
+    synchronize()
+    window = (64 << 20) // (2 if bf else 4)
+    for start in (0, window - m // 2, n - m):
+        xs = [ffref.fill_uniform(seed, r, m, start=start) for r in range(k)]
+        if bf:
+            want = ffref.tree_sum_bf16([ffref.f32_to_bf16(x) for x in xs])
+            np.testing.assert_array_equal(_download(out, start, m, np.uint16), want)
+        else:
+            bits_equal(_download(out, start, m, np.float32), ffref.tree_sum(xs))
