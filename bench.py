@@ -461,6 +461,61 @@ def c3_over_rccl(comm, dev, rank, world, count, steps=20):
             "xgmi_frac": round(t_min / t, 4), "parity_rank_slice": "bitwise" if ok else "MISMATCH"}
 
 
+def c3_wire_bf16(comm, dev, rank, world, count, steps=20):
+    """C3 (solo-allreduce, 256 MiB fp32 per rank) with bf16 on the wire
+    (ESGD_SCHED_WIRE_BF16): peers read a bf16 copy of every
+    bucket, half the xGMI bytes of the fp32 headline, for one more local pass.  Measured
+    A/B against the fp32 round in the same leg, the same way (median of per-step max over
+    ranks).  The result is the bf16-rounded tree (an extension; parity vs the oracle's
+    convention on head/tail slices).  xgmi_frac is against the wire bytes:
+    t_min = 2 (S/2) / (P x 153 GB/s)."""
+    import numpy as np
+
+    from oracle import ffref
+    rb = dev.DeviceBuffer(count)
+    dev.fill_uniform(rb, SEED, rank)
+    dev.synchronize()
+    sw = comm.Schedule(comm.SOLO, None, rb, count, async_=32, seed=6545343, buf=comm.BUF_DEVICE,
+                       flags=comm.WIRE_BF16)
+    sf = comm.Schedule(comm.SOLO, None, rb, count, async_=32, seed=6545343, buf=comm.BUF_DEVICE)
+
+    def stepper(sch):
+        def step():
+            sch.post()
+            sch.wait()
+        return step
+
+    for _ in range(3):
+        stepper(sw)()
+        stepper(sf)()
+    tw, tf = [], []
+    for _ in range(4):   # interleaved A/B blocks
+        tw.append(_timed_steps(comm, stepper(sw), steps // 4))
+        tf.append(_timed_steps(comm, stepper(sf), steps // 4))
+    t, t32 = float(np.median(tw)), float(np.median(tf))
+    stages = _stages_us(sw.timeline()[-(steps // 4):])
+    dev.fill_uniform(rb, SEED + 1, rank)
+    dev.synchronize()
+    comm.barrier()
+    stepper(sw)()
+    got = rb.download()
+    m = min(count, 1 << 18)
+    ok = True
+    for start in (0, count - m):
+        xs = [ffref.f32_to_bf16(ffref.fill_uniform(SEED + 1, r, m, start=start)) for r in range(world)]
+        want = ffref.bf16_to_f32(ffref.tree_sum_bf16(xs))
+        ok &= bool(np.array_equal(got[start:start + m].view(np.uint32), want.view(np.uint32)))
+    _defer(sw, rb)
+    _defer(sf)
+    S = count * 4
+    t_min = 2 * (S / 2) / (world * XGMI_LINK_GBS * 1e9)
+    return {"bucket_bytes": S, "wire_bytes": S // 2, "round_ms_median": round(t * 1e3, 4),
+            "fp32_round_ms_median": round(t32 * 1e3, 4), "speedup_vs_fp32": round(t32 / t, 3),
+            "value_GBs": round(world * S / t / 1e9, 2), "algbw_GBs": round(S / t / 1e9, 2),
+            "xgmi_frac": None if SHARED_GPU else round(t_min / t, 4), "rank0_stages_us": stages,
+            "parity_head_tail": "bf16 convention, bitwise" if ok else "MISMATCH"}
+
+
 def c1_host_majority(comm, dev, rank, world, count=262144, warmup=20, iters=50):
     """BASELINE's C1 shape on the GPU path and the reference's contract: majority-allreduce
     of a 1 MiB fp32 HOST bucket (calloc'd in the wrapper, opt_esgd_majority...py:288-298;
@@ -799,6 +854,7 @@ def run_allreduce(args, rank, world):
         # alive until the end, and small rounds measured after them were bimodal
         legs = [("sweep_c5_majority", lambda: sweep_c5(comm, dev, world, dt, es)),
                 ("sweep_c5_majority_bf16", lambda: sweep_c5(comm, dev, world, _lib.BF16, 2)),
+                ("c3_wire_bf16", lambda: c3_wire_bf16(comm, dev, rank, world, int(args.bucket_mib * MiB) // 4)),
                 ("c1_host_majority", lambda: c1_host_majority(comm, dev, rank, world)),
                 ("small_round_after_idle", lambda: small_round_after_idle(comm, dev, rank, world)),
                 ("straggler_c4_majority", lambda: straggler_c4(comm, dev, rank, world)),

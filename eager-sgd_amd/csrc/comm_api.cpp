@@ -34,14 +34,18 @@ namespace esgd {
 int create_schedule(int kind, int buf, const void *sb, void *rb, uint64_t count, int dtype, int async,
                     unsigned seed, unsigned flags, int tag, uint64_t *out) {
     ESGD_ARG(out, "esgd_schedule_create: null output");
-    ESGD_ARG((flags & ~unsigned(ESGD_SCHED_HOLD | ESGD_SCHED_ZERO_SB)) == 0,
+    ESGD_ARG((flags & ~unsigned(ESGD_SCHED_HOLD | ESGD_SCHED_ZERO_SB | ESGD_SCHED_WIRE_BF16)) == 0,
              "esgd_schedule_create: unknown flags 0x%x", flags);
+    ESGD_ARG(!(flags & ESGD_SCHED_WIRE_BF16) || dtype == ESGD_FLOAT,
+             "esgd_schedule_create: ESGD_SCHED_WIRE_BF16 needs FLOAT buckets (dtype %d)", dtype);
     ESGD_ARG(buf == ESGD_BUF_DEVICE || buf == ESGD_BUF_HOST || buf == ESGD_BUF_NONE,
              "esgd_schedule_create: bad buffer kind %d", buf);
     ESGD_ARG(esgd_dtype_size(dtype) > 0, "esgd_schedule_create: unsupported dtype %d", dtype);
     ESGD_ARG(buf == ESGD_BUF_NONE || rb || count == 0, "esgd_schedule_create: null receive buffer");
     const bool rccl = !std::strcmp(transport_name(), "rccl");
     ESGD_ARG(rccl || !std::strcmp(transport_name(), "ipc"), "unknown transport '%s'", transport_name());
+    ESGD_ARG(!(flags & ESGD_SCHED_WIRE_BF16) || !rccl || buf == ESGD_BUF_NONE,
+             "esgd_schedule_create: ESGD_SCHED_WIRE_BF16 runs on the ipc transport only");
     Transport *tp = default_transport(buf == ESGD_BUF_NONE);
     Sched *s = nullptr;
     int rc = sched_create(kind, dtype, count, const_cast<void *>(sb), rb, buf == ESGD_BUF_HOST,

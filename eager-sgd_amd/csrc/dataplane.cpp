@@ -39,6 +39,9 @@ int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64
 int gather_remote(int n, const void *const *src, void *const *dst, const uint64_t *bytes,
                   hipStream_t s);
 int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s);
+int narrow_bf16(const float *src, uint16_t *dst, uint64_t n, hipStream_t s);
+int reduce_wire(int k, const void *const *inputs, uint16_t *outb, float *outf, uint64_t count, hipStream_t s);
+int gather_widen(int n, const void *const *src, void *const *dst, const uint64_t *count, hipStream_t s);
 int store_fin(uint32_t *fin, uint32_t value, hipStream_t s);
 
 int round_small(int dtype, const void *const *src, void *out, void *pub, uint64_t n, int nseg,
@@ -406,7 +409,11 @@ struct IpcState : BaseState {
     char *pub = nullptr;
     size_t pub_cap = 0;
     uint32_t pub_round = 0;
-    char *peer[kMaxRanks] = {};       // every rank's rb (own included)
+    char *peer[kMaxRanks] = {};       // every rank's rb (own included); its wire copy in wire mode
+    // ESGD_SCHED_WIRE_BF16: this rank's bf16 copy of rb (arena, exported instead of rb;
+    // count x 2 bytes).  Peers read only this: rb itself is never mapped by a peer.
+    char *wire = nullptr;
+    size_t wire_cap = 0;
     PeerMap rbmap[kMaxRanks], pubmap[kMaxRanks];
 };
 
@@ -717,8 +724,11 @@ struct IpcTransport final : Transport {
 
     // size of this round's bucket, read by peers' size check (no re-map needed)
     static void publish_size(Sched &s) {
-        s.sh->slot[s.rank].bytes = s.count * s.esize;
+        s.sh->slot[s.rank].bytes = s.count * wire_esize(s);
     }
+
+    // bytes per element of what peers read: the bf16 wire copy, or the bucket itself
+    static size_t wire_esize(const Sched &s) { return s.wire_bf16 ? 2 : s.esize; }
 
     // Publish rb_dev (arena memory: the chunk's handle + the offset); ESGD_INVALID_ARG
     // when rb_dev is foreign memory, which is never exported.
@@ -740,13 +750,19 @@ struct IpcTransport final : Transport {
     }
 
     static int publish(Sched &s, IpcState &st) {
+        if (s.wire_bf16) {   // peers read the wire copy; rb stays private (never shadowed)
+            if (!st.wire)
+                if (int rc = alloc_bucket(s.count * 2, &st.wire, &st.wire_cap)) return rc;
+            st.peer[s.rank] = st.wire;
+            return publish_buf(s, s.sh->slot[s.rank], st.wire, s.count * 2, "wire");
+        }
         st.peer[s.rank] = st.rb_dev;
         return publish_buf(s, s.sh->slot[s.rank], st.rb_dev, s.count * s.esize, "rb");
     }
 
     // rounds of this size run as one k_round_small launch
     static bool one_launch(const Sched &s) {
-        return s.world > 1 && s.world <= ESGD_MAX_FANIN && s.count * s.esize <= small_round_bytes();
+        return s.world > 1 && s.world <= ESGD_MAX_FANIN && !s.wire_bf16 && s.count * s.esize <= small_round_bytes();
     }
 
     // the published shard (one-launch rounds only): grown and re-published when the
@@ -783,7 +799,7 @@ struct IpcTransport final : Transport {
 
     // (re)map every peer's rb and published shard
     static int map_peers(Sched &s, IpcState &st) {
-        const size_t bytes = s.count * s.esize;
+        const size_t bytes = s.count * wire_esize(s);
         for (int q = 0; q < s.world; ++q) {
             if (q == s.rank) continue;
             IpcSlot &ps = s.sh->slot[q];
@@ -810,6 +826,10 @@ struct IpcTransport final : Transport {
         if (int rc = base_setup(s, *st)) return rc;
         st->peer[s.rank] = st->rb_dev;
         if (s.world == 1) return ESGD_SUCCESS;
+        if (s.wire_bf16 && s.resolve) {
+            set_error("schedule: ESGD_SCHED_WIRE_BF16 does not take FFCOLL_BUFFERS buffers");
+            return ESGD_INVALID_ARG;
+        }
         if (int rc = register_segment()) return rc;
         if (device_flags())
             if (int rc = flags_publish(s.rank)) return rc;
@@ -818,7 +838,7 @@ struct IpcTransport final : Transport {
         // re-allocated between rounds; also how the tests reach the fallback)
         static const bool force_shadow = getenv("ESGD_SHADOW") && *getenv("ESGD_SHADOW") == '1';
         if (int rc = publish_pub(s, *st)) return rc;
-        if (s.host_mode) return publish(s, *st);
+        if (s.host_mode || s.wire_bf16) return publish(s, *st);
         int rc = force_shadow ? ESGD_INVALID_ARG : publish(s, *st);
         if (rc == ESGD_INVALID_ARG) {
             // foreign device memory (torch tensors, plain hipMalloc) is never exported:
@@ -858,7 +878,7 @@ struct IpcTransport final : Transport {
             publish_size(s);
             if (int rc = publish_pub(s, st)) return rc;   // larger shards need a larger pub
         }
-        st.peer[s.rank] = st.rb_dev;
+        st.peer[s.rank] = s.wire_bf16 ? st.wire : st.rb_dev;   // what peers read
         ESGD_TRACE("r%d sched %d round %u join count=%llu rb_dev=%p moved=%d staged=%d\n", s.rank, s.id,
                    round, (unsigned long long)s.count, (void *)st.rb_dev, moved, int(staged(s, st)));
         return base_prepare(s, st);
@@ -875,7 +895,8 @@ struct IpcTransport final : Transport {
         IpcState &st = S(s);
         hipStream_t cs = st.stream;
         st.fin_mode = false;
-        if (s.host_mode && !s.resolve && host_chunk_bytes() && s.count * s.esize >= 2 * host_chunk_bytes())
+        if (s.host_mode && !s.resolve && !s.wire_bf16 && host_chunk_bytes() &&
+            s.count * s.esize >= 2 * host_chunk_bytes())
             return launch_chunked(s, st, round, fresh);
         if (int rc = base_copy_in(s, st, round, fresh, cs)) return rc;
         if (s.world > 1) {
@@ -892,6 +913,9 @@ struct IpcTransport final : Transport {
                 }
                 return base_copy_out(s, st, cs);
             }
+            if (s.wire_bf16) {
+                if (int rc = wire_phases(s, st, round, cs)) return rc;
+            } else {
             if (int rc = pair_ranks(s, s.sh->ready, 0, round, cs)) return rc;
             // Launches move at most kPiece bytes per input / segment (the kernels address
             // a shard through 32-bit buffer offsets); buckets up to the reference's
@@ -926,6 +950,7 @@ struct IpcTransport final : Transport {
             }
             if (m)
                 if (int rc = gather_remote(m, src, dst, bytes, cs)) return rc;
+            }
             // device buckets: the done pairing ends the round and reports it in fin, which
             // the host polls (as for one-launch rounds; the event only reports faults)
             const bool last = !s.host_mode && !st.shadow;
@@ -938,6 +963,48 @@ struct IpcTransport final : Transport {
             }
         }
         return base_copy_out(s, st, cs);
+    }
+
+    // Both phases of a wire-mode round (ESGD_SCHED_WIRE_BF16), up to the done pairing:
+    //   wire = bf16(rb) -> [pair: ready] -> phase 1: shard `rank` of every rank's wire copy
+    //   (peer HBM), folded in fp32, rounded once -> own wire shard (bf16) + rb shard (fp32)
+    //   -> [pair: reduced] -> phase 2: every other rank's reduced wire shard, widened into rb.
+    // Peers read S/2 bytes per phase and rank pair instead of S: half the xGMI traffic, for
+    // one more local pass (4 B read + 2 B written per element).  The done pairing that
+    // follows keeps the wire copy unchanged until every peer has gathered from it.
+    static int wire_phases(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) {
+        if (int rc = narrow_bf16(reinterpret_cast<const float *>(st.rb_dev), reinterpret_cast<uint16_t *>(st.wire),
+                                 s.count, cs))
+            return rc;
+        if (int rc = pair_ranks(s, s.sh->ready, 0, round, cs)) return rc;
+        const uint64_t piece = piece_bytes() / 4;   // elements, as for fp32 rounds
+        const int r = s.rank;
+        for (uint64_t o = 0; o < st.len[r]; o += piece) {
+            const uint64_t c = std::min(piece, st.len[r] - o);
+            const void *in[kMaxRanks];
+            for (int j = 0; j < s.world; ++j) in[j] = st.peer[j] + (st.off[r] + o) * 2;
+            if (int rc = reduce_wire(s.world, in, reinterpret_cast<uint16_t *>(st.wire + (st.off[r] + o) * 2),
+                                     reinterpret_cast<float *>(st.rb_dev + (st.off[r] + o) * 4), c, cs))
+                return rc;
+        }
+        if (int rc = pair_ranks(s, s.sh->reduced, 1, round, cs)) return rc;
+        const void *src[kMaxSegs];
+        void *dst[kMaxSegs];
+        uint64_t cnt[kMaxSegs];
+        int m = 0;
+        for (int j = 0; j < s.world; ++j) {
+            if (j == r) continue;
+            for (uint64_t o = 0; o < st.len[j]; o += piece) {
+                src[m] = st.peer[j] + (st.off[j] + o) * 2;
+                dst[m] = st.rb_dev + (st.off[j] + o) * 4;
+                cnt[m] = std::min(piece, st.len[j] - o);
+                if (++m == kMaxSegs) {
+                    if (int rc = gather_widen(m, src, dst, cnt, cs)) return rc;
+                    m = 0;
+                }
+            }
+        }
+        return m ? gather_widen(m, src, dst, cnt, cs) : ESGD_SUCCESS;
     }
 
     // Host buckets (the reference's contract) of >= 2 chunks: the round runs chunk by
@@ -1077,6 +1144,7 @@ struct IpcTransport final : Transport {
                            s.rank, s.id, st->pub_round);
         }
         if (st->pub && pub_free) free_bucket(st->pub);
+        if (st->wire) free_bucket(st->wire);   // the done pairing: no peer still reads it
         if (!pub_free) st->retired.clear();   // earlier pubs too: a peer may be stuck on any
         base_teardown(s, *st);
         delete st;

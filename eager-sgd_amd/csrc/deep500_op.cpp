@@ -45,6 +45,7 @@ struct OpConfig {
     int mode = -1;
     int async = 32;       // LIMITER, opt_esgd_solo_imagenet_imbalance.py:82
     unsigned seed = 6545343;   // opt_esgd_majority_imagenet_imbalance.py:252
+    int wire = ESGD_FLOAT;     // ESGD_BF16: device ops exchange bf16 copies (ESGD_SCHED_WIRE_BF16)
 };
 
 std::mutex g_op_mu;
@@ -106,7 +107,8 @@ struct AllreduceOp {
         }
         const int kind = cfg.mode == ESGD_OP_MAJORITY ? ESGD_SCHED_MAJORITY
                          : cfg.mode == ESGD_OP_ALLREDUCE ? ESGD_SCHED_ALLREDUCE : ESGD_SCHED_SOLO;
-        const unsigned flags = ESGD_SCHED_HOLD | (dev ? ESGD_SCHED_ZERO_SB : 0u);
+        const unsigned flags = ESGD_SCHED_HOLD | (dev ? ESGD_SCHED_ZERO_SB : 0u) |
+                               (dev && cfg.wire == ESGD_BF16 ? ESGD_SCHED_WIRE_BF16 : 0u);
         if (esgd_schedule_create_ex(kind, dev ? ESGD_BUF_DEVICE : ESGD_BUF_HOST, sb, rb, len,
                                     ESGD_FLOAT, cfg.async, cfg.seed, flags, &sched))
             die("schedule creation");
@@ -172,6 +174,14 @@ int esgd_op_configure(int mode, int async, unsigned seed) {
     g_cfg.mode = mode;
     g_cfg.async = async;
     g_cfg.seed = seed;
+    return ESGD_SUCCESS;
+}
+
+int esgd_op_configure_wire(int wire_dtype) {
+    ESGD_ARG(wire_dtype == ESGD_FLOAT || wire_dtype == ESGD_BF16,
+             "esgd_op_configure_wire: FLOAT or BF16, not %d", wire_dtype);
+    std::lock_guard<std::mutex> lk(g_op_mu);
+    g_cfg.wire = wire_dtype;
     return ESGD_SUCCESS;
 }
 

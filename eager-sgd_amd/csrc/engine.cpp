@@ -207,6 +207,7 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     s->resolve_free = ctx_free;
     s->hold_mode = (flags & ESGD_SCHED_HOLD) != 0;
     s->zero_sb = (flags & ESGD_SCHED_ZERO_SB) != 0 && !host_mode && !s->in_place;
+    s->wire_bf16 = (flags & ESGD_SCHED_WIRE_BF16) != 0;
     // Schedule ids are never reused within a job and the segment starts zeroed, so the
     // shared state of this id needs no reset (no barrier before setup).  Creation is two
     // voted steps: setup (local: buckets, streams, publication) -> barrier -> every rank
@@ -214,7 +215,8 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     // failures -> connect (mapping peers) -> barrier -> failures.  A failure anywhere
     // fails the creation everywhere; no rank is left waiting on a peer that gave up.
     s->gen = 1;   // IpcSlot::gen == 1: published for this id
-    const uint64_t sig = (uint64_t(uint32_t(kind)) << 40) | (uint64_t(uint32_t(dtype) & 0xff) << 32) |
+    const uint64_t sig = (uint64_t(s->wire_bf16) << 48) | (uint64_t(uint32_t(kind)) << 40) |
+                         (uint64_t(uint32_t(dtype) & 0xff) << 32) |
                          (tag == kNoTag ? 0 : (0x10000u | uint16_t(tag)));
     int rc = ESGD_SUCCESS;
     auto vote = [&](int r) -> int {
@@ -239,7 +241,7 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
         if (o != sig) {
             set_error("schedule create: rank %d created (kind %d, dtype %d, tag %d), rank %d (kind %d, "
                       "dtype %d, tag %d): creation order must match", g_rank, kind, dtype,
-                      tag == kNoTag ? -1 : tag, q, int(o >> 40), int((o >> 32) & 0xff),
+                      tag == kNoTag ? -1 : tag, q, int((o >> 40) & 0xff), int((o >> 32) & 0xff),
                       (o & 0x10000) ? int(int16_t(o & 0xffff)) : -1);
             rc = ESGD_INVALID_ARG;   // every rank sees the same signatures: all fail
         }

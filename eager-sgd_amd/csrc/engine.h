@@ -133,6 +133,9 @@ struct Sched {
     // ESGD_SCHED_ZERO_SB: the snapshot zeroes the send bucket as it reads it (device
     // buckets): the wrapper's zero-after-use (:311-314) fused into the move
     bool zero_sb = false;
+    // ESGD_SCHED_WIRE_BF16 (fp32 buckets, IPC transport): peers read a bf16 copy of the
+    // bucket, half the xGMI bytes; the result is the bf16-rounded tree widened to fp32
+    bool wire_bf16 = false;
     uint8_t fresh_of[256] = {};   // round % 256 -> this rank had posted it before joining
 };
 

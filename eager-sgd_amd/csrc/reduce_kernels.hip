@@ -333,6 +333,139 @@ __global__ __launch_bounds__(256) void k_gather(GatherSet g) {
     }
 }
 
+// ---- bf16 on the wire for fp32 buckets (ESGD_SCHED_WIRE_BF16) ----
+// The bucket stays fp32 in HBM; what peers read over xGMI is a bf16 copy of it (half the
+// bytes in both phases).  Convention (an extension, parity unpinned by the reference, which
+// has no bf16: F/src/ff.h:21-32): every rank's contribution is rounded to bf16 once (RNE),
+// the shard is folded in fp32 in the hypercube tree order and rounded to bf16 once, and every
+// rank widens that same bf16 result back to fp32 -- so all ranks hold identical values, the
+// oracle's bf16 tree of the rounded inputs (oracle/ffref.c ffref_tree_sum_bf16).
+// 8 elements per lane and step: two 16-B fp32 vectors <-> one 16-B bf16 vector.
+__device__ __forceinline__ raw16 narrow8(raw16 a, raw16 b) {
+    uint16_t h[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        h[e] = BF16::store(__uint_as_float(a[e]));
+        h[4 + e] = BF16::store(__uint_as_float(b[e]));
+    }
+    raw16 o;
+    __builtin_memcpy(&o, h, 16);
+    return o;
+}
+
+__device__ __forceinline__ void widen8(raw16 h, raw16 &a, raw16 &b) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        a[e] = (h[e / 2] >> (16 * (e & 1))) << 16;
+        b[e] = (h[2 + e / 2] >> (16 * (e & 1))) << 16;
+    }
+}
+
+// wire = bf16(rb): local HBM, 6 B per element moved (4 read + 2 written)
+__global__ __launch_bounds__(256) void k_narrow_bf16(const float *src, uint16_t *dst, uint64_t n) {
+    const uint64_t nv = n / 8;
+    const raw16 *s = reinterpret_cast<const raw16 *>(src);
+    raw16 *d = reinterpret_cast<raw16 *>(dst);
+    const uint64_t stride = uint64_t(gridDim.x) * 256 * 2;
+    for (uint64_t i = uint64_t(blockIdx.x) * 512 + threadIdx.x; i < nv; i += stride) {
+        raw16 r[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (i + u * 256 < nv) {
+                r[u][0] = __builtin_nontemporal_load(s + 2 * (i + u * 256));
+                r[u][1] = __builtin_nontemporal_load(s + 2 * (i + u * 256) + 1);
+            }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (i + u * 256 < nv) d[i + u * 256] = narrow8(r[u][0], r[u][1]);
+    }
+    if (blockIdx.x == 0 && nv * 8 + threadIdx.x < n)
+        dst[nv * 8 + threadIdx.x] = BF16::store(src[nv * 8 + threadIdx.x]);
+}
+
+// Phase 1 over the wire: the K ranks' bf16 copies of this rank's shard (peer HBM, system-
+// scope nt loads), folded in fp32 in tree order, rounded once; the bf16 result goes to this
+// rank's wire shard (what peers gather) and its widening to the fp32 bucket.  The own input
+// is the same wire shard: each lane reads its element before it stores it.
+template <int K>
+__global__ __launch_bounds__(256) void k_tree_sum_wire(InputSet in, uint16_t *outb, float *outf, uint32_t nvec,
+                                                       uint64_t count) {
+    constexpr int U = 2, B = 256;
+    const int bytes = int(nvec * 16u);
+    __amdgpu_buffer_rsrc_t rs[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(in.p[j]), (short)0, bytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t wb = __builtin_amdgcn_make_buffer_rsrc(outb, (short)0, bytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t wf = __builtin_amdgcn_make_buffer_rsrc(outf, (short)0, 2 * bytes, 0x00020000);
+    const uint32_t step = gridDim.x * (B * U);
+    for (uint32_t i = blockIdx.x * (B * U) + threadIdx.x; i < nvec; i += step) {
+        raw16 r[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                r[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs[j], (i + u * B) * 16, 0, 19);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const raw16 h = fold16<BF16, K, false>(r[u], 1.0f);
+            raw16 a, b;
+            widen8(h, a, b);
+            __builtin_amdgcn_raw_buffer_store_b128(h, wb, (i + u * B) * 16, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(a, wf, (i + u * B) * 32, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(b, wf, (i + u * B) * 32 + 16, 0, 16);
+        }
+    }
+    const uint64_t e = uint64_t(nvec) * 8 + threadIdx.x;
+    if (blockIdx.x == 0 && e < count) {
+        float v[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            v[j] = BF16::load(__hip_atomic_load(static_cast<const uint16_t *>(in.p[j]) + e, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_SYSTEM));
+        tree_fold<BF16, K>(v);
+        const uint16_t h = BF16::store(v[0]);
+        outb[e] = h;
+        outf[e] = BF16::load(h);
+    }
+}
+
+// Phase 2 over the wire: every other rank's reduced bf16 shard (peer HBM), widened into the
+// fp32 bucket.  blockIdx.y picks the segment; n = elements.
+struct WidenSet {
+    const uint16_t *src[kMaxSeg];
+    float *dst[kMaxSeg];
+    uint32_t n[kMaxSeg];
+};
+
+__global__ __launch_bounds__(256) void k_gather_widen(WidenSet g) {
+    constexpr int B = 256, U = 4;
+    const int seg = blockIdx.y;
+    const uint32_t n = g.n[seg], nvec = n / 8;
+    if (nvec) {
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(g.src[seg]), (short)0,
+                                                                     int(nvec * 16u), 0x00020000);
+        __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(g.dst[seg], (short)0, int(nvec * 32u),
+                                                                     0x00020000);
+        const uint32_t step = gridDim.x * (B * U);
+        for (uint32_t i = blockIdx.x * (B * U) + threadIdx.x; i < nvec; i += step) {
+            raw16 r[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (i + u * B) * 16, 0, 19);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                raw16 a, b;
+                widen8(r[u], a, b);
+                __builtin_amdgcn_raw_buffer_store_b128(a, ws, (i + u * B) * 32, 0, 16);
+                __builtin_amdgcn_raw_buffer_store_b128(b, ws, (i + u * B) * 32 + 16, 0, 16);
+            }
+        }
+    }
+    const uint32_t e = nvec * 8 + threadIdx.x;
+    if (blockIdx.x == 0 && e < n)
+        g.dst[seg][e] = BF16::load(__hip_atomic_load(g.src[seg] + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+
 // ---- the snapshot with the zero-after-use fused: dst = src, src = 0 ----
 // The round's move (colls/ffallreduce.c:126-130) and the wrapper's zeroing of the send
 // bucket after the wait (opt_esgd_solo_imagenet_imbalance.py:311-314) in one pass:
@@ -740,6 +873,61 @@ int gather_remote(int n, const void *const *src, void *const *dst, const uint64_
     unsigned per_seg = std::max(1u, (unsigned(cu_count()) * 4 + n - 1) / unsigned(n));
     if (gx > per_seg) gx = per_seg;
     hipLaunchKernelGGL((k_gather<4>), dim3(gx, n), dim3(256), 0, s, g);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+// ---- bf16-wire entry points (dataplane.cpp, ESGD_SCHED_WIRE_BF16) ----
+int narrow_bf16(const float *src, uint16_t *dst, uint64_t n, hipStream_t s) {
+    if (!n) return ESGD_SUCCESS;
+    ESGD_ARG(((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0,
+             "wire: buckets must be 16-B aligned");
+    hipLaunchKernelGGL(k_narrow_bf16, dim3(grid_for(512, n / 8 ? n / 8 : 1, 8)), dim3(256), 0, s, src, dst, n);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+int reduce_wire(int k, const void *const *inputs, uint16_t *outb, float *outf, uint64_t count, hipStream_t s) {
+    ESGD_ARG(k >= 1 && k <= ESGD_MAX_FANIN, "wire: fan-in %d", k);
+    if (!count) return ESGD_SUCCESS;
+    ESGD_ARG(count / 8 * 32 + 2 * 256 * 32 < (1ull << 31), "wire: shard piece of %llu elements too large",
+             (unsigned long long)count);
+    InputSet in;
+    std::memset(&in, 0, sizeof(in));
+    uintptr_t al = reinterpret_cast<uintptr_t>(outb) | reinterpret_cast<uintptr_t>(outf);
+    for (int j = 0; j < k; ++j) { in.p[j] = inputs[j]; al |= reinterpret_cast<uintptr_t>(inputs[j]); }
+    ESGD_ARG((al & 15) == 0, "wire: shards must be 16-B aligned");
+    const uint32_t nvec = uint32_t(count / 8);
+    const unsigned grid = grid_for(512, nvec ? nvec : 1, 4);
+    switch (k) {
+#define ESGD_WK(K) case K: hipLaunchKernelGGL((k_tree_sum_wire<K>), dim3(grid), dim3(256), 0, s, in, outb, outf, nvec, count); break;
+    ESGD_WK(1) ESGD_WK(2) ESGD_WK(3) ESGD_WK(4) ESGD_WK(5) ESGD_WK(6) ESGD_WK(7) ESGD_WK(8)
+#undef ESGD_WK
+    }
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+int gather_widen(int n, const void *const *src, void *const *dst, const uint64_t *count, hipStream_t s) {
+    ESGD_ARG(n >= 0 && n <= kMaxSeg, "wire gather: %d segments", n);
+    if (n == 0) return ESGD_SUCCESS;
+    WidenSet g;
+    std::memset(&g, 0, sizeof(g));
+    uint64_t maxvec = 0;
+    for (int i = 0; i < n; ++i) {
+        ESGD_ARG(count[i] * 4 < (1ull << 31), "wire gather: segment of %llu elements too large",
+                 (unsigned long long)count[i]);
+        ESGD_ARG(((reinterpret_cast<uintptr_t>(src[i]) | reinterpret_cast<uintptr_t>(dst[i])) & 15) == 0,
+                 "wire gather: segment %d not 16-B aligned", i);
+        g.src[i] = static_cast<const uint16_t *>(src[i]);
+        g.dst[i] = static_cast<float *>(dst[i]);
+        g.n[i] = uint32_t(count[i]);
+        maxvec = std::max<uint64_t>(maxvec, count[i] / 8);
+    }
+    unsigned gx = grid_for(256 * 4, maxvec ? maxvec : 1, 8);
+    unsigned per_seg = std::max(1u, (unsigned(cu_count()) * 4 + n - 1) / unsigned(n));
+    if (gx > per_seg) gx = per_seg;
+    hipLaunchKernelGGL(k_gather_widen, dim3(gx, n), dim3(256), 0, s, g);
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;
 }

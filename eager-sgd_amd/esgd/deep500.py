@@ -36,6 +36,7 @@ class TensorDesc:
 def _bind(h):
     vp = C.c_void_p
     h.esgd_op_configure.restype, h.esgd_op_configure.argtypes = C.c_int, [C.c_int, C.c_int, C.c_uint]
+    h.esgd_op_configure_wire.restype, h.esgd_op_configure_wire.argtypes = C.c_int, [C.c_int]
     h.create_new_op.restype = vp
     h.create_new_op.argtypes = [C.POINTER(tensor_t), C.c_int, C.POINTER(tensor_t), C.c_int]
     h.allreducef_forward.restype, h.allreducef_forward.argtypes = None, [vp, vp, vp, vp]
@@ -54,11 +55,17 @@ def _bind(h):
 _lib.register_signatures(_bind)
 
 
-def configure(mode: str = "solo", async_: int = 32, seed: int = 6545343):
+WIRES = {"fp32": _lib.FLOAT, "bf16": _lib.BF16}
+
+
+def configure(mode: str = "solo", async_: int = 32, seed: int = 6545343, wire: str = "fp32"):
     """Mode of the ops created afterwards (solo LIMITER 32 / majority seed 6545343 as
-    in opt_esgd_{solo,majority}_imagenet_imbalance.py)."""
+    in opt_esgd_{solo,majority}_imagenet_imbalance.py).  wire="bf16": device ops exchange
+    bf16 copies of their fp32 buckets (half the xGMI bytes; an extension, the result is
+    the bf16-rounded tree)."""
     _lib.check(lib().esgd_op_configure(MODES[mode], int(async_), int(seed) & 0xFFFFFFFF),
                "esgd_op_configure")
+    _lib.check(lib().esgd_op_configure_wire(WIRES[wire]), "esgd_op_configure_wire")
 
 
 class AllreduceOp:

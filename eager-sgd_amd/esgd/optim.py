@@ -32,15 +32,18 @@ from . import deep500
 
 class EagerSGDOptimizer:
     def __init__(self, optimizer, comm_size: int, mode: str = "solo", async_: int = 32,
-                 seed: int = 6545343, fuse: bool = False):
+                 seed: int = 6545343, fuse: bool = False, wire: str = "fp32"):
         if mode not in deep500.MODES:
             raise ValueError(f"mode must be one of {sorted(deep500.MODES)}")
+        if wire not in deep500.WIRES:
+            raise ValueError(f"wire must be one of {sorted(deep500.WIRES)}")
         if comm_size < 1:
             raise ValueError("comm_size must be >= 1")
         self.optimizer = optimizer
         self.comm_size = int(comm_size)
         self.mode, self.async_, self.seed = mode, int(async_), int(seed)
         self.fuse = bool(fuse)
+        self.wire = wire        # "bf16": bf16 copies between ranks
         self._ops = {}          # parameter -> op instance (one bucket per tensor)
         self._fused = None      # (layout, op, packed bucket, reduced bucket)
         self._configured = False
@@ -54,7 +57,7 @@ class EagerSGDOptimizer:
     def apply_gradients(self, grads_and_vars: Iterable, global_step=None):
         import torch
         if not self._configured:
-            deep500.configure(self.mode, self.async_, self.seed)
+            deep500.configure(self.mode, self.async_, self.seed, self.wire)
             self._configured = True
         stream = torch.cuda.current_stream().cuda_stream
         gvs = list(grads_and_vars)

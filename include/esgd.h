@@ -180,9 +180,17 @@ int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t c
  *                      (opt_esgd_solo_imagenet_imbalance.py:309-314);
  *   ESGD_SCHED_ZERO_SB the snapshot (move sb -> rb) zeroes sb as it reads it (device
  *                      buckets, not in place): the wrapper's zero-after-use (:311-314)
- *                      fused into the move, one HBM pass fewer. */
+ *                      fused into the move, one HBM pass fewer;
+ *   ESGD_SCHED_WIRE_BF16 FLOAT buckets, ipc transport: peers exchange a bf16 copy of the
+ *                      bucket (half the xGMI bytes).  Every rank's
+ *                      bucket is rounded to bf16 (RNE), each shard is folded in fp32 in the
+ *                      tree order and rounded once, and every rank receives that bf16 result
+ *                      widened to fp32 (identical on all ranks).  Not in the reference (no
+ *                      bf16 in ff.h): parity unpinned, checked against the oracle's
+ *                      convention (ffref_tree_sum_bf16 of the rounded inputs). */
 #define ESGD_SCHED_HOLD 0x1
 #define ESGD_SCHED_ZERO_SB 0x2
+#define ESGD_SCHED_WIRE_BF16 0x4
 int esgd_schedule_create_ex(int kind, int buf, const void *sb, void *rb, uint64_t count,
                             int dtype, int async, unsigned seed, unsigned flags,
                             esgd_sched_h *out);

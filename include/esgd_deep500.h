@@ -39,6 +39,10 @@ typedef struct {
 /* Mode of the ops created afterwards (defaults: env ESGD_OP_MODE=solo|majority|allreduce,
  * ESGD_OP_ASYNC=32, ESGD_OP_SEED=6545343, ESGD_OP_DEVICE=0|1). */
 int esgd_op_configure(int mode, int async, unsigned seed);
+/* Extension: what device ops created afterwards exchange between ranks -- ESGD_FLOAT (the
+ * reference's fp32, default) or ESGD_BF16 (fp32 buckets, bf16 copies on the wire:
+ * ESGD_SCHED_WIRE_BF16 in esgd.h; parity unpinned).  Host-buffer ops stay fp32. */
+int esgd_op_configure_wire(int wire_dtype);
 
 void *create_new_op(esgd_d5_tensor_t *input_descriptors, int num_inputs,
                     esgd_d5_tensor_t *output_descriptors, int num_outputs);

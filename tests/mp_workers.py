@@ -122,12 +122,14 @@ def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0
 
 def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0, buf="device",
                   in_place=False, transport="ipc", shadow_ranks=(), small_bytes=None,
-                  piece_bytes=None, host_chunk=None, device_flags=None):
+                  piece_bytes=None, host_chunk=None, device_flags=None, wire=False):
     """Data plane on the GPU: every rank reduces its splitmix bucket; returns the
     result bytes' digest per round plus a bit-exactness verdict against the oracle.
     shadow_ranks: ranks whose device buckets go through the owned shadow bucket.
     small_bytes: ESGD_SMALL_ROUND_BYTES (buckets up to it run as one launch per round;
-    "0" forces the five-launch path)."""
+    "0" forces the five-launch path).
+    wire: fp32 buckets with bf16 on the wire (ESGD_SCHED_WIRE_BF16): the expected result
+    is the oracle's bf16 tree of the bf16-rounded inputs, widened to fp32."""
     import numpy as np
 
     if rank in shadow_ranks:
@@ -153,12 +155,14 @@ def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0
     if buf == "device":
         rb = dev.DeviceBuffer(count, dt)
         sb = None if in_place else dev.DeviceBuffer(count, dt)
-        s = comm.Schedule(kind, sb, rb, count, dtype=dt, buf=comm.BUF_DEVICE)
+        s = comm.Schedule(kind, sb, rb, count, dtype=dt, buf=comm.BUF_DEVICE,
+                          flags=comm.WIRE_BF16 if wire else 0)
     else:
         npdt = dev.NP_DTYPE[dt]
         sb_h = None if in_place else np.zeros(count, npdt)
         rb_h = np.zeros(count, npdt)
-        s = comm.Schedule(kind, sb_h, rb_h, count, dtype=dt, buf=comm.BUF_HOST)
+        s = comm.Schedule(kind, sb_h, rb_h, count, dtype=dt, buf=comm.BUF_HOST,
+                          flags=comm.WIRE_BF16 if wire else 0)
     for t in range(rounds):
         xs = []
         for r in range(world):
@@ -183,7 +187,9 @@ def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0
         # Every rank gets rank 0's recursive-doubling result.  For power-of-two P that is
         # what every reference rank holds; for other P the reference leaves some ranks
         # with partial sums (ffallreduce.c:140) and esgd deliberately completes them.
-        if dt == _lib.BF16:
+        if wire and world > 1:
+            want = ffref.bf16_to_f32(ffref.tree_sum_bf16([ffref.f32_to_bf16(x) for x in xs]))
+        elif dt == _lib.BF16:
             want = ffref.tree_sum_bf16(xs)
         elif dt in (_lib.INT32, _lib.INT64):
             want = ffref.allreduce_rd(xs)[0]
@@ -363,11 +369,12 @@ def op_device_late(rank, world, async_=3, steps=9, count=100003):
     return {"ok": ok, "sync_rounds": fresh}
 
 
-def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False):
+def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp32"):
     """EagerSGDOptimizer on PyTorch-ROCm: every rank's p.grad after apply_gradients must
     equal the oracle tree of (grad_r / P) over ranks, bit for bit (allreduce), or over
     expected_inputs' contributors when the ranks call every op in late_ranks' order
-    (solo / majority; step 0, which creates the schedules collectively, is not checked)."""
+    (solo / majority; step 0, which creates the schedules collectively, is not checked).
+    wire="bf16": the same contributors, the oracle's bf16 tree of the rounded inputs, widened."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -381,7 +388,7 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False):
     torch.cuda.set_device(dev)
     model = torch.nn.Sequential(torch.nn.Linear(64, 48), torch.nn.ReLU(), torch.nn.Linear(48, 10)).to(dev)
     opt = EagerSGDOptimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9), world, mode=mode,
-                            fuse=fuse)
+                            fuse=fuse, wire=wire)
     ok = []
     for t in range(steps):
         g = torch.Generator().manual_seed(100 * t + rank)
@@ -412,7 +419,9 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False):
         if t == 0 and mode != "allreduce":
             continue
         for i, (_, p) in enumerate(gvs):
-            want = ffref.tree_sum(expected_inputs(mode, [allg[r][i] for r in range(world)]))
+            xs = expected_inputs(mode, [allg[r][i] for r in range(world)])
+            want = (ffref.bf16_to_f32(ffref.tree_sum_bf16([ffref.f32_to_bf16(x) for x in xs]))
+                    if wire == "bf16" else ffref.tree_sum(xs))
             got = p.grad.detach().float().cpu().numpy().ravel()
             ok.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
     params = torch.cat([p.detach().float().cpu().ravel() for p in model.parameters()]).numpy()

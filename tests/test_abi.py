@@ -69,3 +69,19 @@ def test_argument_validation_without_device():
     assert lib.esgd_dtype_size(_lib.BF16) == 2 and lib.esgd_dtype_size(7) == 0
     assert lib.esgd_set_tuning(b"unroll", 3) == _lib.INVALID_ARG
     assert lib.esgd_set_tuning(b"bogus", 1) == _lib.INVALID_ARG
+
+
+def test_wire_flag_argument_checks():
+    # ESGD_SCHED_WIRE_BF16 needs FLOAT buckets; unknown flags are refused (checked before
+    # any communicator or device is touched)
+    import ctypes as C
+
+    import esgd
+    from esgd import _lib, comm
+    h = C.c_uint64()
+    rc = esgd.lib().esgd_schedule_create_ex(0, comm.BUF_DEVICE, None, C.c_void_p(16), 64, _lib.BF16, 0, 0,
+                                            comm.WIRE_BF16, C.byref(h))
+    assert rc == _lib.INVALID_ARG and "WIRE_BF16" in _lib.last_error()
+    rc = esgd.lib().esgd_schedule_create_ex(0, comm.BUF_DEVICE, None, C.c_void_p(16), 64, _lib.FLOAT, 0, 0,
+                                            0x80, C.byref(h))
+    assert rc == _lib.INVALID_ARG and "unknown flags" in _lib.last_error()

@@ -48,3 +48,15 @@ def test_eager_sgd_optimizer(mode, fuse):
         assert o["bytes"] > 0
     if mode == "allreduce":   # synchronous averaging keeps the replicas identical
         assert outs[0]["params_digest"] == outs[1]["params_digest"]
+
+
+@pytest.mark.parametrize("fuse", [False, True])
+@pytest.mark.parametrize("mode", ["allreduce", "solo", "majority"])
+def test_eager_sgd_optimizer_wire_bf16(mode, fuse):
+    # EagerSGDOptimizer(wire="bf16"): fp32 gradients, bf16 copies between the ranks
+    # (ESGD_SCHED_WIRE_BF16); same contributors as the fp32 test, bf16 convention
+    outs = run("optimizer_step", 2, mode=mode, steps=3, fuse=fuse, wire="bf16")
+    for o in outs:
+        assert all(o["ok"]) and o["ok"], o["ok"]
+    if mode == "allreduce":
+        assert outs[0]["params_digest"] == outs[1]["params_digest"]
