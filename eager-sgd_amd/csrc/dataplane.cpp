@@ -39,7 +39,7 @@ int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64
 int gather_remote(int n, const void *const *src, void *const *dst, const uint64_t *bytes,
                   hipStream_t s);
 int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s);
-int narrow_bf16(const float *src, uint16_t *dst, uint64_t n, hipStream_t s);
+int narrow_bf16(float *src, uint16_t *dst, uint64_t n, bool zero_src, hipStream_t s);
 int reduce_wire(int k, const void *const *inputs, uint16_t *outb, float *outf, uint64_t count, hipStream_t s);
 int gather_widen(int n, const void *const *src, void *const *dst, const uint64_t *count, hipStream_t s);
 int store_fin(uint32_t *fin, uint32_t value, hipStream_t s);
@@ -898,7 +898,14 @@ struct IpcTransport final : Transport {
         if (s.host_mode && !s.resolve && !s.wire_bf16 && host_chunk_bytes() &&
             s.count * s.esize >= 2 * host_chunk_bytes())
             return launch_chunked(s, st, round, fresh);
-        if (int rc = base_copy_in(s, st, round, fresh, cs)) return rc;
+        if (s.wire_bf16 && s.world > 1 && !s.host_mode) {
+            // wire rounds of device buckets: the snapshot is the narrowing itself (sb, or rb
+            // in place, -> wire copy); rb is entirely rewritten by the two phases
+            if (int rc = consumer_wait(st, cs)) return rc;
+            if (int rc = producer_wait(st, round, fresh, cs)) return rc;
+        } else if (int rc = base_copy_in(s, st, round, fresh, cs)) {
+            return rc;
+        }
         if (s.world > 1) {
             if (s.resolve)
                 if (int rc = map_peers(s, st)) return rc;
@@ -973,8 +980,11 @@ struct IpcTransport final : Transport {
     // one more local pass (4 B read + 2 B written per element).  The done pairing that
     // follows keeps the wire copy unchanged until every peer has gathered from it.
     static int wire_phases(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) {
-        if (int rc = narrow_bf16(reinterpret_cast<const float *>(st.rb_dev), reinterpret_cast<uint16_t *>(st.wire),
-                                 s.count, cs))
+        // device buckets: straight from the send bucket (zeroing it if asked); host buckets
+        // were copied into rb by the snapshot
+        const bool from_sb = !s.host_mode && !s.in_place;
+        float *nsrc = reinterpret_cast<float *>(from_sb ? static_cast<char *>(s.sb) : st.rb_dev);
+        if (int rc = narrow_bf16(nsrc, reinterpret_cast<uint16_t *>(st.wire), s.count, from_sb && s.zero_sb, cs))
             return rc;
         if (int rc = pair_ranks(s, s.sh->ready, 0, round, cs)) return rc;
         const uint64_t piece = piece_bytes() / 4;   // elements, as for fp32 rounds

@@ -340,47 +340,54 @@ __global__ __launch_bounds__(256) void k_gather(GatherSet g) {
 // the shard is folded in fp32 in the hypercube tree order and rounded to bf16 once, and every
 // rank widens that same bf16 result back to fp32 -- so all ranks hold identical values, the
 // oracle's bf16 tree of the rounded inputs (oracle/ffref.c ffref_tree_sum_bf16).
-// 8 elements per lane and step: two 16-B fp32 vectors <-> one 16-B bf16 vector.
-__device__ __forceinline__ raw16 narrow8(raw16 a, raw16 b) {
-    uint16_t h[8];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        h[e] = BF16::store(__uint_as_float(a[e]));
-        h[4 + e] = BF16::store(__uint_as_float(b[e]));
-    }
-    raw16 o;
-    __builtin_memcpy(&o, h, 16);
-    return o;
+// 4 elements per lane and access: 16 B of fp32 <-> 8 B of bf16, so that every load and
+// store instruction of a wave covers one contiguous span (16-B bf16 / 2 x 16-B fp32 per
+// lane left every fp32 store instruction half-filling its cache lines: the wire phases
+// ran at half the HBM rate in the shared-GPU rehearsal).
+using raw8 = __attribute__((ext_vector_type(2))) unsigned int;
+
+__device__ __forceinline__ raw8 narrow4(raw16 a) {
+    raw8 h;
+    h[0] = uint32_t(BF16::store(__uint_as_float(a[0]))) | (uint32_t(BF16::store(__uint_as_float(a[1]))) << 16);
+    h[1] = uint32_t(BF16::store(__uint_as_float(a[2]))) | (uint32_t(BF16::store(__uint_as_float(a[3]))) << 16);
+    return h;
 }
 
-__device__ __forceinline__ void widen8(raw16 h, raw16 &a, raw16 &b) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        a[e] = (h[e / 2] >> (16 * (e & 1))) << 16;
-        b[e] = (h[2 + e / 2] >> (16 * (e & 1))) << 16;
-    }
+__device__ __forceinline__ raw16 widen4(raw8 h) {
+    raw16 a;
+    a[0] = h[0] << 16; a[1] = h[0] & 0xffff0000u;
+    a[2] = h[1] << 16; a[3] = h[1] & 0xffff0000u;
+    return a;
 }
 
-// wire = bf16(rb): local HBM, 6 B per element moved (4 read + 2 written)
-__global__ __launch_bounds__(256) void k_narrow_bf16(const float *src, uint16_t *dst, uint64_t n) {
-    const uint64_t nv = n / 8;
-    const raw16 *s = reinterpret_cast<const raw16 *>(src);
-    raw16 *d = reinterpret_cast<raw16 *>(dst);
-    const uint64_t stride = uint64_t(gridDim.x) * 256 * 2;
-    for (uint64_t i = uint64_t(blockIdx.x) * 512 + threadIdx.x; i < nv; i += stride) {
-        raw16 r[2][2];
+// wire = bf16(src): local HBM, 6 B per element moved (4 read + 2 written).  The snapshot
+// of a wire round: src is the send bucket (or rb in place) -- rb itself is not written
+// before phase 1, which overwrites all of it.  ZERO: the wrapper's zero-after-use of the
+// send bucket fused in (ESGD_SCHED_ZERO_SB), 4 B more written per element.
+template <bool ZERO>
+__global__ __launch_bounds__(256) void k_narrow_bf16(float *src, uint16_t *dst, uint64_t n) {
+    constexpr int U = 4;
+    const uint64_t nq = n / 4;
+    raw16 *s = reinterpret_cast<raw16 *>(src);
+    raw8 *d = reinterpret_cast<raw8 *>(dst);
+    const raw16 z = {0u, 0u, 0u, 0u};
+    const uint64_t stride = uint64_t(gridDim.x) * 256 * U;
+    for (uint64_t i = uint64_t(blockIdx.x) * 256 * U + threadIdx.x; i < nq; i += stride) {
+        raw16 r[U];
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-            if (i + u * 256 < nv) {
-                r[u][0] = __builtin_nontemporal_load(s + 2 * (i + u * 256));
-                r[u][1] = __builtin_nontemporal_load(s + 2 * (i + u * 256) + 1);
+        for (int u = 0; u < U; ++u)
+            if (i + u * 256 < nq) r[u] = __builtin_nontemporal_load(s + i + u * 256);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i + u * 256 < nq) {
+                d[i + u * 256] = narrow4(r[u]);
+                if constexpr (ZERO) __builtin_nontemporal_store(z, s + i + u * 256);
             }
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-            if (i + u * 256 < nv) d[i + u * 256] = narrow8(r[u][0], r[u][1]);
     }
-    if (blockIdx.x == 0 && nv * 8 + threadIdx.x < n)
-        dst[nv * 8 + threadIdx.x] = BF16::store(src[nv * 8 + threadIdx.x]);
+    if (blockIdx.x == 0 && nq * 4 + threadIdx.x < n) {
+        dst[nq * 4 + threadIdx.x] = BF16::store(src[nq * 4 + threadIdx.x]);
+        if constexpr (ZERO) src[nq * 4 + threadIdx.x] = 0.0f;
+    }
 }
 
 // Phase 1 over the wire: the K ranks' bf16 copies of this rank's shard (peer HBM, system-
@@ -388,10 +395,10 @@ __global__ __launch_bounds__(256) void k_narrow_bf16(const float *src, uint16_t 
 // rank's wire shard (what peers gather) and its widening to the fp32 bucket.  The own input
 // is the same wire shard: each lane reads its element before it stores it.
 template <int K>
-__global__ __launch_bounds__(256) void k_tree_sum_wire(InputSet in, uint16_t *outb, float *outf, uint32_t nvec,
+__global__ __launch_bounds__(256) void k_tree_sum_wire(InputSet in, uint16_t *outb, float *outf, uint32_t nq,
                                                        uint64_t count) {
-    constexpr int U = 2, B = 256;
-    const int bytes = int(nvec * 16u);
+    constexpr int U = 4, B = 256;
+    const int bytes = int(nq * 8u);
     __amdgpu_buffer_rsrc_t rs[K];
 #pragma unroll
     for (int j = 0; j < K; ++j)
@@ -399,24 +406,33 @@ __global__ __launch_bounds__(256) void k_tree_sum_wire(InputSet in, uint16_t *ou
     __amdgpu_buffer_rsrc_t wb = __builtin_amdgcn_make_buffer_rsrc(outb, (short)0, bytes, 0x00020000);
     __amdgpu_buffer_rsrc_t wf = __builtin_amdgcn_make_buffer_rsrc(outf, (short)0, 2 * bytes, 0x00020000);
     const uint32_t step = gridDim.x * (B * U);
-    for (uint32_t i = blockIdx.x * (B * U) + threadIdx.x; i < nvec; i += step) {
-        raw16 r[U][K];
+    for (uint32_t i = blockIdx.x * (B * U) + threadIdx.x; i < nq; i += step) {
+        raw8 r[U][K];
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int j = 0; j < K; ++j)
-                r[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs[j], (i + u * B) * 16, 0, 19);
+                r[u][j] = __builtin_amdgcn_raw_buffer_load_b64(rs[j], (i + u * B) * 8, 0, 19);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const raw16 h = fold16<BF16, K, false>(r[u], 1.0f);
-            raw16 a, b;
-            widen8(h, a, b);
-            __builtin_amdgcn_raw_buffer_store_b128(h, wb, (i + u * B) * 16, 0, 16);
-            __builtin_amdgcn_raw_buffer_store_b128(a, wf, (i + u * B) * 32, 0, 16);
-            __builtin_amdgcn_raw_buffer_store_b128(b, wf, (i + u * B) * 32 + 16, 0, 16);
+            uint32_t h[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v[K];
+#pragma unroll
+                for (int j = 0; j < K; ++j) v[j] = __uint_as_float((e & 1) ? (r[u][j][e / 2] & 0xffff0000u)
+                                                                            : (r[u][j][e / 2] << 16));
+                tree_fold<BF16, K>(v);
+                h[e] = BF16::store(v[0]);
+            }
+            raw8 hb;
+            hb[0] = h[0] | (h[1] << 16);
+            hb[1] = h[2] | (h[3] << 16);
+            __builtin_amdgcn_raw_buffer_store_b64(hb, wb, (i + u * B) * 8, 0, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(widen4(hb), wf, (i + u * B) * 16, 0, 16);
         }
     }
-    const uint64_t e = uint64_t(nvec) * 8 + threadIdx.x;
+    const uint64_t e = uint64_t(nq) * 4 + threadIdx.x;
     if (blockIdx.x == 0 && e < count) {
         float v[K];
 #pragma unroll
@@ -439,29 +455,25 @@ struct WidenSet {
 };
 
 __global__ __launch_bounds__(256) void k_gather_widen(WidenSet g) {
-    constexpr int B = 256, U = 4;
+    constexpr int B = 256, U = 8;
     const int seg = blockIdx.y;
-    const uint32_t n = g.n[seg], nvec = n / 8;
-    if (nvec) {
+    const uint32_t n = g.n[seg], nq = n / 4;
+    if (nq) {
         __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(g.src[seg]), (short)0,
-                                                                     int(nvec * 16u), 0x00020000);
-        __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(g.dst[seg], (short)0, int(nvec * 32u),
+                                                                     int(nq * 8u), 0x00020000);
+        __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(g.dst[seg], (short)0, int(nq * 16u),
                                                                      0x00020000);
         const uint32_t step = gridDim.x * (B * U);
-        for (uint32_t i = blockIdx.x * (B * U) + threadIdx.x; i < nvec; i += step) {
-            raw16 r[U];
+        for (uint32_t i = blockIdx.x * (B * U) + threadIdx.x; i < nq; i += step) {
+            raw8 r[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, (i + u * B) * 16, 0, 19);
+            for (int u = 0; u < U; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b64(rs, (i + u * B) * 8, 0, 19);
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                raw16 a, b;
-                widen8(r[u], a, b);
-                __builtin_amdgcn_raw_buffer_store_b128(a, ws, (i + u * B) * 32, 0, 16);
-                __builtin_amdgcn_raw_buffer_store_b128(b, ws, (i + u * B) * 32 + 16, 0, 16);
-            }
+            for (int u = 0; u < U; ++u)
+                __builtin_amdgcn_raw_buffer_store_b128(widen4(r[u]), ws, (i + u * B) * 16, 0, 16);
         }
     }
-    const uint32_t e = nvec * 8 + threadIdx.x;
+    const uint32_t e = nq * 4 + threadIdx.x;
     if (blockIdx.x == 0 && e < n)
         g.dst[seg][e] = BF16::load(__hip_atomic_load(g.src[seg] + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
 }
@@ -878,11 +890,13 @@ int gather_remote(int n, const void *const *src, void *const *dst, const uint64_
 }
 
 // ---- bf16-wire entry points (dataplane.cpp, ESGD_SCHED_WIRE_BF16) ----
-int narrow_bf16(const float *src, uint16_t *dst, uint64_t n, hipStream_t s) {
+int narrow_bf16(float *src, uint16_t *dst, uint64_t n, bool zero_src, hipStream_t s) {
     if (!n) return ESGD_SUCCESS;
     ESGD_ARG(((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0,
              "wire: buckets must be 16-B aligned");
-    hipLaunchKernelGGL(k_narrow_bf16, dim3(grid_for(512, n / 8 ? n / 8 : 1, 8)), dim3(256), 0, s, src, dst, n);
+    const dim3 grid(grid_for(1024, n / 4 ? n / 4 : 1, 8));
+    if (zero_src) hipLaunchKernelGGL(k_narrow_bf16<true>, grid, dim3(256), 0, s, src, dst, n);
+    else hipLaunchKernelGGL(k_narrow_bf16<false>, grid, dim3(256), 0, s, src, dst, n);
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;
 }
@@ -890,17 +904,17 @@ int narrow_bf16(const float *src, uint16_t *dst, uint64_t n, hipStream_t s) {
 int reduce_wire(int k, const void *const *inputs, uint16_t *outb, float *outf, uint64_t count, hipStream_t s) {
     ESGD_ARG(k >= 1 && k <= ESGD_MAX_FANIN, "wire: fan-in %d", k);
     if (!count) return ESGD_SUCCESS;
-    ESGD_ARG(count / 8 * 32 + 2 * 256 * 32 < (1ull << 31), "wire: shard piece of %llu elements too large",
+    ESGD_ARG(count / 4 * 16 + 4 * 256 * 16 < (1ull << 31), "wire: shard piece of %llu elements too large",
              (unsigned long long)count);
     InputSet in;
     std::memset(&in, 0, sizeof(in));
     uintptr_t al = reinterpret_cast<uintptr_t>(outb) | reinterpret_cast<uintptr_t>(outf);
     for (int j = 0; j < k; ++j) { in.p[j] = inputs[j]; al |= reinterpret_cast<uintptr_t>(inputs[j]); }
     ESGD_ARG((al & 15) == 0, "wire: shards must be 16-B aligned");
-    const uint32_t nvec = uint32_t(count / 8);
-    const unsigned grid = grid_for(512, nvec ? nvec : 1, 4);
+    const uint32_t nq = uint32_t(count / 4);
+    const unsigned grid = grid_for(1024, nq ? nq : 1, 4);
     switch (k) {
-#define ESGD_WK(K) case K: hipLaunchKernelGGL((k_tree_sum_wire<K>), dim3(grid), dim3(256), 0, s, in, outb, outf, nvec, count); break;
+#define ESGD_WK(K) case K: hipLaunchKernelGGL((k_tree_sum_wire<K>), dim3(grid), dim3(256), 0, s, in, outb, outf, nq, count); break;
     ESGD_WK(1) ESGD_WK(2) ESGD_WK(3) ESGD_WK(4) ESGD_WK(5) ESGD_WK(6) ESGD_WK(7) ESGD_WK(8)
 #undef ESGD_WK
     }
@@ -922,9 +936,9 @@ int gather_widen(int n, const void *const *src, void *const *dst, const uint64_t
         g.src[i] = static_cast<const uint16_t *>(src[i]);
         g.dst[i] = static_cast<float *>(dst[i]);
         g.n[i] = uint32_t(count[i]);
-        maxvec = std::max<uint64_t>(maxvec, count[i] / 8);
+        maxvec = std::max<uint64_t>(maxvec, count[i] / 4);
     }
-    unsigned gx = grid_for(256 * 4, maxvec ? maxvec : 1, 8);
+    unsigned gx = grid_for(256 * 8, maxvec ? maxvec : 1, 8);
     unsigned per_seg = std::max(1u, (unsigned(cu_count()) * 4 + n - 1) / unsigned(n));
     if (gx > per_seg) gx = per_seg;
     hipLaunchKernelGGL(k_gather_widen, dim3(gx, n), dim3(256), 0, s, g);
