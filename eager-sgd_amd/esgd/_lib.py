@@ -60,6 +60,7 @@ _SIGS = {
     "esgd_event_elapsed_ms": (_i, [_vp, _vp, C.POINTER(_f)]),
     "esgd_stream_wait_event": (_i, [_vp, _vp]),
     "esgd_reduce": (_i, [_i, _i, C.POINTER(_vp), _vp, _u64, _vp]),
+    "esgd_reduce_host": (_i, [_i, _i, C.POINTER(_vp), _vp, _u64, _vp]),
     "esgd_reduce_scaled": (_i, [_i, _i, C.POINTER(_vp), _vp, _u64, _f, _vp]),
     "esgd_vsum": (_i, [_i, _vp, _vp, _vp, _u64, _vp]),
     "esgd_fill_uniform_f32": (_i, [_u64, _i, _vp, _u64, _vp]),

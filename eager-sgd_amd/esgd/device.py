@@ -148,6 +148,17 @@ def reduce(dtype: int, inputs, out, count: int, stream=None, scale: float | None
     return check(rc, "esgd_reduce")
 
 
+def reduce_host(dtype: int, inputs, out, count: int, stream=None):
+    """out = tree(inputs) for HOST buckets (int addresses or numpy arrays; pinned ones
+    move by async DMA): chunked H2D / tree kernel / D2H through HBM staging
+    (esgd_reduce_host).  Stream-ordered: synchronize `stream` before reading `out`."""
+    def hp(x):
+        return x.ctypes.data if hasattr(x, "ctypes") else int(x)
+    ptrs = _lib.ptr_array([hp(x) for x in inputs])
+    return check(lib().esgd_reduce_host(dtype, len(inputs), ptrs, hp(out), count, _sh(stream)),
+                 "esgd_reduce_host")
+
+
 def vsum(dtype: int, a, b, c, count: int, stream=None):
     return check(lib().esgd_vsum(dtype, as_ptr(a), as_ptr(b), as_ptr(c), count, _sh(stream)), "esgd_vsum")
 

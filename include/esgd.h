@@ -83,6 +83,17 @@ int esgd_stream_wait_event(void *stream, void *event);
 int esgd_reduce(int dtype, int k, const void *const *inputs, void *out,
                 uint64_t count, void *stream);
 
+/* The same reduction on the reference's contract: `inputs` (k HOST pointers) and `out`
+ * are host buckets.  Pinned, mapped buckets are reduced in place by the tree kernel
+ * through their device views (zero-copy, PCIe both ways at once); others (pageable, or
+ * ESGD_HOST_REDUCE_MODE=dma) run in chunks (ESGD_HOST_REDUCE_CHUNK bytes per input,
+ * default 16 MiB) through HBM staging: chunk c's H2D, chunk c-1's tree kernel and chunk
+ * c-2's D2H overlap (PCIe is full duplex).  Same bits as esgd_reduce.  Stream-ordered: starts after the work
+ * queued on `stream` (NULL: the library stream; ESGD_STREAM_NULL: the legacy default
+ * stream) and `stream` waits for its last copy; buckets must stay valid until then. */
+int esgd_reduce_host(int dtype, int k, const void *const *inputs, void *out,
+                     uint64_t count, void *stream);
+
 /* c = a + b element-wise: the reference's FFSUM operator
  * (src/components/gcomp/ffop_gcomp_operator.c:33-58) on device memory. */
 int esgd_vsum(int dtype, const void *a, const void *b, void *c, uint64_t count,

@@ -252,3 +252,57 @@ def test_windowed_buckets_ragged(dtype, n):
             np.testing.assert_array_equal(_download(out, start, m, np.uint16), want)
         else:
             bits_equal(_download(out, start, m, np.float32), ffref.tree_sum(xs))
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+@pytest.mark.parametrize("dtype", [_lib.FLOAT, _lib.DOUBLE, _lib.INT32, _lib.INT64])
+@pytest.mark.parametrize("k", [1, 3, 8])
+def test_reduce_host_buckets(k, dtype, pinned):
+    # esgd_reduce_host: host buckets in and out (the reference's contract); pinned ones are
+    # reduced in place through their device views (zero-copy), pageable ones chunked
+    # through HBM staging (16 MiB per input and chunk: 3 chunks, a ragged last one, staging
+    # sets reused within the call and across calls)
+    import ctypes as C
+
+    from esgd._lib import check, lib
+    from esgd.device import reduce_host
+    dt = NP[dtype]
+    n = (37 << 20) // np.dtype(dt).itemsize + 5
+    xs = rand_input(dt, k, n, 1000 + k)
+    held = []
+
+    def host_array(x):
+        if not pinned:
+            return np.array(x, copy=True)
+        p = C.c_void_p()
+        check(lib().esgd_host_alloc(C.byref(p), x.nbytes))
+        held.append(p.value)
+        a = np.frombuffer((C.c_char * x.nbytes).from_address(p.value), dtype=x.dtype)
+        a[:] = x
+        return a
+
+    try:
+        ins = [host_array(x) for x in xs]
+        out = host_array(np.zeros(n, dt))
+        s = Stream()
+        reduce_host(dtype, ins, out, n, stream=s)
+        s.synchronize()
+        want = ffref.tree_sum(xs) if k > 1 else xs[0]
+        bits_equal(out.copy(), want)
+        # again, out aliasing input 0, staging sets carried over from the call above
+        reduce_host(dtype, ins, ins[0], n, stream=s)
+        s.synchronize()
+        bits_equal(ins[0].copy(), want)
+    finally:
+        for p in held:
+            lib().esgd_host_free(p)
+
+
+def test_reduce_host_bf16_and_tiny():
+    from esgd.device import reduce_host
+    for n in (1, 7, 4099):
+        xs = [ffref.f32_to_bf16(ffref.fill_uniform(0x5EED, r, n)) for r in range(5)]
+        out = np.zeros(n, np.uint16)
+        reduce_host(_lib.BF16, xs, out, n)
+        synchronize()
+        assert np.array_equal(out, ffref.tree_sum_bf16(xs)), n
