@@ -36,8 +36,9 @@ namespace esgd {
 
 int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64_t count,
                   float scale, hipStream_t s);
+// max_blocks (0: sized for HBM): a cap for copies that run beside the round's kernels
 int gather_remote(int n, const void *const *src, void *const *dst, const uint64_t *bytes,
-                  hipStream_t s);
+                  hipStream_t s, unsigned max_blocks = 0);
 int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s);
 int narrow_bf16(float *src, uint16_t *dst, uint64_t n, bool zero_src, hipStream_t s);
 int reduce_wire(int k, const void *const *inputs, uint16_t *outb, float *outf, uint64_t count, hipStream_t s);
@@ -547,6 +548,17 @@ static uint64_t host_kernel_copy_bytes() {
     return v;
 }
 
+// Chunked host rounds move their chunks by kernel through the pinned bucket's device view
+// (16-B system-scope accesses over PCIe, at most ESGD_HOST_CHUNK_KERNEL workgroups per
+// copy, beside the round's kernels) instead of DMA copies; 0 = DMA.
+static unsigned host_chunk_kernel_blocks() {
+    static const unsigned v = [] {
+        const char *e = getenv("ESGD_HOST_CHUNK_KERNEL");
+        return (e && *e) ? unsigned(strtoul(e, nullptr, 10)) : 0u;
+    }();
+    return v;
+}
+
 // dst <- src, one of them pinned host memory with device view `view` (or nullptr)
 static int host_move(void *dst, const void *src, const void *view, bool h2d, size_t bytes, hipStream_t cs) {
     const void *ks = h2d ? view : src;
@@ -1046,12 +1058,25 @@ struct IpcTransport final : Transport {
         const bool stg = staged(s, st);
         const char *src = stg ? st.pin : static_cast<const char *>(s.sb ? s.sb : s.rb);
         char *dst = stg ? st.pin : static_cast<char *>(s.rb);
+        // device views of the same host buffers (kernel copies), when asked and aligned
+        const char *vsrc = stg ? st.view_pin : (s.sb ? st.view_sb : st.view_rb);
+        char *vdst = stg ? st.view_pin : st.view_rb;
+        const unsigned kb = host_chunk_kernel_blocks();
+        const bool kcopy = kb && vsrc && vdst &&
+                           ((reinterpret_cast<uintptr_t>(vsrc) | reinterpret_cast<uintptr_t>(vdst)) & 15) == 0;
         const uint64_t salign = 1024 / es;
         for (uint32_t c = 0; c < C; ++c) {
             const uint64_t c0 = uint64_t(c) * Q, n = std::min(Q, count - c0);
             hipEvent_t eh = st.cev[3 * c], er = st.cev[3 * c + 1], ed = st.cev[3 * c + 2];
             if (st.chunked_before) ESGD_HIP(hipStreamWaitEvent(hs, ed, 0));   // last round's D2H
-            ESGD_HIP(hipMemcpyAsync(st.rb_dev + c0 * es, src + c0 * es, n * es, hipMemcpyHostToDevice, hs));
+            if (kcopy) {
+                const void *ks = vsrc + c0 * es;
+                void *kd = st.rb_dev + c0 * es;
+                const uint64_t b = n * es;
+                if (int rc = gather_remote(1, &ks, &kd, &b, hs, kb)) return rc;
+            } else {
+                ESGD_HIP(hipMemcpyAsync(st.rb_dev + c0 * es, src + c0 * es, n * es, hipMemcpyHostToDevice, hs));
+            }
             ESGD_HIP(hipEventRecord(eh, hs));
             ESGD_HIP(hipStreamWaitEvent(cs, eh, 0));
             if (s.world > 1) {
@@ -1088,7 +1113,14 @@ struct IpcTransport final : Transport {
             }
             ESGD_HIP(hipEventRecord(er, cs));
             ESGD_HIP(hipStreamWaitEvent(ds, er, 0));
-            ESGD_HIP(hipMemcpyAsync(dst + c0 * es, st.rb_dev + c0 * es, n * es, hipMemcpyDeviceToHost, ds));
+            if (kcopy) {
+                const void *ks = st.rb_dev + c0 * es;
+                void *kd = vdst + c0 * es;
+                const uint64_t b = n * es;
+                if (int rc = gather_remote(1, &ks, &kd, &b, ds, kb)) return rc;
+            } else {
+                ESGD_HIP(hipMemcpyAsync(dst + c0 * es, st.rb_dev + c0 * es, n * es, hipMemcpyDeviceToHost, ds));
+            }
             ESGD_HIP(hipEventRecord(ed, ds));
         }
         ESGD_HIP(hipStreamWaitEvent(cs, st.cev[3 * (C - 1) + 2], 0));   // ds is in order

@@ -865,7 +865,7 @@ int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64
 }
 
 int gather_remote(int n, const void *const *src, void *const *dst, const uint64_t *bytes,
-                  hipStream_t s) {
+                  hipStream_t s, unsigned max_blocks) {
     ESGD_ARG(n >= 0 && n <= kMaxSeg, "gather: %d segments", n);
     if (n == 0) return ESGD_SUCCESS;
     GatherSet g;
@@ -884,6 +884,7 @@ int gather_remote(int n, const void *const *src, void *const *dst, const uint64_
     unsigned gx = grid_for(256 * 4, maxvec ? maxvec : 1, 8);
     unsigned per_seg = std::max(1u, (unsigned(cu_count()) * 4 + n - 1) / unsigned(n));
     if (gx > per_seg) gx = per_seg;
+    if (max_blocks && gx > max_blocks) gx = max_blocks;
     hipLaunchKernelGGL((k_gather<4>), dim3(gx, n), dim3(256), 0, s, g);
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;

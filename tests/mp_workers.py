@@ -122,7 +122,7 @@ def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0
 
 def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0, buf="device",
                   in_place=False, transport="ipc", shadow_ranks=(), small_bytes=None,
-                  piece_bytes=None, host_chunk=None, device_flags=None, wire=False):
+                  piece_bytes=None, host_chunk=None, device_flags=None, wire=False, chunk_kernel=None):
     """Data plane on the GPU: every rank reduces its splitmix bucket; returns the
     result bytes' digest per round plus a bit-exactness verdict against the oracle.
     shadow_ranks: ranks whose device buckets go through the owned shadow bucket.
@@ -142,6 +142,8 @@ def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0
         os.environ["ESGD_HOST_CHUNK_BYTES"] = str(host_chunk)
     if device_flags is not None:
         os.environ["ESGD_DEVICE_FLAGS"] = str(device_flags)
+    if chunk_kernel is not None:
+        os.environ["ESGD_HOST_CHUNK_KERNEL"] = str(chunk_kernel)
 
     from esgd import _lib
     from esgd import device as dev

@@ -288,3 +288,15 @@ def test_wire_bf16_c3_size():
     # slices checked by gpu_config's digest path is not needed: the whole bucket is compared)
     verdicts = run("gpu_allreduce", 2, rounds=1, wire=True, count=(256 << 20) // 4, timeout=400)
     assert all(all(v) for v in verdicts), verdicts
+
+
+@pytest.mark.parametrize("in_place", [False, True])
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_allreduce_host_chunked_kernel_copies(world, in_place):
+    # ESGD_HOST_CHUNK_KERNEL: the chunks of a host bucket move host <-> HBM by kernel
+    # through the pinned bucket's device view (16 workgroups per copy) instead of DMA;
+    # 64 KiB chunks, ragged last chunk, 3 rounds back to back; fp32 and bf16
+    for dt in ("fp32", "bf16"):
+        verdicts = run("gpu_allreduce", world, dtype_name=dt, count=100003, rounds=3, buf="host",
+                       in_place=in_place, host_chunk=65536, chunk_kernel=16)
+        assert all(all(v) for v in verdicts), (dt, verdicts)
