@@ -22,9 +22,20 @@ def main():
     last_fill = max(i for i, r in enumerate(rows) if "k_fill_uniform" in r[2])
     tree = [(i, r) for i, r in enumerate(rows) if "k_tree_sum_buf<esgd::F32, 8, 4, 2, 16, false" in r[2]]
     c2 = [(r[1] - r[0]) / 1e3 for i, r in tree if i < last_fill]
-    gw = [r for i, r in tree if i > last_fill]
-    calls = [gw[j:j + WINDOWS_PER_GATE_CALL] for j in range(0, len(gw) - WINDOWS_PER_GATE_CALL + 1,
-                                                          WINDOWS_PER_GATE_CALL)]
+    # after the gate's fills the bench also runs host_e2e, whose tree launches are single
+    # (serial leg) or read host memory for ms (esgd_reduce_host): a gate call is a run of
+    # exactly four back-to-back HBM windows (gaps of a few us)
+    gw = [r for i, r in tree if i > last_fill and r[1] - r[0] < 1_000_000]
+    runs, cur = [], []
+    for r in gw:
+        if cur and r[0] - cur[-1][1] > 50_000:
+            runs.append(cur)
+            cur = []
+        cur.append(r)
+    if cur:
+        runs.append(cur)
+    calls = [run[j:j + WINDOWS_PER_GATE_CALL] for run in runs if len(run) % WINDOWS_PER_GATE_CALL == 0
+             for j in range(0, len(run), WINDOWS_PER_GATE_CALL)]
     # a call's kernel time: its windows' durations summed (the gaps between them are
     # dispatch gaps, a few us; the span also swallows host syncs between timed loops)
     gate = [sum(r[1] - r[0] for r in c) / 1e3 for c in calls]
