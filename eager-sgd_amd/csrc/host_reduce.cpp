@@ -85,14 +85,17 @@ int ensure(HostReduce &h) {
         set_error("esgd_reduce_host: first used on device %d, now called on device %d", h.device, dev);
         return ESGD_INVALID_ARG;
     }
-    h.chunk = chunk_bytes();
-    ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&h.stage), size_t(kStages) * (ESGD_MAX_FANIN + 1) * h.chunk));
-    for (hipStream_t *s : {&h.h2d, &h.comp, &h.d2h}) ESGD_HIP(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+    // streams and events first (created once, kept on failure), the staging last: a
+    // call that fails part way leaves nothing half-initialised behind `stage`
+    for (hipStream_t *s : {&h.h2d, &h.comp, &h.d2h})
+        if (!*s) ESGD_HIP(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
     for (int i = 0; i < kStages; ++i)
         for (hipEvent_t *e : {&h.uploaded[i], &h.reduced[i], &h.out_free[i]})
-            ESGD_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    ESGD_HIP(hipEventCreateWithFlags(&h.start, hipEventDisableTiming));
-    ESGD_HIP(hipEventCreateWithFlags(&h.done, hipEventDisableTiming));
+            if (!*e) ESGD_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    for (hipEvent_t *e : {&h.start, &h.done})
+        if (!*e) ESGD_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    h.chunk = chunk_bytes();
+    ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&h.stage), size_t(kStages) * (ESGD_MAX_FANIN + 1) * h.chunk));
     h.device = dev;
     return ESGD_SUCCESS;
 }
