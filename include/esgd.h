@@ -83,7 +83,9 @@ int esgd_stream_wait_event(void *stream, void *event);
 int esgd_reduce(int dtype, int k, const void *const *inputs, void *out,
                 uint64_t count, void *stream);
 
-/* The same reduction on the reference's contract: `inputs` (k HOST pointers) and `out`
+/* The same reduction on the reference's contract -- fflib2 sums host buffers on the CPU
+ * (src/components/gcomp/ffop_gcomp_operator.c:33-58, buckets calloc'd by the wrapper,
+ * opt_esgd_solo_imagenet_imbalance.py:288-298): `inputs` (k HOST pointers) and `out`
  * are host buckets.  Pinned, mapped buckets are reduced in place by the tree kernel
  * through their device views (zero-copy, PCIe both ways at once); others (pageable, or
  * ESGD_HOST_REDUCE_MODE=dma) run in chunks (ESGD_HOST_REDUCE_CHUNK bytes per input,
