@@ -390,6 +390,7 @@ int sched_release(Sched *s, void *stream) {
         if (stream)
             if (int rc = s->tp->note_consumer(*s, stream)) return rc;
         s->held = false;
+        s->released = s->waited;
     }
     seg_wake(g_seg);
     return ESGD_SUCCESS;
@@ -466,7 +467,8 @@ static bool step(Sched &s) {
     switch (s.stage) {
     case ST_IDLE: {
         s.awaiting = false;
-        if (s.held) return false;   // the caller still reads the last round's buckets
+        // hold mode: the caller has not yet taken (wait) and released the last round
+        if (s.hold_mode && s.released < s.joined) return false;
         const uint32_t next = s.joined + 1;
         const bool sync = round_is_sync(s, next);
         const uint32_t posted = s.posted.load(std::memory_order_acquire);

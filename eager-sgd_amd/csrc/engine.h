@@ -125,11 +125,15 @@ struct Sched {
     void mark(uint32_t round, int what);
     std::atomic<bool> live{true};
 
-    // ESGD_SCHED_HOLD: once wait() has returned a round, the next round is not joined
-    // before release() -- the caller copies rb out (and drops its late send bucket)
-    // before a peer-activated round can overwrite them (opt_esgd_solo...py:309-314 runs
-    // those steps synchronously right after the wait)
+    // ESGD_SCHED_HOLD: once a round has completed, the next round is not joined before
+    // wait() has returned it AND release() -- the caller copies rb out (and drops its late
+    // send bucket) before a peer-activated round can overwrite them
+    // (opt_esgd_solo...py:309-314 runs those steps synchronously right after the wait).
+    // `released`: rounds the caller has released; a round is joined only once every
+    // joined round has been (holding from wait() on was not enough: a peer could carry
+    // this rank into the next round between the completion and the wait)
     bool hold_mode = false, held = false;
+    uint32_t released = 0;
     // ESGD_SCHED_ZERO_SB: the snapshot zeroes the send bucket as it reads it (device
     // buckets): the wrapper's zero-after-use (:311-314) fused into the move
     bool zero_sb = false;

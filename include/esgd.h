@@ -186,10 +186,11 @@ typedef struct {
 int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t count,
                          int dtype, int async, unsigned seed, esgd_sched_h *out);
 /* flags (extension, 0 = esgd_schedule_create):
- *   ESGD_SCHED_HOLD    after wait/test returns a round, this rank joins no further round
- *                      of the schedule until esgd_schedule_release(): the caller copies
- *                      rb out and drops a late send bucket first, as the reference
- *                      wrapper does synchronously right after its wait
+ *   ESGD_SCHED_HOLD    once a round has completed, this rank joins no further round of
+ *                      the schedule until wait/test has returned that round and
+ *                      esgd_schedule_release() has been called: the caller copies rb out
+ *                      and drops a late send bucket first, as the reference wrapper does
+ *                      synchronously right after its wait
  *                      (opt_esgd_solo_imagenet_imbalance.py:309-314);
  *   ESGD_SCHED_ZERO_SB the snapshot (move sb -> rb) zeroes sb as it reads it (device
  *                      buckets, not in place): the wrapper's zero-after-use (:311-314)

@@ -300,3 +300,24 @@ def test_allreduce_host_chunked_kernel_copies(world, in_place):
         verdicts = run("gpu_allreduce", world, dtype_name=dt, count=100003, rounds=3, buf="host",
                        in_place=in_place, host_chunk=65536, chunk_kernel=16)
         assert all(all(v) for v in verdicts), (dt, verdicts)
+
+
+@pytest.mark.parametrize("count", [65536, (1 << 20) + 3])   # one-launch and five-launch rounds
+@pytest.mark.parametrize("kind", [SOLO, MAJORITY])
+def test_activation_stress(kind, count):
+    # 600 steps per rank, random delays, no barriers: every round's result carries exactly
+    # round t's bucket of every rank (int32 tags), the limiter cadence / majority activator
+    # sequence hold, and peers' activations really carried ranks through rounds
+    world, rounds, async_, seed = 3, 600, 3, 34495645   # seed of rand_allreduce_correctness.c:64
+    outs = run("gpu_stress", world, kind=kind, count=count, rounds=rounds, async_=async_, seed=seed,
+               timeout=400)
+    acts = ffref.activators(seed, world, rounds)
+    for o in outs:
+        assert o["nbad"] == 0, o["bad"]
+        log = o["log"]
+        assert [e["round"] for e in log] == list(range(1, rounds + 1))
+        if kind == SOLO:
+            assert [e["sync"] for e in log] == [t % (async_ + 1) == 0 for t in range(1, rounds + 1)]
+        else:
+            assert [e["activator"] for e in log] == acts
+    assert sum(o["stats"]["auto_rounds"] for o in outs) > 0   # the stress exercised auto-joins
