@@ -761,7 +761,7 @@ def cp_hold(rank, world, hold_s=0.3):
     return out
 
 
-def gpu_stress(rank, world, kind, count, rounds=600, async_=3, seed=34495645, jitter_us=300):
+def gpu_stress(rank, world, kind, count, rounds=600, async_=3, seed=34495645, jitter_us=300, buf="device"):
     """Activation stress on the GPU data plane (the reference loops its activation test
     300 times to catch nondeterministic failures, test_activation.sh:5-7): every rank
     runs `rounds` steps with a random per-step delay and NO barrier between steps, so
@@ -769,10 +769,12 @@ def gpu_stress(rank, world, kind, count, rounds=600, async_=3, seed=34495645, ji
     (majority) and ranks are carried through rounds they have not posted yet.
     Schedules as the deep500 op uses them (ESGD_SCHED_HOLD | ZERO_SB): the gradient for
     step t+1 is written while round t is held, then released.  int32 round tags: rank r
-    writes (t mod 1024) << (10 r), so every element of round t's result must decode to
-    tag t for EVERY rank -- each round took exactly the right generation of every rank's
-    bucket, whole (no stale, torn or doubly counted data).  Returns per-round verdicts,
-    the round log and the stats."""
+    writes (t mod 2^b) << (b r), b = min(10, 31 // P), so every element of round t's
+    result must decode to tag t for EVERY rank -- each round took exactly the right
+    generation of every rank's bucket, whole (no stale, torn or doubly counted data).
+    buf="host": the reference's
+    host buckets (HOLD only; the host bucket keeps its tag after the snapshot, refilled
+    each step the same way).  Returns per-round verdicts, the round log and the stats."""
     import random
 
     import numpy as np
@@ -780,16 +782,26 @@ def gpu_stress(rank, world, kind, count, rounds=600, async_=3, seed=34495645, ji
     from esgd import _lib
     from esgd import device as dev
     comm = _comm()
-    sb, rb = dev.DeviceBuffer(count, _lib.INT32), dev.DeviceBuffer(count, _lib.INT32)
-    rb.zero()
-    dev.synchronize()
+    host = buf == "host"
+    bits = min(10, 31 // world)   # tag bits per rank (int32, no overflow at any P)
+    if host:
+        sb, rb = np.zeros(count, np.int32), np.zeros(count, np.int32)
+    else:
+        sb, rb = dev.DeviceBuffer(count, _lib.INT32), dev.DeviceBuffer(count, _lib.INT32)
+        rb.zero()
+        dev.synchronize()
 
     def fill(t):
-        sb.upload(np.full(count, (t % 1024) << (10 * rank), np.int32))
+        v = (t % (1 << bits)) << (bits * rank)
+        if host:
+            sb[:] = v
+        else:
+            sb.upload(np.full(count, v, np.int32))
 
     fill(1)
-    s = comm.Schedule(kind, sb, rb, count, dtype=_lib.INT32, async_=async_, seed=seed, buf=comm.BUF_DEVICE,
-                      flags=comm.HOLD | comm.ZERO_SB)
+    s = comm.Schedule(kind, sb, rb, count, dtype=_lib.INT32, async_=async_, seed=seed,
+                      buf=comm.BUF_HOST if host else comm.BUF_DEVICE,
+                      flags=comm.HOLD | (0 if host else comm.ZERO_SB))
     rng = random.Random(1000 + rank)
     m = min(count, 2048)
     bad = []
@@ -799,10 +811,13 @@ def gpu_stress(rank, world, kind, count, rounds=600, async_=3, seed=34495645, ji
         time.sleep(rng.random() * jitter_us * 1e-6)
         s.post()
         fresh.append(s.wait())
-        head, tail = _download_slice(rb, 0, m), _download_slice(rb, count - m, m)
+        if host:
+            head, tail = rb[:m].copy(), rb[count - m:].copy()
+        else:
+            head, tail = _download_slice(rb, 0, m), _download_slice(rb, count - m, m)
         v = int(head[0])
-        tags = [(v >> (10 * q)) & 1023 for q in range(world)]
-        if not (np.all(head == v) and np.all(tail == v) and tags == [t % 1024] * world):
+        tags = [(v >> (bits * q)) & ((1 << bits) - 1) for q in range(world)]
+        if not (np.all(head == v) and np.all(tail == v) and tags == [t % (1 << bits)] * world):
             bad.append((t, tags, bool(np.all(head == v)), bool(np.all(tail == v))))
         fill(t + 1)
         s.release()

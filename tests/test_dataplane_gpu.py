@@ -302,15 +302,21 @@ def test_allreduce_host_chunked_kernel_copies(world, in_place):
         assert all(all(v) for v in verdicts), (dt, verdicts)
 
 
-@pytest.mark.parametrize("count", [65536, (1 << 20) + 3])   # one-launch and five-launch rounds
+STRESS = {"p3-one-launch": (3, 65536, "device"), "p3-five-launch": (3, (1 << 20) + 3, "device"),
+          "p8-one-launch": (8, 65536, "device"), "p3-host-kernel-copy": (3, 65536, "host"),
+          "p3-host-dma": (3, (1 << 20) + 3, "host")}
+
+
+@pytest.mark.parametrize("case", sorted(STRESS))
 @pytest.mark.parametrize("kind", [SOLO, MAJORITY])
-def test_activation_stress(kind, count):
+def test_activation_stress(kind, case):
     # 600 steps per rank, random delays, no barriers: every round's result carries exactly
     # round t's bucket of every rank (int32 tags), the limiter cadence / majority activator
     # sequence hold, and peers' activations really carried ranks through rounds
-    world, rounds, async_, seed = 3, 600, 3, 34495645   # seed of rand_allreduce_correctness.c:64
+    world, count, buf = STRESS[case]
+    rounds, async_, seed = 600, 3, 34495645   # seed of rand_allreduce_correctness.c:64
     outs = run("gpu_stress", world, kind=kind, count=count, rounds=rounds, async_=async_, seed=seed,
-               timeout=400)
+               buf=buf, timeout=400)
     acts = ffref.activators(seed, world, rounds)
     for o in outs:
         assert o["nbad"] == 0, o["bad"]
