@@ -826,3 +826,52 @@ def gpu_stress(rank, world, kind, count, rounds=600, async_=3, seed=34495645, ji
     s.delete()
     comm.finalize()
     return out
+
+
+def gpu_stress_multi(rank, world, kind, counts=(4096, 65536, (1 << 20) + 3, 300007), rounds=200, async_=3,
+                     seed=34495645, jitter_us=200):
+    """gpu_stress over several schedules at once, the way the wrapper drives its 161
+    per-tensor ops (opt_esgd_solo_imagenet_imbalance.py:301-316): every step runs the
+    schedules one after the other (post, wait, read, refill, release), with random delays
+    between them and no barrier, so rounds of different schedules -- one-launch and
+    five-launch sizes mixed -- are activated, issued (the node's issue ring) and carried
+    through in interleaved orders on different ranks.  Same int32 tag check per round."""
+    import random
+
+    import numpy as np
+
+    from esgd import _lib
+    from esgd import device as dev
+    comm = _comm()
+    bits = min(10, 31 // world)
+    scheds = []
+    for i, n in enumerate(counts):
+        sb, rb = dev.DeviceBuffer(n, _lib.INT32), dev.DeviceBuffer(n, _lib.INT32)
+        rb.zero()
+        sb.upload(np.full(n, 1 << (bits * rank), np.int32))
+        s = comm.Schedule(kind, sb, rb, n, dtype=_lib.INT32, async_=async_, seed=seed + i,
+                          buf=comm.BUF_DEVICE, flags=comm.HOLD | comm.ZERO_SB)
+        scheds.append((s, sb, rb, n))
+    rng = random.Random(2000 + rank)
+    bad = []
+    comm.barrier()
+    for t in range(1, rounds + 1):
+        for i, (s, sb, rb, n) in enumerate(scheds):
+            time.sleep(rng.random() * jitter_us * 1e-6)
+            s.post()
+            s.wait()
+            m = min(n, 1024)
+            head, tail = _download_slice(rb, 0, m), _download_slice(rb, n - m, m)
+            v = int(head[0])
+            tags = [(v >> (bits * q)) & ((1 << bits) - 1) for q in range(world)]
+            if not (np.all(head == v) and np.all(tail == v) and tags == [t % (1 << bits)] * world):
+                bad.append((i, t, tags))
+            sb.upload(np.full(n, ((t + 1) % (1 << bits)) << (bits * rank), np.int32))
+            s.release()
+    comm.barrier()
+    logs = [s.log() for s, *_ in scheds]
+    autos = sum(s.stats()["auto_rounds"] for s, *_ in scheds)
+    for s, sb, rb, _ in scheds:
+        s.delete()
+    comm.finalize()
+    return {"bad": bad[:10], "nbad": len(bad), "logs": logs, "auto_rounds": autos}

@@ -327,3 +327,18 @@ def test_activation_stress(kind, case):
         else:
             assert [e["activator"] for e in log] == acts
     assert sum(o["stats"]["auto_rounds"] for o in outs) > 0   # the stress exercised auto-joins
+
+
+@pytest.mark.parametrize("kind", [SOLO, MAJORITY])
+def test_activation_stress_many_schedules(kind):
+    # four schedules driven like the wrapper's per-tensor ops, random delays, no barriers:
+    # every round of every schedule takes exactly its generation of every rank's bucket
+    world, rounds, async_, seed = 3, 200, 3, 34495645
+    outs = run("gpu_stress_multi", world, kind=kind, rounds=rounds, async_=async_, seed=seed, timeout=400)
+    for o in outs:
+        assert o["nbad"] == 0, o["bad"]
+        for i, log in enumerate(o["logs"]):
+            assert [e["round"] for e in log] == list(range(1, rounds + 1))
+            if kind == MAJORITY:
+                assert [e["activator"] for e in log] == ffref.activators(seed + i, world, rounds)
+    assert sum(o["auto_rounds"] for o in outs) > 0
