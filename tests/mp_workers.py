@@ -761,7 +761,8 @@ def cp_hold(rank, world, hold_s=0.3):
     return out
 
 
-def gpu_stress(rank, world, kind, count, rounds=600, async_=3, seed=34495645, jitter_us=300, buf="device"):
+def gpu_stress(rank, world, kind, count, rounds=600, async_=3, seed=34495645, jitter_us=300, buf="device",
+               wire=False):
     """Activation stress on the GPU data plane (the reference loops its activation test
     300 times to catch nondeterministic failures, test_activation.sh:5-7): every rank
     runs `rounds` steps with a random per-step delay and NO barrier between steps, so
@@ -774,7 +775,11 @@ def gpu_stress(rank, world, kind, count, rounds=600, async_=3, seed=34495645, ji
     generation of every rank's bucket, whole (no stale, torn or doubly counted data).
     buf="host": the reference's
     host buckets (HOLD only; the host bucket keeps its tag after the snapshot, refilled
-    each step the same way).  Returns per-round verdicts, the round log and the stats."""
+    each step the same way).  wire=True: fp32 buckets with bf16 on the wire
+    (ESGD_SCHED_WIRE_BF16); the tags are then ((t mod 2) + 1) << (2 r) (P <= 4; a missing
+    share decodes as 0, a stale one as the other parity) or (t mod 2) << r (P > 4), sums
+    below 256 that bf16 carries exactly.
+    Returns per-round verdicts, the round log and the stats."""
     import random
 
     import numpy as np
@@ -783,25 +788,34 @@ def gpu_stress(rank, world, kind, count, rounds=600, async_=3, seed=34495645, ji
     from esgd import device as dev
     comm = _comm()
     host = buf == "host"
-    bits = min(10, 31 // world)   # tag bits per rank (int32, no overflow at any P)
+    # tag bits per rank: int32 without overflow at any P; over the wire the sum must stay
+    # below 256 (bf16's 8 significant bits): 2 bits up to P = 4, 1 bit (the parity) above
+    bits = (2 if world <= 4 else 1) if wire else min(10, 31 // world)
+    dt, npdt = (_lib.FLOAT, np.float32) if wire else (_lib.INT32, np.int32)
+
+    def tag(t):
+        if wire:
+            return (t % 2) + 1 if bits == 2 else t % 2
+        return t % (1 << bits)
+
     if host:
-        sb, rb = np.zeros(count, np.int32), np.zeros(count, np.int32)
+        sb, rb = np.zeros(count, npdt), np.zeros(count, npdt)
     else:
-        sb, rb = dev.DeviceBuffer(count, _lib.INT32), dev.DeviceBuffer(count, _lib.INT32)
+        sb, rb = dev.DeviceBuffer(count, dt), dev.DeviceBuffer(count, dt)
         rb.zero()
         dev.synchronize()
 
     def fill(t):
-        v = (t % (1 << bits)) << (bits * rank)
+        v = tag(t) << (bits * rank)
         if host:
             sb[:] = v
         else:
-            sb.upload(np.full(count, v, np.int32))
+            sb.upload(np.full(count, v, npdt))
 
     fill(1)
-    s = comm.Schedule(kind, sb, rb, count, dtype=_lib.INT32, async_=async_, seed=seed,
+    s = comm.Schedule(kind, sb, rb, count, dtype=dt, async_=async_, seed=seed,
                       buf=comm.BUF_HOST if host else comm.BUF_DEVICE,
-                      flags=comm.HOLD | (0 if host else comm.ZERO_SB))
+                      flags=comm.HOLD | (0 if host else comm.ZERO_SB) | (comm.WIRE_BF16 if wire else 0))
     rng = random.Random(1000 + rank)
     m = min(count, 2048)
     bad = []
@@ -817,8 +831,8 @@ def gpu_stress(rank, world, kind, count, rounds=600, async_=3, seed=34495645, ji
             head, tail = _download_slice(rb, 0, m), _download_slice(rb, count - m, m)
         v = int(head[0])
         tags = [(v >> (bits * q)) & ((1 << bits) - 1) for q in range(world)]
-        if not (np.all(head == v) and np.all(tail == v) and tags == [t % (1 << bits)] * world):
-            bad.append((t, tags, bool(np.all(head == v)), bool(np.all(tail == v))))
+        if not (np.all(head == head[0]) and np.all(tail == head[0]) and tags == [tag(t)] * world):
+            bad.append((t, tags, bool(np.all(head == head[0])), bool(np.all(tail == head[0]))))
         fill(t + 1)
         s.release()
     comm.barrier()

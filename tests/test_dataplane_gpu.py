@@ -342,3 +342,17 @@ def test_activation_stress_many_schedules(kind):
             if kind == MAJORITY:
                 assert [e["activator"] for e in log] == ffref.activators(seed + i, world, rounds)
     assert sum(o["auto_rounds"] for o in outs) > 0
+
+
+@pytest.mark.parametrize("world", [3, 8])
+@pytest.mark.parametrize("kind", [SOLO, MAJORITY])
+def test_activation_stress_wire_bf16(kind, world):
+    # the same stress over the bf16 wire (the optimizer's wire="bf16" path): small
+    # integer tags that bf16 carries exactly
+    rounds, async_, seed = 400, 3, 34495645
+    outs = run("gpu_stress", world, kind=kind, count=(1 << 18) + 3, rounds=rounds, async_=async_, seed=seed,
+               wire=True, timeout=400)
+    for o in outs:
+        assert o["nbad"] == 0, o["bad"]
+        assert [e["round"] for e in o["log"]] == list(range(1, rounds + 1))
+    assert sum(o["stats"]["auto_rounds"] for o in outs) > 0
