@@ -34,7 +34,8 @@ namespace esgd {
 int create_schedule(int kind, int buf, const void *sb, void *rb, uint64_t count, int dtype, int async,
                     unsigned seed, unsigned flags, int tag, uint64_t *out) {
     ESGD_ARG(out, "esgd_schedule_create: null output");
-    ESGD_ARG((flags & ~unsigned(ESGD_SCHED_HOLD | ESGD_SCHED_ZERO_SB | ESGD_SCHED_WIRE_BF16)) == 0,
+    ESGD_ARG((flags & ~unsigned(ESGD_SCHED_HOLD | ESGD_SCHED_ZERO_SB | ESGD_SCHED_WIRE_BF16 |
+                                ESGD_SCHED_FRESH_ONLY)) == 0,
              "esgd_schedule_create: unknown flags 0x%x", flags);
     ESGD_ARG(!(flags & ESGD_SCHED_WIRE_BF16) || dtype == ESGD_FLOAT,
              "esgd_schedule_create: ESGD_SCHED_WIRE_BF16 needs FLOAT buckets (dtype %d)", dtype);

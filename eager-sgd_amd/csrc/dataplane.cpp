@@ -589,9 +589,9 @@ static int ensure_pin(BaseState &st, size_t bytes) {
 // Join-time host work: the move of an unpinned host bucket into the pinned staging
 // buffer happens now, when the rank joins (the reference's move reads sb at activation,
 // colls/ffallreduce.c:126-130).  The previous round has completed, so the buffer is free.
-static int base_prepare(Sched &s, BaseState &st) {
+static int base_prepare(Sched &s, BaseState &st, bool fresh) {
     const size_t bytes = s.count * s.esize;
-    if (bytes && staged(s, st)) {
+    if (bytes && staged(s, st) && !(s.fresh_only && !fresh)) {   // FRESH_ONLY: not read
         if (int rc = ensure_pin(st, bytes)) return rc;
         std::memcpy(st.pin, s.sb ? s.sb : s.rb, bytes);
     }
@@ -614,6 +614,12 @@ static int base_copy_in(Sched &s, BaseState &st, uint32_t round, bool fresh, hip
     if (int rc = producer_wait(st, round, fresh, cs)) return rc;
     const size_t bytes = s.count * s.esize;
     if (!bytes) return ESGD_SUCCESS;
+    if (s.fresh_only && !fresh) {
+        // carried through a round it had not posted: this rank contributes zeros, and its
+        // send bucket -- which the caller may be writing right now -- is not read
+        ESGD_HIP(hipMemsetAsync(st.rb_dev, 0, bytes, cs));
+        return ESGD_SUCCESS;
+    }
     if (s.host_mode) {
         const bool stg = staged(s, st);
         const void *src = stg ? st.pin : (s.sb ? s.sb : s.rb);
@@ -880,7 +886,7 @@ struct IpcTransport final : Transport {
 
     // join: a moved bucket is re-published before this rank's join counts (peers map it
     // when they launch the round); a size change alone only updates the published size
-    int prepare(Sched &s, uint32_t round, bool) override {
+    int prepare(Sched &s, uint32_t round, bool fresh) override {
         IpcState &st = S(s);
         const int moved = base_refit(s, st);
         if (moved < 0) return moved;
@@ -893,7 +899,7 @@ struct IpcTransport final : Transport {
         st.peer[s.rank] = s.wire_bf16 ? st.wire : st.rb_dev;   // what peers read
         ESGD_TRACE("r%d sched %d round %u join count=%llu rb_dev=%p moved=%d staged=%d\n", s.rank, s.id,
                    round, (unsigned long long)s.count, (void *)st.rb_dev, moved, int(staged(s, st)));
-        return base_prepare(s, st);
+        return base_prepare(s, st, fresh);
     }
 
     // The whole round, queued on the round stream:
@@ -933,7 +939,7 @@ struct IpcTransport final : Transport {
                 return base_copy_out(s, st, cs);
             }
             if (s.wire_bf16) {
-                if (int rc = wire_phases(s, st, round, cs)) return rc;
+                if (int rc = wire_phases(s, st, round, fresh, cs)) return rc;
             } else {
             if (int rc = pair_ranks(s, s.sh->ready, 0, round, cs)) return rc;
             // Launches move at most kPiece bytes per input / segment (the kernels address
@@ -991,13 +997,18 @@ struct IpcTransport final : Transport {
     // Peers read S/2 bytes per phase and rank pair instead of S: half the xGMI traffic, for
     // one more local pass (4 B read + 2 B written per element).  The done pairing that
     // follows keeps the wire copy unchanged until every peer has gathered from it.
-    static int wire_phases(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) {
+    static int wire_phases(Sched &s, IpcState &st, uint32_t round, bool fresh, hipStream_t cs) {
         // device buckets: straight from the send bucket (zeroing it if asked); host buckets
-        // were copied into rb by the snapshot
+        // were copied into rb by the snapshot; FRESH_ONLY rounds this rank had not posted
+        // contribute zeros (nothing read)
         const bool from_sb = !s.host_mode && !s.in_place;
-        float *nsrc = reinterpret_cast<float *>(from_sb ? static_cast<char *>(s.sb) : st.rb_dev);
-        if (int rc = narrow_bf16(nsrc, reinterpret_cast<uint16_t *>(st.wire), s.count, from_sb && s.zero_sb, cs))
-            return rc;
+        if (s.fresh_only && !fresh && !s.host_mode) {
+            ESGD_HIP(hipMemsetAsync(st.wire, 0, s.count * 2, cs));
+        } else {
+            float *nsrc = reinterpret_cast<float *>(from_sb ? static_cast<char *>(s.sb) : st.rb_dev);
+            if (int rc = narrow_bf16(nsrc, reinterpret_cast<uint16_t *>(st.wire), s.count, from_sb && s.zero_sb, cs))
+                return rc;
+        }
         if (int rc = pair_ranks(s, s.sh->ready, 0, round, cs)) return rc;
         const uint64_t piece = piece_bytes() / 4;   // elements, as for fp32 rounds
         const int r = s.rank;
@@ -1069,7 +1080,9 @@ struct IpcTransport final : Transport {
             const uint64_t c0 = uint64_t(c) * Q, n = std::min(Q, count - c0);
             hipEvent_t eh = st.cev[3 * c], er = st.cev[3 * c + 1], ed = st.cev[3 * c + 2];
             if (st.chunked_before) ESGD_HIP(hipStreamWaitEvent(hs, ed, 0));   // last round's D2H
-            if (kcopy) {
+            if (s.fresh_only && !fresh) {   // not posted: zeros, the host bucket is not read
+                ESGD_HIP(hipMemsetAsync(st.rb_dev + c0 * es, 0, n * es, hs));
+            } else if (kcopy) {
                 const void *ks = vsrc + c0 * es;
                 void *kd = st.rb_dev + c0 * es;
                 const uint64_t b = n * es;
@@ -1318,12 +1331,12 @@ struct RcclTransport final : Transport {
 
     int note_consumer(Sched &s, void *stream) override { return base_note_consumer(S(s), stream); }
 
-    int prepare(Sched &s, uint32_t, bool) override {
+    int prepare(Sched &s, uint32_t, bool fresh) override {
         RcclState &st = S(s);
         const int moved = base_refit(s, st);
         if (moved < 0) return moved;
         if (int rc = fit_stage(s, st)) return rc;
-        return base_prepare(s, st);
+        return base_prepare(s, st, fresh);
     }
 
     static uint64_t piece(uint64_t len, uint64_t c, uint64_t chunk) {

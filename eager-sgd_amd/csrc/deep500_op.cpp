@@ -14,15 +14,16 @@
 //     graph calls ops in the same order on every rank, which the reference relies on
 //     for its 161 creations at :288-293);
 //   * report() returns the bytes reduced (the reference always returns 0, :273-275);
-//   * the schedule holds after each wait (ESGD_SCHED_HOLD) until the copy-out and the
-//     zeroing are queued, so a round a peer activates next cannot overwrite rb under the
-//     copy-out or snapshot a gradient that is about to be dropped -- the reference gets
-//     the same ordering by doing both synchronously right after its wait (:309-314);
-//   * device path: the zeroing is fused into the next snapshot (ESGD_SCHED_ZERO_SB) and
-//     the wrapper's division by the comm size (:40) into the copy-in
-//     (allreducef_forward_cuda_div); a rank whose round was carried by a peer's
-//     activation before its own post drops its late gradient exactly as the reference's
-//     unconditional zeroing does;
+//   * the schedule holds from each round's completion (ESGD_SCHED_HOLD) until the copy-out
+//     is queued, so a round a peer activates next cannot overwrite rb under the copy-out
+//     -- the reference gets the same ordering by doing it synchronously right after its
+//     wait (:309-314);
+//   * a round a peer's activation carries this rank through before its post contributes
+//     zeros (ESGD_SCHED_FRESH_ONLY): the late gradient is dropped, as the reference's
+//     zeroing after use intends, but never read half-written -- the reference's move can
+//     read the bucket while :301 is still copying into it.  The device path therefore
+//     needs no zeroing pass at all, and the wrapper's division by the comm size (:40) is
+//     fused into the copy-in (allreducef_forward_cuda_div);
 //   * the extension entry points return a status instead of aborting the process.
 #include <hip/hip_runtime.h>
 
@@ -107,7 +108,7 @@ struct AllreduceOp {
         }
         const int kind = cfg.mode == ESGD_OP_MAJORITY ? ESGD_SCHED_MAJORITY
                          : cfg.mode == ESGD_OP_ALLREDUCE ? ESGD_SCHED_ALLREDUCE : ESGD_SCHED_SOLO;
-        const unsigned flags = ESGD_SCHED_HOLD | (dev ? ESGD_SCHED_ZERO_SB : 0u) |
+        const unsigned flags = ESGD_SCHED_HOLD | ESGD_SCHED_FRESH_ONLY |
                                (dev && cfg.wire == ESGD_BF16 ? ESGD_SCHED_WIRE_BF16 : 0u);
         if (esgd_schedule_create_ex(kind, dev ? ESGD_BUF_DEVICE : ESGD_BUF_HOST, sb, rb, len,
                                     ESGD_FLOAT, cfg.async, cfg.seed, flags, &sched))
@@ -122,16 +123,11 @@ struct AllreduceOp {
         // the snapshot of this round waits for the copy-in just queued on the caller's
         // stream (the data plane's streams are non-blocking: the NULL stream is named)
         void *ps = s ? static_cast<void *>(s) : ESGD_STREAM_NULL;
-        int fresh = 1;
+        // a round a peer's activation carried this rank through before this post took
+        // zeros, not the gradient (FRESH_ONLY): the gradient is dropped, and the next
+        // copy-in overwrites the send bucket before it is read again
         if (int rc = esgd_schedule_post(sched, ps, nullptr)) return rc;
-        if (int rc = esgd_schedule_wait_ex(sched, &fresh)) return rc;
-        // a round carried by a peer's activation before this post did not take the
-        // gradient: drop it (the reference zeroes sb after every wait, :311-314; fresh
-        // rounds had sb zeroed by their snapshot)
-        if (!fresh && hipMemsetAsync(sb, 0, nbytes, s) != hipSuccess) {
-            esgd::set_error("allreducef: zeroing the send bucket failed");
-            return ESGD_ERROR;
-        }
+        if (int rc = esgd_schedule_wait(sched)) return rc;
         if (int rc = out()) return rc;
         if (int rc = esgd_schedule_release(sched, ps)) return rc;
         bytes += int64_t(nbytes);

@@ -208,6 +208,7 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     s->hold_mode = (flags & ESGD_SCHED_HOLD) != 0;
     s->zero_sb = (flags & ESGD_SCHED_ZERO_SB) != 0 && !host_mode && !s->in_place;
     s->wire_bf16 = (flags & ESGD_SCHED_WIRE_BF16) != 0;
+    s->fresh_only = (flags & ESGD_SCHED_FRESH_ONLY) != 0;
     // Schedule ids are never reused within a job and the segment starts zeroed, so the
     // shared state of this id needs no reset (no barrier before setup).  Creation is two
     // voted steps: setup (local: buckets, streams, publication) -> barrier -> every rank

@@ -140,6 +140,9 @@ struct Sched {
     // ESGD_SCHED_WIRE_BF16 (fp32 buckets, IPC transport): peers read a bf16 copy of the
     // bucket, half the xGMI bytes; the result is the bf16-rounded tree widened to fp32
     bool wire_bf16 = false;
+    // ESGD_SCHED_FRESH_ONLY: a round joined before this rank posted it contributes zeros
+    // (the snapshot zeroes the bucket instead of reading sb)
+    bool fresh_only = false;
     uint8_t fresh_of[256] = {};   // round % 256 -> this rank had posted it before joining
 };
 

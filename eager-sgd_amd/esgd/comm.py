@@ -23,7 +23,7 @@ from ._lib import check, lib
 
 ALLREDUCE, SOLO, MAJORITY = 0, 1, 2
 BUF_DEVICE, BUF_HOST, BUF_NONE = 0, 1, 2
-HOLD, ZERO_SB, WIRE_BF16 = 0x1, 0x2, 0x4   # esgd_schedule_create_ex flags (esgd.h)
+HOLD, ZERO_SB, WIRE_BF16, FRESH_ONLY = 0x1, 0x2, 0x4, 0x8   # esgd_schedule_create_ex flags (esgd.h)
 
 
 class SchedStats(C.Structure):

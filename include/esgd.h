@@ -202,9 +202,17 @@ int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t c
  *                      widened to fp32 (identical on all ranks).  Not in the reference (no
  *                      bf16 in ff.h): parity unpinned, checked against the oracle's
  *                      convention (ffref_tree_sum_bf16 of the rounded inputs). */
+/*   ESGD_SCHED_FRESH_ONLY a round this rank joins before posting it (a peer's activation
+ *                      carried it through) contributes zeros: its send bucket is not read.
+ *                      The reference's wrapper means the same by zeroing the send bucket
+ *                      after use (opt_esgd_solo_imagenet_imbalance.py:311-314), but its
+ *                      move can read a bucket the caller is still writing (:301); here a
+ *                      late gradient never enters a round, whole or torn, and the send
+ *                      bucket needs no zeroing (the deep500 op uses HOLD | FRESH_ONLY). */
 #define ESGD_SCHED_HOLD 0x1
 #define ESGD_SCHED_ZERO_SB 0x2
 #define ESGD_SCHED_WIRE_BF16 0x4
+#define ESGD_SCHED_FRESH_ONLY 0x8
 int esgd_schedule_create_ex(int kind, int buf, const void *sb, void *rb, uint64_t count,
                             int dtype, int async, unsigned seed, unsigned flags,
                             esgd_sched_h *out);

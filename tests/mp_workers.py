@@ -889,3 +889,57 @@ def gpu_stress_multi(rank, world, kind, counts=(4096, 65536, (1 << 20) + 3, 3000
         s.delete()
     comm.finalize()
     return {"bad": bad[:10], "nbad": len(bad), "logs": logs, "auto_rounds": autos}
+
+
+def gpu_stress_fresh(rank, world, kind, count, rounds=600, async_=3, seed=34495645, jitter_us=300,
+                     buf="device"):
+    """ESGD_SCHED_HOLD | FRESH_ONLY -- how the deep500 op drives its schedule -- under the
+    same stress, in the wrapper's own (racy) order: the gradient for step t is written
+    AFTER round t-1 was released, right before the post (opt_esgd_solo...py:301), so a
+    peer's activation may carry this rank into round t while it is still writing.  int32
+    tags as in gpu_stress; returns every round's decoded result and this rank's fresh
+    flags: a rank's share of round t must be its tag t if it had posted the round before
+    joining it, and 0 if it had not (never a torn or stale bucket)."""
+    import random
+
+    import numpy as np
+
+    from esgd import _lib
+    from esgd import device as dev
+    comm = _comm()
+    host = buf == "host"
+    bits = min(10, 31 // world)
+    if host:
+        sb, rb = np.zeros(count, np.int32), np.zeros(count, np.int32)
+    else:
+        sb, rb = dev.DeviceBuffer(count, _lib.INT32), dev.DeviceBuffer(count, _lib.INT32)
+        rb.zero()
+        dev.synchronize()
+    s = comm.Schedule(kind, sb, rb, count, dtype=_lib.INT32, async_=async_, seed=seed,
+                      buf=comm.BUF_HOST if host else comm.BUF_DEVICE, flags=comm.HOLD | comm.FRESH_ONLY)
+    rng = random.Random(3000 + rank)
+    m = min(count, 2048)
+    vals, fresh, torn = [], [], []
+    comm.barrier()
+    for t in range(1, rounds + 1):
+        time.sleep(rng.random() * jitter_us * 1e-6)
+        v = (t % (1 << bits)) << (bits * rank)
+        if host:
+            sb[:] = v
+        else:
+            sb.upload(np.full(count, v, np.int32))
+        s.post()
+        fresh.append(s.wait())
+        if host:
+            head, tail = rb[:m].copy(), rb[count - m:].copy()
+        else:
+            head, tail = _download_slice(rb, 0, m), _download_slice(rb, count - m, m)
+        vals.append(int(head[0]))
+        if not (np.all(head == head[0]) and np.all(tail == head[0])):
+            torn.append(t)
+        s.release()
+    comm.barrier()
+    out = {"vals": vals, "fresh": fresh, "torn": torn[:10], "bits": bits, "stats": s.stats()}
+    s.delete()
+    comm.finalize()
+    return out

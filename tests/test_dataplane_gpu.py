@@ -356,3 +356,26 @@ def test_activation_stress_wire_bf16(kind, world):
         assert o["nbad"] == 0, o["bad"]
         assert [e["round"] for e in o["log"]] == list(range(1, rounds + 1))
     assert sum(o["stats"]["auto_rounds"] for o in outs) > 0
+
+
+@pytest.mark.parametrize("case", ["p3-one-launch", "p3-five-launch", "p8-one-launch", "p3-host-kernel-copy",
+                                  "p3-host-dma"])
+@pytest.mark.parametrize("kind", [SOLO, MAJORITY])
+def test_fresh_only_stress(kind, case):
+    # ESGD_SCHED_FRESH_ONLY under stress, gradients written in the wrapper's racy order:
+    # every rank sees the same result for every round, and each rank's share of it is
+    # exactly its tag if it had posted the round before joining it, else 0
+    world, count, buf = STRESS[case]
+    rounds = 600
+    outs = run("gpu_stress_fresh", world, kind=kind, count=count, rounds=rounds, buf=buf, timeout=400)
+    bits = outs[0]["bits"]
+    for o in outs:
+        assert not o["torn"], o["torn"]
+        assert o["vals"] == outs[0]["vals"]
+    for t in range(1, rounds + 1):
+        v = outs[0]["vals"][t - 1]
+        for q in range(world):
+            share = (v >> (bits * q)) & ((1 << bits) - 1)
+            want = t % (1 << bits) if outs[q]["fresh"][t - 1] else 0
+            assert share == want, (t, q, share, want, [o["fresh"][t - 1] for o in outs])
+    assert sum(o["stats"]["auto_rounds"] for o in outs) > 0
