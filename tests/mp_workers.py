@@ -943,3 +943,34 @@ def gpu_stress_fresh(rank, world, kind, count, rounds=600, async_=3, seed=344956
     s.delete()
     comm.finalize()
     return out
+
+
+def cp_peer_lost(rank, world, stall_s=5.0):
+    """Failure detection (the reference has none: a lost peer hangs its ranks, SURVEY.md
+    §5): with ESGD_TIMEOUT_S=2 the last rank stops posting after two rounds; every other
+    rank's wait for the synchronous round 3 must fail with a timeout error instead of
+    hanging, and the job must still shut down once the stalled rank returns."""
+    import torch.distributed as dist
+
+    from esgd._lib import EsgdError
+    os.environ["ESGD_TIMEOUT_S"] = "2"
+    comm = _comm()
+    s = comm.Schedule(comm.ALLREDUCE, None, None, 0, buf=comm.BUF_NONE)
+    for _ in range(2):
+        s.post()
+        s.wait()
+    out = {"error": None, "elapsed_s": None}
+    if rank == world - 1:
+        time.sleep(stall_s)
+    else:
+        s.post()
+        t0 = time.perf_counter()
+        try:
+            s.wait()
+        except EsgdError as e:
+            out["error"] = str(e)
+        out["elapsed_s"] = time.perf_counter() - t0
+    dist.barrier()
+    s.delete()
+    comm.finalize()
+    return out

@@ -160,3 +160,10 @@ def test_hold_until_release():
         assert "release() the round" in o["double_wait"], o
     assert outs[0]["round2_s"] >= 0.25, outs[0]      # rank 1 joined only after its release
     assert [e["round"] for e in outs[1]["log"]] == [1, 2]
+
+
+def test_lost_peer_fails_the_round_instead_of_hanging():
+    outs = run("cp_peer_lost", 3, timeout=120)
+    for o in outs[:-1]:
+        assert o["error"] and ("timed out" in o["error"] or "joined" in o["error"]), o
+        assert 1.5 <= o["elapsed_s"] <= 15, o
