@@ -974,3 +974,59 @@ def cp_peer_lost(rank, world, stall_s=5.0):
     s.delete()
     comm.finalize()
     return out
+
+
+def gpu_stress_churn(rank, world, kind, count=65536, rounds=240, every=20,
+                     churn_counts=(16384, (8 << 20) // 4 + 5, 300007, (64 << 20) // 4), jitter_us=200):
+    """Schedules created and deleted while another schedule's rounds run under the random
+    activation stress (the arena recycles the deleted schedules' buckets; peers keep their
+    mappings): every `every` steps all ranks create a temporary allreduce schedule of the
+    next size in `churn_counts`, run two rounds of it (checked bitwise against the oracle
+    tree) and delete it, between steps of the persistent HOLD | FRESH_ONLY schedule, whose
+    rounds are checked as in gpu_stress_fresh."""
+    import random
+
+    import numpy as np
+
+    from esgd import _lib
+    from esgd import device as dev
+    from oracle import ffref
+    comm = _comm()
+    bits = min(10, 31 // world)
+    sb, rb = dev.DeviceBuffer(count, _lib.INT32), dev.DeviceBuffer(count, _lib.INT32)
+    rb.zero()
+    dev.synchronize()
+    s = comm.Schedule(kind, sb, rb, count, dtype=_lib.INT32, async_=3, seed=34495645, buf=comm.BUF_DEVICE,
+                      flags=comm.HOLD | comm.FRESH_ONLY)
+    rng = random.Random(4000 + rank)
+    vals, fresh, torn, churn_ok = [], [], [], []
+    comm.barrier()
+    for t in range(1, rounds + 1):
+        if t % every == 0:
+            n = churn_counts[(t // every) % len(churn_counts)]
+            tb = dev.DeviceBuffer(n)
+            for rr in range(2):
+                tb.upload(ffref.fill_uniform(SEED + t + rr, rank, n))
+                ts = comm.Schedule(comm.ALLREDUCE, None, tb, n, buf=comm.BUF_DEVICE) if rr == 0 else ts
+                ts.post()
+                ts.wait()
+                m = min(n, 4096)
+                got = _download_slice(tb, n - m, m)
+                want = ffref.tree_sum([ffref.fill_uniform(SEED + t + rr, q, m, start=n - m) for q in range(world)])
+                churn_ok.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
+            ts.delete()
+            tb.close()
+        time.sleep(rng.random() * jitter_us * 1e-6)
+        sb.upload(np.full(count, (t % (1 << bits)) << (bits * rank), np.int32))
+        s.post()
+        fresh.append(s.wait())
+        head, tail = _download_slice(rb, 0, 2048), _download_slice(rb, count - 2048, 2048)
+        vals.append(int(head[0]))
+        if not (np.all(head == head[0]) and np.all(tail == head[0])):
+            torn.append(t)
+        s.release()
+    comm.barrier()
+    out = {"vals": vals, "fresh": fresh, "torn": torn[:10], "bits": bits, "churn_ok": churn_ok}
+    s.delete()
+    comm.finalize()
+    return out

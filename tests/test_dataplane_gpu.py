@@ -379,3 +379,21 @@ def test_fresh_only_stress(kind, case):
             want = t % (1 << bits) if outs[q]["fresh"][t - 1] else 0
             assert share == want, (t, q, share, want, [o["fresh"][t - 1] for o in outs])
     assert sum(o["stats"]["auto_rounds"] for o in outs) > 0
+
+
+@pytest.mark.parametrize("kind", [SOLO, MAJORITY])
+def test_schedule_churn_under_stress(kind):
+    # temporary schedules (16 KiB .. 64 MiB) created, used and deleted every 20 steps
+    # while a persistent schedule runs under the activation stress
+    world, rounds = 3, 240
+    outs = run("gpu_stress_churn", world, kind=kind, rounds=rounds, timeout=400)
+    bits = outs[0]["bits"]
+    for o in outs:
+        assert not o["torn"], o["torn"]
+        assert o["vals"] == outs[0]["vals"]
+        assert o["churn_ok"] and all(o["churn_ok"]), o["churn_ok"]
+    for t in range(1, rounds + 1):
+        v = outs[0]["vals"][t - 1]
+        for q in range(world):
+            want = t % (1 << bits) if outs[q]["fresh"][t - 1] else 0
+            assert (v >> (bits * q)) & ((1 << bits) - 1) == want, (t, q)
