@@ -1030,3 +1030,62 @@ def gpu_stress_churn(rank, world, kind, count=65536, rounds=240, every=20,
     s.delete()
     comm.finalize()
     return out
+
+
+def gpu_stress_threads(rank, world, kind, counts=(65536, (1 << 20) + 3, 4096), rounds=200, jitter_us=200):
+    """The ABI's threading contract (post / wait may come from a thread other than the one
+    that initialised, ff.h's callers run ops from framework threads): three
+    schedules, each driven by its own thread through the FRESH_ONLY stress at once, so
+    posts, waits and releases of different schedules interleave inside the library.
+    Returns per schedule the decoded results and this rank's fresh flags."""
+    import random
+    import threading
+
+    import numpy as np
+
+    from esgd import _lib
+    from esgd import device as dev
+    comm = _comm()
+    bits = min(10, 31 // world)
+    scheds = []
+    for i, n in enumerate(counts):
+        sb, rb = dev.DeviceBuffer(n, _lib.INT32), dev.DeviceBuffer(n, _lib.INT32)
+        rb.zero()
+        s = comm.Schedule(kind, sb, rb, n, dtype=_lib.INT32, async_=3, seed=34495645 + i, buf=comm.BUF_DEVICE,
+                          flags=comm.HOLD | comm.FRESH_ONLY)
+        scheds.append((s, sb, rb, n))
+    dev.synchronize()
+    res = [None] * len(scheds)
+    errs = []
+
+    def drive(i):
+        try:
+            s, sb, rb, n = scheds[i]
+            rng = random.Random(5000 + 10 * rank + i)
+            vals, fresh, torn = [], [], []
+            m = min(n, 1024)
+            for t in range(1, rounds + 1):
+                time.sleep(rng.random() * jitter_us * 1e-6)
+                sb.upload(np.full(n, (t % (1 << bits)) << (bits * rank), np.int32))
+                s.post()
+                fresh.append(s.wait())
+                head, tail = _download_slice(rb, 0, m), _download_slice(rb, n - m, m)
+                vals.append(int(head[0]))
+                if not (np.all(head == head[0]) and np.all(tail == head[0])):
+                    torn.append(t)
+                s.release()
+            res[i] = {"vals": vals, "fresh": fresh, "torn": torn[:10]}
+        except Exception as e:   # reported, not swallowed
+            errs.append(repr(e))
+
+    comm.barrier()
+    th = [threading.Thread(target=drive, args=(i,)) for i in range(len(scheds))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    comm.barrier()
+    for s, *_ in scheds:
+        s.delete()
+    comm.finalize()
+    return {"res": res, "errs": errs, "bits": bits}

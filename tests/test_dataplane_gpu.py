@@ -397,3 +397,22 @@ def test_schedule_churn_under_stress(kind):
         for q in range(world):
             want = t % (1 << bits) if outs[q]["fresh"][t - 1] else 0
             assert (v >> (bits * q)) & ((1 << bits) - 1) == want, (t, q)
+
+
+@pytest.mark.parametrize("kind", [SOLO, MAJORITY])
+def test_stress_one_thread_per_schedule(kind):
+    # three schedules driven concurrently from three threads per rank
+    world, rounds = 3, 200
+    outs = run("gpu_stress_threads", world, kind=kind, rounds=rounds, timeout=400)
+    bits = outs[0]["bits"]
+    for o in outs:
+        assert not o["errs"], o["errs"]
+    for i in range(len(outs[0]["res"])):
+        for o in outs:
+            assert not o["res"][i]["torn"], (i, o["res"][i]["torn"])
+            assert o["res"][i]["vals"] == outs[0]["res"][i]["vals"], i
+        for t in range(1, rounds + 1):
+            v = outs[0]["res"][i]["vals"][t - 1]
+            for q in range(world):
+                want = t % (1 << bits) if outs[q]["res"][i]["fresh"][t - 1] else 0
+                assert (v >> (bits * q)) & ((1 << bits) - 1) == want, (i, t, q)
