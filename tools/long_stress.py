@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Long runs of the randomized activation stress (tests/mp_workers.gpu_stress_fresh):
+HOLD | FRESH_ONLY schedules, gradients written in the wrapper's racy order, random delays,
+no barriers; every round checked (shares = tag iff the rank had posted the round, else 0;
+no torn buckets; every rank sees the same result).  One JSON line per configuration.
+  python tools/long_stress.py [--rounds 5000]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "eager-sgd_amd"), os.path.join(ROOT, "tests")]
+
+from mp_workers import run  # noqa: E402
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5000)
+    a = ap.parse_args()
+    for world, count, buf in ((3, 65536, "device"), (3, (1 << 20) + 3, "device"), (8, 65536, "device"),
+                              (3, 65536, "host")):
+        for kind, kname in ((1, "solo"), (2, "majority")):
+            t0 = time.time()
+            outs = run("gpu_stress_fresh", world, kind=kind, count=count, rounds=a.rounds, buf=buf, timeout=900)
+            bits = outs[0]["bits"]
+            bad = sum(len(o["torn"]) for o in outs) + sum(o["vals"] != outs[0]["vals"] for o in outs)
+            for t in range(1, a.rounds + 1):
+                v = outs[0]["vals"][t - 1]
+                for q in range(world):
+                    want = t % (1 << bits) if outs[q]["fresh"][t - 1] else 0
+                    bad += ((v >> (bits * q)) & ((1 << bits) - 1)) != want
+            print(json.dumps({"world": world, "count": count, "buf": buf, "kind": kname, "rounds": a.rounds,
+                              "bad": int(bad), "auto_rounds": sum(o["stats"]["auto_rounds"] for o in outs),
+                              "fresh_rounds": sum(o["stats"]["fresh_rounds"] for o in outs),
+                              "wall_s": round(time.time() - t0, 1)}), flush=True)
+
+
+if __name__ == "__main__":   # spawned workers re-import this module
+    main()
