@@ -18,7 +18,10 @@ from mp_workers import run  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5000)
+    ap.add_argument("--device-flags", default=None, help="ESGD_DEVICE_FLAGS for every rank (1 or 2)")
     a = ap.parse_args()
+    if a.device_flags:
+        os.environ["ESGD_DEVICE_FLAGS"] = a.device_flags   # inherited by the spawned ranks
     for world, count, buf in ((3, 65536, "device"), (3, (1 << 20) + 3, "device"), (8, 65536, "device"),
                               (3, 65536, "host")):
         for kind, kname in ((1, "solo"), (2, "majority")):
@@ -32,6 +35,7 @@ def main():
                     want = t % (1 << bits) if outs[q]["fresh"][t - 1] else 0
                     bad += ((v >> (bits * q)) & ((1 << bits) - 1)) != want
             print(json.dumps({"world": world, "count": count, "buf": buf, "kind": kname, "rounds": a.rounds,
+                              "device_flags": a.device_flags or "0 (host flags)",
                               "bad": int(bad), "auto_rounds": sum(o["stats"]["auto_rounds"] for o in outs),
                               "fresh_rounds": sum(o["stats"]["fresh_rounds"] for o in outs),
                               "wall_s": round(time.time() - t0, 1)}), flush=True)
