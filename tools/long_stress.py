@@ -19,11 +19,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5000)
     ap.add_argument("--device-flags", default=None, help="ESGD_DEVICE_FLAGS for every rank (1 or 2)")
+    ap.add_argument("--configs", default=None, help="world:count:buf,... (default: the four of the suite)")
     a = ap.parse_args()
     if a.device_flags:
         os.environ["ESGD_DEVICE_FLAGS"] = a.device_flags   # inherited by the spawned ranks
-    for world, count, buf in ((3, 65536, "device"), (3, (1 << 20) + 3, "device"), (8, 65536, "device"),
-                              (3, 65536, "host")):
+    configs = ((3, 65536, "device"), (3, (1 << 20) + 3, "device"), (8, 65536, "device"), (3, 65536, "host"))
+    if a.configs:   # world:count:buf,...
+        configs = tuple((int(w), int(c), b) for w, c, b in (x.split(":") for x in a.configs.split(",")))
+    for world, count, buf in configs:
         for kind, kname in ((1, "solo"), (2, "majority")):
             t0 = time.time()
             outs = run("gpu_stress_fresh", world, kind=kind, count=count, rounds=a.rounds, buf=buf, timeout=900)
