@@ -467,6 +467,27 @@ def c3_over_rccl(comm, dev, rank, world, count, steps=20):
         want = ffref.tree_sum([ffref.fill_uniform(SEED + 1, r, m) for r in range(world)])
         ok = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
         sch.delete()
+        # the same round with bf16 on the wire (half the RCCL bytes; the oracle's bf16
+        # convention, as for the IPC wire leg)
+        sw = comm.Schedule(comm.SOLO, None, rb, count, async_=32, seed=6545343, buf=comm.BUF_DEVICE,
+                           flags=comm.WIRE_BF16)
+
+        def wstep():
+            sw.post()
+            sw.wait()
+
+        for _ in range(3):
+            wstep()
+        tw = _timed_steps(comm, wstep, steps)
+        dev.fill_uniform(rb, SEED + 1, rank)
+        dev.synchronize()
+        comm.barrier()
+        wstep()
+        got = rb.download()[:m]
+        want = ffref.bf16_to_f32(ffref.tree_sum_bf16(
+            [ffref.f32_to_bf16(ffref.fill_uniform(SEED + 1, r, m)) for r in range(world)]))
+        okw = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+        sw.delete()
         rb.close()
     finally:
         comm.set_transport("ipc")
@@ -474,7 +495,10 @@ def c3_over_rccl(comm, dev, rank, world, count, steps=20):
     t_min = 2 * S / (world * XGMI_LINK_GBS * 1e9)
     return {"bucket_bytes": S, "round_ms_median": round(t * 1e3, 4),
             "value_GBs": round(world * S / t / 1e9, 2), "algbw_GBs": round(S / t / 1e9, 2),
-            "xgmi_frac": round(t_min / t, 4), "parity_rank_slice": "bitwise" if ok else "MISMATCH"}
+            "xgmi_frac": round(t_min / t, 4), "parity_rank_slice": "bitwise" if ok else "MISMATCH",
+            "wire_bf16": {"round_ms_median": round(tw * 1e3, 4), "value_GBs": round(world * S / tw / 1e9, 2),
+                          "xgmi_frac": round(t_min / 2 / tw, 4),
+                          "parity_rank_slice": "bitwise" if okw else "MISMATCH"}}
 
 
 def c3_wire_bf16(comm, dev, rank, world, count, steps=20):

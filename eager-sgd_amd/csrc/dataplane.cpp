@@ -1246,6 +1246,10 @@ hipStream_t sched_stream(Sched &s) {
 // by issue order: the engine launches rounds in the node's issue-ring order, on the
 // process's round stream, which is also the communicator stream.
 // RCCL refuses two ranks on one GPU, so this transport only runs with one GPU per rank.
+// ESGD_SCHED_WIRE_BF16 rounds move bf16 copies: rb is narrowed into a wire bucket, the
+// reduce-scatter groups carry bf16 shards, the fold is the wire tree kernel (same kernel
+// and operand order as IpcTransport::wire_phases, so both transports give the same bits)
+// and the all-gather carries the reduced bf16 shards, widened into rb.
 }  // namespace esgd
 
 #include <rccl/rccl.h>
@@ -1290,6 +1294,8 @@ void rccl_shutdown() {
 struct RcclState : BaseState {
     hipStream_t red = nullptr;       // tree folds of arrived chunks
     char *stage = nullptr;           // P x L elements: every peer's copy of this rank's shard
+    char *wire = nullptr;            // wire rounds: bf16 copy of rb (count elements)
+    uint64_t wire_n = 0;
     uint64_t L = 0;                  // shard pitch (elements)
     uint64_t chunk = 0;              // pipeline chunk (elements)
     hipEvent_t ev_red = nullptr;
@@ -1301,12 +1307,23 @@ struct RcclTransport final : Transport {
 
     static RcclState &S(Sched &s) { return *static_cast<RcclState *>(s.tstate); }
 
+    // bytes per element on the wire (and in the staging area)
+    static size_t stage_esize(const Sched &s) { return s.wire_bf16 ? 2 : s.esize; }
+
     static int fit_stage(Sched &s, RcclState &st) {
-        if (st.stage && st.L == st.len[0]) return ESGD_SUCCESS;
+        if (s.wire_bf16 && s.world > 1 && st.wire_n != s.count) {
+            if (st.wire) { ESGD_HIP(hipFree(st.wire)); st.wire = nullptr; }
+            st.wire_n = s.count;
+            if (s.count) ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.wire), size_t(s.count) * 2));
+        }
+        // pitch rounded to 8 elements: every staged shard starts 16-B aligned (the wire
+        // kernels' vectors) even when one ragged shard holds the whole bucket
+        const uint64_t pitch = (st.len[0] + 7) / 8 * 8;
+        if (st.stage && st.L == pitch) return ESGD_SUCCESS;
         if (st.stage) { ESGD_HIP(hipFree(st.stage)); st.stage = nullptr; }
-        st.L = st.len[0];
+        st.L = pitch;
         if (s.world > 1 && st.L)
-            ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.stage), size_t(s.world) * st.L * s.esize));
+            ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.stage), size_t(s.world) * st.L * stage_esize(s)));
         // ~8 chunks per shard, at least 1 MiB each, 1 KiB aligned
         const uint64_t align = 1024 / s.esize, minc = (1u << 20) / s.esize;
         const uint64_t c = std::max<uint64_t>(minc, (st.L + 7) / 8);
@@ -1318,6 +1335,10 @@ struct RcclTransport final : Transport {
         auto *st = new RcclState();
         s.tstate = st;
         if (int rc = base_setup(s, *st)) return rc;
+        if (s.wire_bf16 && s.resolve && s.world > 1) {
+            set_error("schedule: ESGD_SCHED_WIRE_BF16 does not take FFCOLL_BUFFERS buffers");
+            return ESGD_INVALID_ARG;
+        }
         ESGD_HIP(hipStreamCreateWithFlags(&st->red, hipStreamNonBlocking));
         ESGD_HIP(hipEventCreateWithFlags(&st->ev_red, hipEventDisableTiming));
         return fit_stage(s, *st);
@@ -1353,7 +1374,9 @@ struct RcclTransport final : Transport {
         const int P = s.world, r = s.rank;
         const size_t es = s.esize;
         if (int rc = base_copy_in(s, st, round, fresh, cs)) return rc;
-        if (P > 1 && st.L) {
+        if (P > 1 && st.L && s.wire_bf16) {
+            if (int rc = wire_round(s, st)) return rc;
+        } else if (P > 1 && st.L) {
             const uint64_t nch = (st.L + st.chunk - 1) / st.chunk;
             while (st.ev_chunk.size() < nch) {
                 hipEvent_t e;
@@ -1397,6 +1420,75 @@ struct RcclTransport final : Transport {
         return base_copy_out(s, st, cs);
     }
 
+    // A wire round after the copy-in (rb = this rank's contribution): rb -> bf16 wire
+    // copy; per chunk, bf16 shard j to rank j and every peer's bf16 copy of shard `rank`
+    // into the staging area, folded by the wire tree kernel in rank order (own operand
+    // from the wire copy, so every rank sums the same rounded inputs) into the own wire
+    // shard (bf16, in place) and rb's shard (its widened value); then the reduced bf16
+    // shards are all-gathered into the wire copy and widened into rb.
+    static int wire_round(Sched &s, RcclState &st) {
+        hipStream_t cs = st.stream;
+        const int P = s.world, r = s.rank;
+        uint16_t *w = reinterpret_cast<uint16_t *>(st.wire);
+        float *rbf = reinterpret_cast<float *>(st.rb_dev);
+        uint16_t *stg = reinterpret_cast<uint16_t *>(st.stage);
+        if (int rc = narrow_bf16(rbf, w, s.count, false, cs)) return rc;
+        const uint64_t nch = (st.L + st.chunk - 1) / st.chunk;
+        while (st.ev_chunk.size() < nch) {
+            hipEvent_t e;
+            ESGD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            st.ev_chunk.push_back(e);
+        }
+        for (uint64_t c = 0; c < nch; ++c) {
+            const uint64_t o = c * st.chunk;
+            ESGD_NCCL(ncclGroupStart());
+            for (int j = 0; j < P; ++j) {
+                if (j == r) continue;
+                const uint64_t ns = piece(st.len[j], c, st.chunk);
+                if (ns) ESGD_NCCL(ncclSend(w + st.off[j] + o, ns * 2, ncclChar, j, g_nccl, cs));
+                const uint64_t nr = piece(st.len[r], c, st.chunk);
+                if (nr) ESGD_NCCL(ncclRecv(stg + uint64_t(j) * st.L + o, nr * 2, ncclChar, j, g_nccl, cs));
+            }
+            ESGD_NCCL(ncclGroupEnd());
+            ESGD_HIP(hipEventRecord(st.ev_chunk[c], cs));
+            const uint64_t n = piece(st.len[r], c, st.chunk);
+            if (!n) continue;
+            ESGD_HIP(hipStreamWaitEvent(st.red, st.ev_chunk[c], 0));
+            const void *in[kMaxRanks];
+            for (int j = 0; j < P; ++j)
+                in[j] = j == r ? static_cast<const void *>(w + st.off[r] + o)
+                               : static_cast<const void *>(stg + uint64_t(j) * st.L + o);
+            if (int rc = reduce_wire(P, in, w + st.off[r] + o, rbf + st.off[r] + o, n, st.red)) return rc;
+        }
+        ESGD_HIP(hipEventRecord(st.ev_red, st.red));
+        ESGD_HIP(hipStreamWaitEvent(cs, st.ev_red, 0));
+        ESGD_NCCL(ncclGroupStart());
+        for (int j = 0; j < P; ++j) {
+            if (j == r) continue;
+            if (st.len[r]) ESGD_NCCL(ncclSend(w + st.off[r], st.len[r] * 2, ncclChar, j, g_nccl, cs));
+            if (st.len[j]) ESGD_NCCL(ncclRecv(w + st.off[j], st.len[j] * 2, ncclChar, j, g_nccl, cs));
+        }
+        ESGD_NCCL(ncclGroupEnd());
+        const uint64_t pc = piece_bytes() / 4;
+        const void *src[kMaxSegs];
+        void *dst[kMaxSegs];
+        uint64_t cnt[kMaxSegs];
+        int m = 0;
+        for (int j = 0; j < P; ++j) {
+            if (j == r) continue;
+            for (uint64_t o = 0; o < st.len[j]; o += pc) {
+                src[m] = w + st.off[j] + o;
+                dst[m] = rbf + st.off[j] + o;
+                cnt[m] = std::min(pc, st.len[j] - o);
+                if (++m == kMaxSegs) {
+                    if (int rc = gather_widen(m, src, dst, cnt, cs)) return rc;
+                    m = 0;
+                }
+            }
+        }
+        return m ? gather_widen(m, src, dst, cnt, cs) : ESGD_SUCCESS;
+    }
+
     int query(Sched &s) override { return base_query(s, S(s)); }
     int complete(Sched &s) override { return base_complete(s, S(s)); }
 
@@ -1406,6 +1498,7 @@ struct RcclTransport final : Transport {
         if (st->stream) (void)hipStreamSynchronize(st->stream);
         if (st->red) { (void)hipStreamSynchronize(st->red); (void)hipStreamDestroy(st->red); }
         if (st->stage) (void)hipFree(st->stage);
+        if (st->wire) (void)hipFree(st->wire);
         for (hipEvent_t e : st->ev_chunk) (void)hipEventDestroy(e);
         if (st->ev_red) (void)hipEventDestroy(st->ev_red);
         base_teardown(s, *st);

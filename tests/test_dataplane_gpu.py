@@ -249,6 +249,11 @@ def test_rccl_transport_multi_gpu(world):
         verdicts = run("gpu_allreduce", world, count=1000003, rounds=2, kind=kind, transport="rccl")
         assert all(all(v) for v in verdicts), (kind, verdicts)
     _all_ok(run("gpu_config", world, kind=SOLO, counts=[64 << 20], rounds=2, transport="rccl", timeout=420))
+    # bf16 on the wire: the same bits as the IPC wire rounds (oracle's bf16 tree of the
+    # rounded inputs, widened); a 5-element bucket is one ragged shard (16-B stage pitch)
+    for kw in (dict(count=1000003), dict(count=5), dict(count=1000003, buf="host", kind=MAJORITY)):
+        verdicts = run("gpu_allreduce", world, rounds=2, wire=True, transport="rccl", **kw)
+        assert all(all(v) for v in verdicts), (kw, verdicts)
 
 
 @pytest.mark.timeout(600)
