@@ -73,7 +73,7 @@ def cpu_baseline(k: int, count: int):
     from oracle import ffref
     threads = k
     t1 = ffref.time_allreduce(k, count, threads, 1)          # warm + size the sample
-    reps = max(1, min(20, int(10.0 / max(t1, 1e-3))))
+    reps = max(1, min(250, int(10.0 / max(t1, 1e-3))))   # ~10 s of CPU work
     t = ffref.time_allreduce(k, count, threads, reps)
     gbs = k * count * 4 / t / 1e9
     return {"value": round(gbs, 3), "unit": "GB/s", "cores": threads, "kind": "port",

@@ -195,7 +195,7 @@ int esgd_schedule_create(int kind, int buf, const void *sb, void *rb, uint64_t c
  *   ESGD_SCHED_ZERO_SB the snapshot (move sb -> rb) zeroes sb as it reads it (device
  *                      buckets, not in place): the wrapper's zero-after-use (:311-314)
  *                      fused into the move, one HBM pass fewer;
- *   ESGD_SCHED_WIRE_BF16 FLOAT buckets, ipc transport: peers exchange a bf16 copy of the
+ *   ESGD_SCHED_WIRE_BF16 FLOAT buckets, ipc or rccl transport: peers exchange a bf16 copy of the
  *                      bucket (half the xGMI bytes).  Every rank's
  *                      bucket is rounded to bf16 (RNE), each shard is folded in fp32 in the
  *                      tree order and rounded once, and every rank receives that bf16 result
