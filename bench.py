@@ -269,7 +269,7 @@ def host_e2e(dev, k, count, s, iters=5):
             "serial_ms": round(t_serial * 1e3, 3), "serial_GBs_bucket_bytes": round(k * nbytes / t_serial / 1e9, 2)}
 
 
-def gate_256(dev, dt, es, k, s, iters=20):
+def gate_256(dev, dt, es, k, s, iters=20, avg_iters=100):
     """BASELINE.json's 1-GPU gate shape (k x 256 MiB buckets, no Infinity-Cache reuse
     possible): per-launch time from HIP event pairs on the launch stream."""
     count = (256 * MiB) // es
@@ -278,7 +278,7 @@ def gate_256(dev, dt, es, k, s, iters=20):
         dev.fill_uniform(b, SEED, r, stream=s)
     out = dev.DeviceBuffer(count, dt)
     ptrs = [b.ptr for b in bufs]
-    for _ in range(3):
+    for _ in range(10):
         dev.reduce(dt, ptrs, out, count, stream=s)
     # per-launch event pairs (each adds its marker packets to the launch it brackets) ...
     ev = [dev.Event() for _ in range(2 * iters)]
@@ -289,14 +289,16 @@ def gate_256(dev, dt, es, k, s, iters=20):
     s.synchronize()
     ts = sorted(ev[2 * i].elapsed_ms(ev[2 * i + 1]) for i in range(iters))
     med = ts[iters // 2]
-    # ... and, like the headline roofline, one pair around `iters` back-to-back launches
+    # ... and, like the headline roofline, one pair around `avg_iters` back-to-back calls
+    # (38 ms of work: 20 calls were too short to average out run-to-run noise, 373 vs
+    # 380 us on one box)
     e0, e1 = dev.Event(), dev.Event()
     e0.record(s)
-    for _ in range(iters):
+    for _ in range(avg_iters):
         dev.reduce(dt, ptrs, out, count, stream=s)
     e1.record(s)
     s.synchronize()
-    avg = e0.elapsed_ms(e1) / iters
+    avg = e0.elapsed_ms(e1) / avg_iters
     algo = (k + 1) * count * es
     for b in bufs:
         b.close()
