@@ -45,8 +45,6 @@ int create_schedule(int kind, int buf, const void *sb, void *rb, uint64_t count,
     ESGD_ARG(buf == ESGD_BUF_NONE || rb || count == 0, "esgd_schedule_create: null receive buffer");
     const bool rccl = !std::strcmp(transport_name(), "rccl");
     ESGD_ARG(rccl || !std::strcmp(transport_name(), "ipc"), "unknown transport '%s'", transport_name());
-    ESGD_ARG(!(flags & ESGD_SCHED_WIRE_BF16) || !rccl || buf == ESGD_BUF_NONE,
-             "esgd_schedule_create: ESGD_SCHED_WIRE_BF16 runs on the ipc transport only");
     Transport *tp = default_transport(buf == ESGD_BUF_NONE);
     Sched *s = nullptr;
     int rc = sched_create(kind, dtype, count, const_cast<void *>(sb), rb, buf == ESGD_BUF_HOST,

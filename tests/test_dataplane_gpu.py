@@ -149,6 +149,9 @@ def test_rccl_transport_single_rank(kind):
         verdicts = run("gpu_allreduce", 1, count=300007, rounds=3, kind=kind, buf=buf,
                        transport="rccl")
         assert all(all(v) for v in verdicts), (buf, verdicts)
+    # the wire flag is accepted on this transport; a world of one returns the bucket
+    verdicts = run("gpu_allreduce", 1, count=300007, rounds=2, kind=kind, wire=True, transport="rccl")
+    assert all(all(v) for v in verdicts), verdicts
 
 
 @pytest.mark.parametrize("in_place", [False, True])
