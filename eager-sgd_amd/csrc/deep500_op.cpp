@@ -79,13 +79,15 @@ struct AllreduceOp {
     float *sb = nullptr, *rb = nullptr;   // persistent buckets (host pinned or HBM)
     int64_t bytes = 0;
 
-    void ensure(bool dev) {
+    // Lazy creation of the buckets and the schedule (:288-298); an esgd status (the void
+    // entry points abort on failure, the status-returning ones pass it on).
+    int ensure(bool dev) {
         if (sched) {
             if (dev != device) {
                 esgd::set_error("op used with both host and device buffers");
-                die("allreducef_forward");
+                return ESGD_INVALID_ARG;
             }
-            return;
+            return ESGD_SUCCESS;
         }
         device = dev;
         const size_t nbytes = size_t(len) * sizeof(float);
@@ -95,13 +97,13 @@ struct AllreduceOp {
                 esgd::arena_alloc(nbytes ? nbytes : 256, reinterpret_cast<void **>(&rb)) ||
                 hipMemset(sb, 0, nbytes) != hipSuccess || hipMemset(rb, 0, nbytes) != hipSuccess) {
                 esgd::set_error("device bucket allocation of %zu bytes", nbytes);
-                die("allreducef_forward_cuda");
+                return ESGD_ENOMEM;
             }
         } else {
             if (hipHostMalloc(reinterpret_cast<void **>(&sb), nbytes ? nbytes : 256, hipHostMallocDefault) != hipSuccess ||
                 hipHostMalloc(reinterpret_cast<void **>(&rb), nbytes ? nbytes : 256, hipHostMallocDefault) != hipSuccess) {
                 esgd::set_error("pinned bucket allocation of %zu bytes", nbytes);
-                die("allreducef_forward");
+                return ESGD_ENOMEM;
             }
             std::memset(sb, 0, nbytes);   // calloc in the reference (:290-291)
             std::memset(rb, 0, nbytes);
@@ -110,9 +112,8 @@ struct AllreduceOp {
                          : cfg.mode == ESGD_OP_ALLREDUCE ? ESGD_SCHED_ALLREDUCE : ESGD_SCHED_SOLO;
         const unsigned flags = ESGD_SCHED_HOLD | ESGD_SCHED_FRESH_ONLY |
                                (dev && cfg.wire == ESGD_BF16 ? ESGD_SCHED_WIRE_BF16 : 0u);
-        if (esgd_schedule_create_ex(kind, dev ? ESGD_BUF_DEVICE : ESGD_BUF_HOST, sb, rb, len,
-                                    ESGD_FLOAT, cfg.async, cfg.seed, flags, &sched))
-            die("schedule creation");
+        return esgd_schedule_create_ex(kind, dev ? ESGD_BUF_DEVICE : ESGD_BUF_HOST, sb, rb, len,
+                                       ESGD_FLOAT, cfg.async, cfg.seed, flags, &sched);
     }
 
     // Device round: the gradient is already in sb (queued on s).  post -> wait -> drop a
@@ -139,7 +140,7 @@ constexpr float kNoDivide = 1.0f;
 
 int forward_cuda_impl(AllreduceOp *op, const float *input, float *output, float divisor, hipStream_t s) {
     ESGD_ARG(op, "allreducef: null handle");
-    op->ensure(true);
+    if (int rc = op->ensure(true)) return rc;
     const size_t nbytes = size_t(op->len) * sizeof(float);
     const uint64_t n = op->len;
     if (divisor == kNoDivide) {
@@ -157,6 +158,22 @@ int forward_cuda_impl(AllreduceOp *op, const float *input, float *output, float 
         }
         return ESGD_SUCCESS;
     });
+}
+
+// Host round, the wrapper's steps (:301-316): copy in -> post -> wait -> copy out ->
+// zero the send bucket -> release.
+int forward_host_impl(AllreduceOp *op, const float *input, float *output) {
+    ESGD_ARG(op && (op->len == 0 || (input && output)), "allreducef_forward: null handle or buffer");
+    if (int rc = op->ensure(false)) return rc;
+    const size_t nbytes = size_t(op->len) * sizeof(float);
+    std::memcpy(op->sb, input, nbytes);
+    if (int rc = esgd_schedule_post(op->sched, nullptr, nullptr)) return rc;
+    if (int rc = esgd_schedule_wait(op->sched)) return rc;
+    std::memcpy(output, op->rb, nbytes);
+    std::memset(op->sb, 0, nbytes);
+    if (int rc = esgd_schedule_release(op->sched, nullptr)) return rc;
+    op->bytes += int64_t(nbytes);
+    return ESGD_SUCCESS;
 }
 
 }  // namespace
@@ -196,16 +213,11 @@ void *create_new_op(esgd_d5_tensor_t *in, int num_inputs, esgd_d5_tensor_t *, in
 }
 
 void allreducef_forward(void *handle, const float *input, const float *, float *output) {
-    auto *op = static_cast<AllreduceOp *>(handle);
-    op->ensure(false);
-    const size_t nbytes = size_t(op->len) * sizeof(float);
-    std::memcpy(op->sb, input, nbytes);
-    if (esgd_schedule_post(op->sched, nullptr, nullptr) || esgd_schedule_wait(op->sched))
-        die("allreducef_forward");
-    std::memcpy(output, op->rb, nbytes);
-    std::memset(op->sb, 0, nbytes);
-    if (esgd_schedule_release(op->sched, nullptr)) die("allreducef_forward");
-    op->bytes += int64_t(nbytes);
+    if (forward_host_impl(static_cast<AllreduceOp *>(handle), input, output)) die("allreducef_forward");
+}
+
+int allreducef_forward_host(void *handle, const float *input, float *output) {
+    return forward_host_impl(static_cast<AllreduceOp *>(handle), input, output);
 }
 
 void allreducef_forward_cuda(void *handle, const float *input, const float *, float *output,
@@ -230,7 +242,7 @@ int allreducef_forward_cuda_packed(void *handle, int n, const float *const *grad
     for (int i = 0; i < n; ++i) total += counts[i];
     ESGD_ARG(total == op->len, "allreducef_forward_cuda_packed: %llu elements for a %llu-element op",
              (unsigned long long)total, (unsigned long long)op->len);
-    op->ensure(true);
+    if (int rc = op->ensure(true)) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (int rc = esgd_pack_div(n, grads, counts, op->sb, divisor, s)) return rc;
     return op->device_round(s, [&]() -> int { return esgd_unpack(n, outs, counts, op->rb, s); });

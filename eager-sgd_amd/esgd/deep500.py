@@ -40,6 +40,8 @@ def _bind(h):
     h.create_new_op.restype = vp
     h.create_new_op.argtypes = [C.POINTER(tensor_t), C.c_int, C.POINTER(tensor_t), C.c_int]
     h.allreducef_forward.restype, h.allreducef_forward.argtypes = None, [vp, vp, vp, vp]
+    h.allreducef_forward_host.restype = C.c_int
+    h.allreducef_forward_host.argtypes = [vp, vp, vp]
     h.allreducef_forward_cuda.restype = None
     h.allreducef_forward_cuda.argtypes = [vp, vp, vp, vp, vp]
     h.allreducef_forward_cuda_div.restype = C.c_int
@@ -82,11 +84,13 @@ class AllreduceOp:
         self.numel = int(np.prod(shape)) if len(shape) else 1
 
     def forward(self, grad: np.ndarray, last: np.ndarray | None = None) -> np.ndarray:
-        """Host path (the reference's CPU-registered kernel)."""
+        """Host path (the reference's CPU-registered kernel); allreducef_forward's status
+        variant, so a failed round raises EsgdError instead of aborting the process."""
         g = np.ascontiguousarray(grad, dtype=np.float32)
         assert g.size == self.numel
         out = np.empty_like(g)
-        lib().allreducef_forward(self.handle, g.ctypes.data, None, out.ctypes.data)
+        _lib.check(lib().allreducef_forward_host(self.handle, g.ctypes.data, out.ctypes.data),
+                   "allreducef_forward_host")
         return out
 
     def forward_cuda(self, grad, out, stream: int | None = None):

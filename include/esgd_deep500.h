@@ -59,6 +59,9 @@ void allreducef_forward_cuda(void *handle, const float *input, const float *last
  *     packed in order into the op's bucket (divided as above), one round, unpacked into
  *     outs[i] (may alias grads[i]): the bucket fusion of one round per step instead of
  *     one per tensor. */
+/* Extension: allreducef_forward (host buffers) returning an esgd status instead of
+ * aborting -- a peer timeout or an allocation failure reaches the framework as an error. */
+int allreducef_forward_host(void *handle, const float *input, float *output);
 int allreducef_forward_cuda_div(void *handle, const float *input, float *output, float divisor,
                                 void *stream);
 int allreducef_forward_cuda_packed(void *handle, int n, const float *const *grads,

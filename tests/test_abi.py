@@ -85,3 +85,15 @@ def test_wire_flag_argument_checks():
     rc = esgd.lib().esgd_schedule_create_ex(0, comm.BUF_DEVICE, None, C.c_void_p(16), 64, _lib.FLOAT, 0, 0,
                                             0x80, C.byref(h))
     assert rc == _lib.INVALID_ARG and "unknown flags" in _lib.last_error()
+
+
+def test_op_status_entry_points_return_errors():
+    # the deep500 op's status variants report a bad call as an esgd status (no abort,
+    # no GPU needed): the host forward, the fused-divide and the packed device forwards
+    from esgd import _lib, deep500  # noqa: F401  (registers the op signatures)
+    lib = _lib.lib()
+    assert lib.allreducef_forward_host(None, None, None) == _lib.INVALID_ARG
+    assert "allreducef_forward" in _lib.last_error()
+    assert lib.allreducef_forward_cuda_div(None, None, None, 0.0, None) == _lib.INVALID_ARG
+    assert lib.allreducef_forward_cuda_div(None, None, None, 2.0, None) == _lib.INVALID_ARG
+    assert lib.allreducef_forward_cuda_packed(None, 0, None, None, None, 1.0, None) == _lib.INVALID_ARG
