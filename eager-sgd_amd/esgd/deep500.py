@@ -94,9 +94,12 @@ class AllreduceOp:
         return out
 
     def forward_cuda(self, grad, out, stream: int | None = None):
-        """Device path: grad / out are device pointers or torch tensors."""
+        """Device path: grad / out are device pointers or torch tensors.  Runs
+        allreducef_forward_cuda's round through its status variant (a divisor of 1 is the
+        plain copy-in), so a failed round raises EsgdError instead of aborting."""
         from .device import as_ptr
-        lib().allreducef_forward_cuda(self.handle, as_ptr(grad), None, as_ptr(out), stream)
+        _lib.check(lib().allreducef_forward_cuda_div(self.handle, as_ptr(grad), as_ptr(out), 1.0, stream),
+                   "allreducef_forward_cuda")
         return out
 
     def forward_cuda_div(self, grad, out, divisor: float, stream: int | None = None):
