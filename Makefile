@@ -2,6 +2,8 @@
 #   make            -> both
 #   make lib        -> eager-sgd_amd/esgd/libesgd.so
 #   make oracle     -> oracle/libffref.so
+#   make sweeps     -> tools/bin/libesgd_sweeps.so (measurement-only kernel variants,
+#                      tools/sweep_reduce.py; never linked into the product)
 # No -ffast-math anywhere: parity with fflib2 is bitwise (SURVEY.md §7 "Hard parts").
 
 ROCM      ?= /opt/rocm
@@ -26,7 +28,7 @@ OBJS      := $(patsubst $(CSRC)/%.hip,$(BUILD)/%.hip.o,$(HIP_SRCS)) \
              $(patsubst $(CSRC)/%.cpp,$(BUILD)/%.cpp.o,$(CPP_SRCS))
 HDRS      := $(wildcard include/*.h) $(wildcard $(CSRC)/*.h)
 
-.PHONY: all lib oracle clean tsan
+.PHONY: all lib oracle sweeps clean tsan
 all: lib oracle
 
 lib: $(OUTLIB)
@@ -42,6 +44,15 @@ $(BUILD)/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
 $(OUTLIB): $(OBJS) $(CSRC)/exports.map
 	$(HIPCC) --offload-arch=$(ARCH) $(OBJS) $(LDFLAGS) -o $@
 
+# ---- sweep variants of the tree kernel (tools only) ----
+SWEEPS    := tools/bin/libesgd_sweeps.so
+
+sweeps: $(SWEEPS)
+
+$(SWEEPS): tools/sweeps/reduce_sweeps.hip $(CSRC)/reduce_core.h $(HDRS)
+	@mkdir -p tools/bin
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $< -L$(ROCM)/lib -lamdhip64
+
 # ---- CPU oracle (test infrastructure only) ----
 oracle: oracle/libffref.so
 
@@ -50,7 +61,7 @@ oracle/libffref.so: oracle/ffref.c oracle/ffref.h
 	    -Wall -o $@ oracle/ffref.c -lpthread
 
 clean:
-	rm -rf $(BUILD) $(OUTLIB) oracle/libffref.so
+	rm -rf $(BUILD) $(OUTLIB) oracle/libffref.so $(SWEEPS)
 
 # ---- ThreadSanitizer build of the host side (CPU control-plane tests only) ----
 # make tsan -> build/tsan/libesgd.so; run e.g.

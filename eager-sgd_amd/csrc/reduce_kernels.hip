@@ -1,23 +1,12 @@
-// reduce_kernels.hip — the gradient-bucket reduction, hand-written for gfx950.
+// reduce_kernels.hip — the gradient-bucket reduction entry points and the data plane's
+// kernels, hand-written for gfx950.
 //
-// Reference behaviour (fflib2, /root/reference/eager-SGD-modules/fflib2):
-//   * FFSUM on a pair of buffers, c = a + b, is a scalar C loop strip-mined in 1024s
-//     on the progress pthread (src/components/gcomp/ffop_gcomp_operator.c:8-25, 33-58).
-//   * ffallreduce applies it log2(P) times in recursive-doubling order
-//     (src/colls/ffallreduce.c:138-171), so every rank ends with the hypercube tree
-//     ((x0+x1)+(x2+x3))+((x4+x5)+(x6+x7)).
-// Here the whole tree is one pass: each lane loads 16 B from each of the k inputs,
-// folds them in exactly that tree order in registers and stores 16 B once.  The
-// result is bit-identical to the reference for fp32/fp64/int32/int64 (no FMA, no
-// reassociation, denormals kept — hipcc's default f32 denorm mode).
-//
-// MI355X mapping: pure HBM streaming (k reads + 1 write per element, ~0.2 FLOP/B),
-// so the design goal is bytes in flight: 64-wide waves, 16-B loads per lane
-// (1 KiB per wave-instruction), U independent vectors per input per lane, a
-// grid-stride loop over <= 8 blocks per CU, optional non-temporal loads/stores so
-// the once-read buckets do not churn L2 / Infinity Cache.  No LDS: there is no
-// reuse to stage, and a round trip through it would only add instructions
-// (cdna_hip_programming.md Appendix B "Element-wise").
+// The tree-order reduction kernel itself (k_tree_sum_buf: k inputs folded in the
+// hypercube order of fflib2's recursive doubling, src/colls/ffallreduce.c:138-171, one
+// HBM pass) and its launch sizing live in reduce_core.h, shared with the tools-only sweep
+// library (tools/sweeps/reduce_sweeps.hip).  This file holds what the product needs
+// besides: the remote (peer-HBM) reduce-scatter / all-gather kernels, the bf16 wire, the
+// fused snapshot, bucket packing, the rank-pairing kernels and the one-launch round.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -27,270 +16,9 @@
 #include <type_traits>
 
 #include "esgd_internal.h"
+#include "reduce_core.h"
 
 namespace esgd {
-
-using raw16 = __attribute__((ext_vector_type(4))) unsigned int;  // one 16-B access
-
-struct InputSet {
-    const void *p[ESGD_MAX_FANIN];
-};
-
-// ---- element traits: T = storage, A = accumulator, E = elements per 16 B ----
-struct F32 {
-    using T = float; using A = float; static constexpr int E = 4;
-    __device__ static A load(T x) { return x; }
-    __device__ static T store(A a) { return a; }
-};
-struct F64 {
-    using T = double; using A = double; static constexpr int E = 2;
-    __device__ static A load(T x) { return x; }
-    __device__ static T store(A a) { return a; }
-};
-struct I32 {  // wrapping two's-complement add, like the reference's int32 SUM
-    using T = uint32_t; using A = uint32_t; static constexpr int E = 4;
-    __device__ static A load(T x) { return x; }
-    __device__ static T store(A a) { return a; }
-};
-struct I64 {
-    using T = uint64_t; using A = uint64_t; static constexpr int E = 2;
-    __device__ static A load(T x) { return x; }
-    __device__ static T store(A a) { return a; }
-};
-struct BF16 {  // extension: fp32 accumulate, one round-to-nearest-even at the end
-    using T = uint16_t; using A = float; static constexpr int E = 8;
-    __device__ static A load(T x) { return __uint_as_float(uint32_t(x) << 16); }
-    __device__ static T store(A a) {
-        uint32_t u = __float_as_uint(a);
-        if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu))
-            return uint16_t((u >> 16) | 0x0040u);            // NaN stays a (quiet) NaN
-        u += 0x7fffu + ((u >> 16) & 1u);
-        return uint16_t(u >> 16);
-    }
-};
-
-// The hypercube tree of ffallreduce.c:138-171 as rank 0 evaluates it: at distance s
-// the partner's partial (operand a, `tmp`) is added to the local one (operand b, `rb`).
-template <class Tr, int K>
-__device__ __forceinline__ void tree_fold(typename Tr::A (&v)[K]) {
-#pragma unroll
-    for (int s = 1; s < K; s <<= 1) {
-#pragma unroll
-        for (int j = 0; j + s < K; j += 2 * s) v[j] = v[j + s] + v[j];
-    }
-}
-
-template <bool NT>
-__device__ __forceinline__ raw16 ld16(const void *base, uint64_t i) {
-    const raw16 *p = static_cast<const raw16 *>(base) + i;
-    if constexpr (NT) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-
-template <bool NT>
-__device__ __forceinline__ void st16(void *base, uint64_t i, raw16 v) {
-    raw16 *p = static_cast<raw16 *>(base) + i;
-    if constexpr (NT) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-
-// fold one 16-B column of K inputs
-template <class Tr, int K, bool SCALE>
-__device__ __forceinline__ raw16 fold16(const raw16 (&r)[K], float scale) {
-    using T = typename Tr::T;
-    using A = typename Tr::A;
-    constexpr int E = Tr::E;
-    T out[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-        A v[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            T x;
-            __builtin_memcpy(&x, reinterpret_cast<const char *>(&r[j]) + e * sizeof(T), sizeof(T));
-            v[j] = Tr::load(x);
-        }
-        tree_fold<Tr, K>(v);
-        if constexpr (SCALE) v[0] = v[0] * scale;
-        out[e] = Tr::store(v[0]);
-    }
-    raw16 o;
-    __builtin_memcpy(&o, out, 16);
-    return o;
-}
-
-// Flat-address body for buckets past the descriptor's 32-bit byte range (> 2 GiB) and
-// for A/B runs (policy 0): `nvec` 16-B columns; the ragged tail (< E elements) is
-// folded by block 0 with scalar accesses.
-template <class Tr, int K, int U, bool NT, bool SCALE>
-__global__ __launch_bounds__(256) void k_tree_sum(InputSet in, void *out, uint64_t nvec,
-                                                   uint64_t count, float scale) {
-    constexpr int B = 256;
-    const uint64_t stride = uint64_t(gridDim.x) * B * U;
-    uint64_t i = uint64_t(blockIdx.x) * B * U + threadIdx.x;
-    for (; i + uint64_t(U - 1) * B < nvec; i += stride) {
-        raw16 r[U][K];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int j = 0; j < K; ++j) r[u][j] = ld16<NT>(in.p[j], i + u * B);
-#pragma unroll
-        for (int u = 0; u < U; ++u) st16<NT>(out, i + u * B, fold16<Tr, K, SCALE>(r[u], scale));
-    }
-    // partial last iteration of this lane (only when U > 1)
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint64_t c = i + u * B;
-        if (c < nvec) {
-            raw16 r[K];
-#pragma unroll
-            for (int j = 0; j < K; ++j) r[j] = ld16<NT>(in.p[j], c);
-            st16<NT>(out, c, fold16<Tr, K, SCALE>(r, scale));
-        }
-    }
-    using T = typename Tr::T;
-    using A = typename Tr::A;
-    const uint64_t tail0 = nvec * Tr::E;
-    if (blockIdx.x == 0 && tail0 + threadIdx.x < count) {
-        const uint64_t e = tail0 + threadIdx.x;
-        A v[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) v[j] = Tr::load(static_cast<const T *>(in.p[j])[e]);
-        tree_fold<Tr, K>(v);
-        if constexpr (SCALE) v[0] = v[0] * scale;
-        static_cast<T *>(out)[e] = Tr::store(v[0]);
-    }
-}
-
-// Production body: buffer-descriptor loads/stores (`buffer_load_dwordx4 ... offen`) with
-// explicit cache-policy bits (aux: 1 = sc0, 2 = nt, 16 = sc1).  Measured on MI355X
-// (profiles/r01/sweep_policy.md): nt loads + sc1 (write-through, not retained in L2)
-// stores move 6.5 TB/s at k = 8 x 256 MiB against 5.9 TB/s for plain global
-// loads/stores — the once-read inputs and the once-written output stop competing for
-// L2 / Infinity Cache.  The descriptor's range check (num_records = bytes of the vector
-// body) turns the ragged last iteration into zero-fill loads and dropped stores, so the
-// loop has no per-element branch (cdna_hip_programming.md §5 item 4c).
-template <class Tr, int K, int U, int LAUX, int SAUX, bool SCALE, int B = 256>
-__global__ __launch_bounds__(B) void k_tree_sum_buf(InputSet in, void *out, uint32_t nvec,
-                                                     uint64_t count, float scale) {
-    const int bytes = int(nvec * 16u);
-    __amdgpu_buffer_rsrc_t rs[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-        rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(in.p[j]), (short)0, bytes,
-                                                  0x00020000);
-    __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, bytes, 0x00020000);
-    const uint32_t step = gridDim.x * (B * U);
-    for (uint32_t i = blockIdx.x * (B * U) + threadIdx.x; i < nvec; i += step) {
-        raw16 r[U][K];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int j = 0; j < K; ++j)
-                r[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs[j], (i + u * B) * 16, 0, LAUX);
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            __builtin_amdgcn_raw_buffer_store_b128(fold16<Tr, K, SCALE>(r[u], scale), ws,
-                                                   (i + u * B) * 16, 0, SAUX);
-    }
-    using T = typename Tr::T;
-    using A = typename Tr::A;
-    const uint64_t tail0 = uint64_t(nvec) * Tr::E;
-    if (blockIdx.x == 0 && tail0 + threadIdx.x < count) {
-        const uint64_t e = tail0 + threadIdx.x;
-        A v[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) v[j] = Tr::load(static_cast<const T *>(in.p[j])[e]);
-        tree_fold<Tr, K>(v);
-        if constexpr (SCALE) v[0] = v[0] * scale;
-        static_cast<T *>(out)[e] = Tr::store(v[0]);
-    }
-}
-
-// LDS-DMA body (experiment, tuning policies 17-20): every wave streams chunks of 64
-// 16-B columns; the K inputs of a chunk arrive by `buffer_load_dwordx4 ... lds` straight
-// into the wave's own LDS ring (no VGPR destination), NB - 1 chunks ahead, and are folded
-// from LDS.  Each wave only reads what it loaded itself, so a counted vmcnt is the only
-// synchronisation (loads retire in order; a store in between only makes the wait stricter).
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    static_assert(N >= 0 && N < 64, "vmcnt");
-    // gfx9 encoding: vmcnt[3:0] | expcnt[6:4] = 7 | lgkmcnt[11:8] = 15 | vmcnt[5:4] << 14
-    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
-
-// K LDS-DMA loads of this lane's 16-B column `col` into the wave's ring stage (past the
-// end of a bucket the descriptor's range check loads zeros)
-typedef __attribute__((address_space(3))) char lds_char;
-
-template <int K, int LAUX>
-__device__ __forceinline__ void lds_issue(__amdgpu_buffer_rsrc_t (&rs)[K], lds_char *stage, uint32_t col) {
-#if defined(__HIP_DEVICE_COMPILE__)   // the LDS-DMA builtin exists for the device target only
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs[j], (__attribute__((address_space(3))) void *)(stage + j * 1024),
-                                                 16, col * 16, 0, 0, LAUX);
-#endif
-}
-
-template <class Tr, int K, int W, int NB, int LAUX, bool SCALE>
-__global__ __launch_bounds__(W * 64) void k_tree_sum_lds(InputSet in, void *out, uint32_t nvec, uint64_t count,
-                                                         float scale) {
-    __shared__ raw16 ring[W][NB][K][64];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int bytes = int(nvec * 16u);
-    __amdgpu_buffer_rsrc_t rs[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-        rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(in.p[j]), (short)0, bytes, 0x00020000);
-    __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, bytes, 0x00020000);
-    const uint32_t nchunk = (nvec + 63) / 64;
-    const uint32_t c0 = blockIdx.x * W + w, step = gridDim.x * W;
-    // the wave's ring in LDS address space (stage st at byte st * K * 1 KiB)
-    lds_char *mine = (lds_char *)(&ring[w][0][0][0]);
-#pragma unroll
-    for (int p = 0; p < NB - 1; ++p) lds_issue<K, LAUX>(rs, mine + p * K * 1024, (c0 + p * step) * 64 + lane);
-    int st = 0;
-    for (uint32_t c = c0; c < nchunk; c += step) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the stage refilled next was read
-        lds_issue<K, LAUX>(rs, mine + ((st + NB - 1) % NB) * K * 1024, (c + (NB - 1) * step) * 64 + lane);
-        wait_vmcnt<K * (NB - 1)>();                            // chunk c has landed
-        raw16 r[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) r[j] = ring[w][st][j][lane];
-        __builtin_amdgcn_raw_buffer_store_b128(fold16<Tr, K, SCALE>(r, scale), ws, (c * 64 + lane) * 16, 0, 16);
-        st = (st + 1) % NB;
-    }
-    using T = typename Tr::T;
-    using A = typename Tr::A;
-    const uint64_t tail0 = uint64_t(nvec) * Tr::E;
-    if (blockIdx.x == 0 && tail0 + threadIdx.x < count) {
-        const uint64_t e = tail0 + threadIdx.x;
-        A v[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) v[j] = Tr::load(static_cast<const T *>(in.p[j])[e]);
-        tree_fold<Tr, K>(v);
-        if constexpr (SCALE) v[0] = v[0] * scale;
-        static_cast<T *>(out)[e] = Tr::store(v[0]);
-    }
-}
-
-// Fallback for pointers that are not 16-B aligned: one element per lane.
-template <class Tr, int K, bool SCALE>
-__global__ __launch_bounds__(256) void k_tree_sum_scalar(InputSet in, void *out, uint64_t count,
-                                                          float scale) {
-    using T = typename Tr::T;
-    using A = typename Tr::A;
-    const uint64_t stride = uint64_t(gridDim.x) * 256;
-    for (uint64_t e = uint64_t(blockIdx.x) * 256 + threadIdx.x; e < count; e += stride) {
-        A v[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) v[j] = Tr::load(static_cast<const T *>(in.p[j])[e]);
-        tree_fold<Tr, K>(v);
-        if constexpr (SCALE) v[0] = v[0] * scale;
-        static_cast<T *>(out)[e] = Tr::store(v[0]);
-    }
-}
 
 // ---- all-gather of peer shards (data plane phase 2) ----
 // Copies up to kMaxSeg segments (one per peer shard) in one launch; blockIdx.y picks
@@ -570,120 +298,14 @@ __global__ void k_fill_uniform_bf16(uint64_t base, uint16_t *out, uint64_t n) {
         out[i] = BF16::store(uniform_pm1(base, i));
 }
 
-// ---- launch configuration ----
-static int g_unroll = 0;   // 0 -> default (4 x 16 B per input per lane)
-static int g_grid = 0;     // 0 -> auto: 8 blocks of 256 per CU, grid-stride
-static int g_nt = -1;      // flat path only: -1/1 -> nt loads/stores
-static int g_policy = -1;  // -1 -> production policy (nt loads, sc1 stores); 0 -> flat path;
-                           // 1..8 -> cache-policy table below (F32, k = 8 only; sweeps)
-
-static int cu_count() {
-    static int cus[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cus[dev]) {
-        hipDeviceProp_t p;
-        cus[dev] = (hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0)
-                       ? p.multiProcessorCount : 256;
-    }
-    return cus[dev];
-}
-
-// Grid-stride launches are sized to what is resident at once (CUs x blocks per CU that
-// the kernel's registers admit): a second, queued wave of blocks only adds a tail
-// (profiles/r01/sweep_grid.md: 1024 blocks = 4/CU beat 2048 at 98 VGPRs).
-static unsigned grid_for(uint64_t items_per_block_pass, uint64_t items, int blocks_per_cu = 8) {
-    if (g_grid > 0) return unsigned(g_grid);
-    uint64_t need = (items + items_per_block_pass - 1) / items_per_block_pass;
-    uint64_t cap = uint64_t(cu_count()) * uint64_t(blocks_per_cu > 0 ? blocks_per_cu : 1);
-    if (need < 1) need = 1;
-    return unsigned(need < cap ? need : cap);
-}
-
-template <typename KernelT>
-static int resident_blocks(KernelT kernel, int block = 256) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, block, 0) != hipSuccess || nb <= 0)
-        nb = 4;
-    return nb < 8 ? nb : 8;
-}
-
-template <class Tr, int K, int U, bool NT, bool SCALE>
-static int launch_flat(const InputSet &in, void *out, uint64_t count, float scale, hipStream_t s) {
-    const uint64_t nvec = count / Tr::E;
-    unsigned grid = grid_for(uint64_t(256) * U, nvec ? nvec : 1);
-    hipLaunchKernelGGL((k_tree_sum<Tr, K, U, NT, SCALE>), dim3(grid), dim3(256), 0, s, in, out,
-                       nvec, count, scale);
-    ESGD_HIP(hipGetLastError());
-    return ESGD_SUCCESS;
-}
-
-template <class Tr, int K, int U, int LA, int SA, bool SCALE, int B = 256>
-static int launch_buf(const InputSet &in, void *out, uint64_t count, float scale, hipStream_t s) {
-    const uint64_t nvec = count / Tr::E;
-    static const int per_cu = resident_blocks(k_tree_sum_buf<Tr, K, U, LA, SA, SCALE, B>, B);
-    unsigned grid = grid_for(uint64_t(B) * U, nvec ? nvec : 1, per_cu);
-    hipLaunchKernelGGL((k_tree_sum_buf<Tr, K, U, LA, SA, SCALE, B>), dim3(grid), dim3(B), 0, s, in,
-                       out, uint32_t(nvec), count, scale);
-    ESGD_HIP(hipGetLastError());
-    return ESGD_SUCCESS;
-}
-
-// Buckets larger than a window run as consecutive launches over window-sized slices of
-// every input (same kernel, same per-element work).  Measured at 8 inputs
-// (profiles/r02/sweeps_windowed.jsonl): one launch over 8 x 256 MiB reached 77.6-78.1 %
-// of 8 TB/s, 64 MiB windows 80.1 %; 8 x 1 GiB 67.8 % -> 74.8 %; at 128 MiB 79.5 -> 81.2 %.
-// Each launch starts its occupancy-sized grid together at the window's start, where one
-// long grid-stride launch lets its workgroups drift apart over the whole footprint.
-// Every window also fits the buffer descriptors' 32-bit range, whatever the bucket size.
-constexpr uint64_t kWindowBytes = uint64_t(64) << 20;
-
-template <class Tr, int K, int U, int LA, int SA, bool SCALE>
-static int launch_windows(const InputSet &in, void *out, uint64_t count, float scale, hipStream_t s,
-                          uint64_t window_bytes = kWindowBytes) {
-    using T = typename Tr::T;
-    const uint64_t w = window_bytes / sizeof(T);
-    if (count <= w + w / 2) return launch_buf<Tr, K, U, LA, SA, SCALE>(in, out, count, scale, s);
-    for (uint64_t o = 0; o < count; o += w) {
-        InputSet sl = in;
-        for (int j = 0; j < K; ++j) sl.p[j] = static_cast<const T *>(in.p[j]) + o;
-        if (int rc = launch_buf<Tr, K, U, LA, SA, SCALE>(sl, static_cast<T *>(out) + o, std::min(w, count - o), scale, s))
-            return rc;
-    }
-    return ESGD_SUCCESS;
-}
-
-template <class Tr, int K, int W, int NB, int LA, bool SCALE>
-static int launch_lds(const InputSet &in, void *out, uint64_t count, float scale, hipStream_t s) {
-    const uint64_t nvec = count / Tr::E;
-    static const int per_cu = resident_blocks(k_tree_sum_lds<Tr, K, W, NB, LA, SCALE>, W * 64);
-    unsigned grid = grid_for(uint64_t(W) * 64, (nvec + 63) / 64 * 64 ? (nvec + 63) / 64 * 64 : 1, per_cu);
-    hipLaunchKernelGGL((k_tree_sum_lds<Tr, K, W, NB, LA, SCALE>), dim3(grid), dim3(W * 64), 0, s, in, out,
-                       uint32_t(nvec), count, scale);
-    ESGD_HIP(hipGetLastError());
-    return ESGD_SUCCESS;
-}
-
-// alternative {load aux, store aux} pairs kept for sweeps (tools/sweep_reduce.py)
-#define ESGD_POLICIES(X) X(1, 2, 16) X(2, 2, 17) X(3, 2, 18) X(4, 2, 19) X(5, 0, 16) X(6, 3, 16) X(7, 18, 16) X(8, 16, 16)
-
-template <class Tr, int K, bool SCALE>
-static int launch_scalar(const InputSet &in, void *out, uint64_t count, float scale, hipStream_t s) {
-    unsigned grid = grid_for(256, count);
-    hipLaunchKernelGGL((k_tree_sum_scalar<Tr, K, SCALE>), dim3(grid), dim3(256), 0, s, in, out,
-                       count, scale);
-    ESGD_HIP(hipGetLastError());
-    return ESGD_SUCCESS;
-}
-
 template <class Tr, int K, bool SCALE>
 static int dispatch_u(const InputSet &in, void *out, uint64_t count, float scale, bool aligned,
                       hipStream_t s, bool remote = false) {
     // bf16 folds 8 lanes per 16 B: two vectors per input keep it under 128 VGPRs
     constexpr int UD = sizeof(typename Tr::T) == 2 ? 2 : 4;
-    const bool fits32 = count / Tr::E * 16 + uint64_t(UD) * 256 * 16 < (1ull << 31);
     if (remote) {
         // inputs live in peer HBM (IPC over xGMI): system-scope nt loads, local sc1 stores
+        const bool fits32 = count / Tr::E * 16 + uint64_t(UD) * 256 * 16 < (1ull << 31);
         if (!aligned || !fits32) {
             set_error("remote reduce: shard must be 16-B aligned and < 2 GiB");
             return ESGD_INVALID_ARG;
@@ -691,48 +313,10 @@ static int dispatch_u(const InputSet &in, void *out, uint64_t count, float scale
         return launch_buf<Tr, K, UD, 19, 16, SCALE>(in, out, count, scale, s);
     }
     if (!aligned) return launch_scalar<Tr, K, SCALE>(in, out, count, scale, s);
-    // the production policy windows any size into the buffer kernel; sweep variants
-    // need the whole bucket inside one 32-bit descriptor range
-    if (g_policy != 0 && (fits32 || g_policy == -1)) {
-        if constexpr (std::is_same<Tr, F32>::value && K == 8) {
-            switch (g_policy) {
-#define ESGD_CASE(ID, LA, SA) \
-            case ID: return launch_buf<Tr, K, 4, LA, SA, SCALE>(in, out, count, scale, s);
-            ESGD_POLICIES(ESGD_CASE)
-#undef ESGD_CASE
-            // block-shape variants of the production policy (sweeps)
-            case 9: return launch_buf<Tr, K, 3, 2, 16, SCALE>(in, out, count, scale, s);
-            case 10: return launch_buf<Tr, K, 2, 2, 16, SCALE, 512>(in, out, count, scale, s);
-            case 11: return launch_buf<Tr, K, 4, 2, 16, SCALE, 512>(in, out, count, scale, s);
-            case 12: return launch_buf<Tr, K, 4, 2, 16, SCALE, 128>(in, out, count, scale, s);
-            case 13: return launch_buf<Tr, K, 2, 2, 16, SCALE, 1024>(in, out, count, scale, s);
-            // store policies: nt-only streaming stores, plain stores
-            case 14: return launch_buf<Tr, K, 4, 2, 2, SCALE>(in, out, count, scale, s);
-            case 15: return launch_buf<Tr, K, 4, 2, 0, SCALE>(in, out, count, scale, s);
-            case 16: return launch_buf<Tr, K, 4, 2, 3, SCALE>(in, out, count, scale, s);
-            // LDS-DMA ring variants: (waves per block, ring depth)
-            case 17: return launch_lds<Tr, K, 4, 2, 2, SCALE>(in, out, count, scale, s);
-            case 18: return launch_lds<Tr, K, 2, 4, 2, SCALE>(in, out, count, scale, s);
-            case 19: return launch_lds<Tr, K, 1, 8, 2, SCALE>(in, out, count, scale, s);
-            case 20: return launch_lds<Tr, K, 2, 3, 2, SCALE>(in, out, count, scale, s);
-            // window sizes for sweeps (production: kWindowBytes = 64 MiB); 24: one launch
-            case 21: return launch_windows<Tr, K, 4, 2, 16, SCALE>(in, out, count, scale, s, uint64_t(32) << 20);
-            case 22: return launch_windows<Tr, K, 4, 2, 16, SCALE>(in, out, count, scale, s, uint64_t(64) << 20);
-            case 23: return launch_windows<Tr, K, 4, 2, 16, SCALE>(in, out, count, scale, s, uint64_t(96) << 20);
-            case 24: return launch_buf<Tr, K, 4, 2, 16, SCALE>(in, out, count, scale, s);
-            default: break;
-            }
-        }
-        if (g_unroll == 2 || g_unroll == 1)
-            return launch_windows<Tr, K, 2, 2, 16, SCALE>(in, out, count, scale, s);
-        return launch_windows<Tr, K, UD, 2, 16, SCALE>(in, out, count, scale, s);
-    }
-    const bool nt = g_nt != 0;
-    if (g_unroll == 1) return nt ? launch_flat<Tr, K, 1, true, SCALE>(in, out, count, scale, s)
-                                 : launch_flat<Tr, K, 1, false, SCALE>(in, out, count, scale, s);
-    return nt ? launch_flat<Tr, K, 2, true, SCALE>(in, out, count, scale, s)
-              : launch_flat<Tr, K, 2, false, SCALE>(in, out, count, scale, s);
+    // nt loads + sc1 stores, any size windowed into the buffer kernel
+    return launch_windows<Tr, K, UD, 2, 16, SCALE>(in, out, count, scale, s);
 }
+
 
 template <class Tr, bool SCALE>
 static int dispatch_k(int k, const InputSet &in, void *out, uint64_t count, float scale,
@@ -1358,38 +942,4 @@ int esgd_fill_uniform_bf16(uint64_t seed, int rank, uint16_t *out, uint64_t n, v
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;
 }
-
-int esgd_set_tuning(const char *key, int value) {
-    ESGD_ARG(key, "esgd_set_tuning: null key");
-    if (!std::strcmp(key, "unroll")) {
-        ESGD_ARG(value == 0 || value == 1 || value == 2 || value == 4, "unroll must be 0/1/2/4");
-        g_unroll = value;
-    } else if (!std::strcmp(key, "grid")) {
-        ESGD_ARG(value >= 0, "grid must be >= 0");
-        g_grid = value;
-    } else if (!std::strcmp(key, "nt")) {
-        g_nt = value ? 1 : 0;
-    } else if (!std::strcmp(key, "policy")) {
-        ESGD_ARG(value >= -1 && value <= 24, "policy must be -1..24");
-        g_policy = value;
-    } else {
-        set_error("esgd_set_tuning: unknown key '%s'", key);
-        return ESGD_INVALID_ARG;
-    }
-    return ESGD_SUCCESS;
-}
-
-int esgd_get_tuning(const char *key, int *value) {
-    ESGD_ARG(key && value, "esgd_get_tuning: null argument");
-    if (!std::strcmp(key, "unroll")) *value = g_unroll;
-    else if (!std::strcmp(key, "grid")) *value = g_grid;
-    else if (!std::strcmp(key, "nt")) *value = g_nt;
-    else if (!std::strcmp(key, "policy")) *value = g_policy;
-    else {
-        set_error("esgd_get_tuning: unknown key '%s'", key);
-        return ESGD_INVALID_ARG;
-    }
-    return ESGD_SUCCESS;
-}
-
 }  // extern "C"

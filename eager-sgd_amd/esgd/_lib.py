@@ -67,8 +67,6 @@ _SIGS = {
     "esgd_pack_div": (_i, [_i, C.POINTER(_vp), C.POINTER(_u64), _vp, _f, _vp]),
     "esgd_unpack": (_i, [_i, C.POINTER(_vp), C.POINTER(_u64), _vp, _vp]),
     "esgd_fill_uniform_bf16": (_i, [_u64, _i, _vp, _u64, _vp]),
-    "esgd_set_tuning": (_i, [C.c_char_p, _i]),
-    "esgd_get_tuning": (_i, [C.c_char_p, C.POINTER(_i)]),
 }
 
 _lib = None

@@ -186,13 +186,3 @@ def fill_uniform(buf: DeviceBuffer, seed: int, rank: int, stream=None):
     else:
         raise ValueError("fill_uniform: FLOAT or BF16 only")
     return check(rc, "esgd_fill_uniform")
-
-
-def set_tuning(key: str, value: int):
-    check(lib().esgd_set_tuning(key.encode(), int(value)), "esgd_set_tuning")
-
-
-def get_tuning(key: str) -> int:
-    v = C.c_int()
-    check(lib().esgd_get_tuning(key.encode(), C.byref(v)), "esgd_get_tuning")
-    return v.value

@@ -122,17 +122,6 @@ int esgd_unpack(int n, float *const *dst, const uint64_t *count, const float *sr
 int esgd_fill_uniform_f32(uint64_t seed, int rank, float *out, uint64_t n, void *stream);
 int esgd_fill_uniform_bf16(uint64_t seed, int rank, uint16_t *out, uint64_t n, void *stream);
 
-/* Tuning knobs for the reduction launch (benchmarks only; 0 = default).
- * key: "unroll" (16-B vectors per lane per input: 0 = default, 1, 2, 4),
- *      "grid"   (blocks, 0 = auto: 8 x 256-thread blocks per CU, grid-stride),
- *      "policy" (-1 = production: buffer loads with nt + stores with sc1; 0 = flat
- *                global path; 1..8 = alternative cache-policy pairs, 9..13 = block-shape
- *                variants (unroll 3; 512 / 128 / 1024-thread blocks), fp32 k = 8 only),
- *      "nt"     (flat path only: 1 = non-temporal loads/stores).
- * Unknown keys -> ESGD_INVALID_ARG. */
-int esgd_set_tuning(const char *key, int value);
-int esgd_get_tuning(const char *key, int *value);
-
 /* ---- node communicator (replaces MPI_Init / MPI_Barrier of the reference:
  *      src/components/mpi/ffmpi.c:11-31, opt_esgd_solo_imagenet_imbalance.py:295) ----
  * Collective over the `world` processes of one node that pass the same job id; each

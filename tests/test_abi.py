@@ -67,8 +67,6 @@ def test_argument_validation_without_device():
     assert lib.esgd_reduce(_lib.FLOAT, 0, ptrs, ctypes.c_void_p(0x3000), 16, None) == _lib.INVALID_ARG
     assert lib.esgd_reduce(99, 2, ptrs, ctypes.c_void_p(0x3000), 16, None) in (_lib.INVALID_ARG, _lib.NO_DEVICE)
     assert lib.esgd_dtype_size(_lib.BF16) == 2 and lib.esgd_dtype_size(7) == 0
-    assert lib.esgd_set_tuning(b"unroll", 3) == _lib.INVALID_ARG
-    assert lib.esgd_set_tuning(b"bogus", 1) == _lib.INVALID_ARG
 
 
 def test_wire_flag_argument_checks():

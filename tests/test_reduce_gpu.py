@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from esgd import _lib
-from esgd.device import DeviceBuffer, Stream, fill_uniform, reduce, set_tuning, synchronize, vsum
+from esgd.device import DeviceBuffer, Stream, fill_uniform, reduce, synchronize, vsum
 from oracle import ffref
 
 pytestmark = pytest.mark.gpu
@@ -145,24 +145,6 @@ def test_fill_uniform_bitwise():
         b = DeviceBuffer(100003)
         fill_uniform(b, 0x5EEDE56D, rank)
         bits_equal(b.download(), ffref.fill_uniform(0x5EEDE56D, rank, 100003))
-
-
-@pytest.mark.parametrize("policy,unroll,nt,grid", [
-    (-1, 0, 1, 0), (-1, 2, 1, 7), (-1, 4, 1, 1), (0, 1, 0, 0), (0, 2, 1, 0), (0, 4, 0, 7),
-    (1, 0, 1, 0), (3, 0, 1, 5), (5, 0, 1, 0), (8, 0, 1, 3), (9, 0, 1, 0), (10, 0, 1, 0),
-    (11, 0, 1, 3), (12, 0, 1, 0), (13, 0, 1, 0), (14, 0, 1, 0), (16, 0, 1, 0),
-    # LDS-DMA ring variants (sweep only): (waves, depth) 4/2, 2/4, 1/8, 2/3
-    (17, 0, 1, 0), (18, 0, 1, 3), (19, 0, 1, 0), (20, 0, 1, 5)])
-@pytest.mark.parametrize("k", [2, 8])
-def test_tuning_variants_identical(policy, unroll, nt, grid, k):
-    xs = rand_input(np.float32, k, 300007, seed=3)
-    want = ffref.tree_sum(xs)
-    try:
-        set_tuning("policy", policy); set_tuning("unroll", unroll); set_tuning("nt", nt)
-        set_tuning("grid", grid)
-        bits_equal(gpu_reduce(xs, _lib.FLOAT), want)
-    finally:
-        set_tuning("policy", -1); set_tuning("unroll", 0); set_tuning("nt", 1); set_tuning("grid", 0)
 
 
 def test_full_size_c2_bitwise():

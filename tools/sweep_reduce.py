@@ -2,10 +2,14 @@
 """Interleaved A/B sweep of the reduction launch parameters in ONE process
 (cdna_hip_programming.md §5.4 rule 24): every variant is timed once per round, for
 several rounds, and the median/min per-launch time from HIP event pairs is reported.
+The variants live in the tools-only library tools/bin/libesgd_sweeps.so (`make sweeps`,
+tools/sweeps/reduce_sweeps.hip: fp32, fan-in 8); libesgd.so carries only the production
+launch (policy -1 here).
 
-  python tools/sweep_reduce.py [--k 8] [--mib 64] [--rounds 7] [--iters 30]
+  python tools/sweep_reduce.py [--mib 64] [--rounds 7] [--iters 30] [--policies -1,0,17]
 """
 import argparse
+import ctypes as C
 import itertools
 import json
 import os
@@ -19,11 +23,10 @@ import esgd  # noqa: E402
 from esgd import device as dev  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--k", type=int, default=8)
+ap.add_argument("--k", type=int, default=8, choices=[8], help="fan-in (the sweep library is k = 8 only)")
 ap.add_argument("--mib", type=float, default=64)
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--iters", type=int, default=30)
-ap.add_argument("--dtype", default="fp32")
 ap.add_argument("--grids", default="0,1024,2048,4096,8192,16384")
 ap.add_argument("--unrolls", default="2,4")
 ap.add_argument("--nts", default="0,1")
@@ -31,9 +34,11 @@ ap.add_argument("--policies", default="-1")
 ap.add_argument("--stagger", type=int, default=0,
                 help="bytes between consecutive buckets in one arena (0 = separate allocations)")
 a = ap.parse_args()
-
-dt = esgd.FLOAT if a.dtype == "fp32" else esgd.BF16
-es = 4 if dt == esgd.FLOAT else 2
+dt, es = esgd.FLOAT, 4
+sw = C.CDLL(os.path.join(ROOT, "tools", "bin", "libesgd_sweeps.so"))
+sw.esgd_sweep_reduce.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.c_void_p,
+                                 C.c_uint64, C.c_void_p]
+sw.esgd_sweep_last_error.restype = C.c_char_p
 count = int(a.mib * (1 << 20)) // es
 s = dev.Stream()
 if a.stagger:
@@ -56,18 +61,24 @@ variants = list(itertools.product([int(x) for x in a.unrolls.split(",")],
                                   [int(x) for x in a.policies.split(",")]))
 # every variant's output must be the production variant's, bit for bit
 import numpy as np  # noqa: E402
-dev.set_tuning("policy", -1); dev.set_tuning("unroll", 0); dev.set_tuning("grid", 0); dev.set_tuning("nt", 1)
+pa = (C.c_void_p * 8)(*ptrs)
+optr = out if a.stagger else out.ptr
+
+
+def run(v):
+    u, nt, g, pol = v
+    if sw.esgd_sweep_reduce(pol, u, nt, g, pa, optr, count, s.handle):
+        raise RuntimeError(sw.esgd_sweep_last_error().decode())
+
+
 dev.reduce(dt, ptrs, out, count, stream=s)
 s.synchronize()
 ref = out.download() if not a.stagger else None
 bad = {}
 for v in variants:
-    u, nt, g, pol = v
-    dev.set_tuning("unroll", u); dev.set_tuning("nt", nt); dev.set_tuning("grid", g)
-    dev.set_tuning("policy", pol)
     if ref is not None:
         out.zero(stream=s)
-        dev.reduce(dt, ptrs, out, count, stream=s)
+        run(v)
         s.synchronize()
         got = out.download()
         nbad = int(np.count_nonzero(got.view(np.uint8) != ref.view(np.uint8)))
@@ -77,14 +88,11 @@ ev = [dev.Event() for _ in range(2 * a.iters)]
 times = {v: [] for v in variants}
 for rnd in range(a.rounds):
     for v in variants:
-        u, nt, g, pol = v
-        dev.set_tuning("unroll", u); dev.set_tuning("nt", nt); dev.set_tuning("grid", g)
-        dev.set_tuning("policy", pol)
         for _ in range(3):
-            dev.reduce(dt, ptrs, out, count, stream=s)
+            run(v)
         for i in range(a.iters):
             ev[2 * i].record(s)
-            dev.reduce(dt, ptrs, out, count, stream=s)
+            run(v)
             ev[2 * i + 1].record(s)
         s.synchronize()
         times[v].extend(ev[2 * i].elapsed_ms(ev[2 * i + 1]) for i in range(a.iters))

@@ -1,0 +1,207 @@
+// reduce_sweeps.hip — measurement-only variants of the tree reduction (NOT the product).
+//
+// `make sweeps` builds tools/bin/libesgd_sweeps.so from this file; tools/sweep_reduce.py
+// loads it with ctypes next to libesgd.so (which provides memory and streams).  Every
+// variant here was measured against the production kernel (reduce_core.h,
+// k_tree_sum_buf with nt loads + sc1 stores, 64 MiB windows) and lost; they are kept so
+// the sweeps behind profiles/r01 and profiles/r02 stay reproducible:
+//   policy 0        flat-address global loads/stores (nt = non-temporal both ways)
+//   policy 1..8     other {load aux, store aux} cache-policy pairs of the buffer kernel
+//   policy 9..13    block shapes (unroll 3; 512 / 128 / 1024-thread blocks)
+//   policy 14..16   store policies (nt only, plain, sc0+sc1)
+//   policy 17..20   LDS-DMA ring (buffer_load ... lds), (waves per block, ring depth)
+//   policy 21..23   window sizes 32 / 64 / 96 MiB; 24 one launch over the whole bucket
+//   policy -1       the production launch (the baseline every variant is timed against)
+// fp32, fan-in 8 only.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+
+#include "reduce_core.h"
+
+namespace esgd {
+
+// this library's own error plumbing (libesgd.so keeps its internals local)
+static thread_local char g_err[256] = "";
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+int hip_fail(hipError_t e, const char *what, const char *file, int line) {
+    set_error("%s failed: %s (%s:%d)", what, hipGetErrorString(e), file, line);
+    return ESGD_ERROR;
+}
+
+template <bool NT>
+__device__ __forceinline__ raw16 ld16(const void *base, uint64_t i) {
+    const raw16 *p = static_cast<const raw16 *>(base) + i;
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16(void *base, uint64_t i, raw16 v) {
+    raw16 *p = static_cast<raw16 *>(base) + i;
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// flat-address body: `nvec` 16-B columns, ragged tail by block 0
+template <class Tr, int K, int U, bool NT>
+__global__ __launch_bounds__(256) void k_tree_sum_flat(InputSet in, void *out, uint64_t nvec, uint64_t count) {
+    constexpr int B = 256;
+    const uint64_t stride = uint64_t(gridDim.x) * B * U;
+    uint64_t i = uint64_t(blockIdx.x) * B * U + threadIdx.x;
+    for (; i + uint64_t(U - 1) * B < nvec; i += stride) {
+        raw16 r[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j) r[u][j] = ld16<NT>(in.p[j], i + u * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) st16<NT>(out, i + u * B, fold16<Tr, K, false>(r[u], 1.0f));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t c = i + u * B;
+        if (c < nvec) {
+            raw16 r[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) r[j] = ld16<NT>(in.p[j], c);
+            st16<NT>(out, c, fold16<Tr, K, false>(r, 1.0f));
+        }
+    }
+    fold_tail<Tr, K, false>(in, out, nvec * Tr::E, count, 1.0f);
+}
+
+// LDS-DMA body: every wave streams chunks of 64 16-B columns; the K inputs of a chunk
+// arrive by `buffer_load_dwordx4 ... lds` straight into the wave's own LDS ring, NB - 1
+// chunks ahead, and are folded from LDS.  Each wave only reads what it loaded itself, so
+// a counted vmcnt is the only synchronisation.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    // gfx9 encoding: vmcnt[3:0] | expcnt[6:4] = 7 | lgkmcnt[11:8] = 15 | vmcnt[5:4] << 14
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+typedef __attribute__((address_space(3))) char lds_char;
+
+template <int K, int LAUX>
+__device__ __forceinline__ void lds_issue(__amdgpu_buffer_rsrc_t (&rs)[K], lds_char *stage, uint32_t col) {
+#if defined(__HIP_DEVICE_COMPILE__)   // the LDS-DMA builtin exists for the device target only
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs[j], (__attribute__((address_space(3))) void *)(stage + j * 1024),
+                                                 16, col * 16, 0, 0, LAUX);
+#endif
+}
+
+template <class Tr, int K, int W, int NB, int LAUX>
+__global__ __launch_bounds__(W * 64) void k_tree_sum_lds(InputSet in, void *out, uint32_t nvec, uint64_t count) {
+    __shared__ raw16 ring[W][NB][K][64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int bytes = int(nvec * 16u);
+    __amdgpu_buffer_rsrc_t rs[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(in.p[j]), (short)0, bytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, bytes, 0x00020000);
+    const uint32_t nchunk = (nvec + 63) / 64;
+    const uint32_t c0 = blockIdx.x * W + w, step = gridDim.x * W;
+    lds_char *mine = (lds_char *)(&ring[w][0][0][0]);
+#pragma unroll
+    for (int p = 0; p < NB - 1; ++p) lds_issue<K, LAUX>(rs, mine + p * K * 1024, (c0 + p * step) * 64 + lane);
+    int st = 0;
+    for (uint32_t c = c0; c < nchunk; c += step) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the stage refilled next was read
+        lds_issue<K, LAUX>(rs, mine + ((st + NB - 1) % NB) * K * 1024, (c + (NB - 1) * step) * 64 + lane);
+        wait_vmcnt<K * (NB - 1)>();                            // chunk c has landed
+        raw16 r[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) r[j] = ring[w][st][j][lane];
+        __builtin_amdgcn_raw_buffer_store_b128(fold16<Tr, K, false>(r, 1.0f), ws, (c * 64 + lane) * 16, 0, 16);
+        st = (st + 1) % NB;
+    }
+    fold_tail<Tr, K, false>(in, out, uint64_t(nvec) * Tr::E, count, 1.0f);
+}
+
+template <int U, bool NT>
+static int launch_flat(const InputSet &in, void *out, uint64_t count, hipStream_t s, unsigned grid) {
+    const uint64_t nvec = count / F32::E;
+    const unsigned g = grid_for(uint64_t(256) * U, nvec ? nvec : 1, 8, grid);
+    hipLaunchKernelGGL((k_tree_sum_flat<F32, 8, U, NT>), dim3(g), dim3(256), 0, s, in, out, nvec, count);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+template <int W, int NB, int LA>
+static int launch_lds(const InputSet &in, void *out, uint64_t count, hipStream_t s, unsigned grid) {
+    const uint64_t nvec = count / F32::E;
+    static const int per_cu = resident_blocks(k_tree_sum_lds<F32, 8, W, NB, LA>, W * 64);
+    const unsigned g = grid_for(uint64_t(W) * 64, (nvec + 63) / 64 * 64 ? (nvec + 63) / 64 * 64 : 1, per_cu, grid);
+    hipLaunchKernelGGL((k_tree_sum_lds<F32, 8, W, NB, LA>), dim3(g), dim3(W * 64), 0, s, in, out,
+                       uint32_t(nvec), count);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+}  // namespace esgd
+
+using namespace esgd;
+
+extern "C" {
+
+const char *esgd_sweep_last_error(void) { return g_err; }
+
+// One fp32 fan-in-8 reduction with variant `policy` (see the table at the top); unroll
+// (2 or 4) and nt apply to policy 0; grid > 0 fixes the grid of the buffer / flat / LDS
+// kernels.  Same bits as esgd_reduce for every variant (tools/sweep_reduce.py checks).
+int esgd_sweep_reduce(int policy, int unroll, int nt, int grid, const void *const *inputs, void *out,
+                      uint64_t count, void *stream) {
+    if (!inputs || !out) { set_error("null argument"); return ESGD_INVALID_ARG; }
+    InputSet in;
+    std::memset(&in, 0, sizeof(in));
+    for (int j = 0; j < 8; ++j) in.p[j] = inputs[j];
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const unsigned g = grid > 0 ? unsigned(grid) : 0u;
+    const bool fits32 = count / 4 * 16 + uint64_t(4) * 256 * 16 < (1ull << 31);
+    if (policy != -1 && policy != 0 && !fits32) {
+        set_error("policy %d needs the bucket inside one 32-bit descriptor range", policy);
+        return ESGD_INVALID_ARG;
+    }
+    switch (policy) {
+    case -1: return launch_windows<F32, 8, 4, 2, 16, false>(in, out, count, 1.0f, s, kWindowBytes, g);
+    case 0:
+        if (unroll == 4) return nt ? launch_flat<4, true>(in, out, count, s, g) : launch_flat<4, false>(in, out, count, s, g);
+        return nt ? launch_flat<2, true>(in, out, count, s, g) : launch_flat<2, false>(in, out, count, s, g);
+#define ESGD_POL(ID, LA, SA) case ID: return launch_buf<F32, 8, 4, LA, SA, false>(in, out, count, 1.0f, s, g);
+    ESGD_POL(1, 2, 16) ESGD_POL(2, 2, 17) ESGD_POL(3, 2, 18) ESGD_POL(4, 2, 19)
+    ESGD_POL(5, 0, 16) ESGD_POL(6, 3, 16) ESGD_POL(7, 18, 16) ESGD_POL(8, 16, 16)
+#undef ESGD_POL
+    case 9: return launch_buf<F32, 8, 3, 2, 16, false>(in, out, count, 1.0f, s, g);
+    case 10: return launch_buf<F32, 8, 2, 2, 16, false, 512>(in, out, count, 1.0f, s, g);
+    case 11: return launch_buf<F32, 8, 4, 2, 16, false, 512>(in, out, count, 1.0f, s, g);
+    case 12: return launch_buf<F32, 8, 4, 2, 16, false, 128>(in, out, count, 1.0f, s, g);
+    case 13: return launch_buf<F32, 8, 2, 2, 16, false, 1024>(in, out, count, 1.0f, s, g);
+    case 14: return launch_buf<F32, 8, 4, 2, 2, false>(in, out, count, 1.0f, s, g);
+    case 15: return launch_buf<F32, 8, 4, 2, 0, false>(in, out, count, 1.0f, s, g);
+    case 16: return launch_buf<F32, 8, 4, 2, 3, false>(in, out, count, 1.0f, s, g);
+    case 17: return launch_lds<4, 2, 2>(in, out, count, s, g);
+    case 18: return launch_lds<2, 4, 2>(in, out, count, s, g);
+    case 19: return launch_lds<1, 8, 2>(in, out, count, s, g);
+    case 20: return launch_lds<2, 3, 2>(in, out, count, s, g);
+    case 21: return launch_windows<F32, 8, 4, 2, 16, false>(in, out, count, 1.0f, s, uint64_t(32) << 20, g);
+    case 22: return launch_windows<F32, 8, 4, 2, 16, false>(in, out, count, 1.0f, s, uint64_t(64) << 20, g);
+    case 23: return launch_windows<F32, 8, 4, 2, 16, false>(in, out, count, 1.0f, s, uint64_t(96) << 20, g);
+    case 24: return launch_buf<F32, 8, 4, 2, 16, false>(in, out, count, 1.0f, s, g);
+    default: break;
+    }
+    set_error("unknown policy %d", policy);
+    return ESGD_INVALID_ARG;
+}
+
+}  // extern "C"
