@@ -16,10 +16,16 @@
 // finalize.  Foreign device memory (torch tensors, plain hipMalloc) is never exported:
 // schedules over it reduce through an arena bucket (the shadow path, dataplane.cpp).
 //
-// Size classes: powers of two from 4 KiB to 1 MiB carved out of 2 MiB slabs; larger
-// blocks are chunks of their own, rounded up to 2 MiB, reused for requests within 25 %
-// of their size.  Chunks that were never exported go back to the driver when an
-// allocation fails and at finalize (arena_trim).
+// Size classes: powers of two from 4 KiB to 1 MiB carved out of 2 MiB slabs.  Larger
+// blocks are carved from free chunk space best-fit, in 2 MiB granules: a request takes
+// the smallest free run that holds it (splitting off the rest), freed runs coalesce with
+// free neighbours of the same chunk, and only when no free run fits is a new chunk
+// allocated.  So the arena's footprint is bounded by the peak of live bucket bytes (plus
+// fragmentation), not by the number of distinct sizes ever used.  Chunks that were never
+// exported and hold no live block go back to the driver whenever a new chunk is needed
+// and at finalize (arena_trim).  Exported chunks stay until the process exits, so their
+// total is the sum of the successive record bucket sizes (below 2x the largest bucket for
+// C5's doubling sweep; one 8 GiB bucket reserves 8 GiB for good).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -55,8 +61,11 @@ std::mutex g_mu;
 std::vector<Chunk *> g_chunks;
 std::map<uintptr_t, Block> g_live;                        // block start -> block
 std::map<std::pair<int, size_t>, std::vector<char *>> g_small;   // (device, class) -> free blocks
-std::multimap<std::pair<int, size_t>, char *> g_large;   // (device, bytes) -> free chunks
+// free runs of large-block chunks: best-fit index and address index (for coalescing)
+std::multimap<std::pair<int, size_t>, char *> g_large;    // (device, bytes) -> run start
+std::map<uintptr_t, std::pair<size_t, Chunk *>> g_runs;   // run start -> (bytes, chunk)
 std::map<uintptr_t, Chunk *> g_by_base;                   // chunk base -> chunk
+size_t g_live_bytes = 0;
 
 size_t small_class(size_t bytes) {
     size_t c = kMinBlock;
@@ -64,26 +73,53 @@ size_t small_class(size_t bytes) {
     return c;
 }
 
-int new_chunk(size_t bytes, int dev, Chunk **out) {
-    char *p = nullptr;
-    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), bytes);
-    if (e == hipErrorOutOfMemory) {
-        (void)hipGetLastError();
-        // give never-exported free chunks back and retry once
-        for (auto it = g_large.begin(); it != g_large.end();) {
-            auto c = g_by_base.find(reinterpret_cast<uintptr_t>(it->second));
-            if (c != g_by_base.end() && !c->second->exported && c->second->device == dev) {
-                (void)hipFree(c->second->base);
-                g_chunks.erase(std::remove(g_chunks.begin(), g_chunks.end(), c->second), g_chunks.end());
-                delete c->second;
-                g_by_base.erase(c);
-                it = g_large.erase(it);
-            } else {
-                ++it;
-            }
-        }
-        e = hipMalloc(reinterpret_cast<void **>(&p), bytes);
+void run_insert(char *p, size_t bytes, Chunk *c) {
+    g_runs[reinterpret_cast<uintptr_t>(p)] = {bytes, c};
+    g_large.insert({{c->device, bytes}, p});
+}
+
+void run_erase(uintptr_t p) {
+    auto it = g_runs.find(p);
+    if (it == g_runs.end()) return;
+    const auto key = std::make_pair(it->second.second->device, it->second.first);
+    for (auto r = g_large.equal_range(key); r.first != r.second; ++r.first)
+        if (reinterpret_cast<uintptr_t>(r.first->second) == p) { g_large.erase(r.first); break; }
+    g_runs.erase(it);
+}
+
+// every free entry of chunk c is dropped and its memory goes back to the driver
+void release_chunk(Chunk *c) {
+    for (auto &fl : g_small) {
+        auto &v = fl.second;
+        v.erase(std::remove_if(v.begin(), v.end(), [&](char *p) { return p >= c->base && p < c->base + c->bytes; }),
+                v.end());
     }
+    for (auto it = g_runs.lower_bound(reinterpret_cast<uintptr_t>(c->base));
+         it != g_runs.end() && it->first < reinterpret_cast<uintptr_t>(c->base) + c->bytes;) {
+        const uintptr_t p = it->first;
+        ++it;
+        run_erase(p);
+    }
+    g_by_base.erase(reinterpret_cast<uintptr_t>(c->base));
+    g_chunks.erase(std::remove(g_chunks.begin(), g_chunks.end(), c), g_chunks.end());
+    (void)hipFree(c->base);
+    delete c;
+}
+
+// chunks never exported and holding no live block (dev < 0: every device)
+void release_idle(int dev) {
+    std::vector<Chunk *> idle;
+    for (Chunk *c : g_chunks)
+        if (!c->exported && !c->live && (dev < 0 || c->device == dev)) idle.push_back(c);
+    for (Chunk *c : idle) release_chunk(c);
+}
+
+int new_chunk(size_t bytes, int dev, Chunk **out) {
+    // nothing free fits: idle chunks no peer ever mapped go back to the driver first, so
+    // never-exported memory stays at its peak of live bytes
+    release_idle(dev);
+    char *p = nullptr;
+    const hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), bytes);
     if (e != hipSuccess) return hip_fail(e, "hipMalloc (bucket arena)", __FILE__, __LINE__);
     auto *c = new Chunk();
     c->base = p;
@@ -119,25 +155,28 @@ int arena_alloc(size_t bytes, void **out) {
         Chunk *c = base->second;
         ++c->live;
         g_live[reinterpret_cast<uintptr_t>(p)] = {c, cls};
+        g_live_bytes += cls;
         *out = p;
         return ESGD_SUCCESS;
     }
     const size_t need = (bytes + kSlab - 1) / kSlab * kSlab;
-    auto it = g_large.lower_bound({dev, need});
-    if (it != g_large.end() && it->first.first == dev && it->first.second <= need + need / 4) {
-        char *p = it->second;
-        g_large.erase(it);
-        Chunk *c = g_by_base[reinterpret_cast<uintptr_t>(p)];
-        ++c->live;
-        g_live[reinterpret_cast<uintptr_t>(p)] = {c, c->bytes};
-        *out = p;
-        return ESGD_SUCCESS;
-    }
+    char *p = nullptr;
     Chunk *c = nullptr;
-    if (int rc = new_chunk(need, dev, &c)) return rc;
+    auto it = g_large.lower_bound({dev, need});
+    if (it != g_large.end() && it->first.first == dev) {   // best fit: the smallest run that holds it
+        p = it->second;
+        const size_t have = it->first.second;
+        c = g_runs[reinterpret_cast<uintptr_t>(p)].second;
+        run_erase(reinterpret_cast<uintptr_t>(p));
+        if (have > need) run_insert(p + need, have - need, c);
+    } else {
+        if (int rc = new_chunk(need, dev, &c)) return rc;
+        p = c->base;
+    }
     ++c->live;
-    g_live[reinterpret_cast<uintptr_t>(c->base)] = {c, need};
-    *out = c->base;
+    g_live[reinterpret_cast<uintptr_t>(p)] = {c, need};
+    g_live_bytes += need;
+    *out = p;
     return ESGD_SUCCESS;
 }
 
@@ -148,10 +187,50 @@ bool arena_free(void *p) {
     if (it == g_live.end()) return false;
     Block b = it->second;
     g_live.erase(it);
+    g_live_bytes -= b.cls;
     --b.chunk->live;
-    if (b.cls <= kSlab / 2) g_small[{b.chunk->device, b.cls}].push_back(static_cast<char *>(p));
-    else g_large.insert({{b.chunk->device, b.chunk->bytes}, static_cast<char *>(p)});
+    if (b.cls <= kSlab / 2) {
+        g_small[{b.chunk->device, b.cls}].push_back(static_cast<char *>(p));
+        return true;
+    }
+    // coalesce with the free runs right after and right before it in the same chunk
+    uintptr_t start = reinterpret_cast<uintptr_t>(p);
+    size_t bytes = b.cls;
+    auto nx = g_runs.find(start + bytes);
+    if (nx != g_runs.end() && nx->second.second == b.chunk) {
+        bytes += nx->second.first;
+        run_erase(nx->first);
+    }
+    auto pv = g_runs.lower_bound(start);
+    if (pv != g_runs.begin()) {
+        --pv;
+        if (pv->second.second == b.chunk && pv->first + pv->second.first == start) {
+            start = pv->first;
+            bytes += pv->second.first;
+            run_erase(start);
+        }
+    }
+    run_insert(reinterpret_cast<char *>(start), bytes, b.chunk);
     return true;
+}
+
+// device of the arena block starting at p, -1 if p is not one
+int arena_device(const void *p) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_live.find(reinterpret_cast<uintptr_t>(p));
+    return it == g_live.end() ? -1 : it->second.chunk->device;
+}
+
+void arena_stats(uint64_t *reserved, uint64_t *live, uint64_t *exported) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    uint64_t r = 0, x = 0;
+    for (Chunk *c : g_chunks) {
+        r += c->bytes;
+        if (c->exported) x += c->bytes;
+    }
+    if (reserved) *reserved = r;
+    if (live) *live = g_live_bytes;
+    if (exported) *exported = x;
 }
 
 // The arena chunk holding [p, p + bytes) of a live block: its base, the offset of p and
@@ -192,23 +271,7 @@ int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_
 // (and freeing exported memory is what this arena exists to avoid).
 void arena_trim() {
     std::lock_guard<std::mutex> lk(g_mu);
-    for (auto it = g_chunks.begin(); it != g_chunks.end();) {
-        Chunk *c = *it;
-        if (c->exported || c->live) { ++it; continue; }
-        for (auto fl = g_small.begin(); fl != g_small.end(); ++fl) {
-            auto &v = fl->second;
-            v.erase(std::remove_if(v.begin(), v.end(), [&](char *p) { return p >= c->base && p < c->base + c->bytes; }),
-                    v.end());
-        }
-        for (auto fl = g_large.begin(); fl != g_large.end();) {
-            if (fl->second == c->base) fl = g_large.erase(fl);
-            else ++fl;
-        }
-        g_by_base.erase(reinterpret_cast<uintptr_t>(c->base));
-        (void)hipFree(c->base);
-        delete c;
-        it = g_chunks.erase(it);
-    }
+    release_idle(-1);
 }
 
 }  // namespace esgd

@@ -81,6 +81,10 @@ int esgd_set_transport(const char *name) {
     return ESGD_SUCCESS;
 }
 
+int esgd_set_config(const char *key, int64_t value) { return config_set(key, value); }
+
+int esgd_get_config(const char *key, int64_t *value) { return config_get(key, value); }
+
 int esgd_comm_issue_log(uint32_t *sched, uint32_t *round, uint32_t cap, uint32_t *n) {
     return engine_issue_log(sched, round, cap, n);
 }

@@ -77,6 +77,55 @@ static uint64_t small_round_bytes() {
     return v;
 }
 
+// Where the rank-pairing flags live (dataplane.cpp, "device pairing flags"): 0 host
+// memory (default), 1 uncached HBM, 2 fine-grained HBM; ESGD_DEVICE_FLAGS overrides.
+static int device_flags_env() {
+    static const int m = getenv("ESGD_DEVICE_FLAGS") ? atoi(getenv("ESGD_DEVICE_FLAGS")) : 0;
+    return m;
+}
+
+// esgd_set_config: what schedules created afterwards capture (-1 = the env default).
+// All ranks must set the same values before the same creations (the creation signature
+// checks it), so a benchmark can A/B them inside one job.
+static std::atomic<int64_t> g_cfg_small{-1}, g_cfg_flags{-1};
+
+uint64_t config_small_round_bytes() {
+    const int64_t v = g_cfg_small.load();
+    return v >= 0 ? uint64_t(v) : small_round_bytes();
+}
+
+int config_device_flags() {
+    const int64_t v = g_cfg_flags.load();
+    const int m = v >= 0 ? int(v) : device_flags_env();
+    return (m >= 0 && m <= 2) ? m : 0;
+}
+
+int config_set(const char *key, int64_t value) {
+    ESGD_ARG(key, "esgd_set_config: null key");
+    if (!std::strcmp(key, "small_round_bytes")) {
+        ESGD_ARG(value >= -1, "small_round_bytes: >= 0 (or -1: the default)");
+        g_cfg_small.store(value);
+    } else if (!std::strcmp(key, "device_flags")) {
+        ESGD_ARG(value >= -1 && value <= 2, "device_flags: 0 host, 1 uncached HBM, 2 fine-grained HBM (-1: the default)");
+        g_cfg_flags.store(value);
+    } else {
+        set_error("esgd_set_config: unknown key '%s' (small_round_bytes, device_flags)", key);
+        return ESGD_INVALID_ARG;
+    }
+    return ESGD_SUCCESS;
+}
+
+int config_get(const char *key, int64_t *value) {
+    ESGD_ARG(key && value, "esgd_get_config: null argument");
+    if (!std::strcmp(key, "small_round_bytes")) *value = int64_t(config_small_round_bytes());
+    else if (!std::strcmp(key, "device_flags")) *value = config_device_flags();
+    else {
+        set_error("esgd_get_config: unknown key '%s' (small_round_bytes, device_flags)", key);
+        return ESGD_INVALID_ARG;
+    }
+    return ESGD_SUCCESS;
+}
+
 // ---- IPC mapping cache: one hipIpcOpenMemHandle per (peer, arena chunk) ----
 // Every exported bucket lives in an arena chunk that is never freed while the process
 // runs (arena.cpp), so handle bytes never repeat and a mapping, once open, stays valid:
@@ -113,11 +162,22 @@ static int ipc_open(int peer, const uint8_t *h, void **base) {
     return ESGD_SUCCESS;
 }
 
-// every mapping, at data-plane shutdown (after the last round has drained)
+// every mapping, at data-plane shutdown (after the last round has drained).  Once a
+// mapping has been closed, this process must not start another multi-process job: its
+// peers' arena chunks keep their handles, and re-opening handle bytes that were opened
+// and closed before is the illegal-access trigger of DESIGN.md §5 (engine_init refuses).
+static bool g_mappings_closed = false;
+
 static void ipc_close_all() {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
     for (auto &kv : g_ipc) (void)hipIpcCloseMemHandle(kv.second);
+    if (!g_ipc.empty()) g_mappings_closed = true;
     g_ipc.clear();
+}
+
+bool dataplane_mappings_closed() {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    return g_mappings_closed;
 }
 
 // ---- process-wide data-plane resources -----------------------------------------------
@@ -197,75 +257,75 @@ static void *host_view(void *host) {
 int round_sync(const PairFlags &f, int world, uint32_t value, long long timeout_ticks,
                uint32_t *err, uint32_t errval, uint64_t *ts, uint32_t *gate, uint32_t *fin, hipStream_t s);
 
-// ---- device pairing flags (ESGD_DEVICE_FLAGS=1, opt-in) ----
-// Each rank owns a page of uncached HBM (hipDeviceMallocUncached: loads and stores go to
-// memory, no cache holds a flag) with one word per (schedule, pairing, peer); a rank
-// publishes a round by storing it in its word of EVERY rank's page (peers' pages are
-// IPC-mapped, stores cross xGMI) and polls its own page -- no PCIe round trip to host
-// memory.  Opt-in: cross-GPU visibility of these stores has only been exercised with the
-// ranks sharing one GPU.  The page, like every exported buffer, is never
-// freed while the process runs; it is zeroed for every new job.
-static int device_flags_mode() {   // 0 host flags, 1 uncached HBM, 2 fine-grained HBM
-    static const int m = getenv("ESGD_DEVICE_FLAGS") ? atoi(getenv("ESGD_DEVICE_FLAGS")) : 0;
-    return m;
-}
-static bool device_flags() { return device_flags_mode() > 0; }
+// ---- device pairing flags (schedules with flag_mode 1 or 2, opt-in) ----
+// Each rank owns a page of HBM per mode -- uncached (hipDeviceMallocUncached: loads and
+// stores go to memory, no cache holds a flag) or fine-grained -- with one word per
+// (schedule, pairing, peer); a rank publishes a round by storing it in its word of EVERY
+// rank's page (peers' pages are IPC-mapped, stores cross xGMI) and polls its own page --
+// no PCIe round trip to host memory.  Opt-in: cross-GPU visibility of these stores has
+// only been exercised with the ranks sharing one GPU.  A page, like every
+// exported buffer, is never freed while the process runs; it is zeroed for every new job.
 constexpr size_t kPageWords = size_t(kMaxSched) * 3 * kMaxRanks;
-static uint32_t *g_page = nullptr;                 // this rank's page
-static Segment *g_page_seg = nullptr;              // the job it was published for
-static uint32_t *g_peer_page[kMaxRanks] = {};      // every rank's page (own included)
-static bool g_pages_mapped = false;
+struct FlagPages {
+    uint32_t *page = nullptr;                 // this rank's page
+    Segment *seg = nullptr;                   // the job it was published for
+    uint32_t *peer[kMaxRanks] = {};           // every rank's page (own included)
+    bool mapped = false;
+};
+static FlagPages g_pages[3];                  // [mode]; [0] unused (host flags)
 
-static int flags_publish(int rank) {
+static int flags_publish(int rank, int mode) {
     std::lock_guard<std::mutex> lk(g_dp_mu);
+    FlagPages &fp = g_pages[mode];
     Segment *seg = engine_segment();
-    if (g_page_seg == seg) return ESGD_SUCCESS;
-    if (!g_page)
-        ESGD_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&g_page), kPageWords * sizeof(uint32_t),
-                                       device_flags_mode() == 2 ? hipDeviceMallocFinegrained
-                                                                : hipDeviceMallocUncached));
+    if (fp.seg == seg) return ESGD_SUCCESS;
+    if (!fp.page)
+        ESGD_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&fp.page), kPageWords * sizeof(uint32_t),
+                                       mode == 2 ? hipDeviceMallocFinegrained : hipDeviceMallocUncached));
     // the null stream: rounds run on non-blocking streams, nothing in flight is waited for
-    ESGD_HIP(hipMemsetAsync(g_page, 0, kPageWords * sizeof(uint32_t), nullptr));
+    ESGD_HIP(hipMemsetAsync(fp.page, 0, kPageWords * sizeof(uint32_t), nullptr));
     ESGD_HIP(hipStreamSynchronize(nullptr));
     hipIpcMemHandle_t h;
-    ESGD_HIP(hipIpcGetMemHandle(&h, g_page));
-    IpcSlot &mine = seg->flagpage[rank];
+    ESGD_HIP(hipIpcGetMemHandle(&h, fp.page));
+    IpcSlot &mine = seg->flagpage[mode - 1][rank];
     std::memcpy(mine.handle, &h, 64);
     mine.offset = 0;
     mine.bytes = kPageWords * sizeof(uint32_t);
     mine.gen.store(1, std::memory_order_release);
-    g_page_seg = seg;
-    g_pages_mapped = false;
+    fp.seg = seg;
+    fp.mapped = false;
     return ESGD_SUCCESS;
 }
 
 // after the creation vote: every peer has published its page
-static int flags_connect(int rank, int world) {
+static int flags_connect(int rank, int world, int mode) {
     std::lock_guard<std::mutex> lk(g_dp_mu);
-    if (g_pages_mapped) return ESGD_SUCCESS;
+    FlagPages &fp = g_pages[mode];
+    if (fp.mapped) return ESGD_SUCCESS;
     Segment *seg = engine_segment();
     for (int q = 0; q < world; ++q) {
-        if (q == rank) { g_peer_page[q] = g_page; continue; }
-        if (seg->flagpage[q].gen.load(std::memory_order_acquire) != 1) {
-            set_error("device flags: rank %d did not publish its flag page (ESGD_DEVICE_FLAGS must be "
-                      "set on every rank)", q);
+        if (q == rank) { fp.peer[q] = fp.page; continue; }
+        if (seg->flagpage[mode - 1][q].gen.load(std::memory_order_acquire) != 1) {
+            set_error("device flags: rank %d did not publish its mode-%d flag page (every rank must create "
+                      "the schedule with the same device_flags setting)", q, mode);
             return ESGD_ERROR;
         }
         void *p = nullptr;
-        if (int rc = ipc_open(q, seg->flagpage[q].handle, &p)) return rc;
-        g_peer_page[q] = static_cast<uint32_t *>(p);
+        if (int rc = ipc_open(q, seg->flagpage[mode - 1][q].handle, &p)) return rc;
+        fp.peer[q] = static_cast<uint32_t *>(p);
     }
-    g_pages_mapped = true;
+    fp.mapped = true;
     return ESGD_SUCCESS;
 }
 
 // the flags of pairing `which` (0 ready, 1 reduced, 2 done) of schedule s
 static PairFlags pair_flags(Sched &s, std::atomic<uint32_t> *host, int which) {
     PairFlags f{};
-    if (device_flags()) {
+    if (s.flag_mode > 0) {
+        const FlagPages &fp = g_pages[s.flag_mode];
         const size_t base = (size_t(s.id) * 3 + size_t(which)) * kMaxRanks;
-        f.mine = g_page + base;
-        for (int q = 0; q < s.world; ++q) f.dst[q] = g_peer_page[q] + base + s.rank;
+        f.mine = fp.page + base;
+        for (int q = 0; q < s.world; ++q) f.dst[q] = fp.peer[q] + base + s.rank;
         f.ndst = s.world;
     } else {
         f.mine = dev_flag(host);
@@ -346,9 +406,11 @@ void dataplane_shutdown() {
         if (*c) { (void)hipStreamSynchronize(*c); (void)hipStreamDestroy(*c); *c = nullptr; }
     if (g_ctr_pool) { (void)hipFree(g_ctr_pool); g_ctr_pool = nullptr; }
     ipc_close_all();
-    for (auto &p : g_peer_page) p = nullptr;   // g_page itself stays (exported memory)
-    g_pages_mapped = false;
-    g_page_seg = nullptr;
+    for (FlagPages &fp : g_pages) {   // the pages themselves stay (exported memory)
+        for (auto &p : fp.peer) p = nullptr;
+        fp.mapped = false;
+        fp.seg = nullptr;
+    }
     arena_trim();
     if (g_seg_reg) { (void)hipHostUnregister(g_seg_reg); g_seg_reg = nullptr; g_seg_dev = nullptr; }
 }
@@ -672,7 +734,7 @@ static int base_complete(Sched &s, BaseState &st) {
 }
 
 static std::string base_diagnose(Sched &s) {
-    if (device_flags()) return "(pairing flags in device memory, ESGD_DEVICE_FLAGS=1)";
+    if (s.flag_mode > 0) return "(pairing flags in device memory, device_flags mode " + std::to_string(s.flag_mode) + ")";
     std::string m = "(flags ready/reduced/done per rank:";
     char buf[64];
     for (int q = 0; q < s.world; ++q) {
@@ -780,7 +842,7 @@ struct IpcTransport final : Transport {
 
     // rounds of this size run as one k_round_small launch
     static bool one_launch(const Sched &s) {
-        return s.world > 1 && s.world <= ESGD_MAX_FANIN && !s.wire_bf16 && s.count * s.esize <= small_round_bytes();
+        return s.world > 1 && s.world <= ESGD_MAX_FANIN && !s.wire_bf16 && s.count * s.esize <= s.small_bytes;
     }
 
     // the published shard (one-launch rounds only): grown and re-published when the
@@ -849,8 +911,8 @@ struct IpcTransport final : Transport {
             return ESGD_INVALID_ARG;
         }
         if (int rc = register_segment()) return rc;
-        if (device_flags())
-            if (int rc = flags_publish(s.rank)) return rc;
+        if (s.flag_mode > 0)
+            if (int rc = flags_publish(s.rank, s.flag_mode)) return rc;
         // publish this rank's rb (peers map it in connect())
         // ESGD_SHADOW=1 shadows every device bucket (caller buckets that are freed and
         // re-allocated between rounds; also how the tests reach the fallback)
@@ -873,8 +935,8 @@ struct IpcTransport final : Transport {
 
     int connect(Sched &s) override {
         if (s.world == 1) return ESGD_SUCCESS;
-        if (device_flags())
-            if (int rc = flags_connect(s.rank, s.world)) return rc;
+        if (s.flag_mode > 0)
+            if (int rc = flags_connect(s.rank, s.world, s.flag_mode)) return rc;
         return map_peers(s, S(s));
     }
 

@@ -109,6 +109,12 @@ int engine_init(const char *job, int rank, int world, bool start_progress) {
         set_error("esgd: already initialised as rank %d/%d", g_rank, g_world);
         return ESGD_INVALID_ARG;
     }
+    if (world > 1 && dataplane_mappings_closed()) {
+        set_error("esgd: this process already finalized a job whose peers' buckets it mapped over IPC; "
+                  "re-opening closed IPC handles is unsafe on this driver (DESIGN.md §5): run each "
+                  "multi-process job in a fresh process");
+        return ESGD_ERROR;
+    }
     if (const char *t = getenv("ESGD_TIMEOUT_S")) g_timeout = atof(t) > 0 ? atof(t) : g_timeout;
     Segment *seg = shm_attach(job, rank, world, g_timeout);
     if (!seg) return ESGD_ERROR;
@@ -209,6 +215,8 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     s->zero_sb = (flags & ESGD_SCHED_ZERO_SB) != 0 && !host_mode && !s->in_place;
     s->wire_bf16 = (flags & ESGD_SCHED_WIRE_BF16) != 0;
     s->fresh_only = (flags & ESGD_SCHED_FRESH_ONLY) != 0;
+    s->small_bytes = config_small_round_bytes();
+    s->flag_mode = config_device_flags();
     // Schedule ids are never reused within a job and the segment starts zeroed, so the
     // shared state of this id needs no reset (no barrier before setup).  Creation is two
     // voted steps: setup (local: buckets, streams, publication) -> barrier -> every rank
@@ -216,7 +224,9 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     // failures -> connect (mapping peers) -> barrier -> failures.  A failure anywhere
     // fails the creation everywhere; no rank is left waiting on a peer that gave up.
     s->gen = 1;   // IpcSlot::gen == 1: published for this id
-    const uint64_t sig = (uint64_t(s->wire_bf16) << 48) | (uint64_t(uint32_t(kind)) << 40) |
+    const bool small = count * s->esize <= s->small_bytes;
+    const uint64_t sig = (uint64_t(small) << 52) | (uint64_t(s->flag_mode & 3) << 50) |
+                         (uint64_t(s->wire_bf16) << 48) | (uint64_t(uint32_t(kind)) << 40) |
                          (uint64_t(uint32_t(dtype) & 0xff) << 32) |
                          (tag == kNoTag ? 0 : (0x10000u | uint16_t(tag)));
     int rc = ESGD_SUCCESS;
@@ -240,10 +250,11 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     for (int q = 0; !rc && q < g_world; ++q) {
         const uint64_t o = s->sh->sig[q].load(std::memory_order_acquire);
         if (o != sig) {
-            set_error("schedule create: rank %d created (kind %d, dtype %d, tag %d), rank %d (kind %d, "
-                      "dtype %d, tag %d): creation order must match", g_rank, kind, dtype,
-                      tag == kNoTag ? -1 : tag, q, int((o >> 40) & 0xff), int((o >> 32) & 0xff),
-                      (o & 0x10000) ? int(int16_t(o & 0xffff)) : -1);
+            set_error("schedule create: rank %d created (kind %d, dtype %d, tag %d, flags mode %d, one-launch %d), "
+                      "rank %d (kind %d, dtype %d, tag %d, flags mode %d, one-launch %d): creation order and "
+                      "data-plane settings must match", g_rank, kind, dtype, tag == kNoTag ? -1 : tag,
+                      s->flag_mode, int(small), q, int((o >> 40) & 0xff), int((o >> 32) & 0xff),
+                      (o & 0x10000) ? int(int16_t(o & 0xffff)) : -1, int((o >> 50) & 3), int((o >> 52) & 1));
             rc = ESGD_INVALID_ARG;   // every rank sees the same signatures: all fail
         }
     }
@@ -377,7 +388,10 @@ int sched_wait_ex(Sched *s, int *fresh) {
     s->waited = target;
     s->mark(target, 5);
     if (s->hold_mode) s->held = true;
-    if (fresh) *fresh = s->fresh_of[target % 256];
+    // the fresh bit of the round returned (joined rounds are queued in order)
+    const int f = s->fresh_q.empty() ? 0 : s->fresh_q.front();
+    if (!s->fresh_q.empty()) s->fresh_q.pop_front();
+    if (fresh) *fresh = f;
     return ESGD_SUCCESS;
 }
 
@@ -405,6 +419,7 @@ int sched_test(Sched *s, int *flag) {
     *flag = s->completed >= s->waited + 1;
     if (*flag) {
         ++s->waited;
+        if (!s->fresh_q.empty()) s->fresh_q.pop_front();
         if (s->hold_mode) s->held = true;
     }
     return ESGD_SUCCESS;
@@ -481,7 +496,7 @@ static bool step(Sched &s) {
         s.cur = next;
         s.cur_fresh = posted >= next;
         s.joined = next;
-        s.fresh_of[next % 256] = uint8_t(s.cur_fresh);
+        s.fresh_q.push_back(uint8_t(s.cur_fresh));
         // FFCOLL_BUFFERS: a round joined on a peer's activation re-resolves the buffers
         // here (a fresh round did at its post)
         if (s.resolve && !s.cur_fresh && !check(s.resolve(s), "join")) return true;

@@ -24,6 +24,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -143,7 +144,14 @@ struct Sched {
     // ESGD_SCHED_FRESH_ONLY: a round joined before this rank posted it contributes zeros
     // (the snapshot zeroes the bucket instead of reading sb)
     bool fresh_only = false;
-    uint8_t fresh_of[256] = {};   // round % 256 -> this rank had posted it before joining
+    // data-plane settings captured at creation (esgd_set_config / env defaults; part of
+    // the creation signature, so every rank runs the schedule the same way)
+    uint64_t small_bytes = 0;   // buckets up to this many bytes: one-launch rounds
+    int flag_mode = 0;          // pairing flags: 0 host memory, 1 uncached HBM, 2 fine-grained HBM
+    // whether this rank had posted each joined round before joining it, for every round
+    // not yet returned by wait()/test(), oldest first: without HOLD, peers' activations
+    // can carry the progress thread any number of rounds past the caller's last wait
+    std::deque<uint8_t> fresh_q;
 };
 
 // Round kind / activator rules (pure functions of the schedule parameters).
@@ -192,5 +200,12 @@ bool engine_progress_once();
 // Data-plane resources shared by all schedules of the process (dataplane.cpp): freed at
 // finalize, before the node segment is unmapped.
 void dataplane_shutdown();
+// a finalized job of this process had mapped peers' buckets (no new job with peers then)
+bool dataplane_mappings_closed();
+// settings new schedules capture (esgd_set_config; ESGD_SMALL_ROUND_BYTES / ESGD_DEVICE_FLAGS)
+uint64_t config_small_round_bytes();
+int config_device_flags();
+int config_set(const char *key, int64_t value);
+int config_get(const char *key, int64_t *value);
 
 }  // namespace esgd

@@ -42,6 +42,8 @@ struct PairFlags {
 
 int arena_alloc(size_t bytes, void **out);
 bool arena_free(void *p);
+int arena_device(const void *p);   // device of an arena block, -1 if p is not one
+void arena_stats(uint64_t *reserved, uint64_t *live, uint64_t *exported);
 int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_t handle[64]);
 void arena_trim();
 

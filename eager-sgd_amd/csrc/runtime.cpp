@@ -108,10 +108,28 @@ int esgd_malloc(void **ptr, size_t bytes) {
     return arena_alloc(bytes ? bytes : 256, ptr);
 }
 
+// hipFree's contract is kept: the block is reused only after the work queued on its
+// device so far has finished (a kernel still reading or writing it on any stream), so
+// the device is synchronised before the block goes back to the free list.
 int esgd_free(void *ptr) {
     if (!ptr) return ESGD_SUCCESS;
-    if (arena_free(ptr)) return ESGD_SUCCESS;
-    ESGD_HIP(hipFree(ptr));
+    const int dev = arena_device(ptr);
+    if (dev < 0) {
+        ESGD_HIP(hipFree(ptr));
+        return ESGD_SUCCESS;
+    }
+    int cur = -1;
+    ESGD_HIP(hipGetDevice(&cur));
+    if (cur != dev) ESGD_HIP(hipSetDevice(dev));
+    const hipError_t e = hipDeviceSynchronize();
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize (esgd_free)", __FILE__, __LINE__);
+    arena_free(ptr);
+    return ESGD_SUCCESS;
+}
+
+int esgd_memory_stats(uint64_t *reserved, uint64_t *in_use, uint64_t *exported) {
+    arena_stats(reserved, in_use, exported);
     return ESGD_SUCCESS;
 }
 

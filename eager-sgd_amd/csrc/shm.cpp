@@ -54,10 +54,28 @@ void seg_idle_wait(Segment *seg, uint32_t seen, unsigned usec) {
     seg->sleepers.fetch_sub(1, std::memory_order_acq_rel);
 }
 
-// A segment left behind by a crashed job with the same id: its creator is gone.
+static uint64_t mono_ns() {
+    return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                        std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+
+static uint64_t pid_namespace() {
+    struct stat st;
+    return stat("/proc/self/ns/pid", &st) == 0 ? uint64_t(st.st_ino) : 0;
+}
+
+// A segment left behind by a crashed job with the same id: its creator is gone.  In the
+// creator's PID namespace kill(pid, 0) says so; from another namespace the pid means
+// nothing, and the creator counts as alive while the init barrier's heartbeat is fresh
+// (stamped every millisecond by every waiting rank; a dead job's stops).
 static bool creator_alive(const Segment *seg) {
-    const int32_t pid = seg->pid[0].load();
-    return pid > 0 && (kill(pid, 0) == 0 || errno == EPERM);
+    const uint64_t ns = pid_namespace();
+    if (ns && seg->creator_pidns == ns) {
+        const int32_t pid = seg->pid[0].load();
+        return pid > 0 && (kill(pid, 0) == 0 || errno == EPERM);
+    }
+    const uint64_t beat = seg->beat_ns.load(std::memory_order_acquire);
+    return beat && mono_ns() - beat < uint64_t(2000000000);
 }
 
 static std::string shm_path(const char *job) {
@@ -94,6 +112,8 @@ Segment *shm_attach(const char *job, int rank, int world, double timeout_s) {
         seg->world = uint32_t(world);
         seg->bytes = uint32_t(bytes);
         seg->pid[0].store(int32_t(getpid()));
+        seg->creator_pidns = pid_namespace();
+        seg->beat_ns.store(mono_ns());
         std::atomic_thread_fence(std::memory_order_seq_cst);
         seg->magic = kShmMagic;
         if (rename(tmp.c_str(), path.c_str()) != 0) {
@@ -154,7 +174,13 @@ int shm_barrier(Segment *seg, int world, double timeout_s) {
     }
     const double t0 = now_s();
     unsigned polls = 0;
+    uint64_t beat = 0;
     while (seg->bar_gen.load(std::memory_order_acquire) == gen) {
+        const uint64_t t = mono_ns();
+        if (t - beat > 1000000) {   // the creator-liveness heartbeat (creator_alive)
+            seg->beat_ns.store(t, std::memory_order_release);
+            beat = t;
+        }
         if (seg->aborted.load(std::memory_order_relaxed)) {
             set_error("barrier: job aborted by a peer");
             return ESGD_ERROR;

@@ -76,11 +76,18 @@ struct Segment {
     std::atomic<uint32_t> sleepers;
     std::atomic<uint32_t> nccl_ready;
     uint8_t nccl_id[128];
+    // creator liveness for ranks attaching to a file of this name: rank 0's PID namespace
+    // (inode of /proc/self/ns/pid) and a heartbeat (CLOCK_MONOTONIC ns) that every rank
+    // waiting in the init barrier keeps fresh -- a creator in another PID namespace (one
+    // container per GPU sharing /dev/shm) cannot be probed with kill()
+    uint64_t creator_pidns;
+    std::atomic<uint64_t> beat_ns;
     std::atomic<int32_t> pid[kMaxRanks];
     std::atomic<int32_t> device[kMaxRanks];
     std::atomic<uint64_t> ticket_next;
-    // ESGD_DEVICE_FLAGS=1: rank r's pairing-flag page (uncached HBM, dataplane.cpp)
-    IpcSlot flagpage[kMaxRanks];
+    // device pairing flags: rank r's flag page of mode m + 1 (1 uncached, 2 fine-grained
+    // HBM; dataplane.cpp)
+    IpcSlot flagpage[2][kMaxRanks];
     TicketSlot ring[kRing];
     SchedShm sched[kMaxSched];
 };

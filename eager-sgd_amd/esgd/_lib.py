@@ -43,6 +43,7 @@ _SIGS = {
     "esgd_device_arch": (_i, [_i, C.c_char_p, _sz]),
     "esgd_malloc": (_i, [C.POINTER(_vp), _sz]),
     "esgd_free": (_i, [_vp]),
+    "esgd_memory_stats": (_i, [C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_u64)]),
     "esgd_host_alloc": (_i, [C.POINTER(_vp), _sz]),
     "esgd_host_free": (_i, [_vp]),
     "esgd_host_register": (_i, [_vp, _sz]),

@@ -55,6 +55,8 @@ def _bind(h):
         "esgd_schedule_stream": (i, [u64, C.POINTER(vp)]),
         "esgd_schedule_timeline": (i, [u64, C.POINTER(u64), u32, C.POINTER(u32)]),
         "esgd_set_transport": (i, [C.c_char_p]),
+        "esgd_set_config": (i, [C.c_char_p, C.c_int64]),
+        "esgd_get_config": (i, [C.c_char_p, C.POINTER(C.c_int64)]),
         "esgd_comm_issue_log": (i, [C.POINTER(u32), C.POINTER(u32), u32, C.POINTER(u32)]),
     }
     for name, (res, args) in sigs.items():
@@ -121,6 +123,20 @@ def world() -> int:
 def set_transport(name: str):
     """Data plane of schedules created afterwards: "ipc" (default) or "rccl"."""
     check(lib().esgd_set_transport(name.encode()), "esgd_set_transport")
+
+
+def set_config(key: str, value: int):
+    """Data-plane setting captured by schedules created afterwards (esgd_set_config):
+    "small_round_bytes" (one-launch rounds up to this size) or "device_flags" (0 host,
+    1 uncached HBM, 2 fine-grained HBM pairing flags); -1 restores the default.  Every
+    rank must set the same value before the same creations."""
+    check(lib().esgd_set_config(key.encode(), int(value)), "esgd_set_config")
+
+
+def get_config(key: str) -> int:
+    v = C.c_int64()
+    check(lib().esgd_get_config(key.encode(), C.byref(v)), "esgd_get_config")
+    return v.value
 
 
 def issue_log():

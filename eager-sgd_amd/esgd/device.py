@@ -186,3 +186,11 @@ def fill_uniform(buf: DeviceBuffer, seed: int, rank: int, stream=None):
     else:
         raise ValueError("fill_uniform: FLOAT or BF16 only")
     return check(rc, "esgd_fill_uniform")
+
+
+def memory_stats() -> dict:
+    """The bucket arena's footprint (esgd_memory_stats): bytes reserved from the driver,
+    in use, and reserved in IPC-exported chunks."""
+    r, u, x = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    check(lib().esgd_memory_stats(C.byref(r), C.byref(u), C.byref(x)), "esgd_memory_stats")
+    return {"reserved": r.value, "in_use": u.value, "exported": x.value}

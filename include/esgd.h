@@ -50,8 +50,15 @@ int esgd_device_count(int *n);
 int esgd_set_device(int dev);
 int esgd_get_device(int *dev);
 int esgd_device_arch(int dev, char *name, size_t len); /* e.g. "gfx950:sramecc+:xnack-" */
+/* Device buckets come from the library's IPC arena (exportable to the node's other
+ * processes, never handed back to the driver while a peer may map them).  esgd_free keeps
+ * hipFree's contract: the memory is reused only after the work already queued on its
+ * device has finished. */
 int esgd_malloc(void **ptr, size_t bytes);
 int esgd_free(void *ptr);
+/* arena footprint: bytes reserved from the driver, handed out and not freed, and
+ * reserved in chunks exported over IPC (those stay reserved until the process exits) */
+int esgd_memory_stats(uint64_t *reserved, uint64_t *in_use, uint64_t *exported);
 int esgd_host_alloc(void **ptr, size_t bytes);           /* pinned host memory */
 int esgd_host_free(void *ptr);
 int esgd_host_register(void *ptr, size_t bytes);         /* pin caller-owned memory */
@@ -137,6 +144,18 @@ int esgd_barrier(void);
  * HBM, two kernels per round) or "rccl" (grouped ncclSend/ncclRecv + the tree kernel on
  * a side stream; one GPU per rank).  Env ESGD_TRANSPORT sets the default. */
 int esgd_set_transport(const char *name);
+/* Data-plane settings that schedules created afterwards capture (every rank must use the
+ * same values for the same creation: they are part of the creation signature).
+ *   "small_round_bytes"  buckets up to this many bytes run each round as ONE kernel
+ *                        launch (k_round_small); larger ones as pairing + reduce-scatter +
+ *                        pairing + all-gather + pairing launches.  Default 4 MiB (env
+ *                        ESGD_SMALL_ROUND_BYTES); 0 = never.
+ *   "device_flags"       where the rank-pairing flags live: 0 pinned host memory (default,
+ *                        env ESGD_DEVICE_FLAGS), 1 uncached HBM pages, 2 fine-grained HBM
+ *                        pages (peers' pages written over xGMI).
+ * value -1 restores the default.  Unknown keys / values -> ESGD_INVALID_ARG. */
+int esgd_set_config(const char *key, int64_t value);
+int esgd_get_config(const char *key, int64_t *value);
 /* ordered transports (rccl): (schedule id, round) pairs in the order this rank issued
  * them — identical on every rank by construction (tests). */
 int esgd_comm_issue_log(uint32_t *sched, uint32_t *round, uint32_t cap, uint32_t *n);

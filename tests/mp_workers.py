@@ -78,11 +78,28 @@ def local_device(rank=None):
 
 
 def _comm():
+    """Join the esgd communicator on device rank % device_count.  Where the box has a GPU
+    per rank, the ranks MUST be on distinct devices (the multi-rank tests then cover the
+    cross-GPU data plane: xGMI peer loads, two L2s); a silent fall-back to a shared
+    device would pass as cross-GPU coverage, so it fails here instead."""
+    import ctypes as C
+
     import esgd
     from esgd import comm
-    if esgd.device_count() > 0:
+    n = esgd.device_count()
+    if n > 0:
         esgd.check(esgd.lib().esgd_set_device(local_device()), "esgd_set_device")
     comm.init()
+    world = comm.world()
+    if n > 0 and world > 1:
+        import torch.distributed as dist
+        d = C.c_int()
+        esgd.check(esgd.lib().esgd_get_device(C.byref(d)), "esgd_get_device")
+        devs = [None] * world
+        dist.all_gather_object(devs, d.value)
+        if n >= world:
+            assert len(set(devs)) == world, f"{n} GPUs but ranks share devices: {devs}"
+        os.environ["ESGD_TEST_DEVICES"] = ",".join(map(str, devs))
     return comm
 
 
@@ -601,13 +618,14 @@ def gpu_config(rank, world, kind, counts, dtype_name="fp32", rounds=2, async_=32
     return out
 
 
-def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, delay=None):
+def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, delay=None, delay_frac=None):
     """eager-SGD's partial rounds with a straggler (the last rank), contributor-counted
     like evaluation/rsgd.c:87,100: every rank's gradient is 1.0, zeroed after use, so a
     round's result is the number of ranks whose fresh gradient it took.  On-time ranks
     write theirs before the round's barrier; the straggler writes and posts `delay` after
-    it (default 4x the no-straggler round, at least 20 ms).  Returns this rank's
-    per-round (round, contributors, uniform result) and the round log."""
+    it (default 4x the no-straggler round T, at least 20 ms; delay_frac: that fraction of
+    T, e.g. BASELINE C4's 20 %).  Returns this rank's per-round (round, contributors,
+    uniform result) and the round log."""
     import statistics
 
     import numpy as np
@@ -653,7 +671,7 @@ def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, dela
     tt = torch.tensor([statistics.median(warm)], dtype=torch.float64)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     T = float(tt.item())
-    d = delay if delay is not None else max(4 * T, 0.02)
+    d = delay if delay is not None else (delay_frac * T if delay_frac is not None else max(4 * T, 0.02))
     res = []
     for t in range(4, 4 + rounds):
         _, c, u = one(d)
@@ -1089,3 +1107,65 @@ def gpu_stress_threads(rank, world, kind, counts=(65536, (1 << 20) + 3, 4096), r
         s.delete()
     comm.finalize()
     return {"res": res, "errs": errs, "bits": bits}
+
+
+def gpu_visibility(rank, world, rounds=6, count=(1 << 20) + 3, small_bytes=None, flag_mode=0):
+    """Writer-then-post, the hand-off fflib2 orders with a send after the comp and a comp
+    after the recv (colls/ffallreduce.c:145-162): right before posting round t, every rank
+    rewrites its bucket on a producer stream (no host sync in between) with round t's
+    values, and passes that stream to post().  Every element of every round's result must
+    be the oracle's tree of round t's buckets -- across GPUs that checks the producer
+    ordering, the peers' reads of freshly written HBM over xGMI (the writer's release and
+    the reader's acquire) and the pairing flags of the chosen kind (host memory, uncached
+    or fine-grained HBM)."""
+    import numpy as np
+
+    from esgd import device as dev
+    from oracle import ffref
+    comm = _comm()
+    if small_bytes is not None:
+        comm.set_config("small_round_bytes", small_bytes)
+    comm.set_config("device_flags", flag_mode)
+    rb = dev.DeviceBuffer(count)
+    s = comm.Schedule(comm.ALLREDUCE, None, rb, count, buf=comm.BUF_DEVICE)
+    prod = dev.Stream()
+    bad = []
+    for t in range(rounds):
+        seed = 0x715B + 97 * t
+        comm.barrier()
+        dev.fill_uniform(rb, seed, rank, stream=prod)   # queued, not waited for
+        s.post(prod)
+        s.wait()
+        got = rb.download()
+        want = ffref.tree_sum([ffref.fill_uniform(seed, r, count) for r in range(world)])
+        nbad = int(np.count_nonzero(got.view(np.uint32) != want.view(np.uint32)))
+        if nbad:
+            bad.append((t, nbad))
+        comm.barrier()
+    s.delete()
+    comm.finalize()
+    return {"bad": bad, "devices": os.environ.get("ESGD_TEST_DEVICES")}
+
+
+def gpu_reinit(rank, world, count=4099):
+    """A finalized job that mapped its peers' buckets must refuse a second multi-process
+    job in the same process (re-opening closed IPC handles: DESIGN.md §5)."""
+    import numpy as np
+
+    from esgd import device as dev
+    from esgd._lib import EsgdError
+    comm = _comm()
+    rb = dev.DeviceBuffer(count)
+    rb.upload(np.ones(count, np.float32))
+    s = comm.Schedule(comm.ALLREDUCE, None, rb, count, buf=comm.BUF_DEVICE)
+    s.post(); s.wait()
+    ok = bool(np.all(rb.download() == world))
+    s.delete()
+    comm.finalize()
+    err = None
+    try:
+        comm.init()
+        comm.finalize()
+    except EsgdError as e:
+        err = str(e)
+    return {"ok": ok, "err": err}

@@ -69,6 +69,25 @@ def test_argument_validation_without_device():
     assert lib.esgd_dtype_size(_lib.BF16) == 2 and lib.esgd_dtype_size(7) == 0
 
 
+def test_data_plane_config_keys():
+    # esgd_set_config: what schedules created afterwards capture; checked without a device
+    from esgd import _lib, comm  # noqa: F401
+    lib = _lib.lib()
+    assert lib.esgd_set_config(b"bogus", 1) == _lib.INVALID_ARG
+    assert lib.esgd_set_config(b"device_flags", 3) == _lib.INVALID_ARG
+    assert lib.esgd_set_config(b"small_round_bytes", -2) == _lib.INVALID_ARG
+    try:
+        comm.set_config("small_round_bytes", 16 << 20)
+        comm.set_config("device_flags", 2)
+        assert comm.get_config("small_round_bytes") == 16 << 20
+        assert comm.get_config("device_flags") == 2
+    finally:
+        comm.set_config("small_round_bytes", -1)
+        comm.set_config("device_flags", -1)
+    assert comm.get_config("small_round_bytes") == int(os.environ.get("ESGD_SMALL_ROUND_BYTES", 4 << 20))
+    assert comm.get_config("device_flags") == int(os.environ.get("ESGD_DEVICE_FLAGS", 0))
+
+
 def test_wire_flag_argument_checks():
     # ESGD_SCHED_WIRE_BF16 needs FLOAT buckets; unknown flags are refused (checked before
     # any communicator or device is touched)

@@ -219,6 +219,28 @@ def _check_straggler(outs, world, kind, async_=3, seed=6545343):
                 assert e["activator"] == acts[e["round"] - 1], e
 
 
+def test_majority_straggler_c4_20pct():
+    # BASELINE C4 as stated: 8 ranks, the 25 559 081-float ResNet-50 gradient, one rank
+    # 20 % of a round late.  A 0.2 T delay races the round (the straggler may or may not
+    # make it), so: rounds the straggler activates (rand_r draw, ffrand_allreduce.c:88)
+    # wait for it and take all P; every other round takes P - 1 or P, the same on every
+    # rank (rsgd.c:87,100 contributor counting)
+    world = 8
+    outs = run("gpu_straggler", world, kind=MAJORITY, count=25559081, rounds=8, delay_frac=0.2, timeout=420)
+    acts = ffref.activators(6545343, world, 64)
+    for r, o in enumerate(outs):
+        assert abs(o["delay_s"] - 0.2 * o["T_s"]) < 1e-9, o
+        for t, c, uniform in o["rounds"]:
+            assert uniform, (r, t)
+            if acts[t - 1] == world - 1:
+                assert c == world, (r, t, c)
+            else:
+                assert c in (world - 1, world), (r, t, c)
+            assert c == outs[0]["rounds"][t - 4][1], (r, t)   # same result on every rank
+        for e in o["log"]:
+            assert e["activator"] == acts[e["round"] - 1], e
+
+
 @pytest.mark.parametrize("world,count,rounds", [(4, 1 << 20, 12), (8, 25559081, 8)])
 @pytest.mark.timeout(900)
 def test_majority_straggler_excluded(world, count, rounds):
@@ -424,3 +446,33 @@ def test_stress_one_thread_per_schedule(kind):
             for q in range(world):
                 want = t % (1 << bits) if outs[q]["res"][i]["fresh"][t - 1] else 0
                 assert (v >> (bits * q)) & ((1 << bits) - 1) == want, (i, t, q)
+
+
+# ---- cross-GPU hand-offs (run only where every rank has a GPU of its own) -------------
+
+def _ngpu():
+    import esgd
+    return esgd.device_count()
+
+
+@pytest.mark.parametrize("flags", [0, 1, 2])
+@pytest.mark.parametrize("path", sorted(SMALL))
+def test_writer_then_post_visibility_across_gpus(path, flags):
+    # every rank rewrites its bucket on a producer stream right before posting; each
+    # round's every element must match the oracle (mp_workers.gpu_visibility)
+    n = _ngpu()
+    if n < 2:
+        pytest.skip("needs >= 2 GPUs (ranks on distinct devices)")
+    for world in sorted({2, min(n, 8)}):
+        count = 65536 + 3 if path == "one_launch" else (1 << 20) + 3
+        outs = run("gpu_visibility", world, count=count, small_bytes=SMALL[path], flag_mode=flags)
+        for o in outs:
+            assert not o["bad"], (world, o)
+            assert len(set(o["devices"].split(","))) == world, o
+
+
+def test_second_job_after_ipc_mappings_closed_is_refused():
+    outs = run("gpu_reinit", 2)
+    for o in outs:
+        assert o["ok"], o
+        assert o["err"] and "fresh process" in o["err"], o

@@ -288,3 +288,56 @@ def test_reduce_host_bf16_and_tiny():
         reduce_host(_lib.BF16, xs, out, n)
         synchronize()
         assert np.array_equal(out, ffref.tree_sum_bf16(xs)), n
+
+
+# ---- the bucket arena behind esgd_malloc / esgd_free ----------------------
+
+def test_free_while_kernel_in_flight_keeps_hipfree_semantics():
+    # esgd_free returns a block to the arena for reuse by the next esgd_malloc of its
+    # size; like hipFree it must first let the work queued on the device finish, or a
+    # reduction still writing the freed block clobbers its next owner's data
+    from esgd.device import Stream, memory_stats  # noqa: F401
+    n = (64 << 20) // 4
+    ins = [DeviceBuffer(n) for _ in range(8)]
+    for r, b in enumerate(ins):
+        fill_uniform(b, 0x5EED, r)
+    synchronize()
+    s1, s2 = Stream(), Stream()
+    victim = DeviceBuffer(n)
+    old = victim.ptr
+    for _ in range(20):   # ~2 ms of writes into `victim` on s1
+        reduce(_lib.FLOAT, [b.ptr for b in ins], victim, n, stream=s1)
+    victim.close()        # while they run
+    held = []             # other free runs of this size may be handed out first
+    fresh = DeviceBuffer(n)
+    while fresh.ptr != old and len(held) < 16:
+        held.append(fresh)
+        fresh = DeviceBuffer(n)
+    assert fresh.ptr == old, "the arena should hand the freed block out again"
+    fill_uniform(fresh, 0xABCDEF, 3, stream=s2)
+    s2.synchronize()
+    s1.synchronize()
+    bits_equal(fresh.download(), ffref.fill_uniform(0xABCDEF, 3, n))
+
+
+def test_arena_growth_bounded_over_a_size_sweep():
+    # large blocks are carved best-fit from free chunk space and coalesce when freed, so
+    # a sweep over many distinct bucket sizes reserves about its peak, not the sum
+    from esgd.device import memory_stats
+    MiB = 1 << 20
+    sizes = [3, 300, 17, 129, 64, 250, 5, 96, 200, 33, 280, 7, 150, 301, 2.5, 111]
+    st0 = memory_stats()
+    base = st0["reserved"]
+    for mib in sizes:
+        b = DeviceBuffer(int(mib * MiB) // 4)
+        b.close()
+    grew = memory_stats()["reserved"] - base
+    assert grew <= 304 * MiB, grew / MiB   # one 302 MiB chunk (2 MiB granules): idle ones were given back
+    # two live at once, then freed: the runs coalesce back into one reusable span
+    a, b = DeviceBuffer(150 * MiB // 4), DeviceBuffer(150 * MiB // 4)
+    a.close(); b.close()
+    c = DeviceBuffer(300 * MiB // 4)
+    c.close()
+    st = memory_stats()
+    assert st["reserved"] - base <= 304 * MiB, st
+    assert st["in_use"] == st0["in_use"], (st0, st)
