@@ -251,8 +251,8 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
         const uint64_t o = s->sh->sig[q].load(std::memory_order_acquire);
         if (o != sig) {
             set_error("schedule create: rank %d created (kind %d, dtype %d, tag %d, flags mode %d, one-launch %d), "
-                      "rank %d (kind %d, dtype %d, tag %d, flags mode %d, one-launch %d): creation order and "
-                      "data-plane settings must match", g_rank, kind, dtype, tag == kNoTag ? -1 : tag,
+                      "rank %d (kind %d, dtype %d, tag %d, flags mode %d, one-launch %d): creation order must "
+                      "match, and so must the data-plane settings", g_rank, kind, dtype, tag == kNoTag ? -1 : tag,
                       s->flag_mode, int(small), q, int((o >> 40) & 0xff), int((o >> 32) & 0xff),
                       (o & 0x10000) ? int(int16_t(o & 0xffff)) : -1, int((o >> 50) & 3), int((o >> 52) & 1));
             rc = ESGD_INVALID_ARG;   // every rank sees the same signatures: all fail
