@@ -5,8 +5,11 @@
 
 N = 1 (default): config C2 of BASELINE.json — one MI355X sums 8 staged 64 MiB fp32
 buckets into one output with the hand-written HIP tree kernel (esgd_reduce).
-N > 1 (launched by torch.distributed.run, one rank per GPU): solo-allreduce of one
-256 MiB fp32 bucket per rank (config C3) through the esgd data plane.
+N > 1 (one rank per GPU): solo-allreduce of one 256 MiB fp32 bucket per rank (config C3)
+through the esgd data plane.  Under torch.distributed.run (WORLD_SIZE set) each process
+is one rank; a bare `python bench.py --gpus N` starts its own N ranks the same way (a
+fresh `python -m torch.distributed.run` child, before this process touches HIP) and
+exits with their status -- rank 0 prints the line.
 
 value = bucket bytes reduced per second over the whole job = (#contributing buckets
 x bucket bytes) / wall time of the K timed steps (max over ranks), inputs resident in
@@ -53,7 +56,27 @@ def parse():
     ap.add_argument("--transport", choices=["ipc", "rccl"], default=None,
                     help="N>1 data plane (default: ESGD_TRANSPORT or ipc)")
     ap.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--no-trace", action="store_true",
+                    help="N=1: skip the rocprofv3 kernel-trace pass behind roofline.rocprof_kernel_us")
     return ap.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher: start N ranks as torch.distributed.run
+    would (the reference's launcher starts its ranks the same way,
+    test_scripts_imagenet/daint_eagersgd_imagenet.sh:2-5).  Called before anything in
+    this process touches HIP; the ranks inherit stdout, so rank 0's JSON line is the
+    output, and this process exits with the launcher's status."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (RCCL / peer buckets)
+    env["ESGD_BENCH_SELF_LAUNCHED"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
 
 
 def _cpu_model():
@@ -134,6 +157,76 @@ def pmc_traffic(args, mib):
     return 2 * out["FETCH_SIZE"] * 1024 + out["WRITE_SIZE"] * 1024
 
 
+TRACE_WARM, TRACE_C2, TRACE_GATE = 3, 40, 20   # calls of the kernel-trace child run
+TREE_KERNEL = "k_tree_sum_buf<esgd::F32, 8, 4, 2, 16, false"   # the production fp32 fan-in-8 kernel
+GATE_WINDOWS = 4                                # 256 MiB / kWindowBytes (reduce_core.h)
+
+
+def trace_child(dev, dt, ptrs, out, count, k, s):
+    """The kernel-trace child (rocprofv3 --kernel-trace runs it): C2 launches, then the
+    gate's 8 x 256 MiB calls, each group after its own warm-up, nothing else in between
+    but the fill kernels of the gate buckets (they separate the two groups in the trace)."""
+    for _ in range(TRACE_WARM + TRACE_C2):
+        dev.reduce(dt, ptrs, out, count, stream=s)
+    s.synchronize()
+    gcount = (256 * MiB) // 4
+    gb = [dev.DeviceBuffer(gcount, dt) for _ in range(k)]
+    for r, b in enumerate(gb):
+        dev.fill_uniform(b, SEED, r, stream=s)
+    go = dev.DeviceBuffer(gcount, dt)
+    for _ in range(TRACE_WARM + TRACE_GATE):
+        dev.reduce(dt, [b.ptr for b in gb], go, gcount, stream=s)
+    s.synchronize()
+
+
+def kernel_trace(args):
+    """The dominant kernel's dispatch durations on THIS box: a rocprofv3 --kernel-trace
+    child pass (the program right after `--`) over the same C2 launches and gate calls
+    the line is timed on.  Returns (C2 average dispatch us, gate average call us = the
+    sum of its 4 window dispatches, split summary for profiles/)."""
+    import csv
+    import shutil
+    import statistics
+    d = os.path.join(ROOT, "gpurun_out", "bench_kernel_trace")
+    shutil.rmtree(d, ignore_errors=True)
+    os.makedirs(d, exist_ok=True)
+    cmd = ["rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "kt", "--",
+           sys.executable, os.path.abspath(__file__), "--pmc-child", "trace",
+           "--buckets", str(args.buckets), "--bucket-mib", str(args.bucket_mib), "--dtype", args.dtype]
+    subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                   cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"))
+    rows = []
+    for dp, _, files in os.walk(d):
+        for fn in files:
+            if fn.endswith("kernel_trace.csv"):
+                with open(os.path.join(dp, fn)) as f:
+                    for row in csv.DictReader(f):
+                        rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), row["Kernel_Name"]))
+    rows.sort()
+    fills = [i for i, r in enumerate(rows) if "k_fill_uniform" in r[2]]
+    tree = [(i, r[1] - r[0]) for i, r in enumerate(rows) if TREE_KERNEL in r[2]]
+    if not fills or not tree:
+        return None
+    last_fill = fills[-1]
+    c2 = [dur / 1e3 for i, dur in tree if i < last_fill][TRACE_WARM:]
+    g = [dur for i, dur in tree if i > last_fill][TRACE_WARM * GATE_WINDOWS:]
+    gate = [sum(g[j:j + GATE_WINDOWS]) / 1e3 for j in range(0, len(g) - GATE_WINDOWS + 1, GATE_WINDOWS)]
+    c2_bytes = (args.buckets + 1) * int(args.bucket_mib * MiB)
+    gate_bytes = (args.buckets + 1) * 256 * MiB
+    summary = {"source": "rocprofv3 --kernel-trace of bench.py's trace child (%d C2 launches, %d gate calls "
+                         "of %d windows, after %d warm-up calls each)" % (len(c2), len(gate), GATE_WINDOWS, TRACE_WARM),
+               "kernel": TREE_KERNEL + ", 256>",
+               "C2": {"dispatches": len(c2), "avg_us": round(statistics.fmean(c2), 2),
+                      "median_us": round(statistics.median(c2), 2), "algo_bytes": c2_bytes,
+                      "frac_of_8TBs": round(c2_bytes / (statistics.fmean(c2) * 1e-6) / 8e12, 4)},
+               "gate_8x256MiB": {"calls": len(gate), "avg_us": round(statistics.fmean(gate), 2),
+                                 "median_us": round(statistics.median(gate), 2), "algo_bytes": gate_bytes,
+                                 "frac_of_8TBs": round(gate_bytes / (statistics.fmean(gate) * 1e-6) / 8e12, 4)}}
+    with open(os.path.join(ROOT, "gpurun_out", "bench_kernel_trace_split.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    return summary
+
+
 def run_local(args, esgd, dev):
     """N = 1: k staged buckets -> 1 output (config C2)."""
     from esgd import _lib
@@ -149,6 +242,9 @@ def run_local(args, esgd, dev):
     ptrs = [b.ptr for b in bufs]
     s.synchronize()
 
+    if args.pmc_child == "trace":
+        trace_child(dev, dt, ptrs, out, count, k, s)
+        return None
     if args.pmc_child:
         args.no_gate = True
         for _ in range(PMC_CALLS):
@@ -375,6 +471,81 @@ def sweep_c5(comm, dev, world, dt, es):
                     "busbw_GBs": round(nbytes / t / 1e9 * 2 * (world - 1) / world, 2),
                     "xgmi_frac": None if SHARED_GPU else round(t_min / t, 4), "rounds": iters,
                     "rank0_stages_us": stages})
+    return out
+
+
+def _round_us(comm, dev, count, kind, warm=10, iters=30, dt=None):
+    """Median (and mean) round time of a fresh schedule over a device bucket: `warm`
+    rounds, then `iters` post -> wait rounds back to back, each round's time the max over
+    ranks (as sweep_c5).  Uses whatever esgd_set_config the caller set."""
+    import statistics
+
+    import torch
+    import torch.distributed as dist
+
+    from esgd import _lib
+    dt = _lib.FLOAT if dt is None else dt
+    buf = dev.DeviceBuffer(count, dt)
+    dev.fill_uniform(buf, SEED, comm.rank())
+    dev.synchronize()
+    sch = comm.Schedule(kind, None, buf, count, dtype=dt, seed=6545343, buf=comm.BUF_DEVICE)
+    for _ in range(warm):
+        sch.post(); sch.wait()
+    comm.barrier()
+    ts = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        sch.post(); sch.wait()
+        ts.append(time.perf_counter() - t0)
+    tt = torch.tensor(ts, dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    ts = tt.tolist()
+    _defer(sch, buf)
+    return statistics.median(ts) * 1e6, statistics.fmean(ts) * 1e6
+
+
+def ab_one_launch_threshold(comm, dev, world, sizes_mib=(1, 2, 4, 8, 16)):
+    """The one-launch threshold (esgd_set_config "small_round_bytes", default 4 MiB)
+    A/B'd on this node: majority-allreduce rounds of each size run both ways -- ONE
+    k_round_small launch (pairing + reduce-scatter + pairing + all-gather inside one
+    kernel) and the five-launch round -- in the same job.  `best_threshold_MiB` is the
+    largest size where the one-launch round is still faster (what the default should be
+    on this topology)."""
+    out = {"sizes": []}
+    best = 0
+    try:
+        for mib in sizes_mib:
+            count = int(mib * MiB) // 4
+            comm.set_config("small_round_bytes", count * 4)
+            one, one_mean = _round_us(comm, dev, count, comm.MAJORITY)
+            comm.set_config("small_round_bytes", 0)
+            five, five_mean = _round_us(comm, dev, count, comm.MAJORITY)
+            out["sizes"].append({"bytes": count * 4, "one_launch_us": round(one, 1), "five_launch_us": round(five, 1),
+                                 "one_launch_mean_us": round(one_mean, 1), "five_launch_mean_us": round(five_mean, 1)})
+            if one < five:
+                best = mib
+    finally:
+        comm.set_config("small_round_bytes", -1)
+    out["default_MiB"] = 4
+    out["best_threshold_MiB"] = best
+    return out
+
+
+def ab_flag_pages(comm, dev, world, sizes=(65536, 16 << 20)):
+    """Where the rank-pairing flags live (esgd_set_config "device_flags"): 0 pinned host
+    memory (default; polled over PCIe), 1 uncached HBM pages, 2 fine-grained HBM pages
+    (peers' words written over xGMI), each at a one-launch size (64 KiB) and a
+    five-launch size (16 MiB), median majority round."""
+    out = {}
+    try:
+        for mode, name in ((0, "host"), (1, "hbm_uncached"), (2, "hbm_finegrained")):
+            comm.set_config("device_flags", mode)
+            out[name] = {}
+            for nbytes in sizes:
+                med, mean = _round_us(comm, dev, nbytes // 4, comm.MAJORITY)
+                out[name][str(nbytes)] = {"us": round(med, 1), "mean_us": round(mean, 1)}
+    finally:
+        comm.set_config("device_flags", -1)
     return out
 
 
@@ -865,6 +1036,8 @@ def run_allreduce(args, rank, world):
             "bound": "xgmi", "achieved": round(link_in, 2), "peak": XGMI_LINK_GBS * (world - 1),
             "unit": "GB/s", "frac": round(link_in / (XGMI_LINK_GBS * (world - 1)), 4), "traffic": None},
         "devices": devs,
+        "launcher": ("bench.py (self-launched torch.distributed.run)" if os.environ.get("ESGD_BENCH_SELF_LAUNCHED")
+                     else "torch.distributed.run"),
         "rounds": {"fresh": stats["fresh_rounds"], "auto": stats["auto_rounds"],
                    "activations_rank0": stats["activations"]},
         "rank0_stages_us": stages,
@@ -896,6 +1069,8 @@ def run_allreduce(args, rank, world):
         # alive until the end, and small rounds measured after them were bimodal
         legs = [("sweep_c5_majority", lambda: sweep_c5(comm, dev, world, dt, es)),
                 ("sweep_c5_majority_bf16", lambda: sweep_c5(comm, dev, world, _lib.BF16, 2)),
+                ("ab_one_launch_threshold", lambda: ab_one_launch_threshold(comm, dev, world)),
+                ("ab_flag_pages", lambda: ab_flag_pages(comm, dev, world)),
                 ("c3_wire_bf16", lambda: c3_wire_bf16(comm, dev, rank, world, int(args.bucket_mib * MiB) // 4)),
                 ("c1_host_majority", lambda: c1_host_majority(comm, dev, rank, world)),
                 ("small_round_after_idle", lambda: small_round_after_idle(comm, dev, rank, world)),
@@ -933,6 +1108,8 @@ def run_allreduce(args, rank, world):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.pmc_child:
+        sys.exit(launch_ranks(args))   # before any HIP call in this process
     if args.bucket_mib is None:
         args.bucket_mib = 64.0 if args.gpus == 1 else 256.0
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -989,6 +1166,15 @@ def main():
                 res["gate"]["traffic"] = pmc_traffic(args, 256.0)
         except Exception as e:  # profiler missing or refused: report, keep the line
             line["pmc_error"] = str(e)[:200]
+    trace = None
+    if not args.no_trace:
+        try:
+            trace = kernel_trace(args)
+        except Exception as e:  # profiler missing or refused: report, keep the line
+            line["trace_error"] = str(e)[:200]
+    if trace and res.get("gate"):
+        res["gate"]["rocprof_call_us"] = trace["gate_8x256MiB"]["avg_us"]
+        res["gate"]["rocprof_frac"] = trace["gate_8x256MiB"]["frac_of_8TBs"]
     line["roofline"] = {
         "bound": "hbm", "achieved": round(res["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
         "unit": "GB/s", "frac": round(res["achieved_gbs"] / HBM_PEAK_GBS, 4),
@@ -996,6 +1182,11 @@ def main():
         "kernel_ms": round(res["kernel_ms"], 5),
         # the north star's 1-GPU gate: 8 x 256 MiB fp32 buckets, same kernel, same timing
         "gate_256MiB_frac": res["gate"]["frac"] if res.get("gate") else None,
+        # the same kernel's average dispatch on this box from rocprofv3 --kernel-trace
+        # (profiles/r03/: bench_kernel_trace_split.json); the event pair above also holds
+        # the dispatch gap between back-to-back launches
+        "rocprof_kernel_us": trace["C2"]["avg_us"] if trace else None,
+        "rocprof_frac": trace["C2"]["frac_of_8TBs"] if trace else None,
     }
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(res["k"], res["count"] if args.dtype == "fp32"

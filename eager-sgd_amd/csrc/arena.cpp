@@ -131,6 +131,14 @@ int new_chunk(size_t bytes, int dev, Chunk **out) {
     return ESGD_SUCCESS;
 }
 
+// ESGD_ARENA_BYPASS=1 (diagnostics only, tools/ipc_bisect.py): every block is its own
+// hipMalloc and is freed, exported or not -- the pre-arena behaviour whose re-exports read
+// back wrong, so the trigger can be re-checked on a new driver.
+bool bypass() {
+    static const bool b = getenv("ESGD_ARENA_BYPASS") && *getenv("ESGD_ARENA_BYPASS") == '1';
+    return b;
+}
+
 }  // namespace
 
 int arena_alloc(size_t bytes, void **out) {
@@ -140,6 +148,15 @@ int arena_alloc(size_t bytes, void **out) {
     ESGD_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(g_mu);
     bytes = std::max<size_t>(bytes, 1);
+    if (bypass()) {
+        Chunk *c = nullptr;
+        if (int rc = new_chunk(bytes, dev, &c)) return rc;
+        ++c->live;
+        g_live[reinterpret_cast<uintptr_t>(c->base)] = {c, bytes};
+        g_live_bytes += bytes;
+        *out = c->base;
+        return ESGD_SUCCESS;
+    }
     if (bytes <= kSlab / 2) {
         const size_t cls = small_class(bytes);
         auto &fl = g_small[{dev, cls}];
@@ -189,6 +206,10 @@ bool arena_free(void *p) {
     g_live.erase(it);
     g_live_bytes -= b.cls;
     --b.chunk->live;
+    if (bypass()) {
+        release_chunk(b.chunk);
+        return true;
+    }
     if (b.cls <= kSlab / 2) {
         g_small[{b.chunk->device, b.cls}].push_back(static_cast<char *>(p));
         return true;

@@ -1,0 +1,139 @@
+"""Bisect the IPC re-export fault ("IPC arena").
+
+Round 2 found that once a bucket that peers had mapped is freed and its memory re-used by
+a bigger bucket that is exported again, peers read wrong data through their fresh
+mappings -- in esgd (8 ranks, a 16 MiB bucket, then a 256 MiB one), but not in a plain
+HIP reproducer.  This script starts from that reproducer and adds esgd's steps one at a
+time, cumulatively, in ONE GPU session:
+
+  plain        export, peers map, read the whole buffer through the mapping with the tree
+               kernel, close, free; then the same with a bigger buffer
+  +hostreg     a host page registered with hipHostRegisterMapped (the node segment)
+  +nbstream    the reads on a non-blocking stream (the round stream)
+  +suballoc    the bucket at a 2 MiB offset inside a bigger allocation (arena carving)
+  +keepmaps    mappings kept open and cached per handle, never closed before the free
+               (the (peer, chunk) mapping cache)
+  +engine      the esgd communicator up (progress thread, registered segment, a schedule)
+
+and finally esgd itself with the arena bypassed (ESGD_ARENA_BYPASS=1: every bucket its
+own hipMalloc, freed exported or not) on the C5 churn pattern -- the original trigger.
+Every line prints the mismatches per size and rank.
+
+  python tools/ipc_bisect.py [--world 8] [--only plain,+hostreg,...]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+import mp_workers  # noqa: E402
+
+MiB = 1 << 20
+STEPS = ["plain", "+hostreg", "+nbstream", "+suballoc", "+keepmaps", "+engine"]
+
+
+class Handle(C.Structure):
+    _fields_ = [("reserved", C.c_char * 64)]
+
+
+def worker(rank, world, sizes, steps):
+    import torch.distributed as dist
+
+    import esgd
+    from esgd import device as dev
+    hip = C.CDLL("libamdhip64.so.7")   # the runtime torch (and libesgd) already loaded
+    vp = C.c_void_p
+    hip.hipIpcOpenMemHandle.argtypes = [C.POINTER(vp), Handle, C.c_uint]
+    on = set(steps)
+    if "+engine" in on:
+        from esgd import comm
+        comm.init()
+        eb = dev.DeviceBuffer(4096)
+        s0 = comm.Schedule(0, None, eb, 4096, buf=comm.BUF_DEVICE)
+        s0.post(); s0.wait()
+    if "+hostreg" in on:
+        hb = (C.c_char * (1 << 20))()
+        assert hip.hipHostRegister(hb, C.c_size_t(1 << 20), 2) == 0
+    stream = dev.Stream() if "+nbstream" in on else None
+    loc = dev.DeviceBuffer(max(sizes) // 4)
+    pad = 2 * MiB if "+suballoc" in on else 0
+    cache = {}
+    out = []
+    for si, size in enumerate(sizes):
+        p = vp()
+        assert hip.hipMalloc(C.byref(p), C.c_size_t(size + 2 * pad)) == 0
+        buf = p.value + pad
+        val = (rank * 16 + si + 1) & 0xFF
+        assert hip.hipMemset(vp(buf), val, C.c_size_t(size)) == 0
+        assert hip.hipDeviceSynchronize() == 0
+        h = Handle()
+        assert hip.hipIpcGetMemHandle(C.byref(h), p) == 0
+        hs = [None] * world
+        dist.all_gather_object(hs, bytes(h))
+        opened, bad = [], []
+        for q in range(world):
+            if q == rank:
+                continue
+            key = (q, hs[q])
+            if "+keepmaps" in on and key in cache:
+                m = cache[key]
+            else:
+                mm = vp()
+                rc = hip.hipIpcOpenMemHandle(C.byref(mm), Handle.from_buffer_copy(hs[q]), 1)
+                assert rc == 0, rc
+                m = mm.value
+                cache[key] = m
+                opened.append(m)
+            want = (q * 16 + si + 1) & 0xFF
+            dev.reduce(esgd.FLOAT, [m + pad], loc, size // 4, stream=stream)   # the whole buffer
+            dev.synchronize(stream)
+            for off in (0, size // 2, size - 4096):
+                b = (C.c_uint8 * 4096)()
+                assert hip.hipMemcpy(b, vp(loc.ptr + off), C.c_size_t(4096), 2) == 0
+                got = set(b)
+                if got != {want}:
+                    bad.append((q, off, sorted(got)[:4], want))
+        dist.barrier()
+        if "+keepmaps" not in on:
+            for m in opened:
+                hip.hipIpcCloseMemHandle(vp(m))
+            cache.clear()
+        dist.barrier()
+        hip.hipFree(p)
+        dist.barrier()
+        out.append((size, len(bad), bad[:2]))
+    if "+engine" in on:
+        s0.delete()
+        comm.finalize()
+    return out
+
+
+mp_workers.ipc_bisect_worker = worker
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--only", default=None)
+    ap.add_argument("--no-esgd", action="store_true")
+    a = ap.parse_args()
+    sizes = [16 * MiB, 256 * MiB]
+    names = a.only.split(",") if a.only else STEPS
+    for name in names:
+        steps = STEPS[: STEPS.index(name) + 1]
+        res = mp_workers.run("ipc_bisect_worker", a.world, sizes=sizes, steps=steps, timeout=300)
+        nbad = [[n for _, n, _ in per] for per in res]
+        print(f"world {a.world} {name:10s} mismatches per rank x size {nbad}", flush=True)
+        for r, per in enumerate(res):
+            for size, n, ex in per:
+                if n:
+                    print(f"  rank {r} size {size}: {ex}", flush=True)
+                    break
+    if not a.no_esgd:
+        # esgd itself, arena bypassed: 16 MiB schedule used, deleted, bucket freed, then
+        # 256 MiB (mp_workers.gpu_config: head / middle / tail of every rank vs the oracle)
+        os.environ["ESGD_ARENA_BYPASS"] = "1"
+        outs = mp_workers.run("gpu_config", a.world, kind=2, counts=[(16 * MiB) // 4, (256 * MiB) // 4],
+                              rounds=2, timeout=300)
+        print(f"world {a.world} esgd-arena-bypass ok per rank x size {[[v[3] for v in per] for per in outs]}",
+              flush=True)
