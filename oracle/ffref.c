@@ -74,6 +74,23 @@ int ffref_copy(int dtype, const void *a, void *c, uint32_t n) {
     return 0;
 }
 
+int ffref_comp_custom(ffref_operator_fun_t fun, int dtype, void *a, uint32_t na, void *b, uint32_t nb,
+                      void *c, uint32_t nc) {
+    if (!fun) return -2;
+    uint32_t size = na;                        /* ffop_gcomp.c:52: MIN of the three counts */
+    if (b && nb < size) size = nb;             /* :36-42: buffer 2 is optional */
+    if (nc < size) size = nc;
+    return fun(a, b, c, size, dtype);          /* :56 */
+}
+
+int ffref_op_plus_one(void *a, void *b, void *c, uint32_t count, int dtype) {
+    (void)dtype;                               /* custom_computation.c:14-20: int32 only */
+    const uint32_t *ia = (const uint32_t *)a, *ib = (const uint32_t *)b;
+    uint32_t *ic = (uint32_t *)c;
+    for (uint32_t i = 0; i < count; ++i) ic[i] = ia[i] + ib[i] + 1u;
+    return 0;                                  /* FFSUCCESS */
+}
+
 int ffref_allreduce_rd(int dtype, int P, uint32_t count, const void *const *sb,
                        void *const *rb, void *scratch) {
     size_t es = ffref_dtype_size(dtype);

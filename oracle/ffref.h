@@ -34,6 +34,17 @@ int ffref_vsum(int dtype, const void *a, const void *b, void *c, uint32_t n);
 /* memcpy "move" (src/components/gcomp/ffop_gcomp_operator.c:61-72) */
 int ffref_copy(int dtype, const void *a, void *c, uint32_t n);
 
+/* A computation with a user operator (FFCUSTOM: ffcomp_operator_create, src/ffcomp.c:40-42;
+ * ff.h:134): the gcomp backend calls the operator once over size = MIN(count1, count2,
+ * count3) elements (src/components/gcomp/ffop_gcomp.c:29-56) and the op completes when it
+ * returns FFSUCCESS (0).  Returns the operator's status. */
+typedef int (*ffref_operator_fun_t)(void *a, void *b, void *c, uint32_t count, int dtype);
+int ffref_comp_custom(ffref_operator_fun_t fun, int dtype, void *a, uint32_t na, void *b, uint32_t nb,
+                      void *c, uint32_t nc);
+/* the user operator of evaluation/custom_computation.c:12-24: c[i] = a[i] + b[i] + 1 over
+ * int32 (two's complement wrap, as gcc compiles the reference's int arithmetic) */
+int ffref_op_plus_one(void *a, void *b, void *c, uint32_t count, int dtype);
+
 /* Recursive-doubling allreduce simulated for all P ranks in one process
  * (src/colls/ffallreduce.c:74-177, hot loop :138-171):
  *   rb[r] = sb[r]                       (move, :126-130; skipped when sb == NULL -> in place)

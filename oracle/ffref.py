@@ -150,3 +150,26 @@ def time_c1(P: int, count: int, reps: int):
     ok = C.c_int(0)
     t = float(lib().ffref_time_c1(P, count, reps, C.byref(ok)))
     return t, bool(ok.value)
+
+
+_OPFUN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int)
+
+
+def comp_custom_plus_one(a: np.ndarray, b: np.ndarray, nc: int) -> np.ndarray:
+    """ffcomp with the user operator of evaluation/custom_computation.c:12-24
+    (c = a + b + 1, int32) through the oracle's restatement of the gcomp backend's
+    custom-operator call (ffref_comp_custom: size = MIN of the three counts,
+    ffop_gcomp.c:29-56).  Returns the nc-element c (untouched elements stay 0)."""
+    h = lib()
+    a = np.ascontiguousarray(a, np.int32)
+    b = np.ascontiguousarray(b, np.int32)
+    c = np.zeros(nc, np.int32)
+    fn = C.cast(h.ffref_op_plus_one, C.c_void_p).value
+    comp = h.ffref_comp_custom
+    comp.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p,
+                     C.c_uint32]
+    comp.restype = C.c_int
+    rc = comp(fn, INT32, a.ctypes.data, a.size, b.ctypes.data, b.size, c.ctypes.data, nc)
+    if rc != 0:
+        raise RuntimeError(f"ffref_comp_custom: {rc}")
+    return c

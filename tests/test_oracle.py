@@ -168,3 +168,19 @@ def test_golden_known_int32(golden_dir):
 def test_golden_bf16(golden_dir):
     g = np.load(os.path.join(golden_dir, "tree_bf16_p8.npz"))
     np.testing.assert_array_equal(ffref.tree_sum_bf16(list(g["x"])), g["out"])
+
+
+@pytest.mark.parametrize("na,nb,nc", [(1000, 1000, 1000), (1023, 1500, 2000), (4097, 100, 4097), (0, 5, 5)])
+def test_custom_operator_plus_one_known_answer(na, nb, nc):
+    # SURVEY.md §8(c) pin 4: evaluation/custom_computation.c:53-74 fills a, b with rand()
+    # and checks c[i] == a[i] + b[i] + 1 for the user operator of :12-24; the gcomp
+    # backend calls it over MIN(counts) elements (ffop_gcomp.c:52-56).  Oracle-side only:
+    # FFCUSTOM is not on the GPU path.
+    rng = np.random.default_rng(na + nb + nc)
+    a = rng.integers(0, 2**31 - 1, na, dtype=np.int64).astype(np.int32)   # rand()'s range
+    b = rng.integers(0, 2**31 - 1, nb, dtype=np.int64).astype(np.int32)
+    c = ffref.comp_custom_plus_one(a, b, nc)
+    m = min(na, nb, nc)
+    want = (a[:m].astype(np.int64) + b[:m].astype(np.int64) + 1).astype(np.uint32).view(np.int32)
+    assert np.array_equal(c[:m], want)
+    assert not c[m:].any()
