@@ -1,0 +1,23 @@
+# One GPU session of bench work (round 3): the N = 1 line (PMC + kernel-trace passes), the
+# N = 2 line started the way a bare `bench.py --gpus 2` starts it (self-launched ranks,
+# sharing the box's one GPU: a rehearsal), rocprofv3 kernel statistics of the N = 1 bench,
+# and the IPC re-export bisection.  Each GPU step has its own time limit; the first
+# failure ends the session.
+#   bash tools/bench_round.sh <tag> [steps...]   steps: n1 n2 prof bisect (default: all)
+set -e
+export ESGD_TIMEOUT_S=60
+O=gpurun_out/${1:-bench_round}; shift || true
+STEPS=${*:-n1 n2 prof bisect}
+mkdir -p $O
+R=$PWD
+for s in $STEPS; do
+  case $s in
+  n1) timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench_n1.json 2> $O/bench_n1.err
+      cp -r gpurun_out/bench_kernel_trace_split.json $O/ 2>/dev/null || true ;;
+  n2) timeout -k 10 600 python bench.py --gpus 2 --steps 20 --warmup 5 > $O/bench_n2.json 2> $O/bench_n2.err ;;
+  prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run \
+          --output-format csv -- python $R/bench.py --no-pmc --no-trace --no-cpu-baseline --steps 100 \
+          > $R/$O/bench_prof.json 2>&1) ;;
+  bisect) timeout -k 10 500 python -u tools/ipc_bisect.py > $O/ipc_bisect.txt 2>&1 ;;
+  esac
+done
