@@ -230,12 +230,14 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
                          (uint64_t(uint32_t(dtype) & 0xff) << 32) |
                          (tag == kNoTag ? 0 : (0x10000u | uint16_t(tag)));
     int rc = ESGD_SUCCESS;
-    auto vote = [&](int r) -> int {
-        if (r) s->sh->setup_err.fetch_add(1, std::memory_order_acq_rel);
+    // each vote has its own failure counter: a rank already failing the second vote must
+    // not make a slower rank, still reading the first vote's result, report the wrong cause
+    auto vote = [&](int r, std::atomic<uint32_t> &errs) -> int {
+        if (r) errs.fetch_add(1, std::memory_order_acq_rel);
         const int rb = shm_barrier(g_seg, g_world, g_timeout);
         if (r) return r;
         if (rb) return rb;
-        if (s->sh->setup_err.load(std::memory_order_acquire)) {
+        if (errs.load(std::memory_order_acquire)) {
             set_error("schedule create: another rank failed to register schedule %d", s->id);
             return ESGD_ERROR;
         }
@@ -246,7 +248,7 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     s->sh->sig[g_rank].store(sig, std::memory_order_release);
     if (!rc) rc = tp->setup(*s);     // local: buffers, streams, publication
     const double c1 = now_s();
-    rc = vote(rc);
+    rc = vote(rc, s->sh->setup_err);
     for (int q = 0; !rc && q < g_world; ++q) {
         const uint64_t o = s->sh->sig[q].load(std::memory_order_acquire);
         if (o != sig) {
@@ -261,7 +263,7 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     const double c2 = now_s();
     if (!rc) rc = tp->connect(*s);   // needs every peer's publication
     const double c3 = now_s();
-    rc = vote(rc);
+    rc = vote(rc, s->sh->connect_err);
     if (dbg)
         fprintf(stderr, "[esgd] r%d create sched %d (%llu x %d B): setup %.1f ms, vote %.1f ms, connect %.1f ms, "
                 "vote %.1f ms\n", g_rank, s->id, (unsigned long long)count, int(s->esize), (c1 - c0) * 1e3,

@@ -25,8 +25,11 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def _entry(fn_name, rank, world, port, kw, q):
+def _entry(fn_name, rank, world, port, kw, q, env=None):
     try:
+        if env is not None:   # the parent's environment at run() time (forkserver children
+            os.environ.clear()   # are forked from a server started earlier)
+            os.environ.update(env)
         os.environ.setdefault("ESGD_TIMEOUT_S", "60")
         # one GPU per rank where the box has them (device = rank % device_count, set in
         # _comm()): on a full node the data plane then crosses xGMI; on a 1-GPU box every
@@ -46,11 +49,31 @@ def _entry(fn_name, rank, world, port, kw, q):
         q.put(("err", f"rank {rank}: " + traceback.format_exc()))
 
 
+_CTX = None
+
+
+def _context():
+    """Rank processes start from a forkserver that has imported torch once (ESGD_TEST_START=
+    spawn restores a fresh interpreter per rank): a spawned rank spent ~2-3 s importing
+    torch, most of a multi-rank GPU test.  The server is a fresh interpreter that never
+    touches HIP (torch's import does not initialise the device), so every forked rank
+    initialises its own HIP runtime, as a spawned one does."""
+    global _CTX
+    if _CTX is None:
+        method = os.environ.get("ESGD_TEST_START", "forkserver")
+        ctx = mp.get_context(method)
+        if method == "forkserver":
+            ctx.set_forkserver_preload(["numpy", "torch", "torch.distributed"])
+        _CTX = ctx
+    return _CTX
+
+
 def run(fn_name: str, world: int, timeout: float = 240.0, **kw):
-    ctx = mp.get_context("spawn")
+    ctx = _context()
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_entry, args=(fn_name, r, world, port, kw, q)) for r in range(world)]
+    env = dict(os.environ)
+    procs = [ctx.Process(target=_entry, args=(fn_name, r, world, port, kw, q, env)) for r in range(world)]
     for p in procs:
         p.start()
     try:
