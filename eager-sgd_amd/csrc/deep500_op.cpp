@@ -24,9 +24,12 @@
 //     read the bucket while :301 is still copying into it.  The device path therefore
 //     needs no zeroing pass at all, and the wrapper's division by the comm size (:40) is
 //     fused into the copy-in (allreducef_forward_cuda_div);
-//   * the extension entry points return a status instead of aborting the process.
+//   * the extension entry points return a status instead of aborting the process; the
+//     deep500-shaped void ones abort by default (their ABI has no error channel) or, with
+//     esgd_op_on_error(ESGD_OP_ON_ERROR_LOCAL), carry on with this rank's own gradient.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -71,6 +74,16 @@ OpConfig current_config() {
     std::abort();
 }
 
+// what the void entry points do on a failed round (esgd_op_on_error / ESGD_OP_ON_ERROR)
+std::atomic<int> g_on_error{-1};
+
+int on_error_policy() {
+    const int v = g_on_error.load();
+    if (v >= 0) return v;
+    const char *e = getenv("ESGD_OP_ON_ERROR");
+    return (e && !strcmp(e, "local")) ? ESGD_OP_ON_ERROR_LOCAL : ESGD_OP_ON_ERROR_ABORT;
+}
+
 struct AllreduceOp {
     uint64_t len = 0;
     OpConfig cfg;
@@ -78,6 +91,8 @@ struct AllreduceOp {
     bool device = false;
     float *sb = nullptr, *rb = nullptr;   // persistent buckets (host pinned or HBM)
     int64_t bytes = 0;
+    int status = 0;                       // first failure of a void entry point (ESGD_OP_ON_ERROR_LOCAL)
+    bool warned = false;
 
     // Lazy creation of the buckets and the schedule (:288-298); an esgd status (the void
     // entry points abort on failure, the status-returning ones pass it on).
@@ -176,9 +191,42 @@ int forward_host_impl(AllreduceOp *op, const float *input, float *output) {
     return ESGD_SUCCESS;
 }
 
+// A void entry point's round failed: abort (the default), or keep the job going with
+// this rank's own contribution as the step's gradient -- what a round that only this
+// rank's fresh gradient reached would give (its peers' shares zero, rsgd.c:87,100) --
+// and remember the status for esgd_op_status().
+void fail_void(AllreduceOp *op, int rc, const char *where, const float *input, float *output, bool dev,
+               hipStream_t s) {
+    if (!op || on_error_policy() != ESGD_OP_ON_ERROR_LOCAL) die(where);
+    if (!op->status) op->status = rc;
+    if (!op->warned) {
+        fprintf(stderr, "[esgd] %s failed: %s -- continuing with this rank's own gradient "
+                "(ESGD_OP_ON_ERROR_LOCAL; later failures of this op are not printed)\n", where, esgd_last_error());
+        op->warned = true;
+    }
+    const size_t nbytes = size_t(op->len) * sizeof(float);
+    if (!nbytes || input == output || !input || !output) return;
+    if (dev) {
+        if (hipMemcpyAsync(output, input, nbytes, hipMemcpyDeviceToDevice, s) != hipSuccess) die(where);
+    } else {
+        std::memcpy(output, input, nbytes);
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int esgd_op_on_error(int policy) {
+    ESGD_ARG(policy == ESGD_OP_ON_ERROR_ABORT || policy == ESGD_OP_ON_ERROR_LOCAL || policy == -1,
+             "esgd_op_on_error: ESGD_OP_ON_ERROR_ABORT, ESGD_OP_ON_ERROR_LOCAL or -1 (the default)");
+    g_on_error.store(policy);
+    return ESGD_SUCCESS;
+}
+
+int esgd_op_status(void *handle) {
+    return handle ? static_cast<AllreduceOp *>(handle)->status : ESGD_INVALID_ARG;
+}
 
 int esgd_op_configure(int mode, int async, unsigned seed) {
     ESGD_ARG(mode == ESGD_OP_SOLO || mode == ESGD_OP_MAJORITY || mode == ESGD_OP_ALLREDUCE,
@@ -213,7 +261,8 @@ void *create_new_op(esgd_d5_tensor_t *in, int num_inputs, esgd_d5_tensor_t *, in
 }
 
 void allreducef_forward(void *handle, const float *input, const float *, float *output) {
-    if (forward_host_impl(static_cast<AllreduceOp *>(handle), input, output)) die("allreducef_forward");
+    auto *op = static_cast<AllreduceOp *>(handle);
+    if (int rc = forward_host_impl(op, input, output)) fail_void(op, rc, "allreducef_forward", input, output, false, nullptr);
 }
 
 int allreducef_forward_host(void *handle, const float *input, float *output) {
@@ -222,9 +271,9 @@ int allreducef_forward_host(void *handle, const float *input, float *output) {
 
 void allreducef_forward_cuda(void *handle, const float *input, const float *, float *output,
                              void *stream) {
-    if (forward_cuda_impl(static_cast<AllreduceOp *>(handle), input, output, kNoDivide,
-                          static_cast<hipStream_t>(stream)))
-        die("allreducef_forward_cuda");
+    auto *op = static_cast<AllreduceOp *>(handle);
+    if (int rc = forward_cuda_impl(op, input, output, kNoDivide, static_cast<hipStream_t>(stream)))
+        fail_void(op, rc, "allreducef_forward_cuda", input, output, true, static_cast<hipStream_t>(stream));
 }
 
 int allreducef_forward_cuda_div(void *handle, const float *input, float *output, float divisor,

@@ -37,6 +37,8 @@ def _bind(h):
     vp = C.c_void_p
     h.esgd_op_configure.restype, h.esgd_op_configure.argtypes = C.c_int, [C.c_int, C.c_int, C.c_uint]
     h.esgd_op_configure_wire.restype, h.esgd_op_configure_wire.argtypes = C.c_int, [C.c_int]
+    h.esgd_op_on_error.restype, h.esgd_op_on_error.argtypes = C.c_int, [C.c_int]
+    h.esgd_op_status.restype, h.esgd_op_status.argtypes = C.c_int, [C.c_void_p]
     h.create_new_op.restype = vp
     h.create_new_op.argtypes = [C.POINTER(tensor_t), C.c_int, C.POINTER(tensor_t), C.c_int]
     h.allreducef_forward.restype, h.allreducef_forward.argtypes = None, [vp, vp, vp, vp]
@@ -68,6 +70,13 @@ def configure(mode: str = "solo", async_: int = 32, seed: int = 6545343, wire: s
     _lib.check(lib().esgd_op_configure(MODES[mode], int(async_), int(seed) & 0xFFFFFFFF),
                "esgd_op_configure")
     _lib.check(lib().esgd_op_configure_wire(WIRES[wire]), "esgd_op_configure_wire")
+
+
+def on_error(policy: str):
+    """What the deep500-shaped void entry points do on a failed round: "abort" (default)
+    or "local" (carry on with this rank's own gradient; AllreduceOp.status() keeps the
+    first failure).  The Python methods below use the status variants and raise."""
+    _lib.check(lib().esgd_op_on_error({"abort": 0, "local": 1, "default": -1}[policy]), "esgd_op_on_error")
 
 
 class AllreduceOp:
@@ -123,6 +132,18 @@ class AllreduceOp:
         _lib.check(lib().allreducef_forward_cuda_packed(self.handle, n, src, counts, dst, float(divisor),
                                                         stream), "allreducef_forward_cuda_packed")
         return outs
+
+    def forward_void(self, grad: np.ndarray) -> np.ndarray:
+        """The reference ABI's void allreducef_forward verbatim (host buffers): on a failed
+        round it aborts, or, under on_error("local"), returns this rank's own gradient."""
+        g = np.ascontiguousarray(grad, dtype=np.float32)
+        out = np.empty_like(g)
+        lib().allreducef_forward(self.handle, g.ctypes.data, None, out.ctypes.data)
+        return out
+
+    def status(self) -> int:
+        """First failure of a void entry point under on_error("local"), 0 while none."""
+        return int(lib().esgd_op_status(self.handle))
 
     def supports_cuda(self) -> bool:
         return bool(lib().is_cuda_supported(self.handle))

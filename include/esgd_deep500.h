@@ -67,6 +67,17 @@ int allreducef_forward_cuda_div(void *handle, const float *input, float *output,
 int allreducef_forward_cuda_packed(void *handle, int n, const float *const *grads,
                                    const uint64_t *counts, float *const *outs, float divisor,
                                    void *stream);
+/* Extension: what the void entry points above (allreducef_forward, allreducef_forward_cuda)
+ * do when their round fails (a peer timeout, an allocation failure).  ESGD_OP_ON_ERROR_ABORT
+ * (default; env ESGD_OP_ON_ERROR=abort): print the error and abort the process, as their
+ * ABI has no error channel.  ESGD_OP_ON_ERROR_LOCAL (env ESGD_OP_ON_ERROR=local): print it
+ * once per op, write this rank's own contribution (input) to output and return, so the
+ * training step goes on with the local gradient; esgd_op_status(handle) then returns the
+ * first failure's status (0 while none).  -1 restores the default. */
+#define ESGD_OP_ON_ERROR_ABORT 0
+#define ESGD_OP_ON_ERROR_LOCAL 1
+int esgd_op_on_error(int policy);
+int esgd_op_status(void *handle);
 bool is_cuda_supported(void *handle);
 int64_t report(void *handle, void *data);   /* bytes of gradient reduced so far */
 void delete_op(void *handle);

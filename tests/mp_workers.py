@@ -1192,3 +1192,25 @@ def gpu_reinit(rank, world, count=4099):
     except EsgdError as e:
         err = str(e)
     return {"ok": ok, "err": err}
+
+
+def op_void_peer_lost(rank, world, count=5000):
+    """The deep500-shaped void entry point under ESGD_OP_ON_ERROR_LOCAL: rank 1 runs one
+    step and leaves; rank 0's next (synchronous) round times out, and instead of aborting
+    the process the op writes rank 0's own gradient to the output and keeps the status."""
+    import numpy as np
+
+    from esgd import deep500
+    os.environ["ESGD_TIMEOUT_S"] = "3"
+    comm = _comm()
+    deep500.configure("allreduce", 32, 6545343)
+    deep500.on_error("local")
+    op = deep500.AllreduceOp((count,))
+    x = np.full(count, 0.5 + rank, np.float32)
+    first = op.forward_void(x)          # step 1: both ranks
+    out = {"first_ok": bool(np.all(first == sum(0.5 + r for r in range(world))))}
+    if rank == 0:
+        t0 = time.time()
+        second = op.forward_void(x)     # rank 1 never posts this round
+        out.update(elapsed=time.time() - t0, own=bool(np.array_equal(second, x)), status=op.status())
+    return out

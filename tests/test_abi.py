@@ -88,6 +88,15 @@ def test_data_plane_config_keys():
     assert comm.get_config("device_flags") == int(os.environ.get("ESGD_DEVICE_FLAGS", 0))
 
 
+def test_op_error_policy_argument_checks():
+    from esgd import _lib, deep500
+    lib = _lib.lib()
+    assert lib.esgd_op_on_error(5) == _lib.INVALID_ARG
+    assert lib.esgd_op_status(None) == _lib.INVALID_ARG
+    deep500.on_error("local")
+    deep500.on_error("default")
+
+
 def test_wire_flag_argument_checks():
     # ESGD_SCHED_WIRE_BF16 needs FLOAT buckets; unknown flags are refused (checked before
     # any communicator or device is touched)

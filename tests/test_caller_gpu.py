@@ -60,3 +60,13 @@ def test_eager_sgd_optimizer_wire_bf16(mode, fuse):
         assert all(o["ok"]) and o["ok"], o["ok"]
     if mode == "allreduce":
         assert outs[0]["params_digest"] == outs[1]["params_digest"]
+
+
+def test_void_forward_keeps_going_on_a_lost_peer():
+    # the reference's void allreducef_forward has no error channel; under
+    # esgd_op_on_error(ESGD_OP_ON_ERROR_LOCAL) a lost peer no longer aborts the job: the
+    # step gets this rank's own gradient and the op keeps the failure's status
+    outs = run("op_void_peer_lost", 2, timeout=120)
+    assert all(o["first_ok"] for o in outs), outs
+    o = outs[0]
+    assert o["own"] and o["status"] != 0 and o["elapsed"] < 30, o
