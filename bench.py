@@ -1070,7 +1070,6 @@ def run_allreduce(args, rank, world):
         legs = [("sweep_c5_majority", lambda: sweep_c5(comm, dev, world, dt, es)),
                 ("sweep_c5_majority_bf16", lambda: sweep_c5(comm, dev, world, _lib.BF16, 2)),
                 ("ab_one_launch_threshold", lambda: ab_one_launch_threshold(comm, dev, world)),
-                ("ab_flag_pages", lambda: ab_flag_pages(comm, dev, world)),
                 ("c3_wire_bf16", lambda: c3_wire_bf16(comm, dev, rank, world, int(args.bucket_mib * MiB) // 4)),
                 ("c1_host_majority", lambda: c1_host_majority(comm, dev, rank, world)),
                 ("small_round_after_idle", lambda: small_round_after_idle(comm, dev, rank, world)),
@@ -1080,6 +1079,9 @@ def run_allreduce(args, rank, world):
                                                                   int(args.bucket_mib * MiB) // 4))]
         if os.environ.get("ESGD_BENCH_RCCL", "1") == "1":
             legs.append(("c3_rccl_transport", lambda: c3_over_rccl(comm, dev, rank, world, count)))
+        # last: device flag pages have never run across GPUs; a hang there costs the
+        # round timeout, and no other leg is lost to it
+        legs.append(("ab_flag_pages", lambda: ab_flag_pages(comm, dev, world)))
         only = os.environ.get("ESGD_BENCH_LEGS")   # comma-separated subset, in this order
         if only:
             pick = only.split(",")
