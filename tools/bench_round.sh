@@ -3,7 +3,7 @@
 # sharing the box's one GPU: a rehearsal), rocprofv3 kernel statistics of the N = 1 bench,
 # and the IPC re-export bisection.  Each GPU step has its own time limit; the first
 # failure ends the session.
-#   bash tools/bench_round.sh <tag> [steps...]   steps: n1 n2 prof bisect (default: all)
+#   bash tools/bench_round.sh <tag> [steps...]   steps: n1 n2 prof bisect sweep (default: n1 n2 prof bisect)
 set -e
 export ESGD_TIMEOUT_S=60
 O=gpurun_out/${1:-bench_round}; shift || true
@@ -19,5 +19,10 @@ for s in $STEPS; do
           --output-format csv -- python $R/bench.py --no-pmc --no-trace --no-cpu-baseline --steps 100 \
           > $R/$O/bench_prof.json 2>&1) ;;
   bisect) timeout -k 10 500 python -u tools/ipc_bisect.py > $O/ipc_bisect.txt 2>&1 ;;
+  sweep) make -s sweeps >/dev/null 2>&1 || true
+      for m in 256 1024; do
+        timeout -k 10 240 python tools/sweep_reduce.py --mib $m --grids 0 --unrolls 4 --nts 1 \
+            --policies=-1,25,26,27 --rounds 5 --iters 20 > $O/sweep_streams_$m.jsonl 2>&1
+      done ;;
   esac
 done

@@ -11,6 +11,9 @@
 //   policy 14..16   store policies (nt only, plain, sc0+sc1)
 //   policy 17..20   LDS-DMA ring (buffer_load ... lds), (waves per block, ring depth)
 //   policy 21..23   window sizes 32 / 64 / 96 MiB; 24 one launch over the whole bucket
+//   policy 25..27   64 MiB windows dealt round-robin over 2 / 3 / 4 streams (forked from and
+//                   joined back to the caller's stream by events): a window's launch can
+//                   start while the previous one's last workgroups drain
 //   policy -1       the production launch (the baseline every variant is timed against)
 // fp32, fan-in 8 only.
 #include <hip/hip_runtime.h>
@@ -149,6 +152,39 @@ static int launch_lds(const InputSet &in, void *out, uint64_t count, hipStream_t
     return ESGD_SUCCESS;
 }
 
+// windows over NS streams: stream 0 is the caller's, the others fork from it and join back
+static hipStream_t g_aux[4] = {};
+static hipEvent_t g_fork = nullptr, g_join[4] = {};
+
+static int launch_windows_streams(const InputSet &in, void *out, uint64_t count, hipStream_t s, int ns,
+                                  unsigned grid) {
+    const uint64_t w = kWindowBytes / 4;
+    if (count <= w + w / 2) return launch_buf<F32, 8, 4, 2, 16, false>(in, out, count, 1.0f, s, grid);
+    if (!g_fork) {
+        ESGD_HIP(hipEventCreateWithFlags(&g_fork, hipEventDisableTiming));
+        for (int i = 1; i < 4; ++i) {
+            ESGD_HIP(hipStreamCreateWithFlags(&g_aux[i], hipStreamNonBlocking));
+            ESGD_HIP(hipEventCreateWithFlags(&g_join[i], hipEventDisableTiming));
+        }
+    }
+    ESGD_HIP(hipEventRecord(g_fork, s));
+    for (int i = 1; i < ns; ++i) ESGD_HIP(hipStreamWaitEvent(g_aux[i], g_fork, 0));
+    int idx = 0;
+    for (uint64_t o = 0; o < count; o += w, ++idx) {
+        InputSet sl = in;
+        for (int j = 0; j < 8; ++j) sl.p[j] = static_cast<const float *>(in.p[j]) + o;
+        hipStream_t st = (idx % ns) == 0 ? s : g_aux[idx % ns];
+        if (int rc = launch_buf<F32, 8, 4, 2, 16, false>(sl, static_cast<float *>(out) + o, std::min(w, count - o),
+                                                         1.0f, st, grid))
+            return rc;
+    }
+    for (int i = 1; i < ns; ++i) {
+        ESGD_HIP(hipEventRecord(g_join[i], g_aux[i]));
+        ESGD_HIP(hipStreamWaitEvent(s, g_join[i], 0));
+    }
+    return ESGD_SUCCESS;
+}
+
 }  // namespace esgd
 
 using namespace esgd;
@@ -198,6 +234,9 @@ int esgd_sweep_reduce(int policy, int unroll, int nt, int grid, const void *cons
     case 22: return launch_windows<F32, 8, 4, 2, 16, false>(in, out, count, 1.0f, s, uint64_t(64) << 20, g);
     case 23: return launch_windows<F32, 8, 4, 2, 16, false>(in, out, count, 1.0f, s, uint64_t(96) << 20, g);
     case 24: return launch_buf<F32, 8, 4, 2, 16, false>(in, out, count, 1.0f, s, g);
+    case 25: return launch_windows_streams(in, out, count, s, 2, g);
+    case 26: return launch_windows_streams(in, out, count, s, 3, g);
+    case 27: return launch_windows_streams(in, out, count, s, 4, g);
     default: break;
     }
     set_error("unknown policy %d", policy);
