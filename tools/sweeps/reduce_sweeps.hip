@@ -13,7 +13,8 @@
 //   policy 21..23   window sizes 32 / 64 / 96 MiB; 24 one launch over the whole bucket
 //   policy 25..27   64 MiB windows dealt round-robin over 2 / 3 / 4 streams (forked from and
 //                   joined back to the caller's stream by events): a window's launch can
-//                   start while the previous one's last workgroups drain
+//                   start while the previous one's last workgroups drain; 28 / 29 the same
+//                   with 32 / 16 MiB windows over 2 streams
 //   policy -1       the production launch (the baseline every variant is timed against)
 // fp32, fan-in 8 only.
 #include <hip/hip_runtime.h>
@@ -157,8 +158,8 @@ static hipStream_t g_aux[4] = {};
 static hipEvent_t g_fork = nullptr, g_join[4] = {};
 
 static int launch_windows_streams(const InputSet &in, void *out, uint64_t count, hipStream_t s, int ns,
-                                  unsigned grid) {
-    const uint64_t w = kWindowBytes / 4;
+                                  unsigned grid, uint64_t window_bytes = kWindowBytes) {
+    const uint64_t w = window_bytes / 4;
     if (count <= w + w / 2) return launch_buf<F32, 8, 4, 2, 16, false>(in, out, count, 1.0f, s, grid);
     if (!g_fork) {
         ESGD_HIP(hipEventCreateWithFlags(&g_fork, hipEventDisableTiming));
@@ -237,6 +238,8 @@ int esgd_sweep_reduce(int policy, int unroll, int nt, int grid, const void *cons
     case 25: return launch_windows_streams(in, out, count, s, 2, g);
     case 26: return launch_windows_streams(in, out, count, s, 3, g);
     case 27: return launch_windows_streams(in, out, count, s, 4, g);
+    case 28: return launch_windows_streams(in, out, count, s, 2, g, uint64_t(32) << 20);
+    case 29: return launch_windows_streams(in, out, count, s, 2, g, uint64_t(16) << 20);
     default: break;
     }
     set_error("unknown policy %d", policy);
