@@ -17,6 +17,13 @@ time, cumulatively, in ONE GPU session:
 
 and finally esgd itself with the arena bypassed (ESGD_ARENA_BYPASS=1: every bucket its
 own hipMalloc, freed exported or not) on the C5 churn pattern -- the original trigger.
+Round 3's first session: every step above correct, and the bypassed esgd correct too
+(its peers now keep their mappings until shutdown).  What the cumulative steps never did
+is round 2's ORDER: deletion was local, so an owner freed its bucket while peers still
+mapped it, and the peers closed their old mapping only later, around opening the next
+bucket.  The `late-close` lines do exactly that (on top of `plain` and of `+engine`):
+the owner frees right after the reads, the peers close the old mapping only after opening
+the next buffer's handle.
 Every line prints the mismatches per size and rank.
 
   python tools/ipc_bisect.py [--world 8] [--only plain,+hostreg,...]
@@ -37,7 +44,7 @@ class Handle(C.Structure):
     _fields_ = [("reserved", C.c_char * 64)]
 
 
-def worker(rank, world, sizes, steps):
+def worker(rank, world, sizes, steps, late_close=False):
     import torch.distributed as dist
 
     import esgd
@@ -59,6 +66,7 @@ def worker(rank, world, sizes, steps):
     loc = dev.DeviceBuffer(max(sizes) // 4)
     pad = 2 * MiB if "+suballoc" in on else 0
     cache = {}
+    pending = []
     out = []
     for si, size in enumerate(sizes):
         p = vp()
@@ -95,6 +103,17 @@ def worker(rank, world, sizes, steps):
                 if got != {want}:
                     bad.append((q, off, sorted(got)[:4], want))
         dist.barrier()
+        if late_close:
+            # round 2's order: the owner frees at once; peers close the old mappings only
+            # after they opened the next buffer's (below, at the next size)
+            hip.hipFree(p)
+            for m in pending:
+                hip.hipIpcCloseMemHandle(vp(m))
+            pending = opened
+            cache.clear()
+            dist.barrier()
+            out.append((size, len(bad), bad[:2]))
+            continue
         if "+keepmaps" not in on:
             for m in opened:
                 hip.hipIpcCloseMemHandle(vp(m))
@@ -118,10 +137,13 @@ if __name__ == "__main__":
     ap.add_argument("--no-esgd", action="store_true")
     a = ap.parse_args()
     sizes = [16 * MiB, 256 * MiB]
-    names = a.only.split(",") if a.only else STEPS
+    names = a.only.split(",") if a.only else STEPS + ["late-close", "late-close+engine", "late-close-3"]
     for name in names:
-        steps = STEPS[: STEPS.index(name) + 1]
-        res = mp_workers.run("ipc_bisect_worker", a.world, sizes=sizes, steps=steps, timeout=300)
+        late = name.startswith("late-close")
+        steps = (["plain", "+engine"] if name.endswith("+engine") else ["plain"]) if late \
+            else STEPS[: STEPS.index(name) + 1]
+        sz = [16 * MiB, 256 * MiB, 64 * MiB] if name == "late-close-3" else sizes
+        res = mp_workers.run("ipc_bisect_worker", a.world, sizes=sz, steps=steps, late_close=late, timeout=300)
         nbad = [[n for _, n, _ in per] for per in res]
         print(f"world {a.world} {name:10s} mismatches per rank x size {nbad}", flush=True)
         for r, per in enumerate(res):
