@@ -134,8 +134,9 @@ int new_chunk(size_t bytes, int dev, Chunk **out) {
 // ESGD_ARENA_BYPASS=1 (diagnostics only, tools/ipc_bisect.py): every block is its own
 // hipMalloc and is freed, exported or not -- the pre-arena behaviour whose re-exports read
 // back wrong, so the trigger can be re-checked on a new driver.
-bool bypass() {
-    static const bool b = getenv("ESGD_ARENA_BYPASS") && *getenv("ESGD_ARENA_BYPASS") == '1';
+bool bypass() {   // 1: bypass; 2: also close peer mappings at schedule deletion (dataplane.cpp)
+    static const bool b = getenv("ESGD_ARENA_BYPASS") &&
+                          (*getenv("ESGD_ARENA_BYPASS") == '1' || *getenv("ESGD_ARENA_BYPASS") == '2');
     return b;
 }
 

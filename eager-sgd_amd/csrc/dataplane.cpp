@@ -175,6 +175,25 @@ static void ipc_close_all() {
     g_ipc.clear();
 }
 
+// ESGD_ARENA_BYPASS=2 (diagnostics only, tools/ipc_bisect.py): besides the arena bypass
+// (arena.cpp), a schedule's teardown closes the peer mappings it opened -- round 2's
+// pre-arena lifetime, where deletion was local and every rank closed its peers' buckets.
+static bool close_on_delete() {
+    static const bool b = getenv("ESGD_ARENA_BYPASS") && *getenv("ESGD_ARENA_BYPASS") == '2';
+    return b;
+}
+
+static void ipc_close_one(int peer, const uint8_t *h) {
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    IpcKey k;
+    k.peer = peer;
+    std::memcpy(k.h, h, 64);
+    auto it = g_ipc.find(k);
+    if (it == g_ipc.end()) return;
+    (void)hipIpcCloseMemHandle(it->second);
+    g_ipc.erase(it);
+}
+
 bool dataplane_mappings_closed() {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
     return g_mappings_closed;
@@ -1260,6 +1279,12 @@ struct IpcTransport final : Transport {
                 ESGD_TRACE("r%d sched %d: a peer never finished round %u, its published shard is kept\n",
                            s.rank, s.id, st->pub_round);
         }
+        if (close_on_delete())
+            for (int q = 0; q < s.world; ++q) {
+                if (q == s.rank) continue;
+                if (st->rbmap[q].base) ipc_close_one(q, st->rbmap[q].handle);
+                if (st->pubmap[q].base) ipc_close_one(q, st->pubmap[q].handle);
+            }
         if (st->pub && pub_free) free_bucket(st->pub);
         if (st->wire) free_bucket(st->wire);   // the done pairing: no peer still reads it
         if (!pub_free) st->retired.clear();   // earlier pubs too: a peer may be stuck on any

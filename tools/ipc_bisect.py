@@ -138,6 +138,8 @@ if __name__ == "__main__":
     a = ap.parse_args()
     sizes = [16 * MiB, 256 * MiB]
     names = a.only.split(",") if a.only else STEPS + ["late-close", "late-close+engine", "late-close-3"]
+    if a.only == "none":
+        names = []
     for name in names:
         late = name.startswith("late-close")
         steps = (["plain", "+engine"] if name.endswith("+engine") else ["plain"]) if late \
@@ -153,9 +155,11 @@ if __name__ == "__main__":
                     break
     if not a.no_esgd:
         # esgd itself, arena bypassed: 16 MiB schedule used, deleted, bucket freed, then
-        # 256 MiB (mp_workers.gpu_config: head / middle / tail of every rank vs the oracle)
-        os.environ["ESGD_ARENA_BYPASS"] = "1"
-        outs = mp_workers.run("gpu_config", a.world, kind=2, counts=[(16 * MiB) // 4, (256 * MiB) // 4],
-                              rounds=2, timeout=300)
-        print(f"world {a.world} esgd-arena-bypass ok per rank x size {[[v[3] for v in per] for per in outs]}",
-              flush=True)
+        # 256 MiB (mp_workers.gpu_config: head / middle / tail of every rank vs the oracle);
+        # mode 2 also closes the peers' mappings at each deletion (round 2's lifetime)
+        for mode in ("1", "2"):
+            os.environ["ESGD_ARENA_BYPASS"] = mode
+            outs = mp_workers.run("gpu_config", a.world, kind=2, counts=[(16 * MiB) // 4, (256 * MiB) // 4],
+                                  rounds=2, timeout=300)
+            print(f"world {a.world} esgd-arena-bypass={mode} ok per rank x size "
+                  f"{[[v[3] for v in per] for per in outs]}", flush=True)
