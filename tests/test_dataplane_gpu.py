@@ -8,6 +8,8 @@ int32 also matches the known answer of evaluation/allreduce.c:59-63.  Partial
 (solo / majority) rounds are checked through round tags: rank r contributes
 t * 64**r in round t, so the reduced value names the round each rank's buffer held.
 """
+import os
+
 import pytest
 
 from mp_workers import run
@@ -476,3 +478,26 @@ def test_second_job_after_ipc_mappings_closed_is_refused():
     for o in outs:
         assert o["ok"], o
         assert o["err"] and "fresh process" in o["err"], o
+
+
+@pytest.mark.parametrize("bypass", [None, "2"])
+def test_ipc_reexport_sequence_bitexact(bypass):
+    # the sequence behind round 2's wrong sums ("IPC arena"): 8 ranks, a
+    # 16 MiB bucket exported, mapped by every peer, its schedule deleted and the bucket
+    # freed, then a 256 MiB bucket exported and mapped.  Production (the arena: exported
+    # memory never freed) and ESGD_ARENA_BYPASS=2 (every bucket its own hipMalloc, freed,
+    # and the peers' mappings closed at deletion: round 2's lifetime) must both be
+    # bit-exact -- the second was in round 3 (tools/ipc_bisect.py); if a driver brings
+    # the fault back, this says so while the arena keeps production correct
+    counts = [(16 << 20) // 4, (256 << 20) // 4]
+    env = {} if bypass is None else {"ESGD_ARENA_BYPASS": bypass}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        _all_ok(run("gpu_config", 8, kind=MAJORITY, counts=counts, rounds=2, timeout=300))
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
