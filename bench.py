@@ -947,7 +947,7 @@ def run_allreduce(args, rank, world):
     from oracle import ffref
 
     import datetime
-    os.environ.setdefault("ESGD_TIMEOUT_S", "120")   # a stuck peer fails the run, not hangs it
+    os.environ.setdefault("ESGD_TIMEOUT_S", "60")    # a stuck peer fails the run, not hangs it
     dist.init_process_group("gloo", rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=180))
     comm.init(rank=rank, world=world)            # job id broadcast over gloo
@@ -967,49 +967,77 @@ def run_allreduce(args, rank, world):
     es = _lib.dtype_size(dt)
     count = int(args.bucket_mib * MiB) // es
     kind = {"solo": comm.SOLO, "majority": comm.MAJORITY, "allreduce": comm.ALLREDUCE}[args.schedule]
-    rb = dev.DeviceBuffer(count, dt)
-    dev.fill_uniform(rb, SEED, rank)
-    dev.synchronize()
-    sched = comm.Schedule(kind, None, rb, count, dtype=dt, async_=32, seed=6545343,
-                          buf=comm.BUF_DEVICE)
 
-    def step():
-        sched.post()
-        sched.wait()
-
-    for _ in range(args.warmup):
-        step()
-    dist.barrier(); comm.barrier(); dev.device_synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    dev.device_synchronize()
-    dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    wall = float(el.item())
-    t_step = wall / args.steps
-    stats = sched.stats()
-    stages = _stages_us(sched.timeline()[-args.steps:])
-
-    # parity outside the timed region: fresh inputs, one round, slices vs the oracle
-    parity = "skipped"
-    if dt == _lib.FLOAT:
-        dev.fill_uniform(rb, SEED + 1, rank)
+    def headline():
+        """The timed C3 rounds on the current transport, then a parity round."""
+        rb = dev.DeviceBuffer(count, dt)
+        dev.fill_uniform(rb, SEED, rank)
         dev.synchronize()
-        comm.barrier()
-        step()
-        got = rb.download()
-        m = min(count, 1 << 18)
-        ok = True
-        for start in (0, count - m):
-            xs = [ffref.fill_uniform(SEED + 1, r, m, start=start) for r in range(world)]
-            want = ffref.tree_sum(xs)
-            ok &= bool(np.array_equal(got[start:start + m].view(np.uint32), want.view(np.uint32)))
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        parity = "bitwise (head+tail slices, every rank)" if flag.item() else "MISMATCH"
-    _defer(sched, rb)
+        sched = comm.Schedule(kind, None, rb, count, dtype=dt, async_=32, seed=6545343,
+                              buf=comm.BUF_DEVICE)
+
+        def step():
+            sched.post()
+            sched.wait()
+
+        for _ in range(args.warmup):
+            step()
+        dist.barrier(); comm.barrier(); dev.device_synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        dev.device_synchronize()
+        dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        wall = float(el.item())
+        out = {"wall": wall, "stats": sched.stats(), "stages": _stages_us(sched.timeline()[-args.steps:])}
+        # parity outside the timed region: fresh inputs, one round, slices vs the oracle
+        out["parity"] = "skipped"
+        if dt == _lib.FLOAT:
+            dev.fill_uniform(rb, SEED + 1, rank)
+            dev.synchronize()
+            comm.barrier()
+            step()
+            got = rb.download()
+            m = min(count, 1 << 18)
+            ok = True
+            for start in (0, count - m):
+                xs = [ffref.fill_uniform(SEED + 1, r, m, start=start) for r in range(world)]
+                want = ffref.tree_sum(xs)
+                ok &= bool(np.array_equal(got[start:start + m].view(np.uint32), want.view(np.uint32)))
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            out["parity"] = "bitwise (head+tail slices, every rank)" if flag.item() else "MISMATCH"
+        _defer(sched, rb)
+        return out
+
+    # The headline runs on the default transport (IPC pull).  Should it fail on this node
+    # (the IPC data plane has not crossed xGMI before the driver's first 8-GPU run), every
+    # rank learns it through gloo and the line is measured over RCCL instead, saying so,
+    # rather than ending the run without a line.
+    transport = args.transport or os.environ.get("ESGD_TRANSPORT") or "ipc"
+    fallback = None
+    try:
+        h, failed = headline(), 0
+    except Exception as e:   # noqa: BLE001 -- reported in the line
+        import traceback
+        traceback.print_exc()
+        h, failed, err = None, 1, f"rank {rank}: {e!r}"[:300]
+    flag = torch.tensor([failed], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    if flag.item():
+        import esgd
+        if transport == "rccl" or world > esgd.device_count():
+            raise RuntimeError("C3 headline failed on " + transport)
+        errs = [None] * world
+        dist.all_gather_object(errs, err if failed else None)
+        fallback = {"from": transport, "errors": [e for e in errs if e]}
+        comm.set_transport("rccl")
+        transport = "rccl"
+        h = headline()
+    wall, stats, stages, parity = h["wall"], h["stats"], h["stages"], h["parity"]
+    t_step = wall / args.steps
 
     S = count * es
     algbw = S / t_step / 1e9
@@ -1027,8 +1055,7 @@ def run_allreduce(args, rank, world):
         "config": {"workload": f"C3: {args.schedule}-allreduce of one {args.bucket_mib:g} MiB "
                                f"{args.dtype} bucket per GPU, in place",
                    "bucket_bytes": S, "parallelism": f"dp{world} (one rank per GPU)",
-                   "transport": ("rccl p2p send/recv + tree kernel on a side stream"
-                                 if (args.transport or os.environ.get("ESGD_TRANSPORT")) == "rccl"
+                   "transport": ("rccl p2p send/recv + tree kernel on a side stream" if transport == "rccl"
                                  else "ipc pull (reduce-scatter tree kernel + all-gather) over xGMI")},
         "algbw_GBs": round(algbw, 2), "busbw_GBs": round(busbw, 2),
         "xgmi_frac": None if SHARED_GPU else round(t_min / t_step, 4),
@@ -1043,6 +1070,9 @@ def run_allreduce(args, rank, world):
         "rank0_stages_us": stages,
         "parity": parity,
     }
+    if fallback:
+        line["headline_fallback"] = fallback
+        args.no_extras = True   # the extra legs run on the IPC data plane that just failed
     if SHARED_GPU:
         line["rehearsal"] = "ranks share a GPU (HBM, not xGMI): no xGMI fraction or roofline"
 
