@@ -15,6 +15,7 @@ for s in $STEPS; do
   n1) timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench_n1.json 2> $O/bench_n1.err
       cp -r gpurun_out/bench_kernel_trace_split.json $O/ 2>/dev/null || true ;;
   n2) timeout -k 10 600 python bench.py --gpus 2 --steps 20 --warmup 5 > $O/bench_n2.json 2> $O/bench_n2.err ;;
+  n4) timeout -k 10 600 python bench.py --gpus 4 --steps 20 --warmup 5 > $O/bench_n4.json 2> $O/bench_n4.err ;;
   prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run \
           --output-format csv -- python $R/bench.py --no-pmc --no-trace --no-cpu-baseline --steps 100 \
           > $R/$O/bench_prof.json 2>&1) ;;
