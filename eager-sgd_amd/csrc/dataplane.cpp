@@ -1299,6 +1299,16 @@ struct NullTransport final : Transport {
     bool ordered_;   // the "rccl" flavour (same protocol; named for the issue-order tests)
     const char *name() const override { return ordered_ ? "none-ordered" : "none"; }
     int setup(Sched &) override { return ESGD_SUCCESS; }
+    // ESGD_TEST_FAIL_CONNECT=<rank>: that rank's connect fails (control-plane tests of the
+    // creation protocol; this transport moves no data)
+    int connect(Sched &s) override {
+        const char *e = getenv("ESGD_TEST_FAIL_CONNECT");
+        if (e && *e && atoi(e) == s.rank) {
+            set_error("connect failed on rank %d (ESGD_TEST_FAIL_CONNECT)", s.rank);
+            return ESGD_ERROR;
+        }
+        return ESGD_SUCCESS;
+    }
     int note_producer(Sched &, uint32_t, void *) override { return ESGD_SUCCESS; }
     int prepare(Sched &, uint32_t, bool) override { return ESGD_SUCCESS; }
     int launch(Sched &, uint32_t, bool) override { return ESGD_SUCCESS; }

@@ -218,11 +218,15 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     s->small_bytes = config_small_round_bytes();
     s->flag_mode = config_device_flags();
     // Schedule ids are never reused within a job and the segment starts zeroed, so the
-    // shared state of this id needs no reset (no barrier before setup).  Creation is two
-    // voted steps: setup (local: buckets, streams, publication) -> barrier -> every rank
-    // checks every rank's signature (kind, dtype, tag: creation order must match) and
-    // failures -> connect (mapping peers) -> barrier -> failures.  A failure anywhere
-    // fails the creation everywhere; no rank is left waiting on a peer that gave up.
+    // shared state of this id needs no reset (no barrier before setup).  Creation costs ONE
+    // node barrier: setup (local: buckets, streams, publication) -> barrier (the vote:
+    // setup failures) -> every rank checks every rank's signature (kind, dtype, tag,
+    // data-plane settings: the same data on every rank, so all fail alike) -> connect
+    // (mapping peers' publications, which the barrier guarantees).  A rank whose connect
+    // fails raises the schedule's connect_err and fails its creation; its peers' copies
+    // fail at their first join instead of waiting for a rank that gave up (step()).  No
+    // peer can join a round before every rank finished connect: a schedule is registered
+    // with the progress thread only when its creation returns.
     s->gen = 1;   // IpcSlot::gen == 1: published for this id
     const bool small = count * s->esize <= s->small_bytes;
     const uint64_t sig = (uint64_t(small) << 52) | (uint64_t(s->flag_mode & 3) << 50) |
@@ -261,13 +265,17 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
         }
     }
     const double c2 = now_s();
-    if (!rc) rc = tp->connect(*s);   // needs every peer's publication
-    const double c3 = now_s();
-    rc = vote(rc, s->sh->connect_err);
+    if (!rc) {
+        rc = tp->connect(*s);   // needs every peer's publication
+        if (rc) {
+            s->sh->connect_err.fetch_add(1, std::memory_order_acq_rel);
+            seg_wake(g_seg);
+        }
+    }
     if (dbg)
-        fprintf(stderr, "[esgd] r%d create sched %d (%llu x %d B): setup %.1f ms, vote %.1f ms, connect %.1f ms, "
-                "vote %.1f ms\n", g_rank, s->id, (unsigned long long)count, int(s->esize), (c1 - c0) * 1e3,
-                (c2 - c1) * 1e3, (c3 - c2) * 1e3, (now_s() - c3) * 1e3);
+        fprintf(stderr, "[esgd] r%d create sched %d (%llu x %d B): setup %.1f ms, vote %.1f ms, connect %.1f ms\n",
+                g_rank, s->id, (unsigned long long)count, int(s->esize), (c1 - c0) * 1e3, (c2 - c1) * 1e3,
+                (now_s() - c2) * 1e3);
     if (rc) {
         if (s->tstate) tp->teardown(*s);
         s->resolve_free = nullptr;   // the caller still owns ctx on failure
@@ -482,6 +490,11 @@ static bool step(Sched &s) {
         }
         return true;
     };
+    // a peer failed to connect its copy of this schedule (sched_create): it will never join
+    if (s.stage != ST_INFLIGHT && sh->connect_err.load(std::memory_order_acquire)) {
+        fail_locked(s, ESGD_ERROR, "another rank failed to connect this schedule (its own error says why)");
+        return true;
+    }
     switch (s.stage) {
     case ST_IDLE: {
         s.awaiting = false;

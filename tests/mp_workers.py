@@ -1214,3 +1214,36 @@ def op_void_peer_lost(rank, world, count=5000):
         second = op.forward_void(x)     # rank 1 never posts this round
         out.update(elapsed=time.time() - t0, own=bool(np.array_equal(second, x)), status=op.status())
     return out
+
+
+def cp_connect_failure(rank, world, bad_rank=1):
+    """One rank's connect fails: its creation fails; the others' creations succeed (one
+    barrier per creation) and their first round fails fast instead of waiting for the rank
+    that gave up; the communicator stays usable for the next schedule."""
+    if rank == bad_rank:
+        os.environ["ESGD_TEST_FAIL_CONNECT"] = str(rank)
+    from esgd import comm
+    from esgd._lib import EsgdError
+    comm.init()
+    err, round_err, t_fail = None, None, None
+    try:
+        s = comm.Schedule(comm.ALLREDUCE, None, None, 0, buf=comm.BUF_NONE)
+    except EsgdError as e:
+        err, s = str(e), None
+    if s is not None:
+        t0 = time.time()
+        try:
+            s.post()
+            s.wait()
+        except EsgdError as e:
+            round_err = str(e)
+        t_fail = time.time() - t0
+    os.environ.pop("ESGD_TEST_FAIL_CONNECT", None)
+    comm.barrier()
+    s2 = comm.Schedule(comm.ALLREDUCE, None, None, 0, buf=comm.BUF_NONE)
+    for _ in range(2):
+        s2.post()
+        s2.wait()
+    s2.delete()
+    comm.finalize()
+    return {"create_err": err, "round_err": round_err, "t_fail": t_fail}

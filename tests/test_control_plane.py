@@ -112,6 +112,19 @@ def test_failed_creation_fails_every_rank(world):
         assert o["recovered_s"] < 30
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_connect_failure_fails_peers_at_first_join(world):
+    # creation costs one barrier: a rank whose connect fails fails its creation, and its
+    # peers' copies fail at their first round within a progress pass, not after the timeout
+    outs = run("cp_connect_failure", world, bad_rank=world - 1)
+    bad = outs[-1]
+    assert bad["create_err"] and "ESGD_TEST_FAIL_CONNECT" in bad["create_err"], bad
+    for o in outs[:-1]:
+        assert o["create_err"] is None, o
+        assert o["round_err"] and "failed to connect" in o["round_err"], o
+        assert o["t_fail"] < 5, o
+
+
 def test_delete_while_rounds_in_flight():
     # sched_delete vs a progress pass holding the registry copy
     outs = run("cp_churn_inflight", 2, rounds=300, churn=40)
