@@ -1247,3 +1247,32 @@ def cp_connect_failure(rank, world, bad_rank=1):
     s2.delete()
     comm.finalize()
     return {"create_err": err, "round_err": round_err, "t_fail": t_fail}
+
+
+def cp_fresh_queue(rank, world, rounds=300):
+    """wait()'s fresh bit survives any run-ahead: rank 0 posts round 1, then
+    rank 1 activates rounds 1..`rounds` (solo, no synchronous round in between), so rank
+    0's progress thread joins rounds 2..rounds on those activations before rank 0 waits
+    for anything.  Rank 0's waits must then report round 1 fresh and every later one not
+    (a 256-slot ring indexed by round reported round 1 as round 257's)."""
+    comm = _comm()
+    s = comm.Schedule(comm.SOLO, None, None, 0, async_=100000, buf=comm.BUF_NONE)
+    if rank == 0:
+        s.post()
+    comm.barrier()
+    if rank == 1:
+        for _ in range(rounds):
+            s.post()
+    comm.barrier()
+    t0 = time.time()
+    while s.stats()["joined"] < rounds and time.time() - t0 < 30:
+        time.sleep(0.001)
+    fresh = [s.wait() for _ in range(rounds)] if rank == 0 else []
+    if rank == 1:
+        for _ in range(rounds):
+            s.wait()
+    joined = s.stats()["joined"]
+    comm.barrier()
+    s.delete()
+    comm.finalize()
+    return {"fresh": fresh, "joined": joined}

@@ -125,6 +125,13 @@ def test_connect_failure_fails_peers_at_first_join(world):
         assert o["t_fail"] < 5, o
 
 
+def test_wait_fresh_bit_survives_run_ahead():
+    outs = run("cp_fresh_queue", 2, rounds=300)
+    assert outs[0]["joined"] == 300, outs[0]["joined"]
+    fresh = outs[0]["fresh"]
+    assert fresh[0] is True and not any(fresh[1:]), [i + 1 for i, f in enumerate(fresh) if f]
+
+
 def test_delete_while_rounds_in_flight():
     # sched_delete vs a progress pass holding the registry copy
     outs = run("cp_churn_inflight", 2, rounds=300, churn=40)
