@@ -187,3 +187,81 @@ def test_lost_peer_fails_the_round_instead_of_hanging():
     for o in outs[:-1]:
         assert o["error"] and ("timed out" in o["error"] or "joined" in o["error"]), o
         assert 1.5 <= o["elapsed_s"] <= 15, o
+
+
+# ---- ranks in different PID namespaces (one container per GPU sharing /dev/shm) -------
+
+def _unshare_ok():
+    import subprocess
+    try:
+        return subprocess.run(["unshare", "-p", "-f", "--kill-child", "true"], capture_output=True,
+                              timeout=10).returncode == 0
+    except Exception:
+        return False
+
+
+_RANK = ("import sys; sys.path.insert(0, %r); from esgd import comm; "
+         "comm.init(job_id=%r, rank=%d, world=2); "
+         "s = comm.Schedule(comm.ALLREDUCE, None, None, 0, buf=comm.BUF_NONE)\n"
+         "for _ in range(3):\n    s.post(); s.wait()\n"
+         "s.delete(); comm.finalize(); print('rank done')")
+
+
+def _rank_cmd(job, rank, ns):
+    import sys
+
+    from conftest import PKG
+    cmd = [sys.executable, "-c", _RANK % (PKG, job, rank)]
+    return (["unshare", "-p", "-f", "--kill-child"] + cmd) if ns else cmd
+
+
+@pytest.mark.skipif(not _unshare_ok(), reason="needs unshare -p (PID namespaces)")
+def test_creator_in_another_pid_namespace_is_joined():
+    # rank 0 in its own PID namespace -- its pid means nothing to rank 1, which
+    # must still attach (creator liveness = rank 0's init-barrier heartbeat there)
+    import subprocess
+    import uuid
+    job = "pidns-" + uuid.uuid4().hex[:12]
+    env = dict(os.environ, ESGD_TIMEOUT_S="30")
+    p0 = subprocess.Popen(_rank_cmd(job, 0, True), env=env, stdout=subprocess.PIPE, text=True)
+    p1 = subprocess.Popen(_rank_cmd(job, 1, False), env=env, stdout=subprocess.PIPE, text=True)
+    out0, _ = p0.communicate(timeout=90)
+    out1, _ = p1.communicate(timeout=90)
+    assert p0.returncode == 0 and "rank done" in out0
+    assert p1.returncode == 0 and "rank done" in out1
+
+
+@pytest.mark.skipif(not _unshare_ok(), reason="needs unshare -p (PID namespaces)")
+def test_stale_segment_from_another_pid_namespace_is_not_joined():
+    # a crashed rank 0 of another PID namespace left its segment behind: its heartbeat
+    # stops, so once it is stale a new job with the same id does not attach to it
+    import signal
+    import subprocess
+    import time
+    import uuid
+    job = "pidns-stale-" + uuid.uuid4().hex[:12]
+    path = "/dev/shm/esgd-" + job
+    env = dict(os.environ, ESGD_TIMEOUT_S="60")
+    p = subprocess.Popen(_rank_cmd(job, 0, True), env=env)
+    try:
+        t0 = time.time()
+        while not os.path.exists(path) and time.time() - t0 < 60:
+            time.sleep(0.05)
+        assert os.path.exists(path), "rank 0 never published its segment"
+    finally:
+        p.send_signal(signal.SIGKILL)
+        p.wait()
+    try:
+        assert os.path.exists(path)
+        time.sleep(2.5)          # past the 2 s heartbeat window
+        env = dict(os.environ, ESGD_TIMEOUT_S="30")
+        p1 = subprocess.Popen(_rank_cmd(job, 1, False), env=env, stdout=subprocess.PIPE, text=True)
+        time.sleep(1.0)          # rank 1 meets the stale file first
+        p0 = subprocess.Popen(_rank_cmd(job, 0, False), env=env, stdout=subprocess.PIPE, text=True)
+        out0, _ = p0.communicate(timeout=90)
+        out1, _ = p1.communicate(timeout=90)
+        assert p0.returncode == 0 and "rank done" in out0
+        assert p1.returncode == 0 and "rank done" in out1
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
