@@ -3,7 +3,7 @@
 # sharing the box's one GPU: a rehearsal), rocprofv3 kernel statistics of the N = 1 bench,
 # and the IPC re-export bisection.  Each GPU step has its own time limit; the first
 # failure ends the session.
-#   bash tools/bench_round.sh <tag> [steps...]   steps: n1 n2 prof bisect sweep (default: n1 n2 prof bisect)
+#   bash tools/bench_round.sh <tag> [steps...]   steps: smoke n1 n2 n4 prof bisect sweep (default: n1 n2 prof bisect)
 set -e
 export ESGD_TIMEOUT_S=60
 O=gpurun_out/${1:-bench_round}; shift || true
@@ -12,6 +12,7 @@ mkdir -p $O
 R=$PWD
 for s in $STEPS; do
   case $s in
+  smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
   n1) timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench_n1.json 2> $O/bench_n1.err
       cp -r gpurun_out/bench_kernel_trace_split.json $O/ 2>/dev/null || true ;;
   n2) timeout -k 10 600 python bench.py --gpus 2 --steps 20 --warmup 5 > $O/bench_n2.json 2> $O/bench_n2.err ;;
