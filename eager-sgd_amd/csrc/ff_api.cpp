@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -215,5 +216,127 @@ int ffschedule_post_stream(ffschedule_h sched, void *stream) { return esgd_sched
 int ffschedule_wait(ffschedule_h sched) { return esgd_schedule_wait(sched); }
 int ffschedule_test(ffschedule_h sched, int *flag) { return esgd_schedule_test(sched, flag); }
 int ffschedule_delete(ffschedule_h sched) { return esgd_schedule_delete(sched); }
+
+}  // extern "C"
+
+// ---- single computations: ffcomp (src/ffcomp.c:7-38) -----------------------------------
+// The reference's direct handle on its reduction kernel: an op that, when posted, runs
+// ffop_gcomp_execute once -- size = MIN of the three buffers' counts, c = a + b (FFSUM,
+// ffop_gcomp_operator.c:33-58, operand a first) or c = a (FFIDENTITY, the move, :61-72) --
+// and completes (ffop_gcomp.c:29-64).  Here the post queues the tree kernel (k = 2, the
+// same operand order as esgd_vsum) on the library stream: host buffers through
+// esgd_reduce_host (the reference's buffers are host memory), device buffers with
+// ESGD_FF_DEVICE_BUFFERS; an event marks completion for ffop_wait / ffop_test.
+namespace {
+struct FFComp {
+    void *a = nullptr, *b = nullptr, *c = nullptr;   // addresses (ffcomp)
+    FFBuf *ba = nullptr, *bb = nullptr, *bc = nullptr;   // descriptors (ffcomp_b)
+    int count = 0, dtype = 0, op = FFSUM;
+    bool device = false;
+    hipEvent_t ev = nullptr;
+    bool posted = false;
+};
+
+int comp_make(FFComp *o, ffop_h *out) {
+    ESGD_ARG(o->op == FFSUM || o->op == FFIDENTITY,
+             "ffcomp: operator %d -- libesgd runs FFSUM and FFIDENTITY (custom operators are host "
+             "functions, not GPU code: DESIGN.md §8)", o->op);
+    ESGD_ARG(esgd_dtype_size(o->dtype) > 0, "ffcomp: unsupported datatype %d", o->dtype);
+    *out = reinterpret_cast<ffop_h>(o);
+    return FFSUCCESS;
+}
+}  // namespace
+
+extern "C" {
+
+int ffcomp(void *addr1, void *addr2, int count, ffdatatype_h datatype, ffoperator_h op, int options,
+           void *addr3, ffop_h *out) {
+    ESGD_ARG(out && addr1 && addr3 && count >= 0, "ffcomp: null buffer or output, or negative count");
+    ESGD_ARG(op == FFIDENTITY || addr2, "ffcomp: FFSUM needs two inputs");
+    auto *o = new FFComp();
+    o->a = addr1; o->b = addr2; o->c = addr3;
+    o->count = count; o->dtype = datatype; o->op = op;
+    o->device = (options & ESGD_FF_DEVICE_BUFFERS) != 0;
+    if (int rc = comp_make(o, out)) { delete o; return rc; }
+    return FFSUCCESS;
+}
+
+int ffcomp_b(ffbuffer_h b1, ffbuffer_h b2, ffoperator_h op, int options, ffbuffer_h b3, ffop_h *out) {
+    ESGD_ARG(out && b1 && b3, "ffcomp_b: null buffer or output");
+    ESGD_ARG(op == FFIDENTITY || b2, "ffcomp_b: FFSUM needs two inputs");
+    auto *o = new FFComp();
+    o->ba = reinterpret_cast<FFBuf *>(b1);
+    o->bb = reinterpret_cast<FFBuf *>(b2);
+    o->bc = reinterpret_cast<FFBuf *>(b3);
+    o->dtype = o->ba->dtype;   // "they are the same" (ffop_gcomp.c:53)
+    o->op = op;
+    o->device = (options & ESGD_FF_DEVICE_BUFFERS) != 0;
+    if (int rc = comp_make(o, out)) { delete o; return rc; }
+    return FFSUCCESS;
+}
+
+int ffcomp_operator_create(ffoperator_fun_t, int, ffoperator_h *) {
+    esgd::set_error("ffcomp_operator_create: custom operators are host functions and do not run on the GPU "
+                    "path (DESIGN.md §8)");
+    return FFINVALID_ARG;
+}
+
+int ffcomp_operator_delete(ffoperator_h) { return FFINVALID_ARG; }
+
+int ffop_post(ffop_h h) {
+    auto *o = reinterpret_cast<FFComp *>(h);
+    ESGD_ARG(o, "ffop_post: null op");
+    // buffers re-read at every post, size = MIN of the counts (ffop_gcomp.c:32-52)
+    void *a = o->ba ? o->ba->ptr : o->a, *b = o->bb ? o->bb->ptr : o->b, *c = o->bc ? o->bc->ptr : o->c;
+    int64_t n = o->ba ? int64_t(o->ba->count) : int64_t(o->count);
+    if (o->bb) n = std::min<int64_t>(n, o->bb->count);
+    if (o->bc) n = std::min<int64_t>(n, o->bc->count);
+    if (!o->ev) ESGD_HIP(hipEventCreateWithFlags(&o->ev, hipEventDisableTiming));
+    hipStream_t s = default_stream();
+    if (n > 0) {
+        if (o->op == FFIDENTITY) {
+            ESGD_HIP(hipMemcpyAsync(c, a, size_t(n) * esgd_dtype_size(o->dtype), hipMemcpyDefault, s));
+        } else {
+            const void *in[2] = {b, a};   // tree order x1 + x0 = a + b, as esgd_vsum
+            const int rc = o->device ? esgd_reduce(o->dtype, 2, in, c, uint64_t(n), s)
+                                     : esgd_reduce_host(o->dtype, 2, in, c, uint64_t(n), s);
+            if (rc) return rc;
+        }
+    }
+    ESGD_HIP(hipEventRecord(o->ev, s));
+    o->posted = true;
+    return FFSUCCESS;
+}
+
+int ffop_wait(ffop_h h) {
+    auto *o = reinterpret_cast<FFComp *>(h);
+    ESGD_ARG(o && o->posted, "ffop_wait: op not posted");
+    ESGD_HIP(hipEventSynchronize(o->ev));
+    o->posted = false;
+    return FFSUCCESS;
+}
+
+int ffop_test(ffop_h h, int *flag) {
+    auto *o = reinterpret_cast<FFComp *>(h);
+    ESGD_ARG(o && flag, "ffop_test: null argument");
+    if (!o->posted) { *flag = 1; return FFSUCCESS; }
+    const hipError_t e = hipEventQuery(o->ev);
+    if (e == hipErrorNotReady) { *flag = 0; return FFSUCCESS; }
+    if (e != hipSuccess) return hip_fail(e, "ffop_test", __FILE__, __LINE__);
+    *flag = 1;
+    o->posted = false;
+    return FFSUCCESS;
+}
+
+int ffop_free(ffop_h h) {
+    auto *o = reinterpret_cast<FFComp *>(h);
+    if (!o) return FFSUCCESS;
+    if (o->ev) {
+        (void)hipEventSynchronize(o->ev);
+        (void)hipEventDestroy(o->ev);
+    }
+    delete o;
+    return FFSUCCESS;
+}
 
 }  // extern "C"

@@ -59,6 +59,8 @@ typedef int ffdatatype_h;
 typedef int ffoperator_h;
 typedef uint64_t ffschedule_h;
 typedef uint64_t ffbuffer_h;
+typedef uint64_t ffop_h;
+typedef int (*ffoperator_fun_t)(void *, void *, void *, uint32_t, ffdatatype_h);
 
 /* buffer descriptors (src/ffbuffer.c:10-95): addr NULL = library-allocated (grows on
  * resize like the reference's realloc).  With FFCOLL_BUFFERS a collective takes
@@ -94,6 +96,23 @@ int ffschedule_delete(ffschedule_h sched);
 
 /* extension: post with the stream that produced sndbuff (device buffers) */
 int ffschedule_post_stream(ffschedule_h sched, void *stream);
+
+/* One computation (src/ffcomp.c:7-38, ff.h:132-135): posting it runs the reduction kernel
+ * once over MIN(count1, count2, count3) elements (src/components/gcomp/ffop_gcomp.c:29-64):
+ * FFSUM c = a + b, FFIDENTITY c = a (b may be NULL).  Host buffers (the reference's); with
+ * ESGD_FF_DEVICE_BUFFERS device buffers.  ffcomp_b takes ffbuffer_h descriptors and re-reads
+ * them at every post.  Other operators and ffcomp_operator_create (user host functions)
+ * return FFINVALID_ARG: no host compute path exists here. */
+int ffcomp(void *addr1, void *addr2, int count, ffdatatype_h datatype, ffoperator_h ffoperator, int options,
+           void *addr3, ffop_h *op);
+int ffcomp_b(ffbuffer_h buffer1, ffbuffer_h buffer2, ffoperator_h ffoperator, int options, ffbuffer_h buffer3,
+             ffop_h *op);
+int ffcomp_operator_create(ffoperator_fun_t fun, int commutative, ffoperator_h *handle);
+int ffcomp_operator_delete(ffoperator_h handle);
+int ffop_post(ffop_h op);              /* src/ffop.c:59-72 */
+int ffop_wait(ffop_h op);              /* src/ffop.c:143-177 */
+int ffop_test(ffop_h op, int *flag);
+int ffop_free(ffop_h op);
 
 #ifdef __cplusplus
 }

@@ -10,7 +10,11 @@
  *     user-managed and one library-managed (evaluation/allreduce_buffers_user_managed.c,
  *     allreduce_buffers_fflib_managed.c), same (i + j) * size answer;
  *   - FFCOLL_BUFFERS under ffsolo_allreduce with a late rank (posts of rounds a peer
- *     already ran are accepted).
+ *     already ran are accepted);
+ *   - single computations: ffcomp(a, b, FFSUM) -> c == a + b for rand() int32 inputs
+ *     (evaluation/simple_computation.c:48-75), the same in fp32 against C's own IEEE add,
+ *     FFIDENTITY, ffcomp_b over descriptors of different counts (MIN of the counts,
+ *     ffop_gcomp.c:52), and ffcomp_operator_create refused (no host compute path).
  * Ranks come from RANK / WORLD_SIZE / ESGD_JOB_ID (no MPI).  Exit status 0 = passed.
  */
 #define _POSIX_C_SOURCE 199309L
@@ -36,6 +40,56 @@ static int check_int(const int32_t *got, const int32_t *want, int n, const char 
     return 0;
 }
 
+/* simple_computation.c on the GPU kernel, every rank on its own */
+static int single_computations(int count) {
+    int32_t *a = malloc(count * sizeof(int32_t)), *b = malloc(count * sizeof(int32_t)),
+            *c = calloc(count, sizeof(int32_t)), *w = malloc(count * sizeof(int32_t));
+    float *fa = malloc(count * sizeof(float)), *fb = malloc(count * sizeof(float)), *fc = calloc(count, sizeof(float));
+    srand(12345);
+    for (int i = 0; i < count; ++i) {
+        a[i] = rand(); b[i] = rand();
+        w[i] = (int32_t)((uint32_t)a[i] + (uint32_t)b[i]);   /* the reference's int add, wrapped */
+        fa[i] = (float)rand() / RAND_MAX - 0.5f; fb[i] = (float)rand() / RAND_MAX * 1e-3f;
+    }
+    ffop_h op;
+    if (ffcomp(a, b, count, FFINT32, FFSUM, 0, c, &op) != FFSUCCESS || ffop_post(op) != FFSUCCESS ||
+        ffop_wait(op) != FFSUCCESS) {
+        fprintf(stderr, "ffcomp int32: %s\n", esgd_last_error());
+        return 1;
+    }
+    ffop_free(op);
+    if (check_int(c, w, count, "ffcomp FFSUM int32", 0)) return 1;
+    if (ffcomp(fa, fb, count, FFFLOAT, FFSUM, 0, fc, &op) != FFSUCCESS || ffop_post(op) != FFSUCCESS) return 1;
+    int flag = 0;
+    while (!flag)
+        if (ffop_test(op, &flag) != FFSUCCESS) return 1;
+    ffop_free(op);
+    for (int i = 0; i < count; ++i)
+        if (fc[i] != fa[i] + fb[i]) { fprintf(stderr, "ffcomp FFSUM fp32: element %d\n", i); return 1; }
+    /* FFIDENTITY: the move */
+    if (ffcomp(a, NULL, count, FFINT32, FFIDENTITY, 0, c, &op) != FFSUCCESS || ffop_post(op) != FFSUCCESS ||
+        ffop_wait(op) != FFSUCCESS) return 1;
+    ffop_free(op);
+    if (check_int(c, a, count, "ffcomp FFIDENTITY", 0)) return 1;
+    /* descriptors of different counts: size = MIN(counts), the rest of c untouched */
+    ffbuffer_h ba, bb, bc;
+    for (int i = 0; i < count; ++i) c[i] = -7;
+    const int m = count / 2;
+    ffbuffer_create(a, count, FFINT32, 0, &ba);
+    ffbuffer_create(b, m, FFINT32, 0, &bb);
+    ffbuffer_create(c, count, FFINT32, 0, &bc);
+    if (ffcomp_b(ba, bb, FFSUM, 0, bc, &op) != FFSUCCESS || ffop_post(op) != FFSUCCESS || ffop_wait(op) != FFSUCCESS)
+        return 1;
+    ffop_free(op);
+    if (check_int(c, w, m, "ffcomp_b MIN(counts)", 0)) return 1;
+    for (int i = m; i < count; ++i) if (c[i] != -7) { fprintf(stderr, "ffcomp_b wrote past MIN(counts)\n"); return 1; }
+    ffbuffer_delete(ba); ffbuffer_delete(bb); ffbuffer_delete(bc);
+    ffoperator_h custom;
+    if (ffcomp_operator_create(NULL, 1, &custom) != FFINVALID_ARG) return 1;
+    free(a); free(b); free(c); free(w); free(fa); free(fb); free(fc);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     const int count = argc > 1 ? atoi(argv[1]) : 10007;
     const int iters = argc > 2 ? atoi(argv[2]) : 4;
@@ -43,6 +97,7 @@ int main(int argc, char **argv) {
     int rank, size, failed = 0;
     ffrank(&rank);
     ffsize(&size);
+    if (single_computations(count)) { fprintf(stderr, "[rank %d] single computations failed\n", rank); return 1; }
     int32_t *to_reduce = calloc(count, sizeof(int32_t));
     int32_t *reduced = calloc(count, sizeof(int32_t));
     int32_t *want = calloc(count, sizeof(int32_t));

@@ -22,6 +22,7 @@ def declared_functions():
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         text = re.sub(r"//[^\n]*", "", text)
         text = re.sub(r"^\s*#.*$", "", text, flags=re.M)
+        text = re.sub(r"^\s*typedef[^;]*;", "", text, flags=re.M)   # function-pointer typedefs
         for m in DECL.finditer(text):
             name = m.group(1)
             if name in ("if", "while", "for", "return", "sizeof", "typedef"):
