@@ -218,15 +218,15 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     s->small_bytes = config_small_round_bytes();
     s->flag_mode = config_device_flags();
     // Schedule ids are never reused within a job and the segment starts zeroed, so the
-    // shared state of this id needs no reset (no barrier before setup).  Creation costs ONE
-    // node barrier: setup (local: buckets, streams, publication) -> barrier (the vote:
-    // setup failures) -> every rank checks every rank's signature (kind, dtype, tag,
-    // data-plane settings: the same data on every rank, so all fail alike) -> connect
-    // (mapping peers' publications, which the barrier guarantees).  A rank whose connect
-    // fails raises the schedule's connect_err and fails its creation; its peers' copies
-    // fail at their first join instead of waiting for a rank that gave up (step()).  No
-    // peer can join a round before every rank finished connect: a schedule is registered
-    // with the progress thread only when its creation returns.
+    // shared state of this id needs no reset (no barrier before setup).  Creation costs TWO
+    // node barriers: setup (local: buckets, streams, publication) -> vote 1 (setup failures)
+    // -> every rank checks every rank's signature (kind, dtype, tag, data-plane settings: the
+    // same data on every rank, so all fail alike) -> connect (mapping peers' publications,
+    // which vote 1 guarantees) -> vote 2 (connect failures).  Vote 2 is not optional: without
+    // it a rank that returned early posts round 1 while a peer is still mapping its
+    // publication, and a resolve-mode schedule re-publishes its bucket at that post -- the
+    // peer then maps a torn (handle, offset, ver) and pulls a stale bucket (round 3's r03f
+    // session: FFCOLL_BUFFERS sums with zeroed shards at 4 ranks).
     s->gen = 1;   // IpcSlot::gen == 1: published for this id
     const bool small = count * s->esize <= s->small_bytes;
     const uint64_t sig = (uint64_t(small) << 52) | (uint64_t(s->flag_mode & 3) << 50) |
@@ -267,10 +267,7 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     const double c2 = now_s();
     if (!rc) {
         rc = tp->connect(*s);   // needs every peer's publication
-        if (rc) {
-            s->sh->connect_err.fetch_add(1, std::memory_order_acq_rel);
-            seg_wake(g_seg);
-        }
+        rc = vote(rc, s->sh->connect_err);
     }
     if (dbg)
         fprintf(stderr, "[esgd] r%d create sched %d (%llu x %d B): setup %.1f ms, vote %.1f ms, connect %.1f ms\n",
@@ -490,11 +487,6 @@ static bool step(Sched &s) {
         }
         return true;
     };
-    // a peer failed to connect its copy of this schedule (sched_create): it will never join
-    if (s.stage != ST_INFLIGHT && sh->connect_err.load(std::memory_order_acquire)) {
-        fail_locked(s, ESGD_ERROR, "another rank failed to connect this schedule (its own error says why)");
-        return true;
-    }
     switch (s.stage) {
     case ST_IDLE: {
         s.awaiting = false;

@@ -48,7 +48,7 @@ struct alignas(64) SchedShm {
     std::atomic<uint32_t> activations[kMaxRanks];  // diagnostics: rounds activated by r
     std::atomic<uint32_t> ready_count;   // joins so far, all ranks (issue-ring append)
     std::atomic<uint32_t> setup_err;     // ranks whose setup failed (first creation vote)
-    std::atomic<uint32_t> connect_err;   // ranks whose connect failed (their peers fail the first join)
+    std::atomic<uint32_t> connect_err;   // ranks whose connect failed (the second creation vote)
     std::atomic<uint64_t> sig[kMaxRanks];   // creation signature of rank r: kind, dtype, tag
     IpcSlot slot[kMaxRanks];   // rank r's receive bucket (peers read shard q of it in phase 1)
     IpcSlot pub[kMaxRanks];    // rank r's reduced shard, published for the all-gather

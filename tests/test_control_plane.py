@@ -113,15 +113,14 @@ def test_failed_creation_fails_every_rank(world):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_connect_failure_fails_peers_at_first_join(world):
-    # creation costs one barrier: a rank whose connect fails fails its creation, and its
-    # peers' copies fail at their first round within a progress pass, not after the timeout
+def test_connect_failure_fails_every_creation(world):
+    # creation costs two barriers: a rank whose connect fails fails its creation, and its
+    # peers fail theirs at the connect vote, not after the timeout
     outs = run("cp_connect_failure", world, bad_rank=world - 1)
     bad = outs[-1]
     assert bad["create_err"] and "ESGD_TEST_FAIL_CONNECT" in bad["create_err"], bad
     for o in outs[:-1]:
-        assert o["create_err"] is None, o
-        assert o["round_err"] and "failed to connect" in o["round_err"], o
+        assert o["create_err"] and "another rank failed to register" in o["create_err"], o
         assert o["t_fail"] < 5, o
 
 
