@@ -584,7 +584,7 @@ def _download_slice(buf, start, n):
 
 def gpu_config(rank, world, kind, counts, dtype_name="fp32", rounds=2, async_=32, seed=6545343,
                check=65536, transport="ipc", keep=False, detail=False, free=True, env=None,
-               alloc_ahead=False):
+               alloc_ahead=False, close_before_free=False):
     """A BASELINE.json workload: one in-place bucket per rank per size in `counts`, every
     rank's bucket written BEFORE a barrier and then posted (the pattern of
     evaluation/{solo,rand}_allreduce_correctness.c:76-97: whichever rank activates, every
@@ -636,6 +636,10 @@ def gpu_config(rank, world, kind, counts, dtype_name="fp32", rounds=2, async_=32
             kept.append((s, rb))
         else:
             s.delete()
+            if close_before_free:
+                # every rank's deletion (closing its peer mappings under ESGD_ARENA_BYPASS=2)
+                # happens before any rank frees a bucket a peer had mapped
+                comm.barrier()
             if alloc_ahead and i + 1 < len(counts):
                 nxt = dev.DeviceBuffer(counts[i + 1], dt)
             if free:

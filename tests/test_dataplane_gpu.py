@@ -486,15 +486,17 @@ def test_ipc_reexport_sequence_bitexact(bypass):
     # 16 MiB bucket exported, mapped by every peer, its schedule deleted and the bucket
     # freed, then a 256 MiB bucket exported and mapped.  Production (the arena: exported
     # memory never freed) and ESGD_ARENA_BYPASS=2 (every bucket its own hipMalloc, freed,
-    # and the peers' mappings closed at deletion: round 2's lifetime) must both be
-    # bit-exact -- the second was in round 3 (tools/ipc_bisect.py); if a driver brings
-    # the fault back, this says so while the arena keeps production correct
+    # the peers' mappings closed at deletion) with every rank's deletion before any free
+    # must both be bit-exact.  Round 2's order -- an owner freeing while a slower peer still
+    # maps the bucket -- is outside the IPC contract and not tested here: on round 3's
+    # boxes it made the owner's next hipIpcGetMemHandle fail (profiles/r03/README.md)
     counts = [(16 << 20) // 4, (256 << 20) // 4]
     env = {} if bypass is None else {"ESGD_ARENA_BYPASS": bypass}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
-        _all_ok(run("gpu_config", 8, kind=MAJORITY, counts=counts, rounds=2, timeout=300))
+        _all_ok(run("gpu_config", 8, kind=MAJORITY, counts=counts, rounds=2, timeout=300,
+                    close_before_free=bypass is not None))
     finally:
         for k, v in old.items():
             if v is None:

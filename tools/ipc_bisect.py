@@ -135,6 +135,7 @@ if __name__ == "__main__":
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--only", default=None)
     ap.add_argument("--no-esgd", action="store_true")
+    ap.add_argument("--repeat", type=int, default=1, help="runs of each esgd bypass mode")
     a = ap.parse_args()
     sizes = [16 * MiB, 256 * MiB]
     names = a.only.split(",") if a.only else STEPS + ["late-close", "late-close+engine", "late-close-3"]
@@ -156,10 +157,20 @@ if __name__ == "__main__":
     if not a.no_esgd:
         # esgd itself, arena bypassed: 16 MiB schedule used, deleted, bucket freed, then
         # 256 MiB (mp_workers.gpu_config: head / middle / tail of every rank vs the oracle);
-        # mode 2 also closes the peers' mappings at each deletion (round 2's lifetime)
-        for mode in ("1", "2"):
+        # mode 2 also closes the peers' mappings at each deletion (round 2's lifetime: an
+        # owner may free before a slower peer closed); "2 close-first" puts a barrier
+        # between every rank's deletion and any free (the IPC contract: no free under a
+        # peer's mapping)
+        for mode, cbf in (("1", False), ("2", False), ("2", True)):
             os.environ["ESGD_ARENA_BYPASS"] = mode
-            outs = mp_workers.run("gpu_config", a.world, kind=2, counts=[(16 * MiB) // 4, (256 * MiB) // 4],
-                                  rounds=2, timeout=300)
-            print(f"world {a.world} esgd-arena-bypass={mode} ok per rank x size "
-                  f"{[[v[3] for v in per] for per in outs]}", flush=True)
+            for rep in range(a.repeat):
+                try:
+                    outs = mp_workers.run("gpu_config", a.world, kind=2,
+                                          counts=[(16 * MiB) // 4, (256 * MiB) // 4], rounds=2,
+                                          close_before_free=cbf, timeout=300)
+                    res = f"ok per rank x size {[[v[3] for v in per] for per in outs]}"
+                except AssertionError as e:
+                    lines = [ln for ln in str(e).splitlines() if "esgd_schedule_create" in ln]
+                    res = "ERROR " + " | ".join(ln.split("esgd_schedule_create: ")[-1] for ln in lines)
+                print(f"world {a.world} esgd-arena-bypass={mode}{' close-first' if cbf else ''} "
+                      f"#{rep}: {res}", flush=True)
