@@ -1286,3 +1286,24 @@ def cp_fresh_queue(rank, world, rounds=300):
     s.delete()
     comm.finalize()
     return {"fresh": fresh, "joined": joined}
+
+
+def cp_create_many(rank, world, n=161, rounds=1):
+    """`n` schedules created back to back (the per-tensor wrapper's 161 buckets,
+    opt_esgd_solo_imagenet_imbalance.py:85-248), each run for `rounds` rounds, then deleted:
+    the creation cost per schedule (two node barriers each) on the control plane."""
+    from esgd import comm
+    comm.init()
+    comm.barrier()
+    t0 = time.perf_counter()
+    scheds = [comm.Schedule(comm.SOLO, None, None, 0, buf=comm.BUF_NONE) for _ in range(n)]
+    t_create = time.perf_counter() - t0
+    for _ in range(rounds):
+        for s in scheds:
+            s.post()
+        for s in scheds:
+            s.wait()
+    for s in scheds:
+        s.delete()
+    comm.finalize()
+    return {"create_ms_per_schedule": t_create * 1e3 / n}

@@ -264,3 +264,11 @@ def test_stale_segment_from_another_pid_namespace_is_not_joined():
     finally:
         if os.path.exists(path):
             os.unlink(path)
+
+
+def test_creation_cost_161_schedules():
+    # two node barriers per creation: the per-tensor wrapper's 161 buckets
+    # cost a fraction of a millisecond each, once per job (generous bound for a loaded CI box)
+    outs = run("cp_create_many", 4, n=161)
+    worst = max(o["create_ms_per_schedule"] for o in outs)
+    assert worst < 20, worst
