@@ -93,6 +93,7 @@ struct AllreduceOp {
     int64_t bytes = 0;
     int status = 0;                       // first failure of a void entry point (ESGD_OP_ON_ERROR_LOCAL)
     bool warned = false;
+    bool pending = false;                 // a split round posted and not yet waited
 
     // Lazy creation of the buckets and the schedule (:288-298); an esgd status (the void
     // entry points abort on failure, the status-returning ones pass it on).
@@ -132,30 +133,39 @@ struct AllreduceOp {
     }
 
     // Device round: the gradient is already in sb (queued on s).  post -> wait -> drop a
-    // late gradient -> `out` consumes rb on s -> release.  Returns an esgd status.
-    template <class Out>
-    int device_round(hipStream_t s, Out &&out) {
-        const size_t nbytes = size_t(len) * sizeof(float);
+    // late gradient -> `out` consumes rb on s -> release.  Returns an esgd status.  The
+    // split entry points run the same steps as post_round() and finish_round().
+    int post_round(hipStream_t s) {
         // the snapshot of this round waits for the copy-in just queued on the caller's
         // stream (the data plane's streams are non-blocking: the NULL stream is named)
         void *ps = s ? static_cast<void *>(s) : ESGD_STREAM_NULL;
         // a round a peer's activation carried this rank through before this post took
         // zeros, not the gradient (FRESH_ONLY): the gradient is dropped, and the next
         // copy-in overwrites the send bucket before it is read again
-        if (int rc = esgd_schedule_post(sched, ps, nullptr)) return rc;
+        return esgd_schedule_post(sched, ps, nullptr);
+    }
+
+    template <class Out>
+    int finish_round(hipStream_t s, Out &&out) {
+        void *ps = s ? static_cast<void *>(s) : ESGD_STREAM_NULL;
         if (int rc = esgd_schedule_wait(sched)) return rc;
         if (int rc = out()) return rc;
         if (int rc = esgd_schedule_release(sched, ps)) return rc;
-        bytes += int64_t(nbytes);
+        bytes += int64_t(len) * int64_t(sizeof(float));
         return ESGD_SUCCESS;
+    }
+
+    template <class Out>
+    int device_round(hipStream_t s, Out &&out) {
+        if (int rc = post_round(s)) return rc;
+        return finish_round(s, out);
     }
 };
 
 constexpr float kNoDivide = 1.0f;
 
-int forward_cuda_impl(AllreduceOp *op, const float *input, float *output, float divisor, hipStream_t s) {
-    ESGD_ARG(op, "allreducef: null handle");
-    if (int rc = op->ensure(true)) return rc;
+// copy-in of a device round, on s: a plain copy, or the wrapper's division (:40) fused
+int cuda_copy_in(AllreduceOp *op, const float *input, float divisor, hipStream_t s) {
     const size_t nbytes = size_t(op->len) * sizeof(float);
     const uint64_t n = op->len;
     if (divisor == kNoDivide) {
@@ -163,16 +173,25 @@ int forward_cuda_impl(AllreduceOp *op, const float *input, float *output, float 
             esgd::set_error("allreducef: copy-in failed");
             return ESGD_ERROR;
         }
-    } else if (int rc = esgd_pack_div(1, &input, &n, op->sb, divisor, s)) {
-        return rc;
-    }
-    return op->device_round(s, [&]() -> int {
-        if (hipMemcpyAsync(output, op->rb, nbytes, hipMemcpyDeviceToDevice, s) != hipSuccess) {
-            esgd::set_error("allreducef: copy-out failed");
-            return ESGD_ERROR;
-        }
         return ESGD_SUCCESS;
-    });
+    }
+    return esgd_pack_div(1, &input, &n, op->sb, divisor, s);
+}
+
+int cuda_copy_out(AllreduceOp *op, float *output, hipStream_t s) {
+    if (hipMemcpyAsync(output, op->rb, size_t(op->len) * sizeof(float), hipMemcpyDeviceToDevice, s) != hipSuccess) {
+        esgd::set_error("allreducef: copy-out failed");
+        return ESGD_ERROR;
+    }
+    return ESGD_SUCCESS;
+}
+
+int forward_cuda_impl(AllreduceOp *op, const float *input, float *output, float divisor, hipStream_t s) {
+    ESGD_ARG(op, "allreducef: null handle");
+    ESGD_ARG(!op->pending, "allreducef: a split round is posted and not yet waited");
+    if (int rc = op->ensure(true)) return rc;
+    if (int rc = cuda_copy_in(op, input, divisor, s)) return rc;
+    return op->device_round(s, [&]() -> int { return cuda_copy_out(op, output, s); });
 }
 
 // Host round, the wrapper's steps (:301-316): copy in -> post -> wait -> copy out ->
@@ -291,10 +310,33 @@ int allreducef_forward_cuda_packed(void *handle, int n, const float *const *grad
     for (int i = 0; i < n; ++i) total += counts[i];
     ESGD_ARG(total == op->len, "allreducef_forward_cuda_packed: %llu elements for a %llu-element op",
              (unsigned long long)total, (unsigned long long)op->len);
+    ESGD_ARG(!op->pending, "allreducef_forward_cuda_packed: a split round is posted and not yet waited");
     if (int rc = op->ensure(true)) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (int rc = esgd_pack_div(n, grads, counts, op->sb, divisor, s)) return rc;
     return op->device_round(s, [&]() -> int { return esgd_unpack(n, outs, counts, op->rb, s); });
+}
+
+int allreducef_forward_cuda_post(void *handle, const float *input, float divisor, void *stream) {
+    auto *op = static_cast<AllreduceOp *>(handle);
+    ESGD_ARG(op, "allreducef_forward_cuda_post: null handle");
+    ESGD_ARG(divisor == divisor && divisor != 0.0f, "allreducef_forward_cuda_post: bad divisor");
+    ESGD_ARG(!op->pending, "allreducef_forward_cuda_post: the previous round was not waited");
+    if (int rc = op->ensure(true)) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int rc = cuda_copy_in(op, input, divisor, s)) return rc;
+    if (int rc = op->post_round(s)) return rc;
+    op->pending = true;
+    return ESGD_SUCCESS;
+}
+
+int allreducef_forward_cuda_wait(void *handle, float *output, void *stream) {
+    auto *op = static_cast<AllreduceOp *>(handle);
+    ESGD_ARG(op, "allreducef_forward_cuda_wait: null handle");
+    ESGD_ARG(op->pending, "allreducef_forward_cuda_wait: no round posted");
+    op->pending = false;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    return op->finish_round(s, [&]() -> int { return cuda_copy_out(op, output, s); });
 }
 
 bool is_cuda_supported(void *) { return true; }

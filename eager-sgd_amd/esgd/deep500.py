@@ -51,6 +51,10 @@ def _bind(h):
     h.allreducef_forward_cuda_packed.restype = C.c_int
     h.allreducef_forward_cuda_packed.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(C.c_uint64),
                                                  C.POINTER(vp), C.c_float, vp]
+    h.allreducef_forward_cuda_post.restype = C.c_int
+    h.allreducef_forward_cuda_post.argtypes = [vp, vp, C.c_float, vp]
+    h.allreducef_forward_cuda_wait.restype = C.c_int
+    h.allreducef_forward_cuda_wait.argtypes = [vp, vp, vp]
     h.is_cuda_supported.restype, h.is_cuda_supported.argtypes = C.c_bool, [vp]
     h.report.restype, h.report.argtypes = C.c_int64, [vp, vp]
     h.delete_op.restype, h.delete_op.argtypes = None, [vp]
@@ -132,6 +136,21 @@ class AllreduceOp:
         _lib.check(lib().allreducef_forward_cuda_packed(self.handle, n, src, counts, dst, float(divisor),
                                                         stream), "allreducef_forward_cuda_packed")
         return outs
+
+    def post_cuda(self, grad, divisor: float = 1.0, stream: int | None = None):
+        """First half of forward_cuda_div: queue the copy-in (divided) and post the round,
+        without waiting -- post every op's round, then wait_cuda() each, in the same order
+        on every rank.  Raises EsgdError."""
+        from .device import as_ptr
+        _lib.check(lib().allreducef_forward_cuda_post(self.handle, as_ptr(grad), float(divisor), stream),
+                   "allreducef_forward_cuda_post")
+
+    def wait_cuda(self, out, stream: int | None = None):
+        """Second half: wait for the posted round and queue the copy-out into `out`."""
+        from .device import as_ptr
+        _lib.check(lib().allreducef_forward_cuda_wait(self.handle, as_ptr(out), stream),
+                   "allreducef_forward_cuda_wait")
+        return out
 
     def forward_void(self, grad: np.ndarray) -> np.ndarray:
         """The reference ABI's void allreducef_forward verbatim (host buffers): on a failed

@@ -16,6 +16,12 @@ reduced gradient is written back into p.grad in place: per tensor and step 3 HBM
 of the gradient (copy-in with the divide; the move with the zeroing fused; copy-out)
 instead of 5 (divide, copy-in, move, copy-out, memset).
 
+pipeline=True (the per-tensor default): every tensor's round is posted before the first
+is waited for (allreducef_forward_cuda_post / _wait), so the 161 host round trips overlap
+instead of running one after another as the reference's blocking ops do (:304-307); the
+same rounds over the same operands, so the same bits.  pipeline=False keeps the blocking
+chain.
+
 fuse=True (SURVEY.md §8(f) "bucket fusion"): the reference runs one schedule per tensor,
 161 per ResNet-50 step (opt_esgd_solo_imagenet_imbalance.py:85-248), each a
 host-blocking post/wait.  Fused, the scaled gradients are packed in the same reversed
@@ -32,7 +38,8 @@ from . import deep500
 
 class EagerSGDOptimizer:
     def __init__(self, optimizer, comm_size: int, mode: str = "solo", async_: int = 32,
-                 seed: int = 6545343, fuse: bool = False, wire: str = "fp32"):
+                 seed: int = 6545343, fuse: bool = False, wire: str = "fp32",
+                 pipeline: bool = True):
         if mode not in deep500.MODES:
             raise ValueError(f"mode must be one of {sorted(deep500.MODES)}")
         if wire not in deep500.WIRES:
@@ -43,6 +50,7 @@ class EagerSGDOptimizer:
         self.comm_size = int(comm_size)
         self.mode, self.async_, self.seed = mode, int(async_), int(seed)
         self.fuse = bool(fuse)
+        self.pipeline = bool(pipeline)
         self.wire = wire        # "bf16": bf16 copies between ranks
         self._ops = {}          # parameter -> op instance (one bucket per tensor)
         self._fused = None      # (layout, op, packed bucket, reduced bucket)
@@ -64,6 +72,7 @@ class EagerSGDOptimizer:
         if self.fuse:
             self._apply_fused(gvs, stream)
         else:
+            posted = []
             for grad, var in reversed(gvs):
                 if grad is None:      # the reference would still feed None (:35-42); skip
                     continue
@@ -72,13 +81,38 @@ class EagerSGDOptimizer:
                     op = self._ops[var] = deep500.AllreduceOp(tuple(grad.shape))
                 g = grad if (grad.dtype == torch.float32 and grad.is_contiguous()) \
                     else grad.float().contiguous()
-                op.forward_cuda_div(g, g, self.comm_size, stream)          # :40 fused, in place
-                if g is not grad:
-                    var.grad = g.to(grad.dtype).view_as(grad)
+                if self.pipeline:
+                    try:
+                        op.post_cuda(g, self.comm_size, stream)            # :40 fused
+                    except Exception:
+                        self._drain(posted, stream)   # no op is left with a round posted
+                        raise
+                    posted.append((op, g, grad, var))
+                else:
+                    op.forward_cuda_div(g, g, self.comm_size, stream)      # :40 fused, in place
+                    if g is not grad:
+                        var.grad = g.to(grad.dtype).view_as(grad)
+            err = self._drain(posted, stream)
+            if err is not None:
+                raise err
         r = self.optimizer.step()
         if global_step is not None and hasattr(global_step, "add_"):
             global_step.add_(1)
         return r
+
+    @staticmethod
+    def _drain(posted, stream):
+        """Wait every posted round (a failure does not skip the rest); the first error."""
+        err = None
+        for op, g, grad, var in posted:
+            try:
+                op.wait_cuda(g, stream)
+            except Exception as e:   # noqa: BLE001 -- re-raised by the caller
+                err = err or e
+                continue
+            if g is not grad:
+                var.grad = g.to(grad.dtype).view_as(grad)
+        return err
 
     def _apply_fused(self, gvs, stream):
         import torch

@@ -67,6 +67,16 @@ int allreducef_forward_cuda_div(void *handle, const float *input, float *output,
 int allreducef_forward_cuda_packed(void *handle, int n, const float *const *grads,
                                    const uint64_t *counts, float *const *outs, float divisor,
                                    void *stream);
+/* Extension: allreducef_forward_cuda_div split in two, so a caller can post the rounds of
+ * many ops (one per gradient tensor) before waiting for the first -- the reference's ops
+ * block one after another (opt_esgd_solo_imagenet_imbalance.py:304-307); the rounds, their
+ * operands and their sums are the same, the host round trips overlap.  _post queues the
+ * copy-in (divided by divisor; 1.0f = plain copy) on stream and posts; _wait waits for the
+ * round, queues the copy-out into output on stream and releases the round.  One round per
+ * op in flight: a second _post before _wait, a _wait without a _post, or a blocking forward
+ * between them is ESGD_INVALID_ARG.  Every rank must post its ops in the same order. */
+int allreducef_forward_cuda_post(void *handle, const float *input, float divisor, void *stream);
+int allreducef_forward_cuda_wait(void *handle, float *output, void *stream);
 /* Extension: what the void entry points above (allreducef_forward, allreducef_forward_cuda)
  * do when their round fails (a peer timeout, an allocation failure).  ESGD_OP_ON_ERROR_ABORT
  * (default; env ESGD_OP_ON_ERROR=abort): print the error and abort the process, as their

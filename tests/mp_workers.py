@@ -421,7 +421,7 @@ def op_device_late(rank, world, async_=3, steps=9, count=100003):
     return {"ok": ok, "sync_rounds": fresh}
 
 
-def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp32"):
+def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp32", pipeline=True):
     """EagerSGDOptimizer on PyTorch-ROCm: every rank's p.grad after apply_gradients must
     equal the oracle tree of (grad_r / P) over ranks, bit for bit (allreduce), or over
     expected_inputs' contributors when the ranks call every op in late_ranks' order
@@ -440,7 +440,7 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp3
     torch.cuda.set_device(dev)
     model = torch.nn.Sequential(torch.nn.Linear(64, 48), torch.nn.ReLU(), torch.nn.Linear(48, 10)).to(dev)
     opt = EagerSGDOptimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9), world, mode=mode,
-                            fuse=fuse, wire=wire)
+                            fuse=fuse, wire=wire, pipeline=pipeline)
     ok = []
     for t in range(steps):
         g = torch.Generator().manual_seed(100 * t + rank)
@@ -454,19 +454,21 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp3
         dist.all_gather_object(allg, local)
         comm.barrier()
         late = t > 0 and rank in late_ranks(mode, world, t)
-        orig = (deep500.AllreduceOp.forward_cuda_div, deep500.AllreduceOp.forward_cuda_packed)
-        if late:   # every op call of this step comes LATE_S after the peers'
+        names = ("forward_cuda_div", "forward_cuda_packed", "post_cuda")
+        orig = {n: getattr(deep500.AllreduceOp, n) for n in names}
+        if late:   # every op call (or post) of this step comes LATE_S after the peers'
             def delayed(fn):
                 def f(self, *a, **k):
                     time.sleep(LATE_S)
                     return fn(self, *a, **k)
                 return f
-            deep500.AllreduceOp.forward_cuda_div = delayed(orig[0])
-            deep500.AllreduceOp.forward_cuda_packed = delayed(orig[1])
+            for n in names:
+                setattr(deep500.AllreduceOp, n, delayed(orig[n]))
         try:
             opt.apply_gradients(gvs)
         finally:
-            deep500.AllreduceOp.forward_cuda_div, deep500.AllreduceOp.forward_cuda_packed = orig
+            for n in names:
+                setattr(deep500.AllreduceOp, n, orig[n])
         torch.cuda.synchronize()
         if t == 0 and mode != "allreduce":
             continue
@@ -1307,3 +1309,40 @@ def cp_create_many(rank, world, n=161, rounds=1):
         s.delete()
     comm.finalize()
     return {"create_ms_per_schedule": t_create * 1e3 / n}
+
+
+def op_split_misuse(rank, world, count=4096):
+    """allreducef_forward_cuda_post / _wait: one round per op in flight; misuse is
+    ESGD_INVALID_ARG and leaves the op usable; a posted round gives forward_cuda_div's bits."""
+    import torch
+
+    from esgd import deep500
+    from esgd._lib import EsgdError
+    comm = _comm()
+    dev = torch.device("cuda", local_device())
+    torch.cuda.set_device(dev)
+    op = deep500.AllreduceOp((count,))
+    ref = deep500.AllreduceOp((count,))
+    x = torch.arange(count, dtype=torch.float32, device=dev) * (rank + 1)
+    errs = {}
+
+    def expect_err(name, fn):
+        try:
+            fn()
+            errs[name] = None
+        except EsgdError as e:
+            errs[name] = e.rc
+
+    expect_err("wait_without_post", lambda: op.wait_cuda(x.clone()))
+    g = x.clone()
+    op.post_cuda(g, float(world))
+    expect_err("second_post", lambda: op.post_cuda(g, float(world)))
+    expect_err("blocking_between", lambda: op.forward_cuda_div(g, g, float(world)))
+    op.wait_cuda(g)
+    h = x.clone()
+    ref.forward_cuda_div(h, h, float(world))
+    torch.cuda.synchronize()
+    same = bool(torch.equal(g, h))
+    comm.barrier()
+    comm.finalize()
+    return {"errs": errs, "same": same}

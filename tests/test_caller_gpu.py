@@ -37,12 +37,16 @@ def test_deep500_op_device_late_gradient_dropped():
         assert o["sync_rounds"] == [r % 4 == 0 for r in range(2, 10)]
 
 
-@pytest.mark.parametrize("fuse", [False, True])
+VARIANTS = {"blocking": dict(pipeline=False), "pipelined": dict(pipeline=True), "fused": dict(fuse=True)}
+
+
+@pytest.mark.parametrize("variant", list(VARIANTS))
 @pytest.mark.parametrize("mode", ["allreduce", "solo", "majority"])
-def test_eager_sgd_optimizer(mode, fuse):
-    # fuse=True packs every gradient into one bucket (one round per step): the same
-    # bits as one round per tensor
-    outs = run("optimizer_step", 2, mode=mode, steps=3, fuse=fuse)
+def test_eager_sgd_optimizer(mode, variant):
+    # one blocking round per tensor (the reference's op chain), every tensor's round posted
+    # before the first wait (pipeline=True, the default), or every gradient packed into
+    # one bucket (fuse=True): the same bits
+    outs = run("optimizer_step", 2, mode=mode, steps=3, **VARIANTS[variant])
     for o in outs:
         assert all(o["ok"]) and o["ok"], o["ok"]
         assert o["bytes"] > 0
