@@ -36,6 +36,28 @@ XGMI_LINK_GBS = 153.0      # per-link figure used by SURVEY.md §8d
 SHARED_GPU = False         # N > 1 with ranks sharing a device (set in run_allreduce)
 SEED = 0x5EEDE56D
 MiB = 1 << 20
+_LINE_FD = None            # N > 1: the rank's real stdout, kept for the JSON line alone
+
+
+def _quiet_stdout():
+    """Under a launcher every rank shares the job's stdout, and native libraries write
+    to fd 1 (gloo's "[Gloo] Rank r is connected to ..." at init, RCCL/HIP notices).
+    Point fd 1 at stderr for the whole run and keep a private copy of the real stdout,
+    so the only thing a rank ever writes there is rank 0's JSON line."""
+    global _LINE_FD
+    sys.stdout.flush()
+    _LINE_FD = os.dup(1)
+    os.dup2(2, 1)
+
+
+def emit(line: dict) -> None:
+    """Print the one JSON line (to the real stdout when _quiet_stdout ran)."""
+    text = json.dumps(line) + "\n"
+    if _LINE_FD is None:
+        sys.stdout.write(text)
+        sys.stdout.flush()
+    else:
+        os.write(_LINE_FD, text.encode())
 
 
 def parse():
@@ -1105,7 +1127,7 @@ def run_allreduce(args, rank, world):
                 out = dict(line)
                 out.update(extras)
                 out["extras_timeout"] = leg[0]
-                print(json.dumps(out), flush=True)
+                emit(out)
             os._exit(0)
 
         leg = ["none"]
@@ -1167,6 +1189,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and not args.pmc_child:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world > 1:
+        _quiet_stdout()
 
     import esgd
     from esgd import device as dev
@@ -1179,7 +1203,7 @@ def main():
     if world > 1:
         res = run_allreduce(args, rank, world)
         if rank == 0:
-            print(json.dumps(res))
+            emit(res)
         return
 
     res = run_local(args, esgd, dev)
@@ -1243,7 +1267,7 @@ def main():
         line["cpu_baseline"] = cpu_baseline(res["k"], res["count"] if args.dtype == "fp32"
                                             else res["count"])
         line["cpu_baseline_c1"] = cpu_baseline_c1()
-    print(json.dumps(line))
+    emit(line)
 
 
 if __name__ == "__main__":

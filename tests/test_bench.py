@@ -61,3 +61,28 @@ def test_launcher_started_ranks_do_not_relaunch():
                        capture_output=True, text=True, timeout=120, cwd=ROOT)
     assert "torch.distributed.run" not in r.stderr
     assert r.returncode != 0 and "no HIP device" in (r.stderr + r.stdout)
+    assert r.stdout == ""                 # a rank's stdout carries the JSON line or nothing
+
+
+QUIET = r"""
+import os, sys
+sys.path.insert(0, {root!r})
+import bench
+print("python chatter before")
+bench._quiet_stdout()
+print("python chatter after", flush=True)
+os.write(1, b"[Gloo] Rank 1 is connected to 1 peer ranks\n")   # native code on fd 1
+bench.emit({{"metric": "m", "value": 1.0}})
+"""
+
+
+def test_rank_stdout_carries_only_the_json_line():
+    # gloo / RCCL print to fd 1 from native code; under a launcher that stdout is the
+    # job's, which the driver parses for the line
+    r = subprocess.run([sys.executable, "-c", QUIET.format(root=ROOT)], capture_output=True, text=True,
+                       timeout=120, cwd=ROOT)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[0] == "python chatter before"
+    assert [json.loads(x) for x in lines[1:]] == [{"metric": "m", "value": 1.0}]
+    assert "[Gloo]" in r.stderr and "chatter after" in r.stderr
