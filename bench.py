@@ -1156,8 +1156,10 @@ def run_allreduce(args, rank, world):
         if only:
             pick = only.split(",")
             legs = sorted((lg for lg in legs if lg[0] in pick), key=lambda lg: pick.index(lg[0]))
+        legs_s = extras["legs_s"] = {}      # wall time of each leg on rank 0's clock
         for name, fn in legs:
             leg[0] = name
+            t_leg = time.perf_counter()
             try:
                 extras[name] = fn()
             except Exception as e:   # keep the headline line; report what failed
@@ -1165,6 +1167,8 @@ def run_allreduce(args, rank, world):
                 traceback.print_exc()
                 extras[name + "_error"] = f"rank {rank}: " + repr(e)[:300]
                 break                # peers may be inside this leg: do not start another
+            finally:
+                legs_s[name] = round(time.perf_counter() - t_leg, 2)
         leg[0] = "teardown"
         if not any(k.endswith("_error") for k in extras):
             _delete_deferred()       # collective; after a failed leg finalize frees them

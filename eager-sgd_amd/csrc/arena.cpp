@@ -29,9 +29,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "esgd_internal.h"
@@ -102,7 +105,7 @@ void release_chunk(Chunk *c) {
     }
     g_by_base.erase(reinterpret_cast<uintptr_t>(c->base));
     g_chunks.erase(std::remove(g_chunks.begin(), g_chunks.end(), c), g_chunks.end());
-    (void)hipFree(c->base);
+    hip_ignore(hipFree(c->base));
     delete c;
 }
 
@@ -269,7 +272,21 @@ int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_
     Chunk *c = b.chunk;
     if (!c->exported) {
         hipIpcMemHandle_t h;
-        if (hipError_t e = hipIpcGetMemHandle(&h, c->base)) {
+        // On round 3's boxes the dmabuf export of a fresh chunk failed now and then with
+        // hipErrorInvalidValue (a new process's first schedule, after other tests' ranks
+        // had exited; profiles/r03/README.md).  Creation is rare, so a failed export is
+        // retried with growing pauses (1 + 2 + ... + 256 ms) before the schedule fails;
+        // each failed attempt is reported on stderr.
+        hipError_t e = hipSuccess;
+        for (int attempt = 0, pause_ms = 1; attempt < 10; ++attempt, pause_ms *= 2) {
+            e = hipIpcGetMemHandle(&h, c->base);
+            if (e == hipSuccess) break;
+            (void)hipGetLastError();
+            std::fprintf(stderr, "esgd: hipIpcGetMemHandle(%p, %zu B chunk) attempt %d: %s\n",
+                         static_cast<void *>(c->base), c->bytes, attempt + 1, hipGetErrorString(e));
+            if (attempt < 9) std::this_thread::sleep_for(std::chrono::milliseconds(pause_ms));
+        }
+        if (e != hipSuccess) {
             const char *m = getenv("HSA_ENABLE_IPC_MODE_LEGACY");
             int rc = hip_fail(e, "hipIpcGetMemHandle", __FILE__, __LINE__);
             if (!m || std::strcmp(m, "0") != 0) {

@@ -170,7 +170,7 @@ static bool g_mappings_closed = false;
 
 static void ipc_close_all() {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
-    for (auto &kv : g_ipc) (void)hipIpcCloseMemHandle(kv.second);
+    for (auto &kv : g_ipc) hip_ignore(hipIpcCloseMemHandle(kv.second));
     if (!g_ipc.empty()) g_mappings_closed = true;
     g_ipc.clear();
 }
@@ -190,7 +190,7 @@ static void ipc_close_one(int peer, const uint8_t *h) {
     std::memcpy(k.h, h, 64);
     auto it = g_ipc.find(k);
     if (it == g_ipc.end()) return;
-    (void)hipIpcCloseMemHandle(it->second);
+    hip_ignore(hipIpcCloseMemHandle(it->second));
     g_ipc.erase(it);
 }
 
@@ -420,10 +420,10 @@ static int ctr_words(int sched_id, hipStream_t cs, uint32_t **out) {
 void dataplane_shutdown() {
     rccl_shutdown();
     std::lock_guard<std::mutex> lk(g_dp_mu);
-    if (g_rs) { (void)hipStreamSynchronize(g_rs); (void)hipStreamDestroy(g_rs); g_rs = nullptr; }
+    if (g_rs) { hip_ignore(hipStreamSynchronize(g_rs)); hip_ignore(hipStreamDestroy(g_rs)); g_rs = nullptr; }
     for (hipStream_t *c : {&g_h2d, &g_d2h})
-        if (*c) { (void)hipStreamSynchronize(*c); (void)hipStreamDestroy(*c); *c = nullptr; }
-    if (g_ctr_pool) { (void)hipFree(g_ctr_pool); g_ctr_pool = nullptr; }
+        if (*c) { hip_ignore(hipStreamSynchronize(*c)); hip_ignore(hipStreamDestroy(*c)); *c = nullptr; }
+    if (g_ctr_pool) { hip_ignore(hipFree(g_ctr_pool)); g_ctr_pool = nullptr; }
     ipc_close_all();
     for (FlagPages &fp : g_pages) {   // the pages themselves stay (exported memory)
         for (auto &p : fp.peer) p = nullptr;
@@ -431,7 +431,7 @@ void dataplane_shutdown() {
         fp.seg = nullptr;
     }
     arena_trim();
-    if (g_seg_reg) { (void)hipHostUnregister(g_seg_reg); g_seg_reg = nullptr; g_seg_dev = nullptr; }
+    if (g_seg_reg) { hip_ignore(hipHostUnregister(g_seg_reg)); g_seg_reg = nullptr; g_seg_dev = nullptr; }
 }
 
 // State every GPU transport keeps per schedule: the round stream, the completion
@@ -521,7 +521,7 @@ static int alloc_bucket(size_t bytes, char **out, size_t *cap) {
 }
 
 static void free_bucket(char *p) {
-    if (p && !arena_free(p)) (void)hipFree(p);
+    if (p && !arena_free(p)) hip_ignore(hipFree(p));
 }
 
 static int base_setup(Sched &s, BaseState &st) {
@@ -804,16 +804,16 @@ static int base_query(Sched &s, BaseState &st) {
 }
 
 static void base_teardown(Sched &s, BaseState &st) {
-    if (st.stream) (void)hipStreamSynchronize(st.stream);
+    if (st.stream) hip_ignore(hipStreamSynchronize(st.stream));
     if (st.owns_rb) free_bucket(st.rb_dev);
-    if (st.reg_rb) (void)hipHostUnregister(s.rb);
-    if (st.reg_sb) (void)hipHostUnregister(s.sb);
-    for (auto &kv : st.producer) (void)hipEventDestroy(kv.second);
-    for (hipEvent_t e : st.spare) (void)hipEventDestroy(e);
-    if (st.consumer) (void)hipEventDestroy(st.consumer);
-    if (st.pin) (void)hipHostFree(st.pin);
+    if (st.reg_rb) hip_ignore(hipHostUnregister(s.rb));
+    if (st.reg_sb) hip_ignore(hipHostUnregister(s.sb));
+    for (auto &kv : st.producer) hip_ignore(hipEventDestroy(kv.second));
+    for (hipEvent_t e : st.spare) hip_ignore(hipEventDestroy(e));
+    if (st.consumer) hip_ignore(hipEventDestroy(st.consumer));
+    if (st.pin) hip_ignore(hipHostFree(st.pin));
     for (char *p : st.retired) free_bucket(p);
-    if (st.ev) (void)hipEventDestroy(st.ev);
+    if (st.ev) hip_ignore(hipEventDestroy(st.ev));
 }
 
 struct IpcTransport final : Transport {
@@ -1263,8 +1263,8 @@ struct IpcTransport final : Transport {
     void teardown(Sched &s) override {
         IpcState *st = static_cast<IpcState *>(s.tstate);
         if (!st) return;
-        if (st->stream) (void)hipStreamSynchronize(st->stream);
-        for (hipEvent_t e : st->cev) (void)hipEventDestroy(e);
+        if (st->stream) hip_ignore(hipStreamSynchronize(st->stream));
+        for (hipEvent_t e : st->cev) hip_ignore(hipEventDestroy(e));
         bool pub_free = true;
         if (st->pub && st->pub_round && s.world > 1) {
             const double t0 = now_s(), limit = std::min(engine_timeout(), 10.0);
@@ -1384,7 +1384,7 @@ static int nccl_ensure(Sched &s) {
 
 void rccl_shutdown() {
     std::lock_guard<std::mutex> lk(g_nccl_mu);
-    if (g_rs) (void)hipStreamSynchronize(g_rs);
+    if (g_rs) hip_ignore(hipStreamSynchronize(g_rs));
     if (g_nccl) { (void)ncclCommDestroy(g_nccl); g_nccl = nullptr; }
 }
 
@@ -1592,12 +1592,12 @@ struct RcclTransport final : Transport {
     void teardown(Sched &s) override {
         RcclState *st = static_cast<RcclState *>(s.tstate);
         if (!st) return;
-        if (st->stream) (void)hipStreamSynchronize(st->stream);
-        if (st->red) { (void)hipStreamSynchronize(st->red); (void)hipStreamDestroy(st->red); }
-        if (st->stage) (void)hipFree(st->stage);
-        if (st->wire) (void)hipFree(st->wire);
-        for (hipEvent_t e : st->ev_chunk) (void)hipEventDestroy(e);
-        if (st->ev_red) (void)hipEventDestroy(st->ev_red);
+        if (st->stream) hip_ignore(hipStreamSynchronize(st->stream));
+        if (st->red) { hip_ignore(hipStreamSynchronize(st->red)); hip_ignore(hipStreamDestroy(st->red)); }
+        if (st->stage) hip_ignore(hipFree(st->stage));
+        if (st->wire) hip_ignore(hipFree(st->wire));
+        for (hipEvent_t e : st->ev_chunk) hip_ignore(hipEventDestroy(e));
+        if (st->ev_red) hip_ignore(hipEventDestroy(st->ev_red));
         base_teardown(s, *st);
         delete st;
         s.tstate = nullptr;

@@ -86,7 +86,7 @@ static struct ProgressGuard {
 // MPI_Testsome instead, ffprogress.c:39-57).  A round in flight is latency-critical: the
 // thread spins / yields then, never sleeps.
 static void progress_main() {
-    if (g_device >= 0) (void)hipSetDevice(g_device);
+    if (g_device >= 0) hip_ignore(hipSetDevice(g_device));
     unsigned polls = 0;
     while (g_running.load(std::memory_order_acquire)) {
         const uint32_t ws = g_seg->wake_seq.load(std::memory_order_acquire);

@@ -18,6 +18,14 @@ void clear_error();
 // Map a HIP status onto the ABI's codes, recording where it failed.
 int hip_fail(hipError_t e, const char *what, const char *file, int line);
 
+// A HIP call whose failure is tolerated (teardown, best-effort restores).  HIP keeps the
+// thread's last error until hipGetLastError() reads it, and every kernel launch here is
+// checked with hipGetLastError(): an ignored failure left in place would be reported by
+// the thread's next, unrelated launch.  So a tolerated failure is cleared at once.
+inline void hip_ignore(hipError_t e) {
+    if (e != hipSuccess) (void)hipGetLastError();
+}
+
 // Lazily-created library stream for the current device (NULL stream argument).
 hipStream_t default_stream();
 

@@ -332,8 +332,8 @@ int ffop_free(ffop_h h) {
     auto *o = reinterpret_cast<FFComp *>(h);
     if (!o) return FFSUCCESS;
     if (o->ev) {
-        (void)hipEventSynchronize(o->ev);
-        (void)hipEventDestroy(o->ev);
+        hip_ignore(hipEventSynchronize(o->ev));
+        hip_ignore(hipEventDestroy(o->ev));
     }
     delete o;
     return FFSUCCESS;

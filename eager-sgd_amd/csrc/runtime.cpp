@@ -24,6 +24,7 @@ void set_error(const char *fmt, ...) {
 void clear_error() { g_err[0] = 0; }
 
 int hip_fail(hipError_t e, const char *what, const char *file, int line) {
+    (void)hipGetLastError();   // reported here: not again by the thread's next launch check
     set_error("%s failed: %s (%s:%d)", what, hipGetErrorString(e), file, line);
     if (e == hipErrorOutOfMemory) return ESGD_ENOMEM;
     if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return ESGD_NO_DEVICE;
@@ -122,7 +123,7 @@ int esgd_free(void *ptr) {
     ESGD_HIP(hipGetDevice(&cur));
     if (cur != dev) ESGD_HIP(hipSetDevice(dev));
     const hipError_t e = hipDeviceSynchronize();
-    if (cur != dev) (void)hipSetDevice(cur);
+    if (cur != dev) hip_ignore(hipSetDevice(cur));
     if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize (esgd_free)", __FILE__, __LINE__);
     arena_free(ptr);
     return ESGD_SUCCESS;

@@ -12,6 +12,7 @@ import queue
 import socket
 import sys
 import time
+import zlib
 import traceback
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -704,8 +705,11 @@ def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, dela
         head, tail = _download_slice(rb, 0, m), _download_slice(rb, count - m, m)
         comm.barrier()
         uniform = bool(np.all(head == head[0]) and np.all(tail == head[0]))
+        both = np.concatenate([head, tail])
+        slices.append((float(both.min()), float(both.max()), zlib.crc32(both.tobytes())))
         return el, float(head[0]), uniform
 
+    slices = []                            # per round: (min, max, crc32) of head + tail
     warm = [one(0)[0] for _ in range(3)]   # rounds 1..3: everyone on time
     tt = torch.tensor([statistics.median(warm)], dtype=torch.float64)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -715,7 +719,7 @@ def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, dela
     for t in range(4, 4 + rounds):
         _, c, u = one(d)
         res.append((t, c, u))
-    out = {"rounds": res, "log": s.log(), "T_s": T, "delay_s": d}
+    out = {"rounds": res, "log": s.log(), "T_s": T, "delay_s": d, "slices": slices[3:]}
     comm.barrier()
     s.delete()
     comm.finalize()

@@ -225,20 +225,26 @@ def test_majority_straggler_c4_20pct():
     # BASELINE C4 as stated: 8 ranks, the 25 559 081-float ResNet-50 gradient, one rank
     # 20 % of a round late.  A 0.2 T delay races the round (the straggler may or may not
     # make it), so: rounds the straggler activates (rand_r draw, ffrand_allreduce.c:88)
-    # wait for it and take all P; every other round takes P - 1 or P, the same on every
-    # rank (rsgd.c:87,100 contributor counting)
+    # wait for it and take all P; every other round takes P - 1 or P per element, the same
+    # bits on every rank (rsgd.c:87,100 contributor counting).  Per element, not per bucket:
+    # a round another rank activates joins the straggler passively, and its bucket is read
+    # as it stands at that moment -- possibly while the straggler's own copy into it is
+    # still running, so part of the bucket holds the fresh 1.0s and part the zeros.  The
+    # reference has the same race: the activated progress thread moves sb -> rb
+    # (ffallreduce.c:125-127) while the op's memcpy into sb
+    # (opt_esgd_majority_imagenet_imbalance.py:302, before ffschedule_post at :305) may
+    # be in flight.  Every rank then reduces the same snapshot.
     world = 8
     outs = run("gpu_straggler", world, kind=MAJORITY, count=25559081, rounds=8, delay_frac=0.2, timeout=420)
     acts = ffref.activators(6545343, world, 64)
     for r, o in enumerate(outs):
         assert abs(o["delay_s"] - 0.2 * o["T_s"]) < 1e-9, o
-        for t, c, uniform in o["rounds"]:
-            assert uniform, (r, t)
+        for (t, c, uniform), (lo, hi, crc) in zip(o["rounds"], o["slices"]):
             if acts[t - 1] == world - 1:
-                assert c == world, (r, t, c)
+                assert uniform and c == world, (r, t, c)
             else:
-                assert c in (world - 1, world), (r, t, c)
-            assert c == outs[0]["rounds"][t - 4][1], (r, t)   # same result on every rank
+                assert world - 1 <= lo <= hi <= world, (r, t, lo, hi)
+            assert crc == outs[0]["slices"][t - 4][2], (r, t)   # same bits on every rank
         for e in o["log"]:
             assert e["activator"] == acts[e["round"] - 1], e
 
