@@ -105,6 +105,7 @@ void release_chunk(Chunk *c) {
     }
     g_by_base.erase(reinterpret_cast<uintptr_t>(c->base));
     g_chunks.erase(std::remove(g_chunks.begin(), g_chunks.end(), c), g_chunks.end());
+    if (c->exported) ipc_trace("free", -1, c->base, c->bytes, c->handle);
     hip_ignore(hipFree(c->base));
     delete c;
 }
@@ -298,6 +299,7 @@ int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_
         }
         std::memcpy(c->handle, &h, 64);
         c->exported = true;
+        ipc_trace("export", -1, c->base, c->bytes, c->handle);
     }
     *base = c->base;
     *off = uint64_t(a - reinterpret_cast<uintptr_t>(c->base));

@@ -157,6 +157,7 @@ static int ipc_open(int peer, const uint8_t *h, void **base) {
     std::memcpy(&hh, h, sizeof(hh));
     void *p = nullptr;
     ESGD_HIP(hipIpcOpenMemHandle(&p, hh, hipIpcMemLazyEnablePeerAccess));
+    ipc_trace("open", peer, p, 0, h);
     g_ipc[k] = p;
     *base = p;
     return ESGD_SUCCESS;
@@ -170,7 +171,10 @@ static bool g_mappings_closed = false;
 
 static void ipc_close_all() {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
-    for (auto &kv : g_ipc) hip_ignore(hipIpcCloseMemHandle(kv.second));
+    for (auto &kv : g_ipc) {
+        ipc_trace("close", kv.first.peer, kv.second, 0, kv.first.h);
+        hip_ignore(hipIpcCloseMemHandle(kv.second));
+    }
     if (!g_ipc.empty()) g_mappings_closed = true;
     g_ipc.clear();
 }
@@ -190,6 +194,7 @@ static void ipc_close_one(int peer, const uint8_t *h) {
     std::memcpy(k.h, h, 64);
     auto it = g_ipc.find(k);
     if (it == g_ipc.end()) return;
+    ipc_trace("close", peer, it->second, 0, h);
     hip_ignore(hipIpcCloseMemHandle(it->second));
     g_ipc.erase(it);
 }

@@ -48,6 +48,10 @@ struct PairFlags {
     int ndst;
 };
 
+// ESGD_IPC_TRACE=1 (diagnostics): every IPC export / open / close on stderr with the
+// handle's bytes, so a repeated handle or a stale mapping can be seen.
+void ipc_trace(const char *what, int peer, const void *ptr, size_t bytes, const uint8_t handle[64]);
+
 int arena_alloc(size_t bytes, void **out);
 bool arena_free(void *p);
 int arena_device(const void *p);   // device of an arena block, -1 if p is not one

@@ -5,6 +5,10 @@
 // (the ff.h drop-in, the deep500 op, plain C tests) can drive the HIP path.
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -22,6 +26,15 @@ void set_error(const char *fmt, ...) {
 }
 
 void clear_error() { g_err[0] = 0; }
+
+void ipc_trace(const char *what, int peer, const void *ptr, size_t bytes, const uint8_t handle[64]) {
+    static const bool on = getenv("ESGD_IPC_TRACE") && *getenv("ESGD_IPC_TRACE") == '1';
+    if (!on) return;
+    char hex[129];
+    for (int i = 0; i < 64; ++i) std::snprintf(hex + 2 * i, 3, "%02x", handle[i]);
+    std::fprintf(stderr, "esgd-ipc pid %d %s peer %d ptr %p bytes %zu handle %s\n", int(getpid()), what, peer,
+                 ptr, bytes, hex);
+}
 
 int hip_fail(hipError_t e, const char *what, const char *file, int line) {
     (void)hipGetLastError();   // reported here: not again by the thread's next launch check
