@@ -630,8 +630,10 @@ def gpu_config(rank, world, kind, counts, dtype_name="fp32", rounds=2, async_=32
                 if not good and detail:
                     bad = np.nonzero(got.view(np.uint32 if dt == _lib.FLOAT else np.uint16) !=
                                      want.view(np.uint32 if dt == _lib.FLOAT else np.uint16))[0]
-                    print(f"[r{rank}] count={count} t={t} slice@{start}: {bad.size} bad, first {bad[0] + start} "
-                          f"got {got[bad[0]]} want {want[bad[0]]}; last {bad[-1] + start}", flush=True)
+                    e = int(bad[0])
+                    print(f"[r{rank}] count={count} t={t} slice@{start}: {bad.size} bad, first {e + start} "
+                          f"got {got[e]} want {want[e]}; last {bad[-1] + start}; inputs there "
+                          f"{[float(x[e]) for x in xs]}", flush=True)
                 ok &= good
             out.append((count, dtype_name, t, ok))
         comm.barrier()
