@@ -15,6 +15,11 @@
 //                   joined back to the caller's stream by events): a window's launch can
 //                   start while the previous one's last workgroups drain; 28 / 29 the same
 //                   with 32 / 16 MiB windows over 2 streams
+//   policy 30 / 33  ONE launch that walks the 64 / 32 MiB windows itself, a grid-wide barrier
+//                   between windows (the grid is what is resident, so every block is there):
+//                   the windows' compact footprint without their launch boundaries
+//   policy 31 / 32  ONE launch over the whole bucket, each block at most 1 / 2 grid-stride
+//                   iterations ahead of the slowest (a shared progress counter): bounded drift
 //   policy -1       the production launch (the baseline every variant is timed against)
 // fp32, fan-in 8 only.
 #include <hip/hip_runtime.h>
@@ -153,6 +158,156 @@ static int launch_lds(const InputSet &in, void *out, uint64_t count, hipStream_t
     return ESGD_SUCCESS;
 }
 
+// ---- pacing variants (policies 30-33) ----
+// bar[0]: arrivals (barrier) / finished iterations (drift), bar[1]: barrier generation,
+// bar[2]: blocks done.  The last block out resets bar[0] and bar[2], so consecutive launches
+// on one stream start from zero.  Every wait gives up after ~1 s of polling (a block that is
+// not resident can never arrive; the kernel then finishes unpaced instead of hanging).
+// Every counter access is relaxed: the windows share no data, only pacing, and an acquire
+// or release at agent scope costs an L2 invalidate / write-back per block on gfx950 (the
+// first version, with acq_rel, ran 1.5-4x slower than production).
+constexpr uint32_t kSpinLimit = 1u << 20;
+
+__device__ __forceinline__ void grid_barrier(uint32_t *bar) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t gen = __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+            __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(&bar[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            for (uint32_t n = 0; n < kSpinLimit &&
+                                 __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen; ++n)
+                __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void block_exit(uint32_t *bar) {
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+        __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&bar[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// the production loop body over one window [v0, v0 + nv) of 16-B columns
+template <int U>
+__device__ __forceinline__ void window_body(const InputSet &in, void *out, uint64_t v0, uint32_t nv) {
+    constexpr int B = 256, K = 8;
+    const int bytes = int(nv * 16u);
+    __amdgpu_buffer_rsrc_t rs[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(static_cast<const char *>(in.p[j])) + v0 * 16,
+                                                  (short)0, bytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(static_cast<char *>(out) + v0 * 16, (short)0,
+                                                                  bytes, 0x00020000);
+    const uint32_t step = gridDim.x * (B * U);
+    for (uint32_t i = blockIdx.x * (B * U) + threadIdx.x; i < nv; i += step) {
+        raw16 r[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j) r[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs[j], (i + u * B) * 16, 0, 2);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_raw_buffer_store_b128(fold16<F32, K, false>(r[u], 1.0f), ws, (i + u * B) * 16, 0, 16);
+    }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_tree_sum_paced_windows(InputSet in, void *out, uint64_t count,
+                                                                 uint32_t win_vec, uint32_t *bar) {
+    const uint64_t nvec = count / 4;
+    for (uint64_t v0 = 0; v0 < nvec; v0 += win_vec) {
+        if (v0) grid_barrier(bar);
+        window_body<U>(in, out, v0, uint32_t(nvec - v0 < win_vec ? nvec - v0 : win_vec));
+    }
+    fold_tail<F32, 8, false>(in, out, nvec * 4, count, 1.0f);
+    block_exit(bar);
+}
+
+template <int U, int D>
+__global__ __launch_bounds__(256) void k_tree_sum_bounded_drift(InputSet in, void *out, uint32_t nvec,
+                                                                 uint64_t count, uint32_t *bar) {
+    constexpr int B = 256, K = 8;
+    const int bytes = int(nvec * 16u);
+    __amdgpu_buffer_rsrc_t rs[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(in.p[j]), (short)0, bytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, bytes, 0x00020000);
+    const uint32_t step = gridDim.x * (B * U);
+    uint32_t k = 0;
+    for (uint32_t i = blockIdx.x * (B * U) + threadIdx.x; __builtin_amdgcn_readfirstlane(i - threadIdx.x) < nvec;
+         i += step, ++k) {
+        if (k > D) {   // iteration k may start once every block has finished iteration k - D - 1
+            if (threadIdx.x == 0) {
+                const uint32_t need = (k - D) * gridDim.x;
+                for (uint32_t n = 0; n < kSpinLimit &&
+                                     __hip_atomic_load(&bar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need; ++n)
+                    __builtin_amdgcn_s_sleep(2);
+            }
+            __syncthreads();
+        }
+        raw16 r[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j) r[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs[j], (i + u * B) * 16, 0, 2);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_raw_buffer_store_b128(fold16<F32, K, false>(r[u], 1.0f), ws, (i + u * B) * 16, 0, 16);
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // blocks with fewer iterations still count the ones they skip, so `need` is reachable
+    const uint32_t iters = (nvec + step - 1) / step;
+    if (threadIdx.x == 0 && k < iters)
+        __hip_atomic_fetch_add(&bar[0], iters - k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fold_tail<F32, 8, false>(in, out, uint64_t(nvec) * 4, count, 1.0f);
+    block_exit(bar);
+}
+
+static uint32_t *g_bar = nullptr;
+
+static int pace_bar(uint32_t **out) {
+    if (!g_bar) {
+        ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&g_bar), 64));
+        ESGD_HIP(hipMemset(g_bar, 0, 64));
+        ESGD_HIP(hipDeviceSynchronize());
+    }
+    *out = g_bar;
+    return ESGD_SUCCESS;
+}
+
+static int launch_paced_windows(const InputSet &in, void *out, uint64_t count, hipStream_t s, uint64_t window_bytes) {
+    uint32_t *bar = nullptr;
+    if (int rc = pace_bar(&bar)) return rc;
+    static const int per_cu = resident_blocks(k_tree_sum_paced_windows<4>, 256);
+    const uint64_t win_vec = window_bytes / 16;
+    const unsigned grid = grid_for(uint64_t(256) * 4, std::min<uint64_t>(win_vec, count / 4 ? count / 4 : 1), per_cu);
+    hipLaunchKernelGGL((k_tree_sum_paced_windows<4>), dim3(grid), dim3(256), 0, s, in, out, count,
+                       uint32_t(win_vec), bar);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+template <int D>
+static int launch_bounded_drift(const InputSet &in, void *out, uint64_t count, hipStream_t s) {
+    uint32_t *bar = nullptr;
+    if (int rc = pace_bar(&bar)) return rc;
+    static const int per_cu = resident_blocks(k_tree_sum_bounded_drift<4, D>, 256);
+    const uint64_t nvec = count / 4;
+    const unsigned grid = grid_for(uint64_t(256) * 4, nvec ? nvec : 1, per_cu);
+    hipLaunchKernelGGL((k_tree_sum_bounded_drift<4, D>), dim3(grid), dim3(256), 0, s, in, out, uint32_t(nvec),
+                       count, bar);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
 // windows over NS streams: stream 0 is the caller's, the others fork from it and join back
 static hipStream_t g_aux[4] = {};
 static hipEvent_t g_fork = nullptr, g_join[4] = {};
@@ -240,6 +395,10 @@ int esgd_sweep_reduce(int policy, int unroll, int nt, int grid, const void *cons
     case 27: return launch_windows_streams(in, out, count, s, 4, g);
     case 28: return launch_windows_streams(in, out, count, s, 2, g, uint64_t(32) << 20);
     case 29: return launch_windows_streams(in, out, count, s, 2, g, uint64_t(16) << 20);
+    case 30: return launch_paced_windows(in, out, count, s, uint64_t(64) << 20);
+    case 31: return launch_bounded_drift<1>(in, out, count, s);
+    case 32: return launch_bounded_drift<2>(in, out, count, s);
+    case 33: return launch_paced_windows(in, out, count, s, uint64_t(32) << 20);
     default: break;
     }
     set_error("unknown policy %d", policy);
