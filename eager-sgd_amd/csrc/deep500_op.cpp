@@ -112,12 +112,20 @@ struct AllreduceOp {
             if (esgd::arena_alloc(nbytes ? nbytes : 256, reinterpret_cast<void **>(&sb)) ||
                 esgd::arena_alloc(nbytes ? nbytes : 256, reinterpret_cast<void **>(&rb)) ||
                 hipMemset(sb, 0, nbytes) != hipSuccess || hipMemset(rb, 0, nbytes) != hipSuccess) {
+                (void)hipGetLastError();   // reported here, not by the next launch check
+                if (sb) esgd::arena_free(sb);
+                if (rb) esgd::arena_free(rb);
+                sb = rb = nullptr;
                 esgd::set_error("device bucket allocation of %zu bytes", nbytes);
                 return ESGD_ENOMEM;
             }
         } else {
             if (hipHostMalloc(reinterpret_cast<void **>(&sb), nbytes ? nbytes : 256, hipHostMallocDefault) != hipSuccess ||
                 hipHostMalloc(reinterpret_cast<void **>(&rb), nbytes ? nbytes : 256, hipHostMallocDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                if (sb) hip_ignore(hipHostFree(sb));
+                if (rb) hip_ignore(hipHostFree(rb));
+                sb = rb = nullptr;
                 esgd::set_error("pinned bucket allocation of %zu bytes", nbytes);
                 return ESGD_ENOMEM;
             }
@@ -169,8 +177,8 @@ int cuda_copy_in(AllreduceOp *op, const float *input, float divisor, hipStream_t
     const size_t nbytes = size_t(op->len) * sizeof(float);
     const uint64_t n = op->len;
     if (divisor == kNoDivide) {
-        if (hipMemcpyAsync(op->sb, input, nbytes, hipMemcpyDeviceToDevice, s) != hipSuccess) {
-            esgd::set_error("allreducef: copy-in failed");
+        if (const hipError_t e = hipMemcpyAsync(op->sb, input, nbytes, hipMemcpyDeviceToDevice, s)) {
+            (void)hip_fail(e, "allreducef: copy-in", __FILE__, __LINE__);
             return ESGD_ERROR;
         }
         return ESGD_SUCCESS;
@@ -179,8 +187,9 @@ int cuda_copy_in(AllreduceOp *op, const float *input, float divisor, hipStream_t
 }
 
 int cuda_copy_out(AllreduceOp *op, float *output, hipStream_t s) {
-    if (hipMemcpyAsync(output, op->rb, size_t(op->len) * sizeof(float), hipMemcpyDeviceToDevice, s) != hipSuccess) {
-        esgd::set_error("allreducef: copy-out failed");
+    if (const hipError_t e = hipMemcpyAsync(output, op->rb, size_t(op->len) * sizeof(float),
+                                            hipMemcpyDeviceToDevice, s)) {
+        (void)hip_fail(e, "allreducef: copy-out", __FILE__, __LINE__);
         return ESGD_ERROR;
     }
     return ESGD_SUCCESS;
