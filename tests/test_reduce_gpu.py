@@ -341,3 +341,19 @@ def test_arena_growth_bounded_over_a_size_sweep():
     st = memory_stats()
     assert st["reserved"] - base <= 304 * MiB, st
     assert st["in_use"] == st0["in_use"], (st0, st)
+
+
+def test_a_reported_hip_failure_does_not_fail_the_next_launch():
+    # HIP keeps a failed call's status in the thread's last-error slot until
+    # hipGetLastError() reads it, and every launch here is checked with hipGetLastError():
+    # a failure the library reported (or tolerated) must not resurface as the next,
+    # unrelated launch's error (round 3: "esgd_fill_uniform: invalid argument" after a
+    # tolerated teardown failure)
+    import ctypes as C
+    import esgd
+    rc = esgd.lib().esgd_free(C.c_void_p(0x7ff0dead0000))   # not a device allocation
+    assert rc != 0
+    b = DeviceBuffer(4099)
+    fill_uniform(b, 0x5EED, 1)
+    synchronize()
+    bits_equal(b.download(), ffref.fill_uniform(0x5EED, 1, 4099))
