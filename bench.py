@@ -425,13 +425,25 @@ def gate_256(dev, dt, es, k, s, iters=20, avg_iters=100):
     s.synchronize()
     avg = e0.elapsed_ms(e1) / avg_iters
     algo = (k + 1) * count * es
+    # also k = 2 in place, the reference's own step rb = tmp + rb
+    # (ffallreduce.c:155-162; tmp is operand a): B = 3 S per call
+    e0.record(s)
+    for _ in range(avg_iters):
+        dev.reduce(dt, [ptrs[0], ptrs[1]], ptrs[0], count, stream=s)
+    e1.record(s)
+    s.synchronize()
+    avg2 = e0.elapsed_ms(e1) / avg_iters
+    algo2 = 3 * count * es
     for b in bufs:
         b.close()
     out.close()
     return {"workload": f"{k} x 256 MiB -> 1", "kernel_ms_avg": round(avg, 4),
             "kernel_ms_median_per_launch_pairs": round(med, 4),
             "achieved_GBs": round(algo / (avg * 1e-3) / 1e9, 1),
-            "frac": round(algo / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            "frac": round(algo / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "k2_inplace": {"workload": "rb = tmp + rb, 2 x 256 MiB, in place", "kernel_ms_avg": round(avg2, 4),
+                           "algo_bytes": algo2, "achieved_GBs": round(algo2 / (avg2 * 1e-3) / 1e9, 1),
+                           "frac": round(algo2 / (avg2 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
 
 
 # N > 1: schedules (and their buckets) stay alive until every leg has run, then are
