@@ -565,6 +565,13 @@ __device__ __forceinline__ void publish_flags(const PairFlags &f, uint32_t value
     for (int q = 0; q < f.ndst; ++q) __hip_atomic_store(f.dst[q], value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The same publication where every byte it announces was stored write-through at system
+// scope (sc0 sc1) and drained: no L2 write-back, only the wait.  Lane 0.
+__device__ __forceinline__ void publish_flags_drained(const PairFlags &f, uint32_t value) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int q = 0; q < f.ndst; ++q) __hip_atomic_store(f.dst[q], value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 //
 // Peer buckets are coarse-grained memory of other processes (other GPUs on a node).  When
 // the phase after this pairing reads peers (`gate` != nullptr), every XCD's L2 (and the
@@ -679,8 +686,11 @@ __device__ __forceinline__ bool block_wait(const SmallRoundArgs &a, const uint32
         bool good = true;
         if (leader) {         // every rank's flag at once, one lane per rank
             good = wave_wait_all(flags, a.world, a.value, t0, a.timeout);
+            // relaxed: the gate carries no data of this workgroup's -- every waiter runs
+            // its own system-scope acquire after seeing it (an agent release here was a
+            // buffer_wbl2 sc1, ~1.7 us, on every pairing's critical path)
             if (good && threadIdx.x == 0)
-                __hip_atomic_store(gate, a.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(gate, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else if (threadIdx.x == 0) {
             good = spin_all(gate, 1, a.value, t0, a.timeout);
         }
@@ -694,12 +704,18 @@ __device__ __forceinline__ bool block_wait(const SmallRoundArgs &a, const uint32
     return *ok != 0;
 }
 
-// every workgroup drains its stores and counts itself; true in the last one to arrive
+// every workgroup drains its stores and counts itself; true in the last one to arrive.
+// The count is a relaxed agent-scope add: every payload store of this kernel is
+// system-scope write-through (sc0 sc1) and every wave has drained its stores (vmcnt(0))
+// before the barrier that precedes the add, so the bytes are in memory before the add
+// is issued (MI355X_MICROARCH.md, hand-off table row 1), and the last workgroup reads
+// none of them itself.  An acq_rel add lowered to buffer_wbl2 sc1 + buffer_inv sc1 in
+// EVERY workgroup, ~3.5 us, twice per round.
 __device__ __forceinline__ bool block_count(uint32_t *ctr, int *last) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *last = old + 1 == gridDim.x;
         if (*last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -764,7 +780,9 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
     const bool last1 = block_count(&a.counter[0], &last);
     if (last1 && lead) {
         if (stamp) a.ts[2] = uint64_t(wall_clock64());
-        publish_flags(a.reduced, a.value);
+        // phase 1 wrote only sc0 sc1 (write-through) stores, drained by every workgroup
+        // before its count: no L2 write-back is needed before the flag
+        publish_flags_drained(a.reduced, a.value);
     }
     if (!block_wait(a, a.reduced.mine, &a.counter[3], last1, t0, &ok)) return;
     // the all-gather span is stamped by ONE workgroup (the last to finish): the wall
