@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -51,6 +52,7 @@ struct Chunk {
     size_t bytes = 0;
     int device = -1;
     bool exported = false;
+    bool unexportable = false;   // the runtime refused its export: no new blocks from it
     uint8_t handle[64] = {};
     int live = 0;          // blocks handed out and not freed
 };
@@ -90,8 +92,8 @@ void run_erase(uintptr_t p) {
     g_runs.erase(it);
 }
 
-// every free entry of chunk c is dropped and its memory goes back to the driver
-void release_chunk(Chunk *c) {
+// every free entry of chunk c is dropped from the free lists
+void drop_free(Chunk *c) {
     for (auto &fl : g_small) {
         auto &v = fl.second;
         v.erase(std::remove_if(v.begin(), v.end(), [&](char *p) { return p >= c->base && p < c->base + c->bytes; }),
@@ -103,6 +105,11 @@ void release_chunk(Chunk *c) {
         ++it;
         run_erase(p);
     }
+}
+
+// every free entry of chunk c is dropped and its memory goes back to the driver
+void release_chunk(Chunk *c) {
+    drop_free(c);
     g_by_base.erase(reinterpret_cast<uintptr_t>(c->base));
     g_chunks.erase(std::remove(g_chunks.begin(), g_chunks.end(), c), g_chunks.end());
     if (c->exported) ipc_trace("free", -1, c->base, c->bytes, c->handle);
@@ -215,6 +222,10 @@ bool arena_free(void *p) {
         release_chunk(b.chunk);
         return true;
     }
+    if (b.chunk->unexportable) {   // never exported: back to the driver with its last block
+        if (!b.chunk->live) release_chunk(b.chunk);
+        return true;
+    }
     if (b.cls <= kSlab / 2) {
         g_small[{b.chunk->device, b.cls}].push_back(static_cast<char *>(p));
         return true;
@@ -238,6 +249,17 @@ bool arena_free(void *p) {
     }
     run_insert(reinterpret_cast<char *>(start), bytes, b.chunk);
     return true;
+}
+
+// true if p lies in an arena chunk whose export the runtime refused (arena_export)
+bool arena_unexportable(const void *p) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    auto it = g_by_base.upper_bound(a);
+    if (it == g_by_base.begin()) return false;
+    --it;
+    const Chunk *c = it->second;
+    return a < it->first + c->bytes && c->unexportable;
 }
 
 // device of the arena block starting at p, -1 if p is not one
@@ -276,10 +298,23 @@ int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_
         // On round 3's boxes the dmabuf export of a fresh chunk failed now and then with
         // hipErrorInvalidValue (a new process's first schedule, after other tests' ranks
         // had exited; profiles/r03/README.md).  Creation is rare, so a failed export is
-        // retried with growing pauses (1 + 2 + ... + 256 ms) before the schedule fails;
-        // each failed attempt is reported on stderr.
+        // retried with growing pauses (1 + 2 + ... + 256 ms); each failed attempt is
+        // reported on stderr.  A chunk that still cannot be exported is marked so.
         hipError_t e = hipSuccess;
-        for (int attempt = 0, pause_ms = 1; attempt < 10; ++attempt, pause_ms *= 2) {
+        // ESGD_FAIL_EXPORTS=N (tests): the process's first N chunk exports fail as the
+        // runtime's did, without calling it, so the fallbacks can be exercised anywhere
+        static int simulated = [] {
+            const char *v = getenv("ESGD_FAIL_EXPORTS");
+            return (v && *v) ? std::max(0, atoi(v)) : 0;
+        }();
+        const bool simulate = simulated > 0;
+        if (simulate) {
+            --simulated;
+            e = hipErrorInvalidValue;
+            std::fprintf(stderr, "esgd: export of %p (%zu B chunk) fails by ESGD_FAIL_EXPORTS\n",
+                         static_cast<void *>(c->base), c->bytes);
+        }
+        for (int attempt = 0, pause_ms = 1; !simulate && attempt < 10; ++attempt, pause_ms *= 2) {
             e = hipIpcGetMemHandle(&h, c->base);
             if (e == hipSuccess) break;
             (void)hipGetLastError();
@@ -288,6 +323,22 @@ int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_
             if (attempt < 9) std::this_thread::sleep_for(std::chrono::milliseconds(pause_ms));
         }
         if (e != hipSuccess) {
+            // no new block comes from this chunk; the data plane re-allocates the buffers
+            // it owns (a fresh chunk) and shadows a caller's bucket that lives here
+            c->unexportable = true;
+            drop_free(c);
+            // diagnostics: can this process export a fresh allocation at all?
+            void *probe = nullptr;
+            if (!simulate && hipMalloc(&probe, kSlab) == hipSuccess) {
+                hipIpcMemHandle_t ph;
+                const hipError_t pe = hipIpcGetMemHandle(&ph, probe);
+                std::fprintf(stderr, "esgd: export of a fresh %zu B allocation at %p: %s\n", kSlab, probe,
+                             hipGetErrorString(pe));
+                (void)hipGetLastError();
+                hip_ignore(hipFree(probe));
+            } else {
+                (void)hipGetLastError();
+            }
             const char *m = getenv("HSA_ENABLE_IPC_MODE_LEGACY");
             int rc = hip_fail(e, "hipIpcGetMemHandle", __FILE__, __LINE__);
             if (!m || std::strcmp(m, "0") != 0) {

@@ -853,15 +853,43 @@ struct IpcTransport final : Transport {
         return ESGD_SUCCESS;
     }
 
+    // Publish a buffer this schedule owns.  When the runtime refuses to export its arena
+    // chunk (arena_export marks the chunk; round 3 saw hipErrorInvalidValue for a fresh
+    // process's first chunk now and then), the buffer is allocated again -- the arena no
+    // longer carves from that chunk -- and the new one is published.  Contents need not
+    // move: every caller publishes before the round that fills the buffer.
+    static int publish_owned(Sched &s, IpcSlot &slot, char **buf, size_t *cap, size_t bytes, const char *what) {
+        for (int attempt = 0;; ++attempt) {
+            const int rc = publish_buf(s, slot, *buf, bytes, what);
+            if (rc == ESGD_SUCCESS || attempt == 2 || !arena_unexportable(*buf)) return rc;
+            char *old = *buf;
+            const size_t want = *cap;
+            if (int ra = alloc_bucket(want, buf, cap)) return ra;
+            std::fprintf(stderr, "esgd: rank %d schedule %d: %s %p could not be exported, moved to %p\n", s.rank,
+                         s.id, what, static_cast<void *>(old), static_cast<void *>(*buf));
+            free_bucket(old);
+        }
+    }
+
     static int publish(Sched &s, IpcState &st) {
         if (s.wire_bf16) {   // peers read the wire copy; rb stays private (never shadowed)
             if (!st.wire)
                 if (int rc = alloc_bucket(s.count * 2, &st.wire, &st.wire_cap)) return rc;
+            const int rc = publish_owned(s, s.sh->slot[s.rank], &st.wire, &st.wire_cap, s.count * 2, "wire");
             st.peer[s.rank] = st.wire;
-            return publish_buf(s, s.sh->slot[s.rank], st.wire, s.count * 2, "wire");
+            return rc;
+        }
+        if (st.owns_rb) {
+            const int rc = publish_owned(s, s.sh->slot[s.rank], &st.rb_dev, &st.cap, s.count * s.esize, "rb");
+            st.peer[s.rank] = st.rb_dev;
+            return rc;
         }
         st.peer[s.rank] = st.rb_dev;
-        return publish_buf(s, s.sh->slot[s.rank], st.rb_dev, s.count * s.esize, "rb");
+        const int rc = publish_buf(s, s.sh->slot[s.rank], st.rb_dev, s.count * s.esize, "rb");
+        // the caller's bucket sits in a chunk the runtime would not export: setup shadows
+        // it, as it does foreign memory
+        if (rc && arena_unexportable(st.rb_dev)) return ESGD_INVALID_ARG;
+        return rc;
     }
 
     // rounds of this size run as one k_round_small launch
@@ -877,7 +905,7 @@ struct IpcTransport final : Transport {
         if (st.pub && need <= st.pub_cap) return ESGD_SUCCESS;
         if (st.pub) st.retired.push_back(st.pub);   // peers may still map it: back at teardown
         if (int rc = alloc_bucket(need, &st.pub, &st.pub_cap)) return rc;
-        return publish_buf(s, s.sh->pub[s.rank], st.pub, st.pub_cap, "pub");
+        return publish_owned(s, s.sh->pub[s.rank], &st.pub, &st.pub_cap, st.pub_cap, "pub");
     }
 
     // (re)map one peer publication if it changed since we last mapped it

@@ -55,6 +55,7 @@ void ipc_trace(const char *what, int peer, const void *ptr, size_t bytes, const 
 int arena_alloc(size_t bytes, void **out);
 bool arena_free(void *p);
 int arena_device(const void *p);   // device of an arena block, -1 if p is not one
+bool arena_unexportable(const void *p);   // p's chunk: the runtime refused its IPC export
 void arena_stats(uint64_t *reserved, uint64_t *live, uint64_t *exported);
 int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_t handle[64]);
 void arena_trim();

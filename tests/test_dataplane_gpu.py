@@ -479,6 +479,26 @@ def test_writer_then_post_visibility_across_gpus(path, flags):
             assert len(set(o["devices"].split(","))) == world, o
 
 
+@pytest.mark.parametrize("fails", [1, 2])
+def test_schedules_survive_refused_exports(fails):
+    # The runtime sometimes refuses to export a fresh process's first chunk
+    # (hipErrorInvalidValue, round 3).  ESGD_FAIL_EXPORTS=N fails each rank's first N chunk
+    # exports the same way: buffers the schedule owns (published shard, host-bucket
+    # staging) move to fresh chunks, a caller's device bucket in a refused chunk is
+    # shadowed, and every round is still bit-exact
+    old = os.environ.get("ESGD_FAIL_EXPORTS")
+    os.environ["ESGD_FAIL_EXPORTS"] = str(fails)
+    try:
+        for kw in (dict(count=4099), dict(count=300007, small_bytes=0), dict(count=70001, buf="host")):
+            verdicts = run("gpu_allreduce", 2, rounds=2, **kw)
+            assert all(all(v) for v in verdicts), (kw, verdicts)
+    finally:
+        if old is None:
+            os.environ.pop("ESGD_FAIL_EXPORTS", None)
+        else:
+            os.environ["ESGD_FAIL_EXPORTS"] = old
+
+
 def test_second_job_after_ipc_mappings_closed_is_refused():
     outs = run("gpu_reinit", 2)
     for o in outs:
