@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""ResNet-50 trained with eager-SGD on PyTorch-ROCm: the reference's use of the path.
+
+The reference trains ResNet-50 on ImageNet with TF 1.x and swaps its optimizer for
+EagerSGDOptimizer (test-models/tf-models-r1.11/official/resnet/resnet_run_loop_solo_
+imagenet_300.py:46), with a synthetic load imbalance: every step, seeded by the step
+counter, up to two randomly drawn ranks sleep 0.32 s before the forward pass (:287-296).
+This script runs the same loop on MI355X -- a ResNet-50 whose 161 trainable tensors hold
+the reference's 25 559 081 parameters (1001 classes, the model garden's ImageNet head;
+the bucket table of opt_esgd_solo_imagenet_imbalance.py:86-248), synthetic images,
+fp32 -- with one of:
+  --mode solo | majority   eager-SGD (esgd.optim.EagerSGDOptimizer, per tensor or --fuse)
+  --mode allreduce         the same optimizer, every round synchronous
+  --mode ddp               torch.distributed all_reduce of each gradient over RCCL, divided
+                           after (opt_sgd_mpi.py:40-44's synchronous baseline; needs one
+                           GPU per rank)
+One JSON line from rank 0: step time, images/s over all ranks, and whether every rank
+ended with bit-identical weights (always so for the synchronous modes; eager-SGD lets
+ranks that missed a round drift, as the paper's partial collectives intend).
+
+  python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
+      examples/resnet50_eager_sgd.py --mode solo --steps 50
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "eager-sgd_amd"))
+
+
+def resnet50(classes: int = 1001):
+    """ResNet-50 v1.5 (stride in the 3x3 conv of each bottleneck): 53 convolutions, 53
+    batch norms (scale + shift) and the dense head = 161 trainable tensors."""
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    class Bottleneck(nn.Module):
+        def __init__(self, cin, width, stride, project):
+            super().__init__()
+            self.conv1, self.bn1 = nn.Conv2d(cin, width, 1, bias=False), nn.BatchNorm2d(width)
+            self.conv2, self.bn2 = nn.Conv2d(width, width, 3, stride, 1, bias=False), nn.BatchNorm2d(width)
+            self.conv3, self.bn3 = nn.Conv2d(width, 4 * width, 1, bias=False), nn.BatchNorm2d(4 * width)
+            self.project = nn.Sequential(nn.Conv2d(cin, 4 * width, 1, stride, bias=False),
+                                         nn.BatchNorm2d(4 * width)) if project else None
+
+        def forward(self, x):
+            skip = x if self.project is None else self.project(x)
+            y = F.relu(self.bn1(self.conv1(x)))
+            y = F.relu(self.bn2(self.conv2(y)))
+            return F.relu(self.bn3(self.conv3(y)) + skip)
+
+    layers = [nn.Conv2d(3, 64, 7, 2, 3, bias=False), nn.BatchNorm2d(64), nn.ReLU(inplace=True),
+              nn.MaxPool2d(3, 2, 1)]
+    cin = 64
+    for width, blocks, stride in ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)):
+        for b in range(blocks):
+            layers.append(Bottleneck(cin, width, stride if b == 0 else 1, b == 0))
+            cin = 4 * width
+    layers += [nn.AdaptiveAvgPool2d(1), nn.Flatten(), nn.Linear(cin, classes)]
+    return nn.Sequential(*layers)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", choices=["solo", "majority", "allreduce", "ddp"], default="solo")
+    ap.add_argument("--fuse", action="store_true", help="eager-SGD: one fused bucket per step")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="images per rank per step")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--delay", type=float, default=0.32,
+                    help="seconds a drawn rank sleeps before its forward pass (0: balanced)")
+    return ap.parse_args()
+
+
+def straggles(step: int, rank: int, world: int) -> bool:
+    """resnet_run_loop_solo_imagenet_300.py:290-294: seeded by the step counter, the rank
+    sleeps if it equals the first draw or (failing that) a second draw."""
+    import numpy as np
+    np.random.seed(step)
+    return rank == np.random.randint(world) or rank == np.random.randint(world)
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    import esgd
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = esgd.device_count()
+    if ndev < 1:
+        raise SystemExit("resnet50_eager_sgd.py: no HIP device")
+    dev = torch.device("cuda", local % ndev)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    if a.mode == "ddp":
+        if world > ndev:
+            raise SystemExit("--mode ddp needs one GPU per rank (RCCL refuses ranks sharing a GPU)")
+        group = dist.new_group(backend="nccl") if world > 1 else None
+    else:
+        from esgd import comm
+        from esgd.optim import EagerSGDOptimizer
+        esgd.check(esgd.lib().esgd_set_device(local % ndev), "esgd_set_device")
+        comm.init()
+
+    torch.manual_seed(42)   # the same initial weights on every rank
+    model = resnet50().to(dev)
+    params = [p for p in model.parameters() if p.requires_grad]
+    sgd = torch.optim.SGD(params, lr=0.1, momentum=0.9)
+    opt = sgd if a.mode == "ddp" else EagerSGDOptimizer(sgd, world, mode=a.mode, fuse=a.fuse)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = torch.randn(a.batch, 3, a.image, a.image, device=dev, generator=g)
+    y = torch.randint(0, 1001, (a.batch,), device=dev, generator=g)
+
+    def step(t):
+        if a.delay > 0 and world > 1 and straggles(t, rank, world):
+            time.sleep(a.delay)
+        loss = torch.nn.functional.cross_entropy(model(x), y)
+        if a.mode == "ddp":
+            sgd.zero_grad()
+            loss.backward()
+            for p in params:   # opt_sgd_mpi.py: allreduce every gradient, then divide
+                if group is not None:
+                    dist.all_reduce(p.grad, group=group)
+                p.grad.div_(world)
+            sgd.step()
+        else:
+            opt.zero_grad()
+            opt.apply_gradients(opt.compute_gradients(loss))
+        torch.cuda.synchronize()
+
+    for t in range(a.warmup):
+        step(t)
+    # one barrier before the timed steps, none between them: a rank that was not drawn
+    # runs ahead (eager-SGD) or waits inside the collective (synchronous modes), as in
+    # the reference's run loop
+    if world > 1:
+        dist.barrier()
+    times = []
+    t_all = time.perf_counter()
+    for t in range(a.warmup, a.warmup + a.steps):
+        t0 = time.perf_counter()
+        step(t)
+        times.append(time.perf_counter() - t0)
+    wall = time.perf_counter() - t_all
+
+    digest = hashlib.sha256()
+    for p in params:
+        digest.update(p.detach().cpu().numpy().tobytes())
+    mine = {"digest": digest.hexdigest(), "wall": wall, "device": local % ndev}
+    alls = [mine]
+    if world > 1:
+        alls = [None] * world
+        dist.all_gather_object(alls, mine)
+    if rank == 0:
+        wall_max = max(o["wall"] for o in alls)
+        print(json.dumps({
+            "model": "resnet50 (1001 classes)", "tensors": len(params),
+            "parameters": sum(p.numel() for p in params), "mode": a.mode, "fuse": a.fuse,
+            "world": world, "batch_per_rank": a.batch, "image": a.image, "dtype": "f32",
+            "data": "synthetic", "straggler_delay_s": a.delay, "steps": a.steps,
+            "step_ms_median": round(statistics.median(times) * 1e3, 2),
+            "images_per_s": round(world * a.batch * a.steps / wall_max, 1),
+            "weights_identical_on_every_rank": len({o["digest"] for o in alls}) == 1,
+            "devices": [o["device"] for o in alls],
+        }), flush=True)
+    if a.mode != "ddp":
+        comm.finalize()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
