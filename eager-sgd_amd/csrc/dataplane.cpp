@@ -40,6 +40,17 @@ int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64
 int gather_remote(int n, const void *const *src, void *const *dst, const uint64_t *bytes,
                   hipStream_t s, unsigned max_blocks = 0);
 int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s);
+int snapshot_copy(void *dst, const void *src, uint64_t bytes, hipStream_t s);
+
+// ESGD_SNAPSHOT_KERNEL: 1 = device-bucket snapshots (rb = sb, rb = 0) by k_snapshot's
+// write-through stores; 0 = hipMemcpyAsync / hipMemsetAsync
+static bool snapshot_kernel() {
+    static const bool on = [] {
+        const char *e = getenv("ESGD_SNAPSHOT_KERNEL");
+        return e && *e == '1';
+    }();
+    return on;
+}
 int narrow_bf16(float *src, uint16_t *dst, uint64_t n, bool zero_src, hipStream_t s);
 int reduce_wire(int k, const void *const *inputs, uint16_t *outb, float *outf, uint64_t count, hipStream_t s);
 int gather_widen(int n, const void *const *src, void *const *dst, const uint64_t *count, hipStream_t s);
@@ -703,6 +714,8 @@ static int base_copy_in(Sched &s, BaseState &st, uint32_t round, bool fresh, hip
     if (s.fresh_only && !fresh) {
         // carried through a round it had not posted: this rank contributes zeros, and its
         // send bucket -- which the caller may be writing right now -- is not read
+        if (snapshot_kernel() && (reinterpret_cast<uintptr_t>(st.rb_dev) & 15) == 0)
+            return snapshot_copy(st.rb_dev, nullptr, bytes, cs);
         ESGD_HIP(hipMemsetAsync(st.rb_dev, 0, bytes, cs));
         return ESGD_SUCCESS;
     }
@@ -715,7 +728,10 @@ static int base_copy_in(Sched &s, BaseState &st, uint32_t round, bool fresh, hip
         // the move and the wrapper's zero-after-use in one pass: rb = sb, sb = 0
         if (int rc = move_zero(st.rb_dev, s.sb, bytes, cs)) return rc;
     } else if (!s.in_place || st.shadow) {
-        ESGD_HIP(hipMemcpyAsync(st.rb_dev, s.in_place ? s.rb : s.sb, bytes, hipMemcpyDeviceToDevice, cs));
+        const void *src = s.in_place ? s.rb : s.sb;
+        if (snapshot_kernel() && ((reinterpret_cast<uintptr_t>(st.rb_dev) | reinterpret_cast<uintptr_t>(src)) & 15) == 0)
+            return snapshot_copy(st.rb_dev, src, bytes, cs);
+        ESGD_HIP(hipMemcpyAsync(st.rb_dev, src, bytes, hipMemcpyDeviceToDevice, cs));
     }
     return ESGD_SUCCESS;
 }

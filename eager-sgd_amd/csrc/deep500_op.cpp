@@ -84,6 +84,12 @@ int on_error_policy() {
     return (e && !strcmp(e, "local")) ? ESGD_OP_ON_ERROR_LOCAL : ESGD_OP_ON_ERROR_ABORT;
 }
 
+// The op's stream argument names the framework's stream; NULL is the legacy default
+// stream (stream 0: torch's default stream, a TF kernel without a device context), never
+// the library's own stream -- work queued for the caller (copy-in, copy-out, the producer
+// and consumer events) must be ordered with the caller's work on that stream.
+void *caller_stream(hipStream_t s) { return s ? static_cast<void *>(s) : ESGD_STREAM_NULL; }
+
 struct AllreduceOp {
     uint64_t len = 0;
     OpConfig cfg;
@@ -146,7 +152,7 @@ struct AllreduceOp {
     int post_round(hipStream_t s) {
         // the snapshot of this round waits for the copy-in just queued on the caller's
         // stream (the data plane's streams are non-blocking: the NULL stream is named)
-        void *ps = s ? static_cast<void *>(s) : ESGD_STREAM_NULL;
+        void *ps = caller_stream(s);
         // a round a peer's activation carried this rank through before this post took
         // zeros, not the gradient (FRESH_ONLY): the gradient is dropped, and the next
         // copy-in overwrites the send bucket before it is read again
@@ -155,7 +161,7 @@ struct AllreduceOp {
 
     template <class Out>
     int finish_round(hipStream_t s, Out &&out) {
-        void *ps = s ? static_cast<void *>(s) : ESGD_STREAM_NULL;
+        void *ps = caller_stream(s);
         if (int rc = esgd_schedule_wait(sched)) return rc;
         if (int rc = out()) return rc;
         if (int rc = esgd_schedule_release(sched, ps)) return rc;
@@ -172,6 +178,7 @@ struct AllreduceOp {
 
 constexpr float kNoDivide = 1.0f;
 
+
 // copy-in of a device round, on s: a plain copy, or the wrapper's division (:40) fused
 int cuda_copy_in(AllreduceOp *op, const float *input, float divisor, hipStream_t s) {
     const size_t nbytes = size_t(op->len) * sizeof(float);
@@ -183,7 +190,7 @@ int cuda_copy_in(AllreduceOp *op, const float *input, float divisor, hipStream_t
         }
         return ESGD_SUCCESS;
     }
-    return esgd_pack_div(1, &input, &n, op->sb, divisor, s);
+    return esgd_pack_div(1, &input, &n, op->sb, divisor, caller_stream(s));
 }
 
 int cuda_copy_out(AllreduceOp *op, float *output, hipStream_t s) {
@@ -322,8 +329,8 @@ int allreducef_forward_cuda_packed(void *handle, int n, const float *const *grad
     ESGD_ARG(!op->pending, "allreducef_forward_cuda_packed: a split round is posted and not yet waited");
     if (int rc = op->ensure(true)) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (int rc = esgd_pack_div(n, grads, counts, op->sb, divisor, s)) return rc;
-    return op->device_round(s, [&]() -> int { return esgd_unpack(n, outs, counts, op->rb, s); });
+    if (int rc = esgd_pack_div(n, grads, counts, op->sb, divisor, caller_stream(s))) return rc;
+    return op->device_round(s, [&]() -> int { return esgd_unpack(n, outs, counts, op->rb, caller_stream(s)); });
 }
 
 int allreducef_forward_cuda_post(void *handle, const float *input, float divisor, void *stream) {

@@ -32,7 +32,12 @@ hipStream_t default_stream();
 // Fails with ESGD_NO_DEVICE (and a message) if no HIP device is usable.
 int require_device();
 
-inline hipStream_t as_stream(void *s) { return s ? static_cast<hipStream_t>(s) : default_stream(); }
+// A stream argument of the ABI: NULL is the library's own stream, ESGD_STREAM_NULL the
+// legacy default stream (stream 0, e.g. torch's default stream), anything else a stream.
+inline hipStream_t as_stream(void *s) {
+    if (s == ESGD_STREAM_NULL) return nullptr;
+    return s ? static_cast<hipStream_t>(s) : default_stream();
+}
 
 // Device memory that peers may map (arena.cpp): never given back while it may be mapped.
 // Where the flags of one rank pairing live (data plane -> round kernels).  A rank

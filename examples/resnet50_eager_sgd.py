@@ -79,6 +79,9 @@ def parse():
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--delay", type=float, default=0.32,
                     help="seconds a drawn rank sleeps before its forward pass (0: balanced)")
+    ap.add_argument("--trace-grads", action="store_true",
+                    help="digest every step's reduced gradients on every rank; report the first step "
+                         "whose reduced gradients differ between ranks (slow: host copies)")
     return ap.parse_args()
 
 
@@ -124,6 +127,8 @@ def main():
     x = torch.randn(a.batch, 3, a.image, a.image, device=dev, generator=g)
     y = torch.randint(0, 1001, (a.batch,), device=dev, generator=g)
 
+    traced = []   # (step, slept, digest of the reduced gradients) with --trace-grads
+
     def step(t):
         if a.delay > 0 and world > 1 and straggles(t, rank, world):
             time.sleep(a.delay)
@@ -140,6 +145,16 @@ def main():
             opt.zero_grad()
             opt.apply_gradients(opt.compute_gradients(loss))
         torch.cuda.synchronize()
+        if a.trace_grads:
+            h = hashlib.sha256()
+            for p in params:
+                h.update(p.grad.detach().cpu().numpy().tobytes())
+            # zero fraction per rank-shard of the fused bucket (its order: reversed params)
+            flat = torch.cat([p.grad.detach().reshape(-1) for p in reversed(params)]).cpu().numpy()
+            per = -(-flat.size // world)
+            zeros = [round(float((flat[q * per:(q + 1) * per] == 0).mean()), 4) for q in range(world)]
+            traced.append((t, straggles(t, rank, world) if a.delay > 0 and world > 1 else False,
+                           h.hexdigest()[:16], zeros))
 
     for t in range(a.warmup):
         step(t)
@@ -159,7 +174,7 @@ def main():
     digest = hashlib.sha256()
     for p in params:
         digest.update(p.detach().cpu().numpy().tobytes())
-    mine = {"digest": digest.hexdigest(), "wall": wall, "device": local % ndev}
+    mine = {"digest": digest.hexdigest(), "wall": wall, "device": local % ndev, "traced": traced}
     alls = [mine]
     if world > 1:
         alls = [None] * world
@@ -175,6 +190,9 @@ def main():
             "images_per_s": round(world * a.batch * a.steps / wall_max, 1),
             "weights_identical_on_every_rank": len({o["digest"] for o in alls}) == 1,
             "devices": [o["device"] for o in alls],
+            **({"first_step_with_different_reduced_gradients": next(
+                (st[0][0] for st in zip(*[o["traced"] for o in alls]) if len({x[2] for x in st}) > 1), None),
+                "traced": [o["traced"] for o in alls]} if a.trace_grads else {}),
         }), flush=True)
     if a.mode != "ddp":
         comm.finalize()

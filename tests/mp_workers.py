@@ -383,12 +383,12 @@ def op_host(rank, world, mode="allreduce", steps=3, count=5000):
     return {"ok": ok, "report": rep, "cuda": op.supports_cuda()}
 
 
-def op_device_late(rank, world, async_=3, steps=9, count=100003):
-    """deep500 op, device path, solo, rank > 0 calling late every step.  Asynchronous
-    rounds: rank 0 activates, the late ranks are carried through with a zeroed send
-    bucket, and their late gradient is DROPPED (not carried into the next round): the
-    result is x0 / P.  Synchronous rounds (every async+1-th, ffsolo_limiter.c:4-35): every
-    rank's fresh gradient.  Both on every rank, bit for bit."""
+def op_device_late(rank, world, async_=3, steps=9, count=100003, on_time=0):
+    """deep500 op, device path, solo, every rank but `on_time` calling late every step.
+    Asynchronous rounds: the on-time rank activates, the late ranks are carried through
+    with a zeroed send bucket, and their late gradient is DROPPED (not carried into the
+    next round): the result is x_on_time / P.  Synchronous rounds (every async+1-th,
+    ffsolo_limiter.c:4-35): every rank's fresh gradient.  Both on every rank, bit for bit."""
     import numpy as np
     import torch
 
@@ -405,7 +405,7 @@ def op_device_late(rank, world, async_=3, steps=9, count=100003):
         xs = [ffref.fill_uniform(0x1A7E + t, r, count) for r in range(world)]
         g = torch.from_numpy(xs[rank]).to(dev)
         comm.barrier()
-        if t > 0 and rank > 0:
+        if t > 0 and rank != on_time:
             time.sleep(LATE_S)
         op.forward_cuda_div(g, g, world, stream)
         got = g.cpu().numpy()
@@ -414,12 +414,69 @@ def op_device_late(rank, world, async_=3, steps=9, count=100003):
         if t == 0:
             continue
         sync = rnd % (async_ + 1) == 0
-        want = ffref.tree_sum(scaled if sync else [scaled[0]] + [np.zeros_like(x) for x in scaled[1:]])
+        want = ffref.tree_sum(scaled if sync else
+                              [x if r == on_time else np.zeros_like(x) for r, x in enumerate(scaled)])
         ok.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
         fresh.append(sync)
     comm.barrier()
     comm.finalize()
     return {"ok": ok, "sync_rounds": fresh}
+
+
+def op_device_pattern(rank, world, count=25559081, steps=9, mode="solo", packed=False, delay=0.05,
+                      barrier=False):
+    """deep500 op, device path, NO barrier between steps (unless `barrier`): in step t the
+    ranks drawn as in the reference's imbalance loop (resnet_run_loop_solo_imagenet_300.py:
+    290-294, seeded by t) sleep `delay` before calling the op.  Every rank must receive
+    the same bits every step, and each step's result must be the tree of SOME subset of
+    the ranks' inputs (the contributors of that partial round) -- returned per step."""
+    import itertools
+
+    import numpy as np
+    import torch
+
+    from esgd import deep500
+    from oracle import ffref
+    comm = _comm()
+    dev = torch.device("cuda", local_device())
+    torch.cuda.set_device(dev)
+    deep500.configure(mode, 32, 6545343)
+    op = deep500.AllreduceOp((count,))
+    stream = torch.cuda.current_stream().cuda_stream
+    m = min(count, 1 << 16)   # checked slice (head)
+    out = []
+    comm.barrier()
+    for t in range(steps):
+        np.random.seed(t)
+        late = rank == np.random.randint(world) or rank == np.random.randint(world)
+        if barrier:
+            comm.barrier()
+        if late and t > 0:
+            time.sleep(delay)
+        x = ffref.fill_uniform(0x7A77 + t, rank, count)
+        g = torch.from_numpy(x).to(dev)
+        if packed:
+            half = count // 3
+            parts = [g[:half], g[half:]]
+            op.forward_cuda_packed(parts, parts, world, stream)
+        else:
+            op.forward_cuda_div(g, g, world, stream)
+        got = g[:m].cpu().numpy()
+        xs = [ffref.fill_uniform(0x7A77 + t, r, m) / np.float32(world) for r in range(world)]
+        who = None
+        for k in range(world, 0, -1):
+            for sub in itertools.combinations(range(world), k):
+                want = ffref.tree_sum([x if r in sub else np.zeros_like(x) for r, x in enumerate(xs)])
+                if np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+                    who = list(sub)
+                    break
+            if who is not None:
+                break
+        out.append({"t": t, "late": bool(late), "contributors": who,
+                    "digest": zlib.crc32(g.cpu().numpy().tobytes())})
+    comm.barrier()
+    comm.finalize()
+    return out
 
 
 def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp32", pipeline=True):

@@ -27,11 +27,15 @@ def test_deep500_op_host_path(mode):
         assert all(o["ok"]) and len(o["ok"]) == 3, o
 
 
-def test_deep500_op_device_late_gradient_dropped():
-    # solo, async 3: rounds 2, 3 (and 5..7) asynchronous -> x0 / P only; round 4 and 8
-    # synchronous -> every rank.  A late gradient carried into the next round (the race
-    # of the unfused copy-out / zeroing) would break the asynchronous rounds' answer.
-    outs = run("op_device_late", 2, async_=3, steps=9)
+@pytest.mark.parametrize("on_time", [0, 1])
+@pytest.mark.parametrize("count", [100003, 25559081])
+def test_deep500_op_device_late_gradient_dropped(on_time, count):
+    # solo, async 3: rounds 2, 3 (and 5..7) asynchronous -> the on-time rank's x / P only;
+    # round 4 and 8 synchronous -> every rank.  A late gradient carried into the next round
+    # (the race of the unfused copy-out / zeroing) would break the asynchronous rounds'
+    # answer.  Either rank late; a one-launch bucket and the ResNet-50 fused bucket (five
+    # launches)
+    outs = run("op_device_late", 2, async_=3, steps=9, count=count, on_time=on_time)
     for o in outs:
         assert all(o["ok"]), o
         assert o["sync_rounds"] == [r % 4 == 0 for r in range(2, 10)]
@@ -74,3 +78,20 @@ def test_void_forward_keeps_going_on_a_lost_peer():
     assert all(o["first_ok"] for o in outs), outs
     o = outs[0]
     assert o["own"] and o["status"] != 0 and o["elapsed"] < 30, o
+
+
+@pytest.mark.parametrize("packed", [False, True])
+def test_op_result_ordered_on_the_callers_default_stream(packed):
+    # torch's default stream is handed to the op as stream 0: the op's copy-in, copy-out
+    # and events must then run on the legacy default stream, NOT the library's own
+    # non-blocking stream -- a read queued on the caller's stream right after the op
+    # returns (g[:m].cpu() here, the optimizer's step in training) must see the reduced
+    # bucket.  Round 3's ResNet-50 example diverged across ranks before this was so.
+    # Steps follow the reference's random-straggler pattern with no barrier between them
+    # (resnet_run_loop_solo_imagenet_300.py:290-294): every step's result must be the tree
+    # of some contributor subset, the same on every rank.
+    outs = run("op_device_pattern", 2, packed=packed, timeout=240)
+    for t in range(len(outs[0])):
+        assert outs[0][t]["contributors"] is not None and outs[1][t]["contributors"] is not None, (t, outs)
+        assert outs[0][t]["contributors"] == outs[1][t]["contributors"], (t, outs)
+        assert outs[0][t]["digest"] == outs[1][t]["digest"], t
