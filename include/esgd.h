@@ -226,7 +226,8 @@ int esgd_schedule_create_ex(int kind, int buf, const void *sb, void *rb, uint64_
                             esgd_sched_h *out);
 /* post: start round `posted+1`.  producer_stream: stream that writes sb; the snapshot of
  * a round this rank posted waits for the work queued on it so far.  NULL = no producer;
- * ESGD_STREAM_NULL = the legacy default (NULL) stream, e.g. torch's default stream. */
+ * ESGD_STREAM_NULL = the legacy default (NULL) stream, e.g. torch's default stream --
+ * accepted by every entry point that takes a stream (NULL there: the library stream). */
 #define ESGD_STREAM_NULL ((void *)1)
 /*
  * role (may be NULL): 1 activated the round, 0 passive, 2 synchronous round. */

@@ -49,6 +49,9 @@ void *create_new_op(esgd_d5_tensor_t *input_descriptors, int num_inputs,
 /* input: this rank's gradient (already divided by the comm size, :40), last: the unused
  * false-dependency input, output: the partially reduced gradient. */
 void allreducef_forward(void *handle, const float *input, const float *last, float *output);
+/* stream (every device entry point below): the framework's stream the op's copy-in and
+ * copy-out are ordered with; NULL is the legacy default stream (stream 0, e.g. torch's
+ * default stream), not the library's own stream. */
 void allreducef_forward_cuda(void *handle, const float *input, const float *last, float *output,
                              void *stream);
 /* Extensions (device path, return an esgd status instead of aborting):
