@@ -32,7 +32,13 @@ def test_model_is_the_reference_bucket_table():
     params = [p for p in ex.resnet50().parameters() if p.requires_grad]
     assert len(params) == 161
     assert sum(p.numel() for p in params) == 25559081
-    table = _reference_table()   # (absent on the GPU box: the CPU suite checks it)
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "resnet50_buckets.json")) as f:
+        golden = json.load(f)["lengths"]   # the table as committed data (bench's C4 leg)
+    assert sorted(golden) == sorted(p.numel() for p in params)
+    table = _reference_table()   # and straight from the reference where it is present
+    if table is not None:
+        assert table == golden
     if table is not None:
         assert sum(table) == 25559081
         # the same 161 bucket sizes (the reference lists them in TF's variable order)
