@@ -424,7 +424,7 @@ def op_device_late(rank, world, async_=3, steps=9, count=100003, on_time=0):
 
 
 def op_device_pattern(rank, world, count=25559081, steps=9, mode="solo", packed=False, delay=0.05,
-                      barrier=False):
+                      barrier=False, host=False):
     """deep500 op, device path, NO barrier between steps (unless `barrier`): in step t the
     ranks drawn as in the reference's imbalance loop (resnet_run_loop_solo_imagenet_300.py:
     290-294, seeded by t) sleep `delay` before calling the op.  Every rank must receive
@@ -454,6 +454,21 @@ def op_device_pattern(rank, world, count=25559081, steps=9, mode="solo", packed=
         if late and t > 0:
             time.sleep(delay)
         x = ffref.fill_uniform(0x7A77 + t, rank, count)
+        if host:   # the reference's contract: host buffers, the wrapper's steps in the op
+            res = op.forward(x / np.float32(world))
+            got = res[:m]
+            xs = [ffref.fill_uniform(0x7A77 + t, r, m) / np.float32(world) for r in range(world)]
+            who = None
+            for k in range(world, 0, -1):
+                for sub in itertools.combinations(range(world), k):
+                    want = ffref.tree_sum([v if r in sub else np.zeros_like(v) for r, v in enumerate(xs)])
+                    if np.array_equal(got.view(np.uint32), want.view(np.uint32)):
+                        who = list(sub)
+                        break
+                if who is not None:
+                    break
+            out.append({"t": t, "late": bool(late), "contributors": who, "digest": zlib.crc32(res.tobytes())})
+            continue
         g = torch.from_numpy(x).to(dev)
         if packed:
             half = count // 3

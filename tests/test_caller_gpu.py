@@ -80,8 +80,8 @@ def test_void_forward_keeps_going_on_a_lost_peer():
     assert o["own"] and o["status"] != 0 and o["elapsed"] < 30, o
 
 
-@pytest.mark.parametrize("packed", [False, True])
-def test_op_result_ordered_on_the_callers_default_stream(packed):
+@pytest.mark.parametrize("packed,host", [(False, False), (True, False), (False, True)])
+def test_op_result_ordered_on_the_callers_default_stream(packed, host):
     # torch's default stream is handed to the op as stream 0: the op's copy-in, copy-out
     # and events must then run on the legacy default stream, NOT the library's own
     # non-blocking stream -- a read queued on the caller's stream right after the op
@@ -90,7 +90,8 @@ def test_op_result_ordered_on_the_callers_default_stream(packed):
     # Steps follow the reference's random-straggler pattern with no barrier between them
     # (resnet_run_loop_solo_imagenet_300.py:290-294): every step's result must be the tree
     # of some contributor subset, the same on every rank.
-    outs = run("op_device_pattern", 2, packed=packed, timeout=240)
+    outs = run("op_device_pattern", 2, packed=packed, host=host, count=(1 << 22) + 5 if host else 25559081,
+               timeout=240)
     for t in range(len(outs[0])):
         assert outs[0][t]["contributors"] is not None and outs[1][t]["contributors"] is not None, (t, outs)
         assert outs[0][t]["contributors"] == outs[1][t]["contributors"], (t, outs)
