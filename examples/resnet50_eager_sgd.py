@@ -73,6 +73,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", choices=["solo", "majority", "allreduce", "ddp"], default="solo")
     ap.add_argument("--fuse", action="store_true", help="eager-SGD: one fused bucket per step")
+    ap.add_argument("--wire", choices=["fp32", "bf16"], default="fp32",
+                    help="eager-SGD: what the ranks exchange (bf16: fp32 buckets, bf16 copies on the wire)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64, help="images per rank per step")
@@ -122,7 +124,7 @@ def main():
     model = resnet50().to(dev)
     params = [p for p in model.parameters() if p.requires_grad]
     sgd = torch.optim.SGD(params, lr=0.1, momentum=0.9)
-    opt = sgd if a.mode == "ddp" else EagerSGDOptimizer(sgd, world, mode=a.mode, fuse=a.fuse)
+    opt = sgd if a.mode == "ddp" else EagerSGDOptimizer(sgd, world, mode=a.mode, fuse=a.fuse, wire=a.wire)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     x = torch.randn(a.batch, 3, a.image, a.image, device=dev, generator=g)
     y = torch.randint(0, 1001, (a.batch,), device=dev, generator=g)
@@ -183,7 +185,7 @@ def main():
         wall_max = max(o["wall"] for o in alls)
         print(json.dumps({
             "model": "resnet50 (1001 classes)", "tensors": len(params),
-            "parameters": sum(p.numel() for p in params), "mode": a.mode, "fuse": a.fuse,
+            "parameters": sum(p.numel() for p in params), "mode": a.mode, "fuse": a.fuse, "wire": a.wire,
             "world": world, "batch_per_rank": a.batch, "image": a.image, "dtype": "f32",
             "data": "synthetic", "straggler_delay_s": a.delay, "steps": a.steps,
             "step_ms_median": round(statistics.median(times) * 1e3, 2),
