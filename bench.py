@@ -185,12 +185,9 @@ GATE_WINDOWS = 4                                # 256 MiB / kWindowBytes (reduce
 
 
 def trace_child(dev, dt, ptrs, out, count, k, s):
-    """The kernel-trace child (rocprofv3 --kernel-trace runs it): C2 launches, then the
-    gate's 8 x 256 MiB calls, each group after its own warm-up, nothing else in between
-    but the fill kernels of the gate buckets (they separate the two groups in the trace)."""
-    for _ in range(TRACE_WARM + TRACE_C2):
-        dev.reduce(dt, ptrs, out, count, stream=s)
-    s.synchronize()
+    """The kernel-trace child (rocprofv3 --kernel-trace runs it), in the order the line is
+    measured: the gate's 8 x 256 MiB calls, then the C2 launches, each group after its own
+    warm-up; one small fill kernel between the groups marks the boundary in the trace."""
     gcount = (256 * MiB) // 4
     gb = [dev.DeviceBuffer(gcount, dt) for _ in range(k)]
     for r, b in enumerate(gb):
@@ -198,6 +195,10 @@ def trace_child(dev, dt, ptrs, out, count, k, s):
     go = dev.DeviceBuffer(gcount, dt)
     for _ in range(TRACE_WARM + TRACE_GATE):
         dev.reduce(dt, [b.ptr for b in gb], go, gcount, stream=s)
+    mark = dev.DeviceBuffer(1024, dt)
+    dev.fill_uniform(mark, SEED, 0, stream=s)
+    for _ in range(TRACE_WARM + TRACE_C2):
+        dev.reduce(dt, ptrs, out, count, stream=s)
     s.synchronize()
 
 
@@ -230,8 +231,8 @@ def kernel_trace(args):
     if not fills or not tree:
         return None
     last_fill = fills[-1]
-    c2 = [dur / 1e3 for i, dur in tree if i < last_fill][TRACE_WARM:]
-    g = [dur for i, dur in tree if i > last_fill][TRACE_WARM * GATE_WINDOWS:]
+    c2 = [dur / 1e3 for i, dur in tree if i > last_fill][TRACE_WARM:]
+    g = [dur for i, dur in tree if i < last_fill][TRACE_WARM * GATE_WINDOWS:]
     gate = [sum(g[j:j + GATE_WINDOWS]) / 1e3 for j in range(0, len(g) - GATE_WINDOWS + 1, GATE_WINDOWS)]
     c2_bytes = (args.buckets + 1) * int(args.bucket_mib * MiB)
     gate_bytes = (args.buckets + 1) * 256 * MiB
@@ -274,6 +275,14 @@ def run_local(args, esgd, dev):
         s.synchronize()
         return None
 
+    # The gate leg (8 x 256 MiB) runs first: ~50 ms of streaming that leaves the GPU at its
+    # steady clocks before the C2 warm-up and timed steps.  Measured cold, the first 40 C2
+    # launches of a process averaged 95.7 us against 91.8 us over 120 launches of a longer
+    # run on the same box (profiles/r03, r03ak).
+    gate = None
+    if not args.no_gate:
+        gate = gate_256(dev, dt, es, k, s)
+
     for _ in range(args.warmup):
         dev.reduce(dt, ptrs, out, count, stream=s)
     s.synchronize()
@@ -310,9 +319,6 @@ def run_local(args, esgd, dev):
         want = ffref.tree_sum([ffref.fill_uniform(SEED, r, m) for r in range(k)])
         parity = "bitwise" if np.array_equal(got.view(np.uint32), want.view(np.uint32)) else "MISMATCH"
 
-    gate = None
-    if not args.no_gate:
-        gate = gate_256(dev, dt, es, k, s)
     e2e = host_e2e(dev, k, count, s) if (dt == _lib.FLOAT and not args.no_gate) else None
     bucket_bytes = count * es
     algo_bytes = (k + 1) * bucket_bytes        # k reads + 1 write per launch

@@ -1,8 +1,7 @@
-"""Split a rocprofv3 kernel trace of `bench.py` into its two shapes: the C2 launches
-(8 x 64 MiB, one dispatch each) and the gate calls (8 x 256 MiB, run as 64 MiB windows:
-four dispatches per call).  The bench fills the gate buckets after the C2 loop, so the
-tree-kernel dispatches after the last fill kernel are the gate's; a call's time is the
-span from its first window's start to its last window's end.
+"""Split a rocprofv3 kernel trace of `bench.py` into its two shapes: the gate calls
+(8 x 256 MiB, run as 64 MiB windows: four dispatches per call), which the bench runs
+first, right after the last fill kernel, and the C2 launches (8 x 64 MiB, one dispatch
+each) that follow them.
 usage: split_trace.py RUN_kernel_trace.csv TAG > kernel_trace_split.json"""
 import csv
 import json
@@ -10,6 +9,7 @@ import statistics
 import sys
 
 WINDOWS_PER_GATE_CALL = 4   # 256 MiB / kWindowBytes (reduce_kernels.hip)
+GATE_CALLS = 130            # bench.gate_256: 10 warm-up + 20 + 100 calls
 
 
 def main():
@@ -20,22 +20,19 @@ def main():
             rows.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), row["Kernel_Name"]))
     rows.sort()
     last_fill = max(i for i, r in enumerate(rows) if "k_fill_uniform" in r[2])
-    tree = [(i, r) for i, r in enumerate(rows) if "k_tree_sum_buf<esgd::F32, 8, 4, 2, 16, false" in r[2]]
-    c2 = [(r[1] - r[0]) / 1e3 for i, r in tree if i < last_fill]
-    # after the gate's fills the bench also runs host_e2e, whose tree launches are single
-    # (serial leg) or read host memory for ms (esgd_reduce_host): a gate call is a run of
-    # exactly four back-to-back HBM windows (gaps of a few us)
-    gw = [r for i, r in tree if i > last_fill and r[1] - r[0] < 1_000_000]
-    runs, cur = [], []
-    for r in gw:
-        if cur and r[0] - cur[-1][1] > 50_000:
-            runs.append(cur)
-            cur = []
-        cur.append(r)
-    if cur:
-        runs.append(cur)
-    calls = [run[j:j + WINDOWS_PER_GATE_CALL] for run in runs if len(run) % WINDOWS_PER_GATE_CALL == 0
-             for j in range(0, len(run), WINDOWS_PER_GATE_CALL)]
+    tree = [r for i, r in enumerate(rows) if "k_tree_sum_buf<esgd::F32, 8, 4, 2, 16, false" in r[2] and i > last_fill]
+    # bench.py runs the gate leg first (10 warm-up + 20 timed-singly + 100 back-to-back
+    # calls of four 64 MiB windows), then the C2 warm-up and timed launches, then host_e2e
+    # (whose launches follow PCIe copies, ms apart)
+    gw = tree[:GATE_CALLS * WINDOWS_PER_GATE_CALL]
+    calls = [gw[j:j + WINDOWS_PER_GATE_CALL] for j in range(0, len(gw), WINDOWS_PER_GATE_CALL)]
+    rest = tree[GATE_CALLS * WINDOWS_PER_GATE_CALL:]
+    c2r = rest[:1]
+    for r in rest[1:]:
+        if r[0] - c2r[-1][1] > 1_000_000:   # the host_e2e leg
+            break
+        c2r.append(r)
+    c2 = [(r[1] - r[0]) / 1e3 for r in c2r]
     # a call's kernel time: its windows' durations summed (the gaps between them are
     # dispatch gaps, a few us; the span also swallows host syncs between timed loops)
     gate = [sum(r[1] - r[0] for r in c) / 1e3 for c in calls]
