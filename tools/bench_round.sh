@@ -21,7 +21,7 @@ for s in $STEPS; do
           --output-format csv -- python $R/bench.py --no-pmc --no-trace --no-cpu-baseline --steps 100 \
           > $R/$O/bench_prof.json 2>&1) ;;
   bisect) timeout -k 10 500 python -u tools/ipc_bisect.py > $O/ipc_bisect.txt 2>&1 ;;
-  sweep) make -s sweeps >/dev/null 2>&1 || true
+  sweep) test -f tools/bin/libesgd_sweeps.so   # built here by `make sweeps` (build() does it)
       for m in 64 256 1024; do
         timeout -k 10 240 python tools/sweep_reduce.py --mib $m --grids 0 --unrolls 4 --nts 1 \
             --policies=-1,25,26,27,28,29 --rounds 5 --iters 20 > $O/sweep_streams_$m.jsonl 2>&1
