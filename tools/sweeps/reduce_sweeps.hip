@@ -20,6 +20,8 @@
 //                   the windows' compact footprint without their launch boundaries
 //   policy 31 / 32  ONE launch over the whole bucket, each block at most 1 / 2 grid-stride
 //                   iterations ahead of the slowest (a shared progress counter): bounded drift
+//   policy 34..36   XCD-aware block placement (k_tree_sum_xcd: remapped grid stride, contiguous
+//                   range per remapped block, contiguous range per block)
 //   policy -1       the production launch (the baseline every variant is timed against)
 // fp32, fan-in 8 only.
 #include <hip/hip_runtime.h>
@@ -271,6 +273,64 @@ __global__ __launch_bounds__(256) void k_tree_sum_bounded_drift(InputSet in, voi
     block_exit(bar);
 }
 
+// XCD-aware block placement.  Workgroups are dealt round-robin over the 8 XCDs (block b on
+// XCD b % 8), so in the production grid-stride order neighbouring 16 KiB slices of every
+// input stream through eight different L2s.  MODE 0: the grid-stride loop over a remapped
+// block index (XCD x owns logical blocks x*G/8 .. (x+1)*G/8-1, a contiguous eighth of
+// every pass); MODE 1: every logical (remapped) block walks one contiguous range of the
+// bucket, so each XCD streams one contiguous eighth of it; MODE 2: contiguous ranges per
+// block without the remap.
+template <int U, int MODE>
+__global__ __launch_bounds__(256) void k_tree_sum_xcd(InputSet in, void *out, uint32_t nvec, uint64_t count) {
+    constexpr int B = 256, K = 8;
+    const int bytes = int(nvec * 16u);
+    __amdgpu_buffer_rsrc_t rs[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(in.p[j]), (short)0, bytes, 0x00020000);
+    __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, bytes, 0x00020000);
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    const uint32_t lb = (MODE == 2) ? b : (b % 8u) * (G / 8u) + b / 8u;
+    uint32_t first, last, step;
+    if constexpr (MODE == 0) {
+        first = lb * (B * U);
+        last = nvec;
+        step = G * (B * U);
+    } else {
+        const uint32_t chunk = B * U;
+        const uint32_t per = ((nvec + G - 1) / G + chunk - 1) / chunk * chunk;
+        first = lb * per;
+        last = first + per < nvec ? first + per : nvec;
+        step = chunk;
+    }
+    for (uint32_t i = first + threadIdx.x; i - threadIdx.x < last; i += step) {
+        raw16 r[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j) r[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs[j], (i + u * B) * 16, 0, 2);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_raw_buffer_store_b128(fold16<F32, K, false>(r[u], 1.0f), ws, (i + u * B) * 16, 0, 16);
+    }
+    fold_tail<F32, 8, false>(in, out, uint64_t(nvec) * 4, count, 1.0f);
+}
+
+template <int MODE>
+static int launch_xcd(const InputSet &in, void *out, uint64_t count, hipStream_t s, unsigned fixed) {
+    const uint64_t nvec = count / 4;
+    if (nvec >= (uint64_t(1) << 27)) {
+        set_error("xcd policies take one descriptor range (< 2 GiB)");
+        return ESGD_INVALID_ARG;
+    }
+    static const int per_cu = resident_blocks(k_tree_sum_xcd<4, MODE>, 256);
+    unsigned grid = grid_for(uint64_t(256) * 4, nvec ? nvec : 1, per_cu, fixed);
+    if (MODE != 2) grid = grid < 8 ? 8 : grid / 8 * 8;   // the remap needs G % 8 == 0
+    hipLaunchKernelGGL((k_tree_sum_xcd<4, MODE>), dim3(grid), dim3(256), 0, s, in, out, uint32_t(nvec), count);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
 static uint32_t *g_bar = nullptr;
 
 static int pace_bar(uint32_t **out) {
@@ -398,6 +458,9 @@ int esgd_sweep_reduce(int policy, int unroll, int nt, int grid, const void *cons
     case 30: return launch_paced_windows(in, out, count, s, uint64_t(64) << 20);
     case 31: return launch_bounded_drift<1>(in, out, count, s);
     case 32: return launch_bounded_drift<2>(in, out, count, s);
+    case 34: return launch_xcd<0>(in, out, count, s, g);
+    case 35: return launch_xcd<1>(in, out, count, s, g);
+    case 36: return launch_xcd<2>(in, out, count, s, g);
     case 33: return launch_paced_windows(in, out, count, s, uint64_t(32) << 20);
     default: break;
     }
