@@ -22,6 +22,7 @@
 //                   iterations ahead of the slowest (a shared progress counter): bounded drift
 //   policy 34..36   XCD-aware block placement (k_tree_sum_xcd: remapped grid stride, contiguous
 //                   range per remapped block, contiguous range per block)
+//   policy 37 / 38  window sizes 128 / 48 MiB
 //   policy -1       the production launch (the baseline every variant is timed against)
 // fp32, fan-in 8 only.
 #include <hip/hip_runtime.h>
@@ -458,6 +459,8 @@ int esgd_sweep_reduce(int policy, int unroll, int nt, int grid, const void *cons
     case 30: return launch_paced_windows(in, out, count, s, uint64_t(64) << 20);
     case 31: return launch_bounded_drift<1>(in, out, count, s);
     case 32: return launch_bounded_drift<2>(in, out, count, s);
+    case 37: return launch_windows<F32, 8, 4, 2, 16, false>(in, out, count, 1.0f, s, uint64_t(128) << 20, g);
+    case 38: return launch_windows<F32, 8, 4, 2, 16, false>(in, out, count, 1.0f, s, uint64_t(48) << 20, g);
     case 34: return launch_xcd<0>(in, out, count, s, g);
     case 35: return launch_xcd<1>(in, out, count, s, g);
     case 36: return launch_xcd<2>(in, out, count, s, g);
