@@ -21,30 +21,50 @@ import esgd  # noqa: E402
 from esgd import device as dev  # noqa: E402
 
 MiB = 1 << 20
-CASES = [  # (alloc MiB, use MiB, offset MiB)
+# (alloc MiB, use MiB, offset MiB); alloc < 0: the 9 buckets carved at a `use` pitch out
+# of ONE allocation of -alloc MiB
+CASES = [
     (256, 256, 0),
     (1024, 256, 0),
     (1024, 256, 768),
     (1024, 1024, 0),
     (512, 512, 0),
+    (64, 64, 0),
+    (256, 64, 0),
+    (1024, 64, 0),
+    (-576, 64, 0),
+    (-1024, 64, 0),
+    (-4096, 256, 0),
 ]
+if len(sys.argv) > 1 and sys.argv[1] == "--c2":
+    CASES = [c for c in CASES if c[1] == 64]
 dt, k = esgd.FLOAT, 8
 s = dev.Stream()
 sets = {}
-for alloc in sorted({c[0] for c in CASES}):
+for alloc in sorted({c[0] for c in CASES if c[0] > 0}):
     bufs = [dev.DeviceBuffer(alloc * MiB // 4, dt) for _ in range(k + 1)]
     for r, b in enumerate(bufs[:k]):
         dev.fill_uniform(b, 0x5EEDE56D, r, stream=s)
-    sets[alloc] = bufs
+    sets[alloc] = [b.ptr for b in bufs]
+    sets[("keep", alloc)] = bufs
+for alloc, use, _ in CASES:
+    if alloc < 0 and alloc not in sets:
+        one = dev.DeviceBuffer(-alloc * MiB // 4, dt)
+        assert (k + 1) * use <= -alloc
+        ptrs = [one.ptr + i * use * MiB for i in range(k + 1)]
+        for r in range(k):
+            esgd.check(esgd.lib().esgd_fill_uniform_f32(0x5EEDE56D, r, ptrs[r], use * MiB // 4, s.handle))
+        sets[alloc] = ptrs
+        sets[("keep", alloc)] = [one]
 s.synchronize()
 e0, e1 = dev.Event(), dev.Event()
 times = {c: [] for c in CASES}
 for _ in range(7):
     for c in CASES:
         alloc, use, off = c
-        bufs = sets[alloc]
-        ptrs = [b.ptr + off * MiB for b in bufs[:k]]
-        out = bufs[k].ptr + off * MiB
+        base = sets[alloc]
+        ptrs = [p + off * MiB for p in base[:k]]
+        out = base[k] + off * MiB
         count = use * MiB // 4
         calls = max(4, 2048 // use)
         for _ in range(2):
