@@ -145,6 +145,12 @@ def cpu_baseline_c1(P: int = 2, count: int = 262144):
 PMC_CALLS = 5   # reduction calls of the PMC child run
 
 
+def _under_profiler():
+    """True when this process runs under rocprofv3 (it configures its tool library
+    through ROCPROF* variables)."""
+    return any(k.startswith("ROCPROF") for k in os.environ)
+
+
 def pmc_traffic(args, mib):
     """HBM bytes per reduction call (k buckets of `mib` MiB) from rocprofv3 PMC counters,
     in separate passes (FETCH_SIZE, WRITE_SIZE), corrected as MI355X_MICROARCH.md §HBM
@@ -654,6 +660,7 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
         fused_step()
     t161 = _timed_steps(comm, chain, steps)
     t161p = _timed_steps(comm, pipelined, steps)
+    breakdown = _step_breakdown_us(scheds)
     t1 = _timed_steps(comm, fused_step, steps)
     for s, b in zip(scheds, bufs):
         _defer(s, b)
@@ -662,7 +669,31 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
             "step_ms_161_buckets": round(t161 * 1e3, 3),
             "step_ms_161_buckets_pipelined": round(t161p * 1e3, 3),
             "step_ms_one_fused_bucket": round(t1 * 1e3, 3),
-            "fused_speedup": round(t161 / t1, 2), "steps": steps}
+            "fused_speedup": round(t161 / t1, 2), "steps": steps,
+            "rank0_pipelined_step_us": breakdown}
+
+
+def _step_breakdown_us(scheds):
+    """Where the last pipelined step's time went on this rank, from every schedule's host
+    timeline (esgd_schedule_timeline) of its last round: stamps relative to the first post,
+    in us -- the last post / join / launch queued / completion seen / wait returned, the
+    host time spent inside launches summed over the buckets."""
+    import numpy as np
+    rows = []
+    for s in scheds:
+        tl = s.timeline().astype(np.int64)
+        tl = tl[(tl[:, 0] > 0) & (tl[:, 5] > 0)]
+        if len(tl):
+            rows.append(tl[-1])
+    if not rows:
+        return None
+    tl = np.array(rows)
+    t0 = tl[:, 0].min()
+    rel = lambda i: round(float(tl[:, i].max() - t0) / 1e3, 1)   # noqa: E731
+    return {"last_post": rel(0), "last_join": rel(1), "last_launch_queued": rel(3), "last_completion": rel(4),
+            "last_wait": rel(5), "launch_host_sum": round(float((tl[:, 3] - tl[:, 2]).sum()) / 1e3, 1),
+            "first_launch": round(float(tl[:, 2].min() - t0) / 1e3, 1),
+            "gpu_us_per_bucket": round(float(tl[:, 4].max() - tl[:, 2].min()) / 1e3 / len(tl), 2)}
 
 
 def c3_over_rccl(comm, dev, rank, world, count, steps=20):
@@ -1255,6 +1286,12 @@ def main():
     if res.get("host_e2e"):
         line["host_e2e"] = res["host_e2e"]
     traffic = None
+    if _under_profiler():
+        # an outer rocprofv3 already traces this process: a nested profiler child would
+        # inherit its environment (a profiler-preloaded launcher re-exec'ing python, which
+        # this pool forbids) and its data would be meaningless
+        args.no_pmc = args.no_trace = True
+        line["profiler_passes"] = "skipped: bench.py runs under a profiler"
     if not args.no_pmc:
         try:
             traffic = pmc_traffic(args, args.bucket_mib)

@@ -22,8 +22,9 @@
 // free neighbours of the same chunk, and only when no free run fits is a new chunk
 // allocated.  So the arena's footprint is bounded by the peak of live bucket bytes (plus
 // fragmentation), not by the number of distinct sizes ever used.  Chunks that were never
-// exported and hold no live block go back to the driver whenever a new chunk is needed
-// and at finalize (arena_trim).  Exported chunks stay until the process exits, so their
+// exported and hold no live block go back to the driver when a caller's allocation needs
+// a new chunk (never on the progress thread: new_chunk), on out-of-memory, and at finalize
+// (arena_trim).  Exported chunks stay until the process exits, so their
 // total is the sum of the successive record bucket sizes (below 2x the largest bucket for
 // C5's doubling sweep; one 8 GiB bucket reserves 8 GiB for good).
 #include <hip/hip_runtime.h>
@@ -37,6 +38,8 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+
+#include <unistd.h>
 
 #include "esgd_internal.h"
 
@@ -125,12 +128,20 @@ void release_idle(int dev) {
     for (Chunk *c : idle) release_chunk(c);
 }
 
-int new_chunk(size_t bytes, int dev, Chunk **out) {
-    // nothing free fits: idle chunks no peer ever mapped go back to the driver first, so
-    // never-exported memory stays at its peak of live bytes
-    release_idle(dev);
+// Nothing free fits.  Idle chunks no peer ever mapped go back to the driver first only
+// when the caller allows it (`release`: esgd_malloc and the op's buckets, on the caller's
+// thread) -- hipFree synchronises the whole device, which must never happen on the progress
+// thread (the data plane's own buckets, allocated at a join, would stall every schedule's
+// rounds in flight) -- or when the device is out of memory.
+int new_chunk(size_t bytes, int dev, bool release, Chunk **out) {
+    if (release) release_idle(dev);
     char *p = nullptr;
-    const hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), bytes);
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), bytes);
+    if (e == hipErrorOutOfMemory && !release) {
+        (void)hipGetLastError();
+        release_idle(dev);
+        e = hipMalloc(reinterpret_cast<void **>(&p), bytes);
+    }
     if (e != hipSuccess) return hip_fail(e, "hipMalloc (bucket arena)", __FILE__, __LINE__);
     auto *c = new Chunk();
     c->base = p;
@@ -153,7 +164,7 @@ bool bypass() {   // 1: bypass; 2: also close peer mappings at schedule deletion
 
 }  // namespace
 
-int arena_alloc(size_t bytes, void **out) {
+int arena_alloc(size_t bytes, void **out, bool release_idle_chunks) {
     ESGD_ARG(out, "arena: null output");
     if (int rc = require_device()) return rc;
     int dev = 0;
@@ -162,7 +173,7 @@ int arena_alloc(size_t bytes, void **out) {
     bytes = std::max<size_t>(bytes, 1);
     if (bypass()) {
         Chunk *c = nullptr;
-        if (int rc = new_chunk(bytes, dev, &c)) return rc;
+        if (int rc = new_chunk(bytes, dev, release_idle_chunks, &c)) return rc;
         ++c->live;
         g_live[reinterpret_cast<uintptr_t>(c->base)] = {c, bytes};
         g_live_bytes += bytes;
@@ -174,7 +185,7 @@ int arena_alloc(size_t bytes, void **out) {
         auto &fl = g_small[{dev, cls}];
         if (fl.empty()) {
             Chunk *c = nullptr;
-            if (int rc = new_chunk(kSlab, dev, &c)) return rc;
+            if (int rc = new_chunk(kSlab, dev, release_idle_chunks, &c)) return rc;
             for (size_t o = kSlab; o >= cls; o -= cls) fl.push_back(c->base + o - cls);
         }
         char *p = fl.back();
@@ -199,7 +210,7 @@ int arena_alloc(size_t bytes, void **out) {
         run_erase(reinterpret_cast<uintptr_t>(p));
         if (have > need) run_insert(p + need, have - need, c);
     } else {
-        if (int rc = new_chunk(need, dev, &c)) return rc;
+        if (int rc = new_chunk(need, dev, release_idle_chunks, &c)) return rc;
         p = c->base;
     }
     ++c->live;
@@ -284,78 +295,86 @@ void arena_stats(uint64_t *reserved, uint64_t *live, uint64_t *exported) {
 // The arena chunk holding [p, p + bytes) of a live block: its base, the offset of p and
 // its IPC handle (created on first use; the chunk is marked exported and is never given
 // back to the driver while the process runs).  ESGD_INVALID_ARG if p is not arena memory.
+//
+// The runtime call runs WITHOUT g_mu (allocations, frees and other schedules' joins on the
+// progress thread go on meanwhile); g_export_mu keeps exports one at a time, so a chunk is
+// exported at most once.  The chunk cannot go away meanwhile: it holds p's live block.
+static std::mutex g_export_mu;
+
 int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_t handle[64]) {
-    std::lock_guard<std::mutex> lk(g_mu);
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    auto it = g_live.upper_bound(a);
-    if (it == g_live.begin()) return ESGD_INVALID_ARG;
-    --it;
-    const Block &b = it->second;
-    if (a + bytes > it->first + b.cls) return ESGD_INVALID_ARG;
-    Chunk *c = b.chunk;
-    if (!c->exported) {
-        hipIpcMemHandle_t h;
-        // On round 3's boxes the dmabuf export of a fresh chunk failed now and then with
-        // hipErrorInvalidValue (a new process's first schedule, after other tests' ranks
-        // had exited; profiles/r03/README.md).  Creation is rare, so a failed export is
-        // retried with growing pauses (1 + 2 + ... + 256 ms); each failed attempt is
-        // reported on stderr.  A chunk that still cannot be exported is marked so.
-        hipError_t e = hipSuccess;
-        // ESGD_FAIL_EXPORTS=N (tests): the process's first N chunk exports fail as the
-        // runtime's did, without calling it, so the fallbacks can be exercised anywhere
-        static int simulated = [] {
-            const char *v = getenv("ESGD_FAIL_EXPORTS");
-            return (v && *v) ? std::max(0, atoi(v)) : 0;
-        }();
-        const bool simulate = simulated > 0;
-        if (simulate) {
-            --simulated;
-            e = hipErrorInvalidValue;
-            std::fprintf(stderr, "esgd: export of %p (%zu B chunk) fails by ESGD_FAIL_EXPORTS\n",
-                         static_cast<void *>(c->base), c->bytes);
-        }
-        for (int attempt = 0, pause_ms = 1; !simulate && attempt < 10; ++attempt, pause_ms *= 2) {
-            e = hipIpcGetMemHandle(&h, c->base);
-            if (e == hipSuccess) break;
-            (void)hipGetLastError();
-            std::fprintf(stderr, "esgd: hipIpcGetMemHandle(%p, %zu B chunk) attempt %d: %s\n",
-                         static_cast<void *>(c->base), c->bytes, attempt + 1, hipGetErrorString(e));
-            if (attempt < 9) std::this_thread::sleep_for(std::chrono::milliseconds(pause_ms));
-        }
-        if (e != hipSuccess) {
-            // no new block comes from this chunk; the data plane re-allocates the buffers
-            // it owns (a fresh chunk) and shadows a caller's bucket that lives here
-            c->unexportable = true;
-            drop_free(c);
-            // diagnostics: can this process export a fresh allocation at all?
-            void *probe = nullptr;
-            if (!simulate && hipMalloc(&probe, kSlab) == hipSuccess) {
-                hipIpcMemHandle_t ph;
-                const hipError_t pe = hipIpcGetMemHandle(&ph, probe);
-                std::fprintf(stderr, "esgd: export of a fresh %zu B allocation at %p: %s\n", kSlab, probe,
-                             hipGetErrorString(pe));
-                (void)hipGetLastError();
-                hip_ignore(hipFree(probe));
-            } else {
-                (void)hipGetLastError();
-            }
-            const char *m = getenv("HSA_ENABLE_IPC_MODE_LEGACY");
-            int rc = hip_fail(e, "hipIpcGetMemHandle", __FILE__, __LINE__);
-            if (!m || std::strcmp(m, "0") != 0) {
-                std::string msg = esgd_last_error();
-                set_error("%s -- this node's driver exports only dmabuf handles: set "
-                          "HSA_ENABLE_IPC_MODE_LEGACY=0 in every rank's environment", msg.c_str());
-            }
-            return rc;
-        }
-        std::memcpy(c->handle, &h, 64);
-        c->exported = true;
-        ipc_trace("export", -1, c->base, c->bytes, c->handle);
+    auto find = [&](Chunk **out) -> int {
+        auto it = g_live.upper_bound(a);
+        if (it == g_live.begin()) return ESGD_INVALID_ARG;
+        --it;
+        if (a + bytes > it->first + it->second.cls) return ESGD_INVALID_ARG;
+        *out = it->second.chunk;
+        return ESGD_SUCCESS;
+    };
+    auto give = [&](Chunk *c) {
+        *base = c->base;
+        *off = uint64_t(a - reinterpret_cast<uintptr_t>(c->base));
+        std::memcpy(handle, c->handle, 64);
+        return ESGD_SUCCESS;
+    };
+    Chunk *c = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (int rc = find(&c)) return rc;
+        if (c->exported) return give(c);
     }
-    *base = c->base;
-    *off = uint64_t(a - reinterpret_cast<uintptr_t>(c->base));
-    std::memcpy(handle, c->handle, 64);
-    return ESGD_SUCCESS;
+    std::lock_guard<std::mutex> xk(g_export_mu);
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (c->exported) return give(c);   // another thread exported it meanwhile
+    }
+    // On round 3's boxes the dmabuf export of a fresh chunk failed now and then with
+    // hipErrorInvalidValue (a new process's first schedule in the middle of a long test
+    // session).  Retrying never cleared it there, so one retry only; each
+    // failed attempt is reported on stderr with the chunk's address and this process's pid.
+    hipIpcMemHandle_t h;
+    hipError_t e = hipSuccess;
+    // ESGD_FAIL_EXPORTS=N (tests): the process's first N chunk exports fail as the
+    // runtime's did, without calling it, so the fallbacks can be exercised anywhere
+    static int simulated = [] {
+        const char *v = getenv("ESGD_FAIL_EXPORTS");
+        return (v && *v) ? std::max(0, atoi(v)) : 0;
+    }();
+    const bool simulate = simulated > 0;
+    if (simulate) {
+        --simulated;
+        e = hipErrorInvalidValue;
+        std::fprintf(stderr, "esgd: export of %p (%zu B chunk) fails by ESGD_FAIL_EXPORTS\n",
+                     static_cast<void *>(c->base), c->bytes);
+    }
+    for (int attempt = 0; !simulate && attempt < 2; ++attempt) {
+        e = hipIpcGetMemHandle(&h, c->base);
+        if (e == hipSuccess) break;
+        (void)hipGetLastError();
+        std::fprintf(stderr, "esgd: pid %d: hipIpcGetMemHandle(%p, %zu B chunk) attempt %d: %s\n", int(getpid()),
+                     static_cast<void *>(c->base), c->bytes, attempt + 1, hipGetErrorString(e));
+        if (attempt == 0) std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (e != hipSuccess) {
+        // no new block comes from this chunk; the data plane re-allocates the buffers it
+        // owns (a fresh chunk) and shadows a caller's bucket that lives here
+        c->unexportable = true;
+        drop_free(c);
+        ipc_trace("export-refused", -1, c->base, c->bytes, nullptr);
+        const char *m = getenv("HSA_ENABLE_IPC_MODE_LEGACY");
+        int rc = hip_fail(e, "hipIpcGetMemHandle", __FILE__, __LINE__);
+        if (!m || std::strcmp(m, "0") != 0) {
+            std::string msg = esgd_last_error();
+            set_error("%s -- this node's driver exports only dmabuf handles: set "
+                      "HSA_ENABLE_IPC_MODE_LEGACY=0 in every rank's environment", msg.c_str());
+        }
+        return rc;
+    }
+    std::memcpy(c->handle, &h, 64);
+    c->exported = true;
+    ipc_trace("export", -1, c->base, c->bytes, c->handle);
+    return give(c);
 }
 
 // Finalize: chunks that were never exported and hold no live block go back to the

@@ -60,7 +60,7 @@ int round_small(int dtype, const void *const *src, void *out, void *pub, uint64_
                 const void *const *gsrc, void *const *gdst, const uint64_t *gbytes,
                 const PairFlags &ready, const PairFlags &reduced, uint32_t *fin, uint32_t *err,
                 uint64_t *ts, uint32_t *counter, int rank, int world, uint32_t value,
-                long long timeout_ticks, hipStream_t s);
+                long long timeout_ticks, int strict, hipStream_t s);
 
 constexpr int kMaxSegs = 16;                      // segments per gather launch (kMaxSeg)
 
@@ -88,6 +88,14 @@ static uint64_t small_round_bytes() {
     return v;
 }
 
+// ESGD_STRICT_HANDOFFS=1: one-launch rounds use acq_rel arrival counts, agent-scope
+// release gates and an L2 write-back before the reduced flag (round 2's hand-offs) instead
+// of the relaxed ones (memory ordering); a cross-GPU A/B.
+static int strict_env() {
+    static const int v = getenv("ESGD_STRICT_HANDOFFS") && *getenv("ESGD_STRICT_HANDOFFS") == '1' ? 1 : 0;
+    return v;
+}
+
 // Where the rank-pairing flags live (dataplane.cpp, "device pairing flags"): 0 host
 // memory (default), 1 uncached HBM, 2 fine-grained HBM; ESGD_DEVICE_FLAGS overrides.
 static int device_flags_env() {
@@ -98,7 +106,12 @@ static int device_flags_env() {
 // esgd_set_config: what schedules created afterwards capture (-1 = the env default).
 // All ranks must set the same values before the same creations (the creation signature
 // checks it), so a benchmark can A/B them inside one job.
-static std::atomic<int64_t> g_cfg_small{-1}, g_cfg_flags{-1};
+static std::atomic<int64_t> g_cfg_small{-1}, g_cfg_flags{-1}, g_cfg_strict{-1};
+
+bool config_strict_handoffs() {
+    const int64_t v = g_cfg_strict.load();
+    return v >= 0 ? v != 0 : strict_env() != 0;
+}
 
 uint64_t config_small_round_bytes() {
     const int64_t v = g_cfg_small.load();
@@ -119,8 +132,11 @@ int config_set(const char *key, int64_t value) {
     } else if (!std::strcmp(key, "device_flags")) {
         ESGD_ARG(value >= -1 && value <= 2, "device_flags: 0 host, 1 uncached HBM, 2 fine-grained HBM (-1: the default)");
         g_cfg_flags.store(value);
+    } else if (!std::strcmp(key, "strict_handoffs")) {
+        ESGD_ARG(value >= -1 && value <= 1, "strict_handoffs: 0 relaxed, 1 strict (-1: the default)");
+        g_cfg_strict.store(value);
     } else {
-        set_error("esgd_set_config: unknown key '%s' (small_round_bytes, device_flags)", key);
+        set_error("esgd_set_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -130,8 +146,9 @@ int config_get(const char *key, int64_t *value) {
     ESGD_ARG(key && value, "esgd_get_config: null argument");
     if (!std::strcmp(key, "small_round_bytes")) *value = int64_t(config_small_round_bytes());
     else if (!std::strcmp(key, "device_flags")) *value = config_device_flags();
+    else if (!std::strcmp(key, "strict_handoffs")) *value = config_strict_handoffs() ? 1 : 0;
     else {
-        set_error("esgd_get_config: unknown key '%s' (small_round_bytes, device_flags)", key);
+        set_error("esgd_get_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -1296,7 +1313,7 @@ struct IpcTransport final : Transport {
                            dst, bytes, pair_flags(s, s.sh->ready, 0), pair_flags(s, s.sh->reduced, 1),
                            (s.host_mode || st.shadow) ? nullptr : dev_flag(&s.sh->fin[s.rank]),
                            dev_flag(&s.sh->gpu_err[s.rank]), ts, st.ctr,
-                           s.rank, s.world, round, ticks, cs);
+                           s.rank, s.world, round, ticks, s.strict ? 1 : 0, cs);
     }
 
     int query(Sched &s) override { return base_query(s, S(s)); }

@@ -115,8 +115,8 @@ struct AllreduceOp {
         const size_t nbytes = size_t(len) * sizeof(float);
         if (dev) {
             // arena buckets: exported to the peers as they are (no shadow copies)
-            if (esgd::arena_alloc(nbytes ? nbytes : 256, reinterpret_cast<void **>(&sb)) ||
-                esgd::arena_alloc(nbytes ? nbytes : 256, reinterpret_cast<void **>(&rb)) ||
+            if (esgd::arena_alloc(nbytes ? nbytes : 256, reinterpret_cast<void **>(&sb), true) ||
+                esgd::arena_alloc(nbytes ? nbytes : 256, reinterpret_cast<void **>(&rb), true) ||
                 hipMemset(sb, 0, nbytes) != hipSuccess || hipMemset(rb, 0, nbytes) != hipSuccess) {
                 (void)hipGetLastError();   // reported here, not by the next launch check
                 if (sb) esgd::arena_free(sb);

@@ -217,6 +217,7 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     s->fresh_only = (flags & ESGD_SCHED_FRESH_ONLY) != 0;
     s->small_bytes = config_small_round_bytes();
     s->flag_mode = config_device_flags();
+    s->strict = config_strict_handoffs();
     // Schedule ids are never reused within a job and the segment starts zeroed, so the
     // shared state of this id needs no reset (no barrier before setup).  Creation costs TWO
     // node barriers: setup (local: buckets, streams, publication) -> vote 1 (setup failures)
@@ -229,7 +230,7 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     // session: FFCOLL_BUFFERS sums with zeroed shards at 4 ranks).
     s->gen = 1;   // IpcSlot::gen == 1: published for this id
     const bool small = count * s->esize <= s->small_bytes;
-    const uint64_t sig = (uint64_t(small) << 52) | (uint64_t(s->flag_mode & 3) << 50) |
+    const uint64_t sig = (uint64_t(s->strict) << 53) | (uint64_t(small) << 52) | (uint64_t(s->flag_mode & 3) << 50) |
                          (uint64_t(s->wire_bf16) << 48) | (uint64_t(uint32_t(kind)) << 40) |
                          (uint64_t(uint32_t(dtype) & 0xff) << 32) |
                          (tag == kNoTag ? 0 : (0x10000u | uint16_t(tag)));
@@ -395,9 +396,8 @@ int sched_wait_ex(Sched *s, int *fresh) {
     s->waited = target;
     s->mark(target, 5);
     if (s->hold_mode) s->held = true;
-    // the fresh bit of the round returned (joined rounds are queued in order)
-    const int f = s->fresh_q.empty() ? 0 : s->fresh_q.front();
-    if (!s->fresh_q.empty()) s->fresh_q.pop_front();
+    // the fresh bit of the round returned
+    const int f = s->fresh_take(target) ? 1 : 0;
     if (fresh) *fresh = f;
     return ESGD_SUCCESS;
 }
@@ -426,7 +426,7 @@ int sched_test(Sched *s, int *flag) {
     *flag = s->completed >= s->waited + 1;
     if (*flag) {
         ++s->waited;
-        if (!s->fresh_q.empty()) s->fresh_q.pop_front();
+        (void)s->fresh_take(s->waited);
         if (s->hold_mode) s->held = true;
     }
     return ESGD_SUCCESS;
@@ -503,7 +503,7 @@ static bool step(Sched &s) {
         s.cur = next;
         s.cur_fresh = posted >= next;
         s.joined = next;
-        s.fresh_q.push_back(uint8_t(s.cur_fresh));
+        s.fresh_set(next, s.cur_fresh);
         // FFCOLL_BUFFERS: a round joined on a peer's activation re-resolves the buffers
         // here (a fresh round did at its post)
         if (s.resolve && !s.cur_fresh && !check(s.resolve(s), "join")) return true;

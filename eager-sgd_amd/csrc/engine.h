@@ -24,7 +24,6 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
-#include <deque>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -148,10 +147,29 @@ struct Sched {
     // the creation signature, so every rank runs the schedule the same way)
     uint64_t small_bytes = 0;   // buckets up to this many bytes: one-launch rounds
     int flag_mode = 0;          // pairing flags: 0 host memory, 1 uncached HBM, 2 fine-grained HBM
-    // whether this rank had posted each joined round before joining it, for every round
-    // not yet returned by wait()/test(), oldest first: without HOLD, peers' activations
-    // can carry the progress thread any number of rounds past the caller's last wait
-    std::deque<uint8_t> fresh_q;
+    bool strict = false;        // one-launch rounds with round 2's strict hand-offs
+    // whether this rank had posted each joined round before joining it, for the rounds
+    // not yet returned by wait()/test(): a bit ring indexed by round, kFreshWindow rounds
+    // deep (allocated at the first join).  Without HOLD, peers' activations can carry the
+    // progress thread any number of rounds past the caller's last wait; a round more than
+    // kFreshWindow rounds behind the newest join has lost its bit and is reported as not
+    // fresh (counted in fresh_lost) -- memory stays bounded however long the caller lags.
+    static constexpr uint32_t kFreshWindow = 1u << 16;
+    std::vector<uint64_t> fresh_bits;
+    uint64_t fresh_lost = 0;
+    void fresh_set(uint32_t round, bool f) {
+        if (fresh_bits.empty()) fresh_bits.assign(kFreshWindow / 64, 0);
+        const uint32_t i = round % kFreshWindow;
+        if (f) fresh_bits[i / 64] |= uint64_t(1) << (i % 64);
+        else fresh_bits[i / 64] &= ~(uint64_t(1) << (i % 64));
+    }
+    // the bit of `round` (joined already), consumed by wait()/test()
+    bool fresh_take(uint32_t round) {
+        if (fresh_bits.empty() || round == 0 || round > joined) return false;
+        if (joined - round >= kFreshWindow) { ++fresh_lost; return false; }
+        const uint32_t i = round % kFreshWindow;
+        return (fresh_bits[i / 64] >> (i % 64)) & 1;
+    }
 };
 
 // Round kind / activator rules (pure functions of the schedule parameters).
@@ -205,6 +223,7 @@ bool dataplane_mappings_closed();
 // settings new schedules capture (esgd_set_config; ESGD_SMALL_ROUND_BYTES / ESGD_DEVICE_FLAGS)
 uint64_t config_small_round_bytes();
 int config_device_flags();
+bool config_strict_handoffs();
 int config_set(const char *key, int64_t value);
 int config_get(const char *key, int64_t *value);
 

@@ -54,10 +54,14 @@ struct PairFlags {
 };
 
 // ESGD_IPC_TRACE=1 (diagnostics): every IPC export / open / close on stderr with the
-// handle's bytes, so a repeated handle or a stale mapping can be seen.
+// handle's bytes, so a repeated handle or a stale mapping can be seen;
+// ESGD_IPC_TRACE_FILE=<path>: the same lines appended to that file (every process of a
+// test session into one log), refused exports included.
 void ipc_trace(const char *what, int peer, const void *ptr, size_t bytes, const uint8_t handle[64]);
 
-int arena_alloc(size_t bytes, void **out);
+// release_idle_chunks: a new chunk may first give idle never-exported chunks back to the
+// driver (hipFree synchronises the device: callers' threads only, never the progress thread)
+int arena_alloc(size_t bytes, void **out, bool release_idle_chunks = false);
 bool arena_free(void *p);
 int arena_device(const void *p);   // device of an arena block, -1 if p is not one
 bool arena_unexportable(const void *p);   // p's chunk: the runtime refused its IPC export

@@ -711,6 +711,10 @@ struct SmallRoundArgs {
     int rank, world;
     uint32_t value;
     long long timeout;
+    // ESGD_STRICT_HANDOFFS / esgd_set_config("strict_handoffs"): round 2's hand-offs --
+    // acq_rel arrival counts, an agent-scope release on the gates and an L2 write-back
+    // before the reduced flag -- instead of the relaxed ones below (a cross-GPU A/B)
+    int strict;
 };
 
 __device__ __forceinline__ bool spin_all(uint32_t *flags, int world, uint32_t value, long long t0,
@@ -737,8 +741,10 @@ __device__ __forceinline__ bool block_wait(const SmallRoundArgs &a, const uint32
             // relaxed: the gate carries no data of this workgroup's -- every waiter runs
             // its own system-scope acquire after seeing it (an agent release here was a
             // buffer_wbl2 sc1, ~1.7 us, on every pairing's critical path)
-            if (good && threadIdx.x == 0)
-                __hip_atomic_store(gate, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (good && threadIdx.x == 0) {
+                if (a.strict) __hip_atomic_store(gate, a.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                else __hip_atomic_store(gate, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         } else if (threadIdx.x == 0) {
             good = spin_all(gate, 1, a.value, t0, a.timeout);
         }
@@ -759,11 +765,13 @@ __device__ __forceinline__ bool block_wait(const SmallRoundArgs &a, const uint32
 // is issued (MI355X_MICROARCH.md, hand-off table row 1), and the last workgroup reads
 // none of them itself.  An acq_rel add lowered to buffer_wbl2 sc1 + buffer_inv sc1 in
 // EVERY workgroup, ~3.5 us, twice per round.
-__device__ __forceinline__ bool block_count(uint32_t *ctr, int *last) {
+// strict: an acq_rel add (round 2's hand-off, ESGD_STRICT_HANDOFFS).
+__device__ __forceinline__ bool block_count(uint32_t *ctr, int *last, int strict) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t old = strict ? __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT)
+                                    : __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *last = old + 1 == gridDim.x;
         if (*last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -825,12 +833,13 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
         __hip_atomic_store(static_cast<T *>(a.pub) + e, Tr::store(v[0]), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    const bool last1 = block_count(&a.counter[0], &last);
+    const bool last1 = block_count(&a.counter[0], &last, a.strict);
     if (last1 && lead) {
         if (stamp) a.ts[2] = uint64_t(wall_clock64());
         // phase 1 wrote only sc0 sc1 (write-through) stores, drained by every workgroup
-        // before its count: no L2 write-back is needed before the flag
-        publish_flags_drained(a.reduced, a.value);
+        // before its count: no L2 write-back is needed before the flag (strict: one anyway)
+        if (a.strict) publish_flags(a.reduced, a.value);
+        else publish_flags_drained(a.reduced, a.value);
     }
     if (!block_wait(a, a.reduced.mine, &a.counter[3], last1, t0, &ok)) return;
     // the all-gather span is stamped by ONE workgroup (the last to finish): the wall
@@ -874,7 +883,7 @@ __global__ __launch_bounds__(256) void k_round_small(SmallRoundArgs a) {
     // No third pairing: peers gather from `pub`, which this rank rewrites only in the
     // next round's phase 1 -- after that round's ready pairing, i.e. after every peer's
     // kernel of this round has finished -- and rb itself is read by peers only in phase 1.
-    if (!block_count(&a.counter[1], &last) || !lead) return;
+    if (!block_count(&a.counter[1], &last, a.strict) || !lead) return;
     if (stamp) {
         a.ts[3] = t_gather;
         a.ts[4] = a.ts[5] = uint64_t(wall_clock64());
@@ -906,7 +915,7 @@ int round_small(int dtype, const void *const *src, void *out, void *pub, uint64_
                 const void *const *gsrc, void *const *gdst, const uint64_t *gbytes,
                 const PairFlags &ready, const PairFlags &reduced, uint32_t *fin, uint32_t *err,
                 uint64_t *ts, uint32_t *counter, int rank, int world, uint32_t value,
-                long long timeout_ticks, hipStream_t s) {
+                long long timeout_ticks, int strict, hipStream_t s) {
     ESGD_ARG(world >= 2 && world <= ESGD_MAX_FANIN && nseg >= 0 && nseg < kMaxSeg,
              "small round: world %d, %d segments", world, nseg);
     const size_t es = esgd_dtype_size(dtype);
@@ -935,6 +944,7 @@ int round_small(int dtype, const void *const *src, void *out, void *pub, uint64_
     a.ts = ts;
     a.counter = counter;
     a.rank = rank; a.world = world; a.value = value; a.timeout = timeout_ticks;
+    a.strict = strict;
     // ESGD_SMALL_GRID caps the workgroups (default kSmallBlocks); every one must be resident
     static const uint64_t cap = [] {
         const char *e = getenv("ESGD_SMALL_GRID");

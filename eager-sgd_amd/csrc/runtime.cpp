@@ -5,7 +5,10 @@
 // (the ff.h drop-in, the deep500 op, plain C tests) can drive the HIP path.
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
 #include <unistd.h>
+
+#include <algorithm>
 
 #include <cstdio>
 #include <cstdlib>
@@ -29,11 +32,22 @@ void clear_error() { g_err[0] = 0; }
 
 void ipc_trace(const char *what, int peer, const void *ptr, size_t bytes, const uint8_t handle[64]) {
     static const bool on = getenv("ESGD_IPC_TRACE") && *getenv("ESGD_IPC_TRACE") == '1';
-    if (!on) return;
+    static const char *file = getenv("ESGD_IPC_TRACE_FILE");
+    if (!on && !(file && *file)) return;
     char hex[129];
-    for (int i = 0; i < 64; ++i) std::snprintf(hex + 2 * i, 3, "%02x", handle[i]);
-    std::fprintf(stderr, "esgd-ipc pid %d %s peer %d ptr %p bytes %zu handle %s\n", int(getpid()), what, peer,
-                 ptr, bytes, hex);
+    for (int i = 0; i < 64; ++i) std::snprintf(hex + 2 * i, 3, "%02x", handle ? handle[i] : 0);
+    char line[512];
+    const int n = std::snprintf(line, sizeof(line), "esgd-ipc pid %d %s peer %d ptr %p bytes %zu handle %s\n",
+                                int(getpid()), what, peer, ptr, bytes, hex);
+    if (on) std::fputs(line, stderr);
+    if (file && *file && n > 0) {   // one write per line, O_APPEND: lines of many processes interleave whole
+        const int fd = open(file, O_WRONLY | O_CREAT | O_APPEND, 0644);
+        if (fd >= 0) {
+            ssize_t w = write(fd, line, size_t(std::min<int>(n, int(sizeof(line)) - 1)));
+            (void)w;
+            close(fd);
+        }
+    }
 }
 
 int hip_fail(hipError_t e, const char *what, const char *file, int line) {
@@ -119,7 +133,7 @@ int esgd_device_arch(int dev, char *name, size_t len) {
 // process, never handed back to the driver while peers may map it.
 int esgd_malloc(void **ptr, size_t bytes) {
     ESGD_ARG(ptr, "esgd_malloc: null pointer");
-    return arena_alloc(bytes ? bytes : 256, ptr);
+    return arena_alloc(bytes ? bytes : 256, ptr, true);
 }
 
 // hipFree's contract is kept: the block is reused only after the work queued on its

@@ -127,8 +127,9 @@ def set_transport(name: str):
 
 def set_config(key: str, value: int):
     """Data-plane setting captured by schedules created afterwards (esgd_set_config):
-    "small_round_bytes" (one-launch rounds up to this size) or "device_flags" (0 host,
-    1 uncached HBM, 2 fine-grained HBM pairing flags); -1 restores the default.  Every
+    "small_round_bytes" (one-launch rounds up to this size), "device_flags" (0 host,
+    1 uncached HBM, 2 fine-grained HBM pairing flags) or "strict_handoffs" (1: acq_rel
+    counts, release gates and an L2 write-back in one-launch rounds); -1 restores the default.  Every
     rank must set the same value before the same creations."""
     check(lib().esgd_set_config(key.encode(), int(value)), "esgd_set_config")
 

@@ -153,6 +153,9 @@ int esgd_set_transport(const char *name);
  *   "device_flags"       where the rank-pairing flags live: 0 pinned host memory (default,
  *                        env ESGD_DEVICE_FLAGS), 1 uncached HBM pages, 2 fine-grained HBM
  *                        pages (peers' pages written over xGMI).
+ *   "strict_handoffs"    1: one-launch rounds use acq_rel arrival counts, release gates
+ *                        and an L2 write-back before the reduced flag; 0 (default, env
+ *                        ESGD_STRICT_HANDOFFS): the relaxed hand-offs of DESIGN.md §5.
  * value -1 restores the default.  Unknown keys / values -> ESGD_INVALID_ARG. */
 int esgd_set_config(const char *key, int64_t value);
 int esgd_get_config(const char *key, int64_t *value);

@@ -17,6 +17,8 @@ ORACLE = os.path.join(ROOT, "oracle", "libffref.so")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")
     config.addinivalue_line("markers", "slow: multi-process or large-size test")
+    config.addinivalue_line("markers", "diagnostic: runtime-behaviour probe, not a product check; "
+                                       "collected only with ESGD_DIAGNOSTIC_TESTS=1")
     # Build on first use (here; the GPU box receives the prebuilt .so files).
     if not os.path.exists(ORACLE):
         subprocess.check_call(["make", "-C", ROOT, "oracle"])
@@ -27,3 +29,48 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(ROOT, "tests", "golden")
+
+
+# ---- collection order ---------------------------------------------------------------
+# On a first multi-GPU box every multi-rank test crosses xGMI for the first time, and the
+# driver runs `pytest -x`: one early cross-GPU failure would stop the suite before the hot
+# kernel's oracle tests and hide which layer failed.  So the GPU suite runs, in order:
+#   0  the single-process kernel tests of test_reduce_gpu.py (tree kernel vs the oracle),
+#   1  its full-size shapes (C2, the 8 x 256 MiB gate, > 2^31 elements),
+#   2  single-rank tests (world 1: copy paths, the RCCL transport's bring-up),
+#   3  the 2-rank cross-GPU canary (first-bad-element diagnostics per transport),
+#   4  every other multi-rank test, in file order,
+#   5  tools-only checks (the sweep library's kernel variants vs the oracle).
+# CPU tests keep their file order ahead of all of them.
+_FULL_SIZE = {"test_full_size_c2_bitwise", "test_full_size_gate_256mib_bitwise",
+              "test_reduce_beyond_int32_elements"}
+_SINGLE_RANK = {"test_rccl_transport_single_rank"}
+_LAST = {"test_sweep_variants_match_oracle"}
+
+
+def _tier(item):
+    if item.get_closest_marker("gpu") is None:
+        return -1
+    name = item.originalname or item.name
+    if name in _LAST:
+        return 5
+    if item.module.__name__.endswith("test_reduce_gpu"):
+        return 1 if name in _FULL_SIZE else 0
+    params = getattr(getattr(item, "callspec", None), "params", {})
+    if name in _SINGLE_RANK or params.get("world") == 1:
+        return 2
+    if name == "test_cross_gpu_canary":
+        return 3
+    return 4
+
+
+def pytest_collection_modifyitems(config, items):
+    if os.environ.get("ESGD_DIAGNOSTIC_TESTS") != "1":
+        keep, drop = [], []
+        for it in items:
+            (drop if it.get_closest_marker("diagnostic") else keep).append(it)
+        if drop:
+            config.hook.pytest_deselected(items=drop)
+            items[:] = keep
+    order = {id(it): i for i, it in enumerate(items)}
+    items.sort(key=lambda it: (_tier(it), order[id(it)]))

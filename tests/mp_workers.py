@@ -1226,7 +1226,7 @@ def gpu_stress_threads(rank, world, kind, counts=(65536, (1 << 20) + 3, 4096), r
     return {"res": res, "errs": errs, "bits": bits}
 
 
-def gpu_visibility(rank, world, rounds=6, count=(1 << 20) + 3, small_bytes=None, flag_mode=0):
+def gpu_visibility(rank, world, rounds=6, count=(1 << 20) + 3, small_bytes=None, flag_mode=0, strict=0):
     """Writer-then-post, the hand-off fflib2 orders with a send after the comp and a comp
     after the recv (colls/ffallreduce.c:145-162): right before posting round t, every rank
     rewrites its bucket on a producer stream (no host sync in between) with round t's
@@ -1243,6 +1243,7 @@ def gpu_visibility(rank, world, rounds=6, count=(1 << 20) + 3, small_bytes=None,
     if small_bytes is not None:
         comm.set_config("small_round_bytes", small_bytes)
     comm.set_config("device_flags", flag_mode)
+    comm.set_config("strict_handoffs", strict)
     rb = dev.DeviceBuffer(count)
     s = comm.Schedule(comm.ALLREDUCE, None, rb, count, buf=comm.BUF_DEVICE)
     prod = dev.Stream()
@@ -1262,6 +1263,46 @@ def gpu_visibility(rank, world, rounds=6, count=(1 << 20) + 3, small_bytes=None,
     s.delete()
     comm.finalize()
     return {"bad": bad, "devices": os.environ.get("ESGD_TEST_DEVICES")}
+
+
+def gpu_canary(rank, world, count, transport="ipc", path="one_launch", strict=0, rounds=3):
+    """The cross-GPU canary (tests/test_dataplane_gpu.py): the writer-then-post pattern of
+    gpu_visibility on one transport / round path, and on a mismatch everything needed to
+    tell the layers apart -- this rank's device and every rank's, the round, the number of
+    bad elements, the first bad index with its value and the oracle's."""
+    import numpy as np
+
+    from esgd import device as dev
+    from oracle import ffref
+    comm = _comm()
+    comm.set_transport(transport)
+    comm.set_config("small_round_bytes", count * 4 if path == "one_launch" else 0)
+    comm.set_config("strict_handoffs", strict)
+    rb = dev.DeviceBuffer(count)
+    s = comm.Schedule(comm.ALLREDUCE, None, rb, count, buf=comm.BUF_DEVICE)
+    prod = dev.Stream()
+    bad = []
+    for t in range(rounds):
+        seed = 0xCA7A + 131 * t
+        comm.barrier()
+        dev.fill_uniform(rb, seed, rank, stream=prod)   # queued, not waited for
+        s.post(prod)
+        s.wait()
+        got = rb.download()
+        want = ffref.tree_sum([ffref.fill_uniform(seed, r, count) for r in range(world)])
+        diff = np.nonzero(got.view(np.uint32) != want.view(np.uint32))[0]
+        if diff.size:
+            i = int(diff[0])
+            bad.append({"round": t + 1, "nbad": int(diff.size), "first": i, "got": float(got[i]),
+                        "want": float(want[i])})
+        comm.barrier()
+    s.delete()
+    for k in ("small_round_bytes", "strict_handoffs"):
+        comm.set_config(k, -1)
+    comm.finalize()
+    return {"rank": rank, "device": local_device(), "devices": os.environ.get("ESGD_TEST_DEVICES", ""),
+            "transport": transport, "path": path, "strict": strict, "count": count, "rounds": rounds,
+            "bad": bad}
 
 
 def gpu_reinit(rank, world, count=4099):

@@ -357,3 +357,38 @@ def test_a_reported_hip_failure_does_not_fail_the_next_launch():
     fill_uniform(b, 0x5EED, 1)
     synchronize()
     bits_equal(b.download(), ffref.fill_uniform(0x5EED, 1, 4099))
+
+
+SWEEPS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "bin",
+                      "libesgd_sweeps.so")
+
+
+@pytest.mark.skipif(not os.path.exists(SWEEPS), reason="tools/bin/libesgd_sweeps.so not built (make sweeps)")
+def test_sweep_variants_match_oracle():
+    # every measurement-only variant of the tree kernel (tools/sweeps/reduce_sweeps.hip,
+    # behind tools/sweep_reduce.py's numbers) computes the oracle's bits: 8 ragged fp32
+    # buckets, each policy of the table, plain and forced-grid launches
+    import ctypes as C
+    sw = C.CDLL(SWEEPS)
+    sw.esgd_sweep_reduce.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.c_void_p,
+                                     C.c_uint64, C.c_void_p]
+    sw.esgd_sweep_last_error.restype = C.c_char_p
+    n, k = (1 << 20) + 4099, 8
+    bufs = [DeviceBuffer(n) for _ in range(k)]
+    for r, b in enumerate(bufs):
+        fill_uniform(b, 0x5EEDE56D, r)
+    out = DeviceBuffer(n)
+    want = ffref.tree_sum([ffref.fill_uniform(0x5EEDE56D, r, n) for r in range(k)])
+    pa = (C.c_void_p * 8)(*[b.ptr for b in bufs])
+    bad = []
+    for pol in [-1] + list(range(0, 39)):
+        for unroll, nt, grid in ((4, 1, 0), (2, 0, 1024)):
+            if pol != 0 and (unroll, nt) != (4, 1):
+                continue
+            out.zero()
+            rc = sw.esgd_sweep_reduce(pol, unroll, nt, grid, pa, out.ptr, n, None)
+            assert rc == 0, (pol, sw.esgd_sweep_last_error())
+            synchronize()
+            if not np.array_equal(out.download().view(np.uint32), want.view(np.uint32)):
+                bad.append((pol, unroll, nt, grid))
+    assert not bad, bad

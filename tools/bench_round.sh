@@ -3,7 +3,7 @@
 # sharing the box's one GPU: a rehearsal), rocprofv3 kernel statistics of the N = 1 bench,
 # and the IPC re-export bisection.  Each GPU step has its own time limit; the first
 # failure ends the session.
-#   bash tools/bench_round.sh <tag> [steps...]   steps: smoke n1 n2 n4 prof bisect sweep (default: n1 n2 prof bisect)
+#   bash tools/bench_round.sh <tag> [steps...]   steps: smoke n1 n2 n4 n2c4 n4c4 prof bisect sweep (default: n1 n2 prof bisect)
 set -e
 export ESGD_TIMEOUT_S=60
 O=gpurun_out/${1:-bench_round}; shift || true
@@ -17,6 +17,9 @@ for s in $STEPS; do
       cp -r gpurun_out/bench_kernel_trace_split.json $O/ 2>/dev/null || true ;;
   n2) timeout -k 10 600 python bench.py --gpus 2 --steps 20 --warmup 5 > $O/bench_n2.json 2> $O/bench_n2.err ;;
   n4) timeout -k 10 600 python bench.py --gpus 4 --steps 20 --warmup 5 > $O/bench_n4.json 2> $O/bench_n4.err ;;
+  n2c4|n4c4) n=${s:1:1}   # the headline N > 1 line plus only the 161-bucket leg
+      ESGD_BENCH_LEGS=c4_resnet50_161_vs_fused ESGD_BENCH_RCCL=0 timeout -k 10 300 python bench.py --gpus $n \
+          --steps 20 --warmup 5 > $O/bench_n${n}_c4.json 2> $O/bench_n${n}_c4.err ;;
   prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run \
           --output-format csv -- python $R/bench.py --no-pmc --no-trace --no-cpu-baseline --steps 100 \
           > $R/$O/bench_prof.json 2>&1) ;;
