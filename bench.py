@@ -659,8 +659,18 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
         pipelined()
         fused_step()
     t161 = _timed_steps(comm, chain, steps)
+    l0 = comm.get_config("launches")
     t161p = _timed_steps(comm, pipelined, steps)
+    launches = (comm.get_config("launches") - l0) / steps
     breakdown = _step_breakdown_us(scheds)
+    # A/B: the same pipelined step with one launch per round (k_round_small), no sharing
+    comm.set_config("batch_rounds", 0)
+    try:
+        pipelined()
+        t161u = _timed_steps(comm, pipelined, steps)
+        breakdown_u = _step_breakdown_us(scheds)
+    finally:
+        comm.set_config("batch_rounds", -1)
     t1 = _timed_steps(comm, fused_step, steps)
     for s, b in zip(scheds, bufs):
         _defer(s, b)
@@ -670,7 +680,10 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
             "step_ms_161_buckets_pipelined": round(t161p * 1e3, 3),
             "step_ms_one_fused_bucket": round(t1 * 1e3, 3),
             "fused_speedup": round(t161 / t1, 2), "steps": steps,
-            "rank0_pipelined_step_us": breakdown}
+            "rank0_launches_per_pipelined_step": launches,
+            "rank0_pipelined_step_us": breakdown,
+            "step_ms_161_buckets_pipelined_one_launch_per_round": round(t161u * 1e3, 3),
+            "rank0_pipelined_step_us_one_launch_per_round": breakdown_u}
 
 
 def _step_breakdown_us(scheds):

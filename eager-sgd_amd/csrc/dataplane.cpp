@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -31,6 +32,7 @@
 #include "engine.h"
 #include "esgd_internal.h"
 #include "esgd.h"
+#include "round_batch.h"
 
 namespace esgd {
 
@@ -106,12 +108,30 @@ static int device_flags_env() {
 // esgd_set_config: what schedules created afterwards capture (-1 = the env default).
 // All ranks must set the same values before the same creations (the creation signature
 // checks it), so a benchmark can A/B them inside one job.
-static std::atomic<int64_t> g_cfg_small{-1}, g_cfg_flags{-1}, g_cfg_strict{-1};
+static std::atomic<int64_t> g_cfg_small{-1}, g_cfg_flags{-1}, g_cfg_strict{-1}, g_cfg_batch{-1};
+
+// One-launch rounds due together in issue order share one launch of at most this many
+// rounds (k_round_batch, round_batch.hip); 0 or 1 = one k_round_small launch per round.
+// ESGD_BATCH_ROUNDS sets the default (kBatchMax).  A process-local setting, not part of
+// the creation signature: ranks may cut the issue ring into launches differently anyway.
+static int64_t batch_rounds() {
+    static const int64_t env = [] {
+        const char *e = getenv("ESGD_BATCH_ROUNDS");
+        return (e && *e) ? int64_t(atoll(e)) : int64_t(kBatchMax);
+    }();
+    const int64_t v = g_cfg_batch.load();
+    return std::min<int64_t>(kBatchMax, v >= 0 ? v : env);
+}
 
 bool config_strict_handoffs() {
     const int64_t v = g_cfg_strict.load();
     return v >= 0 ? v != 0 : strict_env() != 0;
 }
+
+// round kernels launched by this process (k_round_small and k_round_batch launches, and
+// five-launch rounds' first pairing): esgd_get_config("launches"), for the bench's
+// per-step breakdown
+static std::atomic<uint64_t> g_launches{0};
 
 uint64_t config_small_round_bytes() {
     const int64_t v = g_cfg_small.load();
@@ -135,8 +155,13 @@ int config_set(const char *key, int64_t value) {
     } else if (!std::strcmp(key, "strict_handoffs")) {
         ESGD_ARG(value >= -1 && value <= 1, "strict_handoffs: 0 relaxed, 1 strict (-1: the default)");
         g_cfg_strict.store(value);
+    } else if (!std::strcmp(key, "batch_rounds")) {
+        ESGD_ARG(value >= -1 && value <= kBatchMax, "batch_rounds: 0..%d rounds per launch (-1: the default)",
+                 kBatchMax);
+        g_cfg_batch.store(value);
     } else {
-        set_error("esgd_set_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs)", key);
+        set_error("esgd_set_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
+                  "batch_rounds)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -147,8 +172,11 @@ int config_get(const char *key, int64_t *value) {
     if (!std::strcmp(key, "small_round_bytes")) *value = int64_t(config_small_round_bytes());
     else if (!std::strcmp(key, "device_flags")) *value = config_device_flags();
     else if (!std::strcmp(key, "strict_handoffs")) *value = config_strict_handoffs() ? 1 : 0;
+    else if (!std::strcmp(key, "batch_rounds")) *value = batch_rounds();
+    else if (!std::strcmp(key, "launches")) *value = int64_t(g_launches.load());
     else {
-        set_error("esgd_get_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs)", key);
+        set_error("esgd_get_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
+                  "batch_rounds, launches)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -450,7 +478,10 @@ static int ctr_words(int sched_id, hipStream_t cs, uint32_t **out) {
     return ESGD_SUCCESS;
 }
 
+static void batch_shutdown();
+
 void dataplane_shutdown() {
+    batch_shutdown();
     rccl_shutdown();
     std::lock_guard<std::mutex> lk(g_dp_mu);
     if (g_rs) { hip_ignore(hipStreamSynchronize(g_rs)); hip_ignore(hipStreamDestroy(g_rs)); g_rs = nullptr; }
@@ -473,6 +504,9 @@ void dataplane_shutdown() {
 struct BaseState {
     hipStream_t stream = nullptr;     // the process's round stream (not owned)
     hipEvent_t ev = nullptr;
+    // a round that went out in a shared launch (k_round_batch) reports faults through
+    // that launch's event
+    std::shared_ptr<hipEvent_t> batch_ev;
     char *rb_dev = nullptr;
     size_t cap = 0;                   // bytes of rb_dev (owned buckets may grow)
     uint64_t laid_count = ~0ull;      // count the shard layout was computed for
@@ -490,6 +524,7 @@ struct BaseState {
     size_t pin_cap = 0;
     bool copyout_pending = false;
     bool fin_mode = false;            // the round in flight reports through SchedShm::fin
+    int batch_rc = 0;                 // the shared launch of this round failed (its status)
     std::vector<char *> retired;      // grown-out buckets: peers may still map them
     uint64_t off[kMaxRanks] = {}, len[kMaxRanks] = {};   // elements
     std::map<uint32_t, hipEvent_t> producer;
@@ -530,6 +565,9 @@ struct IpcState : BaseState {
     char *wire = nullptr;
     size_t wire_cap = 0;
     PeerMap rbmap[kMaxRanks], pubmap[kMaxRanks];
+    // batched one-launch rounds: this schedule's BatchDesc is in the device table
+    bool desc_built = false;
+    uint32_t t1 = 0, t2 = 0;          // its phase-1 / phase-2 tiles
 };
 
 // shard j = [off_j, off_j + len_j): equal shards rounded up to 1 KiB so every shard
@@ -803,11 +841,19 @@ static std::string base_diagnose(Sched &s) {
 }
 
 static int base_query(Sched &s, BaseState &st) {
+    if (st.batch_rc) return st.batch_rc;   // error message set by the failed launch
     if (st.fin_mode) {   // the round's last kernel writes fin (finish_round, k_round_small, done pairing)
+        // a timed-out flag wait of a batched round still lets its workers finish (and
+        // write fin): the error word is checked first
+        if (s.world > 1 && s.sh->gpu_err[s.rank].load(std::memory_order_acquire) == s.cur) {
+            set_error("this rank's GPU waited more than %.0f s for its peers in round %u %s",
+                      engine_timeout(), s.cur, base_diagnose(s).c_str());
+            return ESGD_ERROR;
+        }
         if (int32_t(s.sh->fin[s.rank].load(std::memory_order_acquire) - s.cur) >= 0) {
             // the kernel may still be retiring (not ready is fine); a fault is reported
             // against this round, not a later one
-            const hipError_t e = hipEventQuery(st.ev);
+            const hipError_t e = hipEventQuery(st.batch_ev ? *st.batch_ev : st.ev);
             if (e != hipSuccess && e != hipErrorNotReady) {
                 (void)hip_fail(e, "one-launch round", __FILE__, __LINE__);
                 std::string m = esgd_last_error();
@@ -816,11 +862,6 @@ static int base_query(Sched &s, BaseState &st) {
                 return ESGD_ERROR;
             }
             return 1;
-        }
-        if (s.sh->gpu_err[s.rank].load(std::memory_order_acquire) == s.cur) {
-            set_error("this rank's GPU waited more than %.0f s for its peers in round %u %s",
-                      engine_timeout(), s.cur, base_diagnose(s).c_str());
-            return ESGD_ERROR;
         }
         return 0;
     }
@@ -852,6 +893,153 @@ static void base_teardown(Sched &s, BaseState &st) {
     if (st.pin) hip_ignore(hipHostFree(st.pin));
     for (char *p : st.retired) free_bucket(p);
     if (st.ev) hip_ignore(hipEventDestroy(st.ev));
+}
+
+// ---- batched one-launch rounds (round_batch.hip) ---------------------------------------
+// Device rounds of one-launch size that come due together in issue order go out in ONE
+// k_round_batch launch: IpcTransport::launch queues each round's snapshot on the round
+// stream and appends the round here; the engine flushes at the end of every pump of the
+// issue ring, and every other launch on the round stream flushes first, so the stream
+// still holds the rounds in ring order (the deadlock argument of DESIGN.md §5).
+static std::mutex g_batch_mu, g_evfree_mu;
+static BatchDesc *g_desc_dev = nullptr, *g_desc_host = nullptr;   // [kMaxSched], by schedule id
+struct BatchEntry {
+    Sched *s;
+    IpcState *st;
+    uint32_t round;
+};
+static std::vector<BatchEntry> g_pend;
+static std::vector<hipEvent_t> g_evfree;   // events of launches no round refers to any more
+
+// this schedule's BatchDesc: built at its first batched round and uploaded on the round
+// stream (ahead of the launch that reads it); its buckets, peers' mappings and flags never
+// move afterwards (FFCOLL_BUFFERS schedules are not batched).  g_batch_mu held.
+static int batch_desc(Sched &s, IpcState &st, hipStream_t cs) {
+    if (st.desc_built) return ESGD_SUCCESS;
+    if (!g_desc_dev) {
+        ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&g_desc_dev), sizeof(BatchDesc) * kMaxSched));
+        ESGD_HIP(hipHostMalloc(reinterpret_cast<void **>(&g_desc_host), sizeof(BatchDesc) * kMaxSched,
+                               hipHostMallocDefault));
+    }
+    if (!st.ctr)
+        if (int rc = ctr_words(s.id, cs, &st.ctr)) return rc;
+    const size_t es = s.esize;
+    const int r = s.rank;
+    BatchDesc d;
+    std::memset(&d, 0, sizeof(d));
+    for (int j = 0; j < s.world; ++j) d.src[j] = st.peer[j] + st.off[r] * es;
+    d.out = st.rb_dev + st.off[r] * es;
+    d.pub = st.pub;
+    d.n = st.len[r];
+    batch_tiling(st.len[r] * es / 16, kBatchWorkers, &d.t1, &d.tv1);
+    uint32_t m = 0;
+    for (int j = 0; j < s.world; ++j)
+        if (j != r && st.len[j]) ++m;
+    const uint32_t per_seg = std::max<uint32_t>(1, kBatchWorkers / std::max<uint32_t>(1, m));
+    m = 0;
+    for (int j = 0; j < s.world; ++j) {
+        if (j == r || st.len[j] == 0) continue;
+        const uint64_t bytes = st.len[j] * es;
+        d.gsrc[m] = st.pubmap[j].ptr;   // peer j's published shard j
+        d.gdst[m] = st.rb_dev + st.off[j] * es;
+        d.gvec[m] = uint32_t(bytes / 16);
+        d.gtail[m] = uint32_t(bytes % 16);
+        uint32_t tiles = 0;
+        batch_tiling(d.gvec[m], per_seg, &tiles, &d.tvg[m]);
+        d.t2pre[m + 1] = d.t2pre[m] + tiles;
+        ++m;
+    }
+    d.nseg = m;
+    d.strict = s.strict ? 1u : 0u;
+    d.ready = pair_flags(s, s.sh->ready, 0);
+    d.reduced = pair_flags(s, s.sh->reduced, 1);
+    d.fin = dev_flag(&s.sh->fin[r]);
+    d.err = dev_flag(&s.sh->gpu_err[r]);
+    d.ctr = st.ctr + 6;   // words 6..9 of the schedule's device counters
+    st.t1 = d.t1;
+    st.t2 = std::max<uint32_t>(1, d.t2pre[m]);   // at least one tile: it writes fin
+    g_desc_host[s.id] = d;
+    ESGD_HIP(hipMemcpyAsync(&g_desc_dev[s.id], &g_desc_host[s.id], sizeof(BatchDesc), hipMemcpyHostToDevice, cs));
+    st.desc_built = true;
+    return ESGD_SUCCESS;
+}
+
+static int batch_flush_locked() {
+    if (g_pend.empty()) return ESGD_SUCCESS;
+    const int n = int(g_pend.size());
+    BatchArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.table = g_desc_dev;
+    a.nent = uint32_t(n);
+    a.timeout = (long long)(engine_timeout() * double(g_ticks_per_s));
+    uint32_t t1 = 0, t2 = 0;
+    for (int e = 0; e < n; ++e) {
+        a.sid[e] = uint16_t(g_pend[e].s->id);
+        a.value[e] = g_pend[e].round;
+        a.tile1[e] = t1;
+        a.tile2[e] = t2;
+        t1 += g_pend[e].st->t1;
+        t2 += g_pend[e].st->t2;
+    }
+    a.tile1[n] = t1;
+    a.tile2[n] = t2;
+    const unsigned workers = std::min<unsigned>(kBatchWorkers, std::max<unsigned>(1, std::max(t1, t2)));
+    hipStream_t cs = g_pend[0].st->stream;
+    int rc = round_batch(g_pend[0].s->dtype, g_pend[0].s->world, a, workers, cs);
+    hipEvent_t ev = nullptr;
+    if (!rc) {
+        {
+            std::lock_guard<std::mutex> lk(g_evfree_mu);
+            if (!g_evfree.empty()) { ev = g_evfree.back(); g_evfree.pop_back(); }
+        }
+        if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+            rc = hip_fail(hipGetLastError(), "hipEventCreateWithFlags", __FILE__, __LINE__);
+        if (!rc && hipEventRecord(ev, cs) != hipSuccess)
+            rc = hip_fail(hipGetLastError(), "hipEventRecord", __FILE__, __LINE__);
+    }
+    std::shared_ptr<hipEvent_t> sp;
+    if (!rc)
+        sp = std::shared_ptr<hipEvent_t>(new hipEvent_t(ev), [](hipEvent_t *p) {
+            std::lock_guard<std::mutex> lk(g_evfree_mu);
+            g_evfree.push_back(*p);
+            delete p;
+        });
+    for (BatchEntry &b : g_pend) {
+        b.st->batch_ev = sp;
+        b.st->batch_rc = rc;
+    }
+    g_pend.clear();
+    ++g_launches;
+    return rc;
+}
+
+int dataplane_flush() {
+    std::lock_guard<std::mutex> lk(g_batch_mu);
+    return batch_flush_locked();
+}
+
+// The round joins the pending launch (its snapshot is already queued on `cs`).
+static int batch_append(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) {
+    std::lock_guard<std::mutex> lk(g_batch_mu);
+    if (!g_pend.empty() && (g_pend[0].s->dtype != s.dtype || g_pend[0].s->world != s.world ||
+                            int64_t(g_pend.size()) >= batch_rounds()))
+        batch_flush_locked();   // a failure is recorded in the rounds of that launch
+    if (int rc = batch_desc(s, st, cs)) return rc;
+    st.pub_round = round;
+    st.fin_mode = true;
+    st.batch_rc = 0;
+    g_pend.push_back({&s, &st, round});
+    return ESGD_SUCCESS;
+}
+
+static void batch_shutdown() {
+    std::lock_guard<std::mutex> lk(g_batch_mu);
+    (void)batch_flush_locked();
+    if (g_desc_dev) { hip_ignore(hipFree(g_desc_dev)); g_desc_dev = nullptr; }
+    if (g_desc_host) { hip_ignore(hipHostFree(g_desc_host)); g_desc_host = nullptr; }
+    std::lock_guard<std::mutex> ek(g_evfree_mu);
+    for (hipEvent_t e : g_evfree) hip_ignore(hipEventDestroy(e));
+    g_evfree.clear();
 }
 
 struct IpcTransport final : Transport {
@@ -1056,10 +1244,22 @@ struct IpcTransport final : Transport {
     // it (the caller may overwrite rb once wait() returns).  Buckets up to
     // small_round_bytes() run as one k_round_small launch instead (launch_small: two
     // pairings, the gather reads the published shards).
+    // rounds that go out in a shared k_round_batch launch
+    static bool batched(const Sched &s, const IpcState &st) {
+        return one_launch(s) && !s.host_mode && !st.shadow && !s.resolve && batch_rounds() > 1 &&
+               !gpu_trace_on() && st.len[0] * s.esize <= (uint64_t(1) << 30);
+    }
+
     int launch(Sched &s, uint32_t round, bool fresh) override {
         IpcState &st = S(s);
         hipStream_t cs = st.stream;
         st.fin_mode = false;
+        st.batch_ev.reset();
+        st.batch_rc = 0;
+        const bool batch = batched(s, st);
+        // anything else queued on the round stream goes behind the pending shared launch
+        if (!batch)
+            if (int rc = dataplane_flush()) return rc;
         if (s.host_mode && !s.resolve && !s.wire_bf16 && host_chunk_bytes() &&
             s.count * s.esize >= 2 * host_chunk_bytes())
             return launch_chunked(s, st, round, fresh);
@@ -1075,6 +1275,8 @@ struct IpcTransport final : Transport {
             if (s.resolve)
                 if (int rc = map_peers(s, st)) return rc;
             if (one_launch(s)) {
+                if (batch) return batch_append(s, st, round, cs);
+                ++g_launches;
                 if (int rc = launch_small(s, st, round, cs)) return rc;
                 // device buckets: nothing follows the kernel, the host polls its fin flag
                 // (the event only reports faults)
@@ -1085,6 +1287,7 @@ struct IpcTransport final : Transport {
                 }
                 return base_copy_out(s, st, cs);
             }
+            ++g_launches;
             if (s.wire_bf16) {
                 if (int rc = wire_phases(s, st, round, fresh, cs)) return rc;
             } else {
@@ -1536,6 +1739,7 @@ struct RcclTransport final : Transport {
         hipStream_t cs = st.stream;
         const int P = s.world, r = s.rank;
         const size_t es = s.esize;
+        if (int rc = dataplane_flush()) return rc;   // ring order on the round stream
         if (int rc = base_copy_in(s, st, round, fresh, cs)) return rc;
         if (P > 1 && st.L && s.wire_bf16) {
             if (int rc = wire_round(s, st)) return rc;

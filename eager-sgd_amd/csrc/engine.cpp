@@ -608,6 +608,9 @@ static bool pump_tickets(const std::vector<Sched *> &snap) {
         ++g_cursor;
         any = true;
     }
+    // the one-launch rounds this pump appended go out now, in one launch; a failure is
+    // recorded in every round of that launch (the transport reports it at its query)
+    if (any) (void)dataplane_flush();
     return any;
 }
 

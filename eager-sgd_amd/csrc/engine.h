@@ -218,6 +218,9 @@ bool engine_progress_once();
 // Data-plane resources shared by all schedules of the process (dataplane.cpp): freed at
 // finalize, before the node segment is unmapped.
 void dataplane_shutdown();
+// launch the rounds appended to the pending shared launch (k_round_batch); the engine calls
+// it after every pump of the issue ring, transports before queuing anything else
+int dataplane_flush();
 // a finalized job of this process had mapped peers' buckets (no new job with peers then)
 bool dataplane_mappings_closed();
 // settings new schedules capture (esgd_set_config; ESGD_SMALL_ROUND_BYTES / ESGD_DEVICE_FLAGS)

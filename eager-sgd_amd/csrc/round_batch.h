@@ -1,0 +1,75 @@
+// round_batch.h — several one-launch rounds in ONE kernel (k_round_batch).
+//
+// The reference's wrapper issues one allreduce per gradient tensor, back to back
+// (opt_esgd_solo_imagenet_imbalance.py:24-44 chains 161 ops per ResNet-50 step; each
+// ffsolo_allreduce / ffrand_allreduce post is its own op-DAG run, ffsolo_allreduce.c:103-114).
+// Run one kernel launch and two rank pairings per round, that call pattern pays a host
+// launch and two flag round trips per bucket.  The data plane instead gathers the
+// one-launch rounds that are due in the node's issue order (engine.cpp) into one launch:
+// a flag-agent wave publishes every entry's `ready` at once and turns peers' flags into
+// device gates, while worker workgroups walk the entries' phase-1 tiles, then their
+// phase-2 tiles, in ring order.  Per-entry semantics are those of k_round_small: the same
+// flags, counters, published shard, fin word and tree order -- only the launch is shared.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "esgd.h"
+#include "esgd_internal.h"
+
+namespace esgd {
+
+constexpr int kBatchMax = 64;          // rounds per launch: one agent lane each
+constexpr uint32_t kBatchWorkers = 64; // worker workgroups at most (k_round_small's grid)
+// A phase's tiles of one entry: at most kBatchWorkers (one arrival count each), at least
+// 1024 16-B vectors (one pass of a 256-lane workgroup, 4 vectors per lane) per tile -- a
+// lone entry gets k_round_small's parallelism, a large one few counts.
+inline void batch_tiling(uint64_t nvec, uint32_t max_tiles, uint32_t *tiles, uint32_t *tv) {
+    const uint64_t want = std::max<uint64_t>(1, std::min<uint64_t>(max_tiles, (nvec + 1023) / 1024));
+    uint64_t per = (nvec + want - 1) / want;
+    per = std::max<uint64_t>(1024, (per + 1023) / 1024 * 1024);
+    *tv = uint32_t(per);
+    *tiles = uint32_t(std::max<uint64_t>(1, (nvec + per - 1) / per));
+}
+
+// One schedule's round, as the batch kernel sees it.  Built once per schedule (its
+// buckets, peers' mappings and flags never move: FFCOLL_BUFFERS schedules are not batched)
+// and kept in device memory, indexed by schedule id.
+struct BatchDesc {
+    const void *src[ESGD_MAX_FANIN];   // phase 1: shard `rank` of every rank's rb, rank order
+    void *out;                         // ... folded into shard `rank` of the local rb
+    void *pub;                         // ... and into this rank's published shard
+    uint64_t n;                        // elements of the local shard
+    const void *gsrc[ESGD_MAX_FANIN];  // phase 2: every other rank's published shard
+    void *gdst[ESGD_MAX_FANIN];        // ... and where it lands in the local rb
+    uint32_t gvec[ESGD_MAX_FANIN];     // 16-B vectors per segment
+    uint32_t gtail[ESGD_MAX_FANIN];    // bytes after the last full vector
+    uint32_t tvg[ESGD_MAX_FANIN];      // 16-B vectors per phase-2 tile of segment sg
+    uint32_t t2pre[ESGD_MAX_FANIN + 1];   // phase-2 tiles before segment sg (prefix)
+    uint32_t nseg;
+    uint32_t tv1, t1;                  // phase 1: 16-B vectors per tile, tiles
+    uint32_t strict;                   // round 2's hand-offs (ESGD_STRICT_HANDOFFS)
+    PairFlags ready, reduced;
+    uint32_t *fin, *err;               // SchedShm::fin[rank], gpu_err[rank] (device views)
+    uint32_t *ctr;                     // device words: [0] phase-1 arrivals, [1] phase-2
+                                       // arrivals, [2] ready gate, [3] reduced gate
+};
+
+// Kernel arguments: the entries of one launch, in issue-ring order.
+struct BatchArgs {
+    const BatchDesc *table;            // device table, indexed by schedule id
+    uint32_t nent;
+    uint32_t tile1[kBatchMax + 1];     // phase-1 tiles before entry e (prefix)
+    uint32_t tile2[kBatchMax + 1];     // phase-2 tiles before entry e (prefix)
+    uint16_t sid[kBatchMax];
+    uint32_t value[kBatchMax];         // the round of entry e
+    long long timeout;                 // wall-clock ticks any flag wait may take
+};
+
+// world: ranks (2..ESGD_MAX_FANIN); grid = workers + 1 (the agent)
+int round_batch(int dtype, int world, const BatchArgs &a, unsigned workers, hipStream_t s);
+
+}  // namespace esgd

@@ -1,0 +1,255 @@
+// round_batch.hip — k_round_batch: the one-launch rounds due in issue order, in one kernel.
+//
+// Grid: `workers` workgroups of 256 threads plus ONE agent workgroup (the last block), all
+// resident (at most kBatchWorkers + 1 workgroups, far below one per CU).
+//
+// Agent (wave 0 of the last block; lane e owns entry e):
+//   * publishes `ready` of every entry at once -- everything the entries' snapshots
+//     wrote was queued on the stream before this launch -- behind one system-scope
+//     release (L2 write-back) and a drain;
+//   * polls every rank's ready / reduced flag of its entry (one system-scope load per rank,
+//     all lanes' loads in flight together) and raises the entry's device gates.
+// Workers walk a global tile list in ring order -- every entry's phase-1 tiles, then every
+// entry's phase-2 tiles -- tile g on worker g % workers:
+//   * phase 1 (reduce-scatter): wait for the entry's ready gate; fold one tile (tv1 16-B
+//     vectors) of shard `rank` of every rank's rb in the reference's tree order
+//     (ffallreduce.c:138-171 via tree_fold) into the local rb and the published shard;
+//     the last tile of an entry to arrive publishes the entry's `reduced` flag;
+//   * phase 2 (all-gather): wait for the entry's reduced gate; copy one tile of a peer's
+//     published shard into the local rb; the last tile to arrive stores the
+//     round in the entry's fin word (the host polls it).
+// The agent never waits for one entry before serving another, and a worker's tiles come
+// in ring order, so a flag of entry i depends only on flags of entries <= i on every rank:
+// ranks that cut the issue ring into launches differently cannot deadlock.
+//
+// Hand-offs (relaxed, as in k_round_small; strict with BatchDesc::strict): payload stores
+// are system-scope write-through (sc0 sc1) and drained by every wave before its workgroup
+// counts itself; peer memory is read with system-scope loads, and each worker drops stale
+// peer lines from its CU's L1 and its XCD's L2 once, at the start of the launch (every
+// read of peer memory in this launch follows its gate, and no entry's buffers are touched
+// by an earlier launch's reads after that point).
+#include "reduce_core.h"
+#include "round_batch.h"
+
+namespace esgd {
+
+namespace {
+
+__device__ __forceinline__ bool reached(uint32_t v, uint32_t want) { return int32_t(v - want) >= 0; }
+
+__device__ __forceinline__ uint32_t load_sys(const uint32_t *p) {
+    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void store_sys(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void store_gate(uint32_t *p, uint32_t v, bool strict) {
+    if (strict) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one entry's flag words in every destination (host memory: one word; device flag pages:
+// this rank's word in every rank's page)
+__device__ __forceinline__ void put_flags(const PairFlags &f, uint32_t v) {
+    for (int q = 0; q < f.ndst; ++q) store_sys(f.dst[q], v);
+}
+
+template <int K>
+__device__ void agent(const BatchArgs &a, long long t0) {
+    const int lane = int(threadIdx.x);
+    const bool act = lane < int(a.nent);
+    const BatchDesc *d = act ? &a.table[a.sid[lane]] : nullptr;
+    const uint32_t v = act ? a.value[lane] : 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: what the snapshots wrote
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (act) put_flags(d->ready, v);
+    int st = act ? 0 : 2;   // 0: waiting for every ready, 1: for every reduced, 2: done
+    for (;;) {
+        if (st < 2) {
+            const uint32_t *f = st == 0 ? d->ready.mine : d->reduced.mine;
+            uint32_t got[K];
+#pragma unroll
+            for (int q = 0; q < K; ++q) got[q] = load_sys(&f[q]);   // all in flight at once
+            bool all = true;
+#pragma unroll
+            for (int q = 0; q < K; ++q) all = all && reached(got[q], v);
+            if (all) {
+                store_gate(d->ctr + 2 + st, v, d->strict != 0);
+                ++st;
+            } else if (wall_clock64() - t0 > a.timeout) {
+                store_sys(d->err, v);              // the host fails the round
+                store_gate(d->ctr + 2, v, false);  // and no worker is left waiting
+                store_gate(d->ctr + 3, v, false);
+                st = 2;
+            }
+        }
+        if (__all(st == 2)) return;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+// phase 1, tile `local` of an entry: fold the shard's vectors [local * tv1, +tv1)
+template <class Tr, int K>
+__device__ __forceinline__ void tile_reduce(const BatchDesc &d, uint32_t local) {
+    using T = typename Tr::T;
+    using A = typename Tr::A;
+    const uint32_t nvec = uint32_t(d.n / Tr::E);
+    const int bytes = int(nvec * 16u);
+    __amdgpu_buffer_rsrc_t rs[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(d.src[j]), (short)0, bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(d.out, (short)0, bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wp = __builtin_amdgcn_make_buffer_rsrc(d.pub, (short)0, bytes, 0x00020000);
+    constexpr int U = sizeof(T) == 2 ? 2 : 4;   // vectors per input per lane in flight
+    const uint32_t v0 = local * d.tv1;
+    for (uint32_t base = v0; base < v0 + d.tv1 && base < nvec; base += 256u * U) {
+        const uint32_t i = base + threadIdx.x;
+        raw16 r[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                r[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs[j], (i + u * 256) * 16, 0, 17);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const raw16 o = fold16<Tr, K, false>(r[u], 1.0f);
+            __builtin_amdgcn_raw_buffer_store_b128(o, ws, (i + u * 256) * 16, 0, 17);
+            __builtin_amdgcn_raw_buffer_store_b128(o, wp, (i + u * 256) * 16, 0, 17);
+        }
+    }
+    // the ragged tail (elements after the last 16-B vector): tile 0, one element per lane
+    if (local == 0 && uint64_t(nvec) * Tr::E + threadIdx.x < d.n) {
+        const uint64_t e = uint64_t(nvec) * Tr::E + threadIdx.x;
+        A v[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            v[j] = Tr::load(__hip_atomic_load(static_cast<const T *>(d.src[j]) + e, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM));
+        tree_fold<Tr, K>(v);
+        __hip_atomic_store(static_cast<T *>(d.out) + e, Tr::store(v[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(static_cast<T *>(d.pub) + e, Tr::store(v[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// phase 2, tile `local` of an entry: tvg[sg] vectors of one peer's published shard
+__device__ __forceinline__ void tile_gather(const BatchDesc &d, uint32_t local) {
+    uint32_t sg = 0;
+    while (sg < d.nseg && local >= d.t2pre[sg + 1]) ++sg;
+    if (sg >= d.nseg) return;   // an entry with nothing to gather (its one dummy tile)
+    const uint32_t gv = d.gvec[sg], tv = d.tvg[sg], first = (local - d.t2pre[sg]) * tv;
+    const __amdgpu_buffer_rsrc_t gs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(d.gsrc[sg]), (short)0, int(gv * 16u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t gd = __builtin_amdgcn_make_buffer_rsrc(d.gdst[sg], (short)0, int(gv * 16u), 0x00020000);
+    for (uint32_t base = first; base < first + tv && base < gv; base += 1024u) {
+        const uint32_t i = base + threadIdx.x;
+        raw16 r[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b128(gs, (i + u * 256) * 16, 0, 17);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(r[u], gd, (i + u * 256) * 16, 0, 17);
+    }
+    if (first == 0 && threadIdx.x < d.gtail[sg]) {   // bytes after the last full vector
+        const uint8_t *src = static_cast<const uint8_t *>(d.gsrc[sg]) + size_t(gv) * 16;
+        uint8_t *dst = static_cast<uint8_t *>(d.gdst[sg]) + size_t(gv) * 16;
+        __hip_atomic_store(dst + threadIdx.x,
+                           __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+}  // namespace
+
+template <class Tr, int K>
+__global__ __launch_bounds__(256) void k_round_batch(BatchArgs a) {
+    const long long t0 = wall_clock64();
+    if (blockIdx.x == gridDim.x - 1) {
+        if (threadIdx.x < 64) agent<K>(a, t0);
+        return;
+    }
+    // stale peer lines of earlier launches out of this CU's L1 and this XCD's L2
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const uint32_t workers = gridDim.x - 1;
+    const uint32_t T1 = a.tile1[a.nent], T = T1 + a.tile2[a.nent];
+    uint32_t e = 0;
+    bool gather = false;
+    for (uint32_t g = blockIdx.x; g < T; g += workers) {
+        if (!gather && g >= T1) { gather = true; e = 0; }
+        const uint32_t t = gather ? g - T1 : g;
+        const uint32_t *pre = gather ? a.tile2 : a.tile1;
+        while (t >= pre[e + 1]) ++e;
+        const BatchDesc &d = a.table[a.sid[e]];
+        const uint32_t v = a.value[e];
+        if (threadIdx.x == 0) {
+            const uint32_t *gate = d.ctr + (gather ? 3 : 2);
+            while (!reached(__hip_atomic_load(const_cast<uint32_t *>(gate), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                            v)) {
+                if (wall_clock64() - t0 > 2 * a.timeout) break;   // the agent's timeout comes first
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (d.strict) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        }
+        __syncthreads();
+        const uint32_t local = t - pre[e];
+        if (!gather) tile_reduce<Tr, K>(d, local);
+        else tile_gather(d, local);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are in memory
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t *cnt = d.ctr + (gather ? 1 : 0);
+            const uint32_t need = pre[e + 1] - pre[e];
+            const uint32_t old = d.strict ? __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT)
+                                          : __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old + 1 == need) {   // the entry's last tile of this phase
+                __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!gather) {
+                    // every tile of the entry was stored write-through and drained before
+                    // its count: no L2 write-back before the flag (strict: one anyway)
+                    if (d.strict) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    put_flags(d.reduced, v);
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    store_sys(d.fin, v);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <class Tr>
+static int launch_batch_t(int world, const BatchArgs &a, unsigned grid, hipStream_t s) {
+    switch (world) {
+#define ESGD_BATCH_K(KK) \
+    case KK: hipLaunchKernelGGL((k_round_batch<Tr, KK>), dim3(grid), dim3(256), 0, s, a); break;
+    ESGD_BATCH_K(2) ESGD_BATCH_K(3) ESGD_BATCH_K(4) ESGD_BATCH_K(5) ESGD_BATCH_K(6) ESGD_BATCH_K(7)
+    ESGD_BATCH_K(8)
+#undef ESGD_BATCH_K
+    default:
+        set_error("batched rounds: %d ranks outside [2, %d]", world, ESGD_MAX_FANIN);
+        return ESGD_INVALID_ARG;
+    }
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+int round_batch(int dtype, int world, const BatchArgs &a, unsigned workers, hipStream_t s) {
+    ESGD_ARG(a.nent >= 1 && a.nent <= uint32_t(kBatchMax) && a.table && workers >= 1 && workers <= kBatchWorkers,
+             "batched rounds: %u entries, %u workers", a.nent, workers);
+    const unsigned grid = workers + 1;
+    switch (dtype) {
+    case ESGD_FLOAT: return launch_batch_t<F32>(world, a, grid, s);
+    case ESGD_BF16: return launch_batch_t<BF16>(world, a, grid, s);
+    case ESGD_DOUBLE: return launch_batch_t<F64>(world, a, grid, s);
+    case ESGD_INT32: return launch_batch_t<I32>(world, a, grid, s);
+    case ESGD_INT64: return launch_batch_t<I64>(world, a, grid, s);
+    default: break;
+    }
+    set_error("batched rounds: unsupported dtype %d", dtype);
+    return ESGD_INVALID_ARG;
+}
+
+}  // namespace esgd

@@ -1305,6 +1305,86 @@ def gpu_canary(rank, world, count, transport="ipc", path="one_launch", strict=0,
             "bad": bad}
 
 
+def _inputs(dname, seed, world, count):
+    """Every rank's bucket of one round: splitmix fp32 (and its bf16 / fp64 forms), or the
+    int patterns of evaluation/allreduce.c:49 -- with the oracle's result for them."""
+    import numpy as np
+
+    from oracle import ffref
+    if dname == "fp32":
+        xs = [ffref.fill_uniform(seed, r, count) for r in range(world)]
+        return xs, ffref.tree_sum(xs)
+    if dname == "bf16":
+        xs = [ffref.f32_to_bf16(ffref.fill_uniform(seed, r, count)) for r in range(world)]
+        return xs, ffref.tree_sum_bf16(xs)
+    if dname == "fp64":
+        xs = [ffref.fill_uniform(seed, r, count).astype(np.float64) * 1e-3 for r in range(world)]
+        return xs, ffref.tree_sum(xs)
+    npdt = {"int32": np.int32, "int64": np.int64}[dname]
+    xs = [(np.arange(count) + seed % 1000 + 7 * r).astype(npdt) for r in range(world)]
+    return xs, ffref.tree_sum(xs)
+
+
+def gpu_many(rank, world, specs, rounds=3, batch=None, small_bytes=None, strict=0, pipelined=True,
+             seed=0xBA7C, straggle_us=0):
+    """One ALLREDUCE schedule per (dtype, count) in `specs` (device buckets, in place), every
+    round: each rank writes all its buckets, a barrier, then posts every schedule and waits
+    for every one (the optimizer's per-tensor pipelining; pipelined=False: post, wait, one
+    schedule after the other).  batch: rounds per shared launch (esgd_set_config
+    "batch_rounds"), one value for every rank or a list with one per rank -- ranks may cut
+    the issue ring into launches differently.  straggle_us: each rank sleeps a random time
+    (up to that) between its posts.  Returns every mismatch and this rank's launch count."""
+    import numpy as np
+
+    from esgd import _lib
+    from esgd import device as dev
+    comm = _comm()
+    if batch is not None:
+        comm.set_config("batch_rounds", batch[rank] if isinstance(batch, (list, tuple)) else batch)
+    if small_bytes is not None:
+        comm.set_config("small_round_bytes", small_bytes)
+    comm.set_config("strict_handoffs", strict)
+    dts = {"fp32": _lib.FLOAT, "bf16": _lib.BF16, "fp64": _lib.DOUBLE, "int32": _lib.INT32, "int64": _lib.INT64}
+    bufs = [dev.DeviceBuffer(c, dts[d]) for d, c in specs]
+    scheds = [comm.Schedule(comm.ALLREDUCE, None, b, c, dtype=dts[d], buf=comm.BUF_DEVICE)
+              for b, (d, c) in zip(bufs, specs)]
+    rng = np.random.default_rng(1000 + rank)
+    bad = []
+    l0 = comm.get_config("launches")
+    for t in range(rounds):
+        wants = []
+        for i, ((d, c), b) in enumerate(zip(specs, bufs)):
+            xs, want = _inputs(d, seed + 7919 * t + 31 * i, world, c)
+            b.upload(xs[rank])
+            wants.append(want)
+        comm.barrier()
+        if pipelined:
+            for s in scheds:
+                if straggle_us:
+                    time.sleep(rng.uniform(0, straggle_us) * 1e-6)
+                s.post()
+            for s in scheds:
+                s.wait()
+        else:
+            for s in scheds:
+                s.post()
+                s.wait()
+        for i, (b, want) in enumerate(zip(bufs, wants)):
+            got = b.download()
+            diff = np.nonzero(got.view(np.uint8) != want.view(np.uint8))[0]
+            if diff.size:
+                bad.append({"round": t + 1, "sched": i, "spec": specs[i], "nbad_bytes": int(diff.size),
+                            "first_byte": int(diff[0])})
+        comm.barrier()
+    launches = comm.get_config("launches") - l0
+    for s in scheds:
+        s.delete()
+    for k in ("batch_rounds", "small_round_bytes", "strict_handoffs"):
+        comm.set_config(k, -1)
+    comm.finalize()
+    return {"bad": bad, "launches": launches, "rounds": rounds * len(specs)}
+
+
 def gpu_reinit(rank, world, count=4099):
     """A finalized job that mapped its peers' buckets must refuse a second multi-process
     job in the same process (re-opening closed IPC handles: DESIGN.md §5)."""

@@ -60,6 +60,58 @@ def test_one_launch_rounds_back_to_back(world):
         assert all(all(v) for v in verdicts), (count, verdicts)
 
 
+# ---- batched one-launch rounds (k_round_batch) -----------------------------------------
+# Rounds that come due together in issue order share one launch: a flag agent publishes
+# every round's ready flag at once and turns peers' flags into gates, workers walk the
+# rounds' tiles in ring order.  Every round must give the oracle's bits, however the
+# ranks cut the ring into launches.
+
+MIXED = [("fp32", 1), ("fp32", 17), ("fp32", 4099), ("fp32", 65536 + 3), ("fp32", 300007),
+         ("fp32", (1 << 20) + 3), ("fp32", 1000), ("fp32", 64), ("fp32", 262144), ("fp32", 5)]
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_batched_rounds_bitwise(world):
+    # ten schedules of ragged sizes posted back to back then waited (the optimizer's
+    # pipelined per-tensor pattern): fewer launches than rounds, every round bit-exact
+    outs = run("gpu_many", world, specs=MIXED, rounds=3)
+    for o in outs:
+        assert not o["bad"], o["bad"]
+        assert o["launches"] < o["rounds"], o
+
+
+def test_batched_rounds_mixed_dtypes_and_five_launch_rounds():
+    # a dtype change cuts the launch; a bucket above the one-launch size goes out as a
+    # five-launch round between batched ones (the pending launch is flushed first)
+    specs = [("fp32", 4099), ("int32", 70001), ("bf16", 65539), ("fp64", 1025), ("fp32", (2 << 20) + 7),
+             ("int64", 333), ("fp32", 100003), ("bf16", 9)]
+    outs = run("gpu_many", 3, specs=specs, rounds=3, small_bytes=1 << 20)
+    for o in outs:
+        assert not o["bad"], o["bad"]
+
+
+def test_batched_rounds_cut_differently_per_rank():
+    # rank 0 batches up to 64 rounds, rank 1 one round per launch (k_round_small), rank 2
+    # three, rank 3 two; random delays between posts: no deadlock, every round bit-exact
+    outs = run("gpu_many", 4, specs=MIXED * 3, rounds=3, batch=[64, 0, 3, 2], straggle_us=300)
+    for o in outs:
+        assert not o["bad"], o["bad"]
+
+
+@pytest.mark.parametrize("strict", [0, 1])
+def test_batched_rounds_resnet50_table(strict):
+    # the reference's 161 per-tensor buckets (opt_esgd_solo_imagenet_imbalance.py:86-248):
+    # at the default one-launch size 156 of them go out in shared launches, 5 as
+    # five-launch rounds; relaxed and strict hand-offs
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "resnet50_buckets.json")) as f:
+        lengths = json.load(f)["lengths"]
+    outs = run("gpu_many", 2, specs=[("fp32", n) for n in lengths], rounds=2, strict=strict, timeout=400)
+    for o in outs:
+        assert not o["bad"], o["bad"][:5]
+        assert o["launches"] < o["rounds"], o
+
+
 @pytest.mark.parametrize("in_place", [False, True])
 def test_allreduce_host_buffers(in_place):
     # the reference's contract: host buckets in, host result out (staged through HBM)
