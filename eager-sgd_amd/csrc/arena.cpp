@@ -361,7 +361,7 @@ int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_
         // owns (a fresh chunk) and shadows a caller's bucket that lives here
         c->unexportable = true;
         drop_free(c);
-        ipc_trace("export-refused", -1, c->base, c->bytes, nullptr);
+        ipc_trace(simulate ? "export-refused-simulated" : "export-refused", -1, c->base, c->bytes, nullptr);
         const char *m = getenv("HSA_ENABLE_IPC_MODE_LEGACY");
         int rc = hip_fail(e, "hipIpcGetMemHandle", __FILE__, __LINE__);
         if (!m || std::strcmp(m, "0") != 0) {

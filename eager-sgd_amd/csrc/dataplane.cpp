@@ -964,6 +964,18 @@ static int batch_desc(Sched &s, IpcState &st, hipStream_t cs) {
     return ESGD_SUCCESS;
 }
 
+// ranks of this job whose GPU is this process's (1 with a GPU per rank; the rehearsal on
+// a 1-GPU box puts every rank there)
+static int ranks_on_my_device() {
+    Segment *seg = engine_segment();
+    const int me = engine_rank(), world = engine_world();
+    if (!seg) return 1;
+    const int dev = seg->device[me].load();
+    int n = 0;
+    for (int q = 0; q < world; ++q) n += seg->device[q].load() == dev;
+    return std::max(1, n);
+}
+
 static int batch_flush_locked() {
     if (g_pend.empty()) return ESGD_SUCCESS;
     const int n = int(g_pend.size());
@@ -983,7 +995,12 @@ static int batch_flush_locked() {
     }
     a.tile1[n] = t1;
     a.tile2[n] = t2;
-    const unsigned workers = std::min<unsigned>(kBatchWorkers, std::max<unsigned>(1, std::max(t1, t2)));
+    unsigned workers = std::min<unsigned>(kBatchWorkers, std::max<unsigned>(1, std::max(t1, t2)));
+    // every workgroup of every rank sharing this GPU must be resident at once (the
+    // workers of one launch wait on each other through the peers): with 8 ranks on one
+    // GPU, 8 x 65 workgroups of the fan-in-8 kernel (2 per CU) did not fit and hung
+    const int cap = round_batch_capacity(g_pend[0].s->dtype, g_pend[0].s->world) / ranks_on_my_device() - 1;
+    workers = std::max(1u, std::min<unsigned>(workers, unsigned(std::max(1, cap))));
     hipStream_t cs = g_pend[0].st->stream;
     int rc = round_batch(g_pend[0].s->dtype, g_pend[0].s->world, a, workers, cs);
     hipEvent_t ev = nullptr;

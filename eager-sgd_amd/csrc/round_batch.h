@@ -71,5 +71,7 @@ struct BatchArgs {
 
 // world: ranks (2..ESGD_MAX_FANIN); grid = workers + 1 (the agent)
 int round_batch(int dtype, int world, const BatchArgs &a, unsigned workers, hipStream_t s);
+// workgroups of the batch kernel for (dtype, world) resident on this GPU at once
+int round_batch_capacity(int dtype, int world);
 
 }  // namespace esgd

@@ -1,7 +1,9 @@
 // round_batch.hip — k_round_batch: the one-launch rounds due in issue order, in one kernel.
 //
-// Grid: `workers` workgroups of 256 threads plus ONE agent workgroup (the last block), all
-// resident (at most kBatchWorkers + 1 workgroups, far below one per CU).
+// Grid: ONE agent workgroup (block 0, dispatched first) plus `workers` workgroups of 256
+// threads, all resident at once: workers wait on each other's entries through peers, so a
+// worker that is not yet dispatched while the others spin would deadlock the launch.  The
+// host caps the grid so that every rank sharing this GPU fits (round_batch_capacity).
 //
 // Agent (wave 0 of the last block; lane e owns entry e):
 //   * publishes `ready` of every entry at once -- everything the entries' snapshots
@@ -10,7 +12,7 @@
 //   * polls every rank's ready / reduced flag of its entry (one system-scope load per rank,
 //     all lanes' loads in flight together) and raises the entry's device gates.
 // Workers walk a global tile list in ring order -- every entry's phase-1 tiles, then every
-// entry's phase-2 tiles -- tile g on worker g % workers:
+// entry's phase-2 tiles -- tile g on worker 1 + g % workers:
 //   * phase 1 (reduce-scatter): wait for the entry's ready gate; fold one tile (tv1 16-B
 //     vectors) of shard `rank` of every rank's rb in the reference's tree order
 //     (ffallreduce.c:138-171 via tree_fold) into the local rb and the published shard;
@@ -165,7 +167,7 @@ __device__ __forceinline__ void tile_gather(const BatchDesc &d, uint32_t local) 
 template <class Tr, int K>
 __global__ __launch_bounds__(256) void k_round_batch(BatchArgs a) {
     const long long t0 = wall_clock64();
-    if (blockIdx.x == gridDim.x - 1) {
+    if (blockIdx.x == 0) {   // dispatched first: the agent never waits for a free slot
         if (threadIdx.x < 64) agent<K>(a, t0);
         return;
     }
@@ -175,7 +177,7 @@ __global__ __launch_bounds__(256) void k_round_batch(BatchArgs a) {
     const uint32_t T1 = a.tile1[a.nent], T = T1 + a.tile2[a.nent];
     uint32_t e = 0;
     bool gather = false;
-    for (uint32_t g = blockIdx.x; g < T; g += workers) {
+    for (uint32_t g = blockIdx.x - 1; g < T; g += workers) {
         if (!gather && g >= T1) { gather = true; e = 0; }
         const uint32_t t = gather ? g - T1 : g;
         const uint32_t *pre = gather ? a.tile2 : a.tile1;
@@ -218,6 +220,43 @@ __global__ __launch_bounds__(256) void k_round_batch(BatchArgs a) {
         }
         __syncthreads();
     }
+}
+
+// workgroups of k_round_batch<Tr, K> resident on the whole GPU at once
+template <class Tr>
+static int capacity_t(int world) {
+    int nb = 0;
+    hipError_t e = hipErrorInvalidValue;
+    switch (world) {
+#define ESGD_BATCH_OCC(KK) \
+    case KK: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_round_batch<Tr, KK>, 256, 0); break;
+    ESGD_BATCH_OCC(2) ESGD_BATCH_OCC(3) ESGD_BATCH_OCC(4) ESGD_BATCH_OCC(5) ESGD_BATCH_OCC(6) ESGD_BATCH_OCC(7)
+    ESGD_BATCH_OCC(8)
+#undef ESGD_BATCH_OCC
+    default: break;
+    }
+    if (e != hipSuccess || nb <= 0) {
+        (void)hipGetLastError();
+        nb = 1;
+    }
+    return nb * cu_count();
+}
+
+int round_batch_capacity(int dtype, int world) {
+    static int cache[8][ESGD_MAX_FANIN + 1] = {};
+    if (dtype < 0 || dtype >= 8 || world < 2 || world > ESGD_MAX_FANIN) return 0;
+    int &c = cache[dtype][world];
+    if (!c) {
+        switch (dtype) {
+        case ESGD_FLOAT: c = capacity_t<F32>(world); break;
+        case ESGD_BF16: c = capacity_t<BF16>(world); break;
+        case ESGD_DOUBLE: c = capacity_t<F64>(world); break;
+        case ESGD_INT32: c = capacity_t<I32>(world); break;
+        case ESGD_INT64: c = capacity_t<I64>(world); break;
+        default: return 0;
+        }
+    }
+    return c;
 }
 
 template <class Tr>

@@ -374,9 +374,10 @@ def test_sweep_variants_match_oracle():
                                      C.c_uint64, C.c_void_p]
     sw.esgd_sweep_last_error.restype = C.c_char_p
     n, k = (1 << 20) + 4099, 8
+    s = Stream()   # every step on ONE stream (the legacy null stream does not order with it)
     bufs = [DeviceBuffer(n) for _ in range(k)]
     for r, b in enumerate(bufs):
-        fill_uniform(b, 0x5EEDE56D, r)
+        fill_uniform(b, 0x5EEDE56D, r, stream=s)
     out = DeviceBuffer(n)
     want = ffref.tree_sum([ffref.fill_uniform(0x5EEDE56D, r, n) for r in range(k)])
     pa = (C.c_void_p * 8)(*[b.ptr for b in bufs])
@@ -385,10 +386,10 @@ def test_sweep_variants_match_oracle():
         for unroll, nt, grid in ((4, 1, 0), (2, 0, 1024)):
             if pol != 0 and (unroll, nt) != (4, 1):
                 continue
-            out.zero()
-            rc = sw.esgd_sweep_reduce(pol, unroll, nt, grid, pa, out.ptr, n, None)
+            out.zero(stream=s)
+            rc = sw.esgd_sweep_reduce(pol, unroll, nt, grid, pa, out.ptr, n, s.handle)
             assert rc == 0, (pol, sw.esgd_sweep_last_error())
-            synchronize()
-            if not np.array_equal(out.download().view(np.uint32), want.view(np.uint32)):
+            s.synchronize()
+            if not np.array_equal(out.download(stream=s).view(np.uint32), want.view(np.uint32)):
                 bad.append((pol, unroll, nt, grid))
     assert not bad, bad
