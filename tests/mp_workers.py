@@ -1489,6 +1489,45 @@ def cp_fresh_queue(rank, world, rounds=300):
     return {"fresh": fresh, "joined": joined}
 
 
+def cp_pipelined_steps(rank, world, steps=50, kind=2, n=161):
+    """The per-tensor call pattern on the control plane alone (ESGD_BUF_NONE: join, ticket,
+    issue ring and completion with a transport that moves nothing): `n` schedules, every
+    step posts all of them, then waits for all.  Median step and, on the last step, the
+    host timeline relative to the first post (tools/host_engine_probe.py)."""
+    import statistics
+
+    import numpy as np
+    comm = _comm()
+    scheds = [comm.Schedule(kind, None, None, 0, seed=6545343, buf=comm.BUF_NONE) for _ in range(n)]
+    ts = []
+    for _ in range(steps):
+        comm.barrier()
+        t0 = time.perf_counter()
+        for s in scheds:
+            s.post()
+        for s in scheds:
+            s.wait()
+        ts.append(time.perf_counter() - t0)
+    rows = []
+    for s in scheds:
+        tl = s.timeline().astype(np.int64)
+        tl = tl[(tl[:, 0] > 0) & (tl[:, 5] > 0)]
+        if len(tl):
+            rows.append(tl[-1])
+    tl = np.array(rows)
+    t0 = tl[:, 0].min()
+    rel = {k: round(float(tl[:, i].max() - t0) / 1e3, 1) for k, i in
+           (("last_post", 0), ("last_join", 1), ("last_launch_queued", 3), ("last_completion", 4),
+            ("last_wait", 5))}
+    # per schedule, in creation order: post, join, launch, completion relative to the first post
+    per = [[round(float(r[i] - t0) / 1e3, 1) for i in (0, 1, 3, 4, 5)] for r in tl]
+    comm.barrier()
+    for s in scheds:
+        s.delete()
+    comm.finalize()
+    return {"step_us_median": round(statistics.median(ts[2:]) * 1e6, 1), "last_step": rel, "per_sched": per}
+
+
 def cp_create_many(rank, world, n=161, rounds=1):
     """`n` schedules created back to back (the per-tensor wrapper's 161 buckets,
     opt_esgd_solo_imagenet_imbalance.py:85-248), each run for `rounds` rounds, then deleted:
