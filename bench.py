@@ -659,15 +659,18 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
         pipelined()
         fused_step()
     t161 = _timed_steps(comm, chain, steps)
-    l0 = comm.get_config("launches")
+    l0, p0 = comm.get_config("launches"), comm.profile()
     t161p = _timed_steps(comm, pipelined, steps)
     launches = (comm.get_config("launches") - l0) / steps
+    prof = _profile_per_step(p0, comm.profile(), steps)
     breakdown = _step_breakdown_us(scheds)
     # A/B: the same pipelined step with one launch per round (k_round_small), no sharing
     comm.set_config("batch_rounds", 0)
     try:
         pipelined()
+        p0 = comm.profile()
         t161u = _timed_steps(comm, pipelined, steps)
+        prof_u = _profile_per_step(p0, comm.profile(), steps)
         breakdown_u = _step_breakdown_us(scheds)
     finally:
         comm.set_config("batch_rounds", -1)
@@ -682,8 +685,20 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
             "fused_speedup": round(t161 / t1, 2), "steps": steps,
             "rank0_launches_per_pipelined_step": launches,
             "rank0_pipelined_step_us": breakdown,
+            "rank0_progress_thread_per_step": prof,
             "step_ms_161_buckets_pipelined_one_launch_per_round": round(t161u * 1e3, 3),
-            "rank0_pipelined_step_us_one_launch_per_round": breakdown_u}
+            "rank0_pipelined_step_us_one_launch_per_round": breakdown_u,
+            "rank0_progress_thread_per_step_one_launch_per_round": prof_u}
+
+
+def _profile_per_step(p0, p1, steps):
+    """esgd_comm_profile differences per step: busy passes, us inside them, us launching
+    (issue-ring pumps), joins and us joining, launches and us flushing shared launches."""
+    d = {k: (p1[k] - p0[k]) / steps for k in p0}
+    return {"passes": round(d["passes"], 1), "pass_us": round(d["pass_ns"] / 1e3, 1),
+            "launch_us": round(d["launch_ns"] / 1e3, 1), "joins": round(d["joins"], 1),
+            "join_us": round(d["join_ns"] / 1e3, 1), "launches": round(d["launches"], 2),
+            "flush_us": round(d["flush_ns"] / 1e3, 1)}
 
 
 def _step_breakdown_us(scheds):

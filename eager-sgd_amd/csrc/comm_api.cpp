@@ -89,6 +89,14 @@ int esgd_comm_issue_log(uint32_t *sched, uint32_t *round, uint32_t cap, uint32_t
     return engine_issue_log(sched, round, cap, n);
 }
 
+int esgd_comm_profile(uint64_t *out, int n) {
+    ESGD_ARG(out || n <= 0, "esgd_comm_profile: null output");
+    uint64_t v[ESGD_PROFILE_WORDS];
+    engine_profile(v);
+    for (int i = 0; i < n && i < ESGD_PROFILE_WORDS; ++i) out[i] = v[i];
+    return ESGD_SUCCESS;
+}
+
 int esgd_comm_rank(int *rank) {
     ESGD_ARG(rank, "esgd_comm_rank: null pointer");
     *rank = engine_rank();

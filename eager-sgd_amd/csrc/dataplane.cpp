@@ -1030,9 +1030,20 @@ static int batch_flush_locked() {
     return rc;
 }
 
+static std::atomic<uint64_t> g_flush_ns{0};
+
 int dataplane_flush() {
     std::lock_guard<std::mutex> lk(g_batch_mu);
-    return batch_flush_locked();
+    if (g_pend.empty()) return ESGD_SUCCESS;
+    const double t0 = now_s();
+    const int rc = batch_flush_locked();
+    g_flush_ns.fetch_add(uint64_t((now_s() - t0) * 1e9), std::memory_order_relaxed);
+    return rc;
+}
+
+void dataplane_profile(uint64_t *launches, uint64_t *flush_ns) {
+    *launches = g_launches.load(std::memory_order_relaxed);
+    *flush_ns = g_flush_ns.load(std::memory_order_relaxed);
 }
 
 // The round joins the pending launch (its snapshot is already queued on `cs`).

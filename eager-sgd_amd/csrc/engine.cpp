@@ -72,6 +72,9 @@ static bool roctx_on() {
 }
 
 static std::atomic<int> g_active{0};   // schedules with a round in flight or a post pending
+// esgd_comm_profile: written by the thread running progress passes, read by any
+static std::atomic<uint64_t> g_prof_passes{0}, g_prof_pass_ns{0}, g_prof_pump_ns{0}, g_prof_joins{0},
+    g_prof_join_ns{0};
 
 // A process that exits without fffinalize / esgd_comm_finalize must not die in
 // std::thread's destructor: stop and join the progress thread at static destruction.
@@ -500,6 +503,14 @@ static bool step(Sched &s) {
             s.awaiting = posted >= next;
             return false;
         }
+        const uint64_t j0 = mono_ns();
+        struct JoinProf {   // rounds joined and the ns they took (esgd_comm_profile)
+            uint64_t t0;
+            ~JoinProf() {
+                g_prof_joins.fetch_add(1, std::memory_order_relaxed);
+                g_prof_join_ns.fetch_add(mono_ns() - t0, std::memory_order_relaxed);
+            }
+        } join_prof{j0};
         s.cur = next;
         s.cur_fresh = posted >= next;
         s.joined = next;
@@ -624,13 +635,25 @@ int engine_issue_log(uint32_t *sched, uint32_t *round, uint32_t cap, uint32_t *n
     return ESGD_SUCCESS;
 }
 
+void engine_profile(uint64_t out[7]) {
+    out[0] = g_prof_passes.load(std::memory_order_relaxed);
+    out[1] = g_prof_pass_ns.load(std::memory_order_relaxed);
+    out[2] = g_prof_pump_ns.load(std::memory_order_relaxed);
+    out[3] = g_prof_joins.load(std::memory_order_relaxed);
+    out[4] = g_prof_join_ns.load(std::memory_order_relaxed);
+    dataplane_profile(&out[5], &out[6]);
+}
+
 bool engine_progress_once() {
+    const uint64_t p0 = mono_ns();
     std::vector<Sched *> snap;
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         snap = g_reg;
     }
     bool any = pump_tickets(snap);
+    const uint64_t p1 = mono_ns();
+    if (any) g_prof_pump_ns.fetch_add(p1 - p0, std::memory_order_relaxed);
     int active = 0;
     for (Sched *s : snap) {
         while (step(*s)) any = true;   // run a schedule until it has to wait
@@ -641,6 +664,10 @@ bool engine_progress_once() {
     }
     g_active.store(active, std::memory_order_relaxed);
     g_epoch.fetch_add(1, std::memory_order_acq_rel);
+    if (any) {   // idle passes are not counted: they only poll
+        g_prof_passes.fetch_add(1, std::memory_order_relaxed);
+        g_prof_pass_ns.fetch_add(mono_ns() - p0, std::memory_order_relaxed);
+    }
     return any;
 }
 

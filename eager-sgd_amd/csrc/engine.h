@@ -211,6 +211,12 @@ Sched *sched_lookup(uint64_t handle);
 // Issue log: (schedule id, round) in the order this rank launched rounds.
 int engine_issue_log(uint32_t *sched, uint32_t *round, uint32_t cap, uint32_t *n);
 
+// esgd_comm_profile: passes, ns in passes, ns launching, joins, ns joining, launches,
+// ns flushing shared launches
+void engine_profile(uint64_t out[7]);
+// dataplane.cpp: kernel launches of rounds and ns spent flushing shared launches
+void dataplane_profile(uint64_t *launches, uint64_t *flush_ns);
+
 // One polling pass over all schedules (the progress thread calls it in a loop; tests
 // without a thread may call it directly).  Returns true if anything advanced.
 bool engine_progress_once();

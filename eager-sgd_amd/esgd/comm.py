@@ -58,6 +58,7 @@ def _bind(h):
         "esgd_set_config": (i, [C.c_char_p, C.c_int64]),
         "esgd_get_config": (i, [C.c_char_p, C.POINTER(C.c_int64)]),
         "esgd_comm_issue_log": (i, [C.POINTER(u32), C.POINTER(u32), u32, C.POINTER(u32)]),
+        "esgd_comm_profile": (i, [C.POINTER(u64), i]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(h, name)
@@ -148,6 +149,17 @@ def issue_log():
     a = (C.c_uint32 * max(1, cap))(); b = (C.c_uint32 * max(1, cap))()
     check(lib().esgd_comm_issue_log(a, b, cap, C.byref(n)))
     return [(a[i], b[i]) for i in range(min(cap, n.value))]
+
+
+PROFILE_KEYS = ("passes", "pass_ns", "launch_ns", "joins", "join_ns", "launches", "flush_ns")
+
+
+def profile() -> dict:
+    """The progress thread's host-side profile since init (esgd_comm_profile): monotonic
+    counters -- subtract two readings."""
+    v = (C.c_uint64 * len(PROFILE_KEYS))()
+    check(lib().esgd_comm_profile(v, len(PROFILE_KEYS)), "esgd_comm_profile")
+    return dict(zip(PROFILE_KEYS, (int(x) for x in v)))
 
 
 def barrier():

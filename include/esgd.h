@@ -162,6 +162,13 @@ int esgd_get_config(const char *key, int64_t *value);
 /* ordered transports (rccl): (schedule id, round) pairs in the order this rank issued
  * them — identical on every rank by construction (tests). */
 int esgd_comm_issue_log(uint32_t *sched, uint32_t *round, uint32_t cap, uint32_t *n);
+/* Host-side profile of this process's progress thread since init (monotonic counters;
+ * take differences): out[0] passes, [1] ns inside passes, [2] ns launching rounds
+ * (issue-ring pumps, shared launches included), [3] rounds joined, [4] ns joining,
+ * [5] kernel launches of rounds, [6] ns in those launches' flushes (k_round_batch).
+ * Fills min(n, 7) values. */
+#define ESGD_PROFILE_WORDS 7
+int esgd_comm_profile(uint64_t *out, int n);
 
 /* ---- persistent partial-allreduce schedules ----
  * kind: ESGD_SCHED_ALLREDUCE (every round synchronous, src/colls/ffallreduce.c),
