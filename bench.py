@@ -724,6 +724,61 @@ def _step_breakdown_us(scheds):
             "gpu_us_per_bucket": round(float(tl[:, 4].max() - tl[:, 2].min()) / 1e3 / len(tl), 2)}
 
 
+def optimizer_resnet50_161(comm, rank, world, steps=8):
+    """The drop-in caller path at C4's shape: EagerSGDOptimizer (majority, the reference's
+    seed) over 161 torch parameters with the ResNet-50 bucket lengths
+    (opt_esgd_majority_imagenet_imbalance.py:6-44; tests/golden/resnet50_buckets.json), the
+    gradients already on the device; one step = apply_gradients() (copy-in with the /P,
+    the rounds, the copy-out, the wrapped SGD step), max over ranks.  Per tensor pipelined
+    (the default; shared launches on and off), per tensor blocking (the reference's chain),
+    fused."""
+    import torch
+
+    import ctypes as C
+
+    from esgd._lib import check, lib
+    from esgd.optim import EagerSGDOptimizer
+    with open(os.path.join(ROOT, "tests", "golden", "resnet50_buckets.json")) as f:
+        lengths = json.load(f)["lengths"]
+    d = C.c_int()
+    check(lib().esgd_get_device(C.byref(d)))
+    torch.cuda.set_device(d.value)   # the rank's GPU (esgd_set_device chose it)
+    dev_t = torch.device("cuda", d.value)
+    gen = torch.Generator(device=dev_t)
+    gen.manual_seed(SEED + rank)
+    out = {}
+    opts = []
+    for name, kw in (("per_tensor_pipelined", dict(fuse=False)), ("per_tensor_blocking", dict(pipeline=False)),
+                     ("fused", dict(fuse=True))):
+        params = [torch.zeros(n, device=dev_t, requires_grad=True) for n in lengths]
+        for p in params:
+            p.grad = torch.rand(p.numel(), device=dev_t, generator=gen) - 0.5
+        opt = EagerSGDOptimizer(torch.optim.SGD(params, lr=1e-3), world, mode="majority", **kw)
+        opts.append(opt)
+
+        def step():
+            opt.step()
+            torch.cuda.synchronize()
+
+        step()   # creates the ops' schedules (collective, first step)
+        step()
+        out[name + "_ms"] = round(_timed_steps(comm, step, steps) * 1e3, 3)
+        if name == "per_tensor_pipelined":
+            comm.set_config("batch_rounds", 0)
+            try:
+                step()
+                out[name + "_one_launch_per_round_ms"] = round(_timed_steps(comm, step, steps) * 1e3, 3)
+            finally:
+                comm.set_config("batch_rounds", -1)
+    _OPTS.extend(opts)   # their schedules stay alive until the end, like every leg's
+    out["tensors"] = len(lengths)
+    out["steps"] = steps
+    return out
+
+
+_OPTS = []
+
+
 def c3_over_rccl(comm, dev, rank, world, count, steps=20):
     """C3 (solo-allreduce, 256 MiB per rank) through the RCCL transport: grouped
     ncclSend/ncclRecv over xGMI, arrived chunks folded by the tree kernel on a side
@@ -1222,6 +1277,7 @@ def run_allreduce(args, rank, world):
                 ("small_round_after_idle", lambda: small_round_after_idle(comm, dev, rank, world)),
                 ("straggler_c4_majority", lambda: straggler_c4(comm, dev, rank, world)),
                 ("c4_resnet50_161_vs_fused", lambda: c4_resnet50_161(comm, dev, rank, world)),
+                ("optimizer_resnet50_161", lambda: optimizer_resnet50_161(comm, rank, world)),
                 ("c3_host_buckets", lambda: c3_host_buckets(comm, dev, rank, world,
                                                                   int(args.bucket_mib * MiB) // 4))]
         if os.environ.get("ESGD_BENCH_RCCL", "1") == "1":

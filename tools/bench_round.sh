@@ -17,8 +17,8 @@ for s in $STEPS; do
       cp -r gpurun_out/bench_kernel_trace_split.json $O/ 2>/dev/null || true ;;
   n2) timeout -k 10 600 python bench.py --gpus 2 --steps 20 --warmup 5 > $O/bench_n2.json 2> $O/bench_n2.err ;;
   n4) timeout -k 10 600 python bench.py --gpus 4 --steps 20 --warmup 5 > $O/bench_n4.json 2> $O/bench_n4.err ;;
-  n2c4|n4c4) n=${s:1:1}   # the headline N > 1 line plus only the 161-bucket leg
-      ESGD_BENCH_LEGS=c4_resnet50_161_vs_fused ESGD_BENCH_RCCL=0 timeout -k 10 300 python bench.py --gpus $n \
+  n2c4|n4c4) n=${s:1:1}   # the headline N > 1 line plus only the 161-bucket legs
+      ESGD_BENCH_LEGS=c4_resnet50_161_vs_fused,optimizer_resnet50_161 ESGD_BENCH_RCCL=0 timeout -k 10 300 python bench.py --gpus $n \
           --steps 20 --warmup 5 > $O/bench_n${n}_c4.json 2> $O/bench_n${n}_c4.err ;;
   prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run \
           --output-format csv -- python $R/bench.py --no-pmc --no-trace --no-cpu-baseline --steps 100 \
