@@ -322,6 +322,10 @@ int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_
         std::lock_guard<std::mutex> lk(g_mu);
         if (int rc = find(&c)) return rc;
         if (c->exported) return give(c);
+        if (c->unexportable) {   // refused once: refused for every block it holds, no new call
+            set_error("arena: chunk %p was refused for IPC export", static_cast<void *>(c->base));
+            return ESGD_INVALID_ARG;
+        }
     }
     std::lock_guard<std::mutex> xk(g_export_mu);
     {

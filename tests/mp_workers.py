@@ -173,7 +173,8 @@ def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0
 
 def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0, buf="device",
                   in_place=False, transport="ipc", shadow_ranks=(), small_bytes=None,
-                  piece_bytes=None, host_chunk=None, device_flags=None, wire=False, chunk_kernel=None):
+                  piece_bytes=None, host_chunk=None, device_flags=None, wire=False, chunk_kernel=None,
+                  fail_exports=None, batch=None):
     """Data plane on the GPU: every rank reduces its splitmix bucket; returns the
     result bytes' digest per round plus a bit-exactness verdict against the oracle.
     shadow_ranks: ranks whose device buckets go through the owned shadow bucket.
@@ -185,6 +186,10 @@ def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0
 
     if rank in shadow_ranks:
         os.environ["ESGD_SHADOW"] = "1"
+    if fail_exports is not None and fail_exports[rank]:   # this rank's first N chunk exports fail
+        os.environ["ESGD_FAIL_EXPORTS"] = str(fail_exports[rank])
+    if batch is not None:
+        os.environ["ESGD_BATCH_ROUNDS"] = str(batch)
     if small_bytes is not None:
         os.environ["ESGD_SMALL_ROUND_BYTES"] = str(small_bytes)
     if piece_bytes is not None:
@@ -1078,6 +1083,67 @@ def gpu_stress_fresh(rank, world, kind, count, rounds=600, async_=3, seed=344956
     s.delete()
     comm.finalize()
     return out
+
+
+def gpu_stress_pipelined(rank, world, kind, counts=(4096, 65536, 17, (1 << 20) + 3, 300007, 1025, 65536 * 3,
+                                                  (5 << 20) + 1), rounds=150, async_=3, seed=34495645,
+                         jitter_us=200, batch=None):
+    """The optimizer's pipelined per-tensor order under the activation stress: HOLD |
+    FRESH_ONLY schedules (how the deep500 op drives them), every step writes each
+    schedule's send bucket in the wrapper's racy order (after the release, right before
+    the post) and posts ALL of them, then waits for all, reads and releases -- so many
+    rounds of different schedules come due together (shared k_round_batch launches, cut
+    differently on every rank, one five-launch size among them) while peers' activations
+    carry ranks through rounds they have not posted.  A rank's share of every round must
+    be its tag iff it had posted the round before joining it, never torn.  batch: rounds
+    per shared launch for this rank (a list: one value per rank)."""
+    import random
+
+    import numpy as np
+
+    from esgd import _lib
+    from esgd import device as dev
+    comm = _comm()
+    if batch is not None:
+        comm.set_config("batch_rounds", batch[rank] if isinstance(batch, (list, tuple)) else batch)
+    bits = min(10, 31 // world)
+    scheds = []
+    for i, n in enumerate(counts):
+        sb, rb = dev.DeviceBuffer(n, _lib.INT32), dev.DeviceBuffer(n, _lib.INT32)
+        rb.zero()
+        s = comm.Schedule(kind, sb, rb, n, dtype=_lib.INT32, async_=async_, seed=seed + i,
+                          buf=comm.BUF_DEVICE, flags=comm.HOLD | comm.FRESH_ONLY)
+        scheds.append((s, sb, rb, n))
+    dev.synchronize()
+    rng = random.Random(4000 + rank)
+    vals = [[] for _ in scheds]
+    fresh = [[] for _ in scheds]
+    torn = []
+    comm.barrier()
+    for t in range(1, rounds + 1):
+        v = (t % (1 << bits)) << (bits * rank)
+        for s, sb, rb, n in scheds:
+            if rng.random() < 0.3:
+                time.sleep(rng.random() * jitter_us * 1e-6)
+            sb.upload(np.full(n, v, np.int32))
+            s.post()
+        for i, (s, sb, rb, n) in enumerate(scheds):
+            fresh[i].append(s.wait())
+            m = min(n, 1024)
+            head, tail = _download_slice(rb, 0, m), _download_slice(rb, n - m, m)
+            vals[i].append(int(head[0]))
+            if not (np.all(head == head[0]) and np.all(tail == head[0])):
+                torn.append((i, t))
+            s.release()
+    comm.barrier()
+    autos = sum(s.stats()["auto_rounds"] for s, *_ in scheds)
+    launches = comm.get_config("launches")
+    for s, *_ in scheds:
+        s.delete()
+    comm.set_config("batch_rounds", -1)
+    comm.finalize()
+    return {"vals": vals, "fresh": fresh, "torn": torn[:10], "bits": bits, "auto_rounds": autos,
+            "launches": launches}
 
 
 def cp_peer_lost(rank, world, stall_s=5.0):

@@ -216,6 +216,28 @@ def test_shadowed_device_buckets(in_place):
     assert all(all(v) for v in verdicts), verdicts
 
 
+@pytest.mark.parametrize("count", [1, 17, 4099])
+def test_shadowed_rank_beside_batched_ranks(count):
+    # a shadowed rank's one-launch rounds go out one per launch (k_round_small + copy-out)
+    # while its peers' go out in shared launches (k_round_batch): the same flags, the same
+    # bits; tiny buckets leave a rank with an empty shard
+    for world, shadow in ((2, (0,)), (2, (1,)), (3, (1,))):
+        verdicts = run("gpu_allreduce", world, count=count, rounds=3, shadow_ranks=shadow)
+        assert all(all(v) for v in verdicts), (world, shadow, verdicts)
+
+
+@pytest.mark.parametrize("batch", [None, 0])
+@pytest.mark.parametrize("count", [1, 17, 4099])
+def test_refused_export_on_one_rank(count, batch):
+    # the runtime refused a fresh process's first chunk export on ONE rank (round 4, r04d:
+    # count 1 at P = 2 then came out wrong on both ranks); ESGD_FAIL_EXPORTS on that rank
+    # only: its published shard moves to a fresh chunk and its bucket is shadowed, while
+    # the peer's rounds stay batched
+    for fails in ((1, 0), (2, 0), (0, 2)):
+        verdicts = run("gpu_allreduce", 2, count=count, rounds=3, fail_exports=fails, batch=batch)
+        assert all(all(v) for v in verdicts), (fails, verdicts)
+
+
 # ---- BASELINE.json's workloads (C1, C3, C4, C5) at their full sizes -----------------
 # Every rank writes its bucket before a barrier and posts (the pattern of
 # evaluation/{solo,rand}_allreduce_correctness.c:76-97): solo / majority rounds then
@@ -469,6 +491,27 @@ def test_fresh_only_stress(kind, case):
             want = t % (1 << bits) if outs[q]["fresh"][t - 1] else 0
             assert share == want, (t, q, share, want, [o["fresh"][t - 1] for o in outs])
     assert sum(o["stats"]["auto_rounds"] for o in outs) > 0
+
+
+@pytest.mark.parametrize("world,batch", [(3, None), (4, [64, 0, 5, 2]), (8, None)])
+@pytest.mark.parametrize("kind", [SOLO, MAJORITY])
+def test_pipelined_stress_batched(kind, world, batch):
+    # eight HOLD | FRESH_ONLY schedules posted all at once every step under random delays
+    # (shared launches of rounds that peers' activations make due in different orders,
+    # one five-launch size among them); a rank's share is its tag iff it had posted the
+    # round, never torn, the same bits on every rank
+    outs = run("gpu_stress_pipelined", world, kind=kind, rounds=120, batch=batch, timeout=400)
+    bits = outs[0]["bits"]
+    for o in outs:
+        assert not o["torn"], o["torn"]
+        assert o["vals"] == outs[0]["vals"]
+    for i in range(len(outs[0]["vals"])):
+        for t in range(1, len(outs[0]["vals"][i]) + 1):
+            v = outs[0]["vals"][i][t - 1]
+            for q in range(world):
+                want = t % (1 << bits) if outs[q]["fresh"][i][t - 1] else 0
+                assert (v >> (bits * q)) & ((1 << bits) - 1) == want, (i, t, q)
+    assert sum(o["auto_rounds"] for o in outs) > 0
 
 
 @pytest.mark.parametrize("kind", [SOLO, MAJORITY])
