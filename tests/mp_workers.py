@@ -1451,6 +1451,39 @@ def gpu_many(rank, world, specs, rounds=3, batch=None, small_bytes=None, strict=
     return {"bad": bad, "launches": launches, "rounds": rounds * len(specs)}
 
 
+def gpu_va_reuse(rank, world, value, count=4099, ready_file=None, hold_file=None, rounds=2):
+    """One job of tools/va_reuse_probe.py: every rank allocates its bucket (the first arena
+    chunk of a fresh process), exports it through an allreduce schedule, checks the sum,
+    and reports the bucket's VA.  ready_file: touched (".<rank>") once the rounds are done;
+    hold_file: the job does not finalize (its exports and its peers' mappings stay alive)
+    until that file exists -- so a second job can export the same VAs meanwhile."""
+    import numpy as np
+
+    from esgd import device as dev
+    comm = _comm()
+    rb = dev.DeviceBuffer(count)
+    s = comm.Schedule(comm.ALLREDUCE, None, rb, count, buf=comm.BUF_DEVICE)
+    ok = []
+    for t in range(rounds):
+        rb.upload(np.full(count, float(value + rank + t), np.float32))
+        comm.barrier()
+        s.post()
+        s.wait()
+        got = rb.download()
+        want = np.float32(sum(float(value + q + t) for q in range(world)))
+        ok.append(int(np.count_nonzero(got != want)))
+        comm.barrier()
+    if ready_file:
+        open(f"{ready_file}.{rank}", "w").close()
+    if hold_file:
+        t0 = time.time()
+        while not os.path.exists(hold_file) and time.time() - t0 < 120:
+            time.sleep(0.05)
+    s.delete()
+    comm.finalize()
+    return {"rank": rank, "pid": os.getpid(), "va": hex(rb.ptr), "bad_elements": ok}
+
+
 def gpu_reinit(rank, world, count=4099):
     """A finalized job that mapped its peers' buckets must refuse a second multi-process
     job in the same process (re-opening closed IPC handles: DESIGN.md §5)."""
