@@ -132,6 +132,7 @@ int engine_init(const char *job, int rank, int world, bool start_progress) {
         g_running.store(true);
         g_thread = std::thread(progress_main);
     }
+    if (world > 1 && g_device >= 0) arena_warm();   // before any bucket of the job is exported
     return ESGD_SUCCESS;
 }
 

@@ -68,6 +68,9 @@ bool arena_unexportable(const void *p);   // p's chunk: the runtime refused its 
 void arena_stats(uint64_t *reserved, uint64_t *live, uint64_t *exported);
 int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_t handle[64]);
 void arena_trim();
+// a multi-process job's first export: one chunk exported (or quarantined if refused)
+// before its buckets are allocated
+void arena_warm();
 
 }  // namespace esgd
 

@@ -10,10 +10,16 @@ cd /tmp && export TMPDIR=/tmp
 P1="TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_UTCL1_PERMISSION_MISS_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE"
 P2="TCP_UTCL1_STALL_INFLIGHT_MAX_sum TCP_UTCL1_STALL_MULTI_MISS_sum TCP_UTCL1_SERIALIZATION_STALL_sum TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum"
 P3="TCP_UTCL1_STALL_LFIFO_NO_RES_sum TCP_UTCL1_LFIFO_FULL_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCP_CLIENT_UTCL1_INFLIGHT_sum"
+# memory side (passes 7, 8): read / write requests and their in-flight sums (average
+# latency = LEVEL / requests), DRAM-credit stalls
+P7="TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_LEVEL_sum TCC_EA0_WRREQ_sum"
+P8="TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_EA0_WRREQ_STALL_sum TCC_EA0_RDREQ_DRAM_sum"
+# TLB_PASSES="7 8" runs only those passes (the numbering of the full list is kept)
 for mib in 256 1024; do
   i=0
-  for pass in "$P1" "$P2" "$P3" FETCH_SIZE WRITE_SIZE trace; do
+  for pass in "$P1" "$P2" "$P3" FETCH_SIZE WRITE_SIZE trace "$P7" "$P8"; do
     i=$((i + 1))
+    if [ -n "$TLB_PASSES" ] && ! echo " $TLB_PASSES " | grep -q " $i "; then continue; fi
     d=$R/$O/${mib}MiB_p$i
     if [ "$pass" = trace ]; then
       timeout -s KILL 150 rocprofv3 --kernel-trace --output-format csv -d $d -o kt -- \

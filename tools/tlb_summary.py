@@ -28,7 +28,7 @@ def main(o):
     for mib in (256, 1024):
         algo = 9 * mib * (1 << 20)
         ent = {"algo_bytes_per_call": algo, "counters_per_call": {}, "per_GiB": {}}
-        for p in range(1, 6):
+        for p in (1, 2, 3, 4, 5, 7, 8):
             d = os.path.join(o, f"{mib}MiB_p{p}")
             acc = {}
             for r in rows(d, "*counter_collection.csv"):
@@ -54,6 +54,11 @@ def main(o):
             # window position within a call: median over calls
             ent["window_us_by_position"] = [round(statistics.median(durs[i * w + j] for i in range(CALLS)), 1)
                                             for j in range(w)]
+        c = ent["counters_per_call"]
+        for kind in ("RD", "WR"):   # average requests in flight / latency proxy per request
+            lv, rq = c.get(f"TCC_EA0_{kind}REQ_LEVEL_sum"), c.get(f"TCC_EA0_{kind}REQ_sum")
+            if lv and rq:
+                ent[f"ea_{kind.lower()}_level_per_request"] = round(lv / rq, 1)
         res[f"{mib}MiB"] = ent
     miss = {k: res[k]["per_GiB"].get("TCP_UTCL1_TRANSLATION_MISS_sum") for k in res}
     res["utcl1_miss_per_GiB_ratio_1024_over_256"] = (miss["1024MiB"] / miss["256MiB"]
