@@ -127,6 +127,30 @@ int esgd_schedule_post(esgd_sched_h h, void *producer_stream, int *role) {
     return sched_post(s, producer_stream, role);
 }
 
+int esgd_schedule_post_group(const esgd_sched_h *hs, int n, void *producer_stream, int *roles) {
+    ESGD_ARG(n >= 0 && (n == 0 || hs), "esgd_schedule_post_group: bad arguments");
+    dataplane_group_begin(0, producer_stream);
+    int rc = ESGD_SUCCESS;
+    for (int i = 0; i < n && !rc; ++i) {
+        Sched *s = handle_to_sched(hs[i]);
+        rc = s ? sched_post(s, producer_stream, roles ? &roles[i] : nullptr) : ESGD_INVALID_ARG;
+    }
+    dataplane_group_end(0);
+    return rc;
+}
+
+int esgd_schedule_release_group(const esgd_sched_h *hs, int n, void *stream) {
+    ESGD_ARG(n >= 0 && (n == 0 || hs), "esgd_schedule_release_group: bad arguments");
+    dataplane_group_begin(1, stream);
+    int rc = ESGD_SUCCESS;
+    for (int i = 0; i < n && !rc; ++i) {
+        Sched *s = handle_to_sched(hs[i]);
+        rc = s ? sched_release(s, stream) : ESGD_INVALID_ARG;
+    }
+    dataplane_group_end(1);
+    return rc;
+}
+
 int esgd_schedule_wait(esgd_sched_h h) {
     Sched *s = handle_to_sched(h);
     if (!s) return ESGD_INVALID_ARG;

@@ -527,10 +527,11 @@ struct BaseState {
     int batch_rc = 0;                 // the shared launch of this round failed (its status)
     std::vector<char *> retired;      // grown-out buckets: peers may still map them
     uint64_t off[kMaxRanks] = {}, len[kMaxRanks] = {};   // elements
-    std::map<uint32_t, hipEvent_t> producer;
-    std::vector<hipEvent_t> spare;
+    // events from the process-wide pool (pooled_event); one recording may be shared by a
+    // group of posts / releases (esgd_schedule_post_group / _release_group)
+    std::map<uint32_t, std::shared_ptr<hipEvent_t>> producer;
     // hold mode: the caller's last reads of rb / writes of sb (esgd_schedule_release)
-    hipEvent_t consumer = nullptr;
+    std::shared_ptr<hipEvent_t> consumer;
     bool consumer_pending = false;
     virtual ~BaseState() {}
 };
@@ -567,6 +568,11 @@ struct IpcState : BaseState {
     PeerMap rbmap[kMaxRanks], pubmap[kMaxRanks];
     // batched one-launch rounds: this schedule's BatchDesc is in the device table
     bool desc_built = false;
+    // the round's snapshot, deferred into the shared launch's copy kernel (k_copy_many):
+    // rb_dev = snap_src (nullptr: zeros), snap_bytes bytes
+    bool snap = false;
+    const void *snap_src = nullptr;
+    size_t snap_bytes = 0;
     uint32_t t1 = 0, t2 = 0;          // its phase-1 / phase-2 tiles
 };
 
@@ -632,21 +638,105 @@ static int base_setup(Sched &s, BaseState &st) {
     return ESGD_SUCCESS;
 }
 
+static std::mutex g_evfree_mu;
+static std::vector<hipEvent_t> g_evfree;   // pooled events no round refers to any more
+
+// ---- events: a process-wide pool, and recordings shared by a group of schedules ----
+// A producer (consumer) event marks where the caller's stream stands at a post (release).
+// esgd_schedule_post_group / _release_group record ONE event for all the schedules they
+// name (dataplane_group_begin/end: this thread's posts / releases on that stream use it),
+// and the round stream waits for a recording once however many rounds refer to it.
+static std::shared_ptr<hipEvent_t> pooled_event() {
+    hipEvent_t e = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_evfree_mu);
+        if (!g_evfree.empty()) { e = g_evfree.back(); g_evfree.pop_back(); }
+    }
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+        (void)hip_fail(hipGetLastError(), "hipEventCreateWithFlags", __FILE__, __LINE__);
+        return nullptr;
+    }
+    return std::shared_ptr<hipEvent_t>(new hipEvent_t(e), [](hipEvent_t *p) {
+        std::lock_guard<std::mutex> lk(g_evfree_mu);
+        g_evfree.push_back(*p);
+        delete p;
+    });
+}
+
+static hipStream_t user_stream(void *stream) {   // ESGD_STREAM_NULL names the legacy default stream
+    return stream == ESGD_STREAM_NULL ? nullptr : static_cast<hipStream_t>(stream);
+}
+
+struct GroupEvent {   // this thread's open group: [0] posts, [1] releases
+    bool open = false;
+    void *stream = nullptr;
+    std::shared_ptr<hipEvent_t> ev;
+};
+static thread_local GroupEvent g_group[2];
+
+int dataplane_group_begin(int which, void *stream) {
+    GroupEvent &g = g_group[which];
+    g.open = true;
+    g.stream = stream;
+    g.ev.reset();   // recorded by the group's first schedule that needs it
+    return ESGD_SUCCESS;
+}
+
+void dataplane_group_end(int which) {
+    g_group[which].open = false;
+    g_group[which].ev.reset();
+}
+
+// the event of a post (which 0) or release (1) on `stream`: the open group's recording,
+// or a new one
+static int note_event(int which, void *stream, std::shared_ptr<hipEvent_t> *out) {
+    GroupEvent &g = g_group[which];
+    if (g.open && g.stream == stream && g.ev) {
+        *out = g.ev;
+        return ESGD_SUCCESS;
+    }
+    std::shared_ptr<hipEvent_t> ev = pooled_event();
+    if (!ev) return ESGD_ERROR;
+    ESGD_HIP(hipEventRecord(*ev, user_stream(stream)));
+    if (g.open && g.stream == stream) g.ev = ev;
+    *out = ev;
+    return ESGD_SUCCESS;
+}
+
+// cs waits for ev -- once per recording: a later wait on the same recording is implied
+// by stream order (the progress thread queues every wait on the round / copy streams)
+static struct {
+    hipStream_t s;
+    std::shared_ptr<hipEvent_t> ev;
+} g_waited[4];
+
+static int stream_wait(hipStream_t cs, const std::shared_ptr<hipEvent_t> &ev) {
+    int slot = -1;
+    for (int i = 0; i < 4; ++i) {
+        if (g_waited[i].s == cs) {
+            if (g_waited[i].ev == ev) return ESGD_SUCCESS;
+            slot = i;
+            break;
+        }
+        if (!g_waited[i].s && slot < 0) slot = i;
+    }
+    ESGD_HIP(hipStreamWaitEvent(cs, *ev, 0));
+    if (slot >= 0) {
+        g_waited[slot].s = cs;
+        g_waited[slot].ev = ev;
+    }
+    return ESGD_SUCCESS;
+}
+
 static int base_note_producer(BaseState &st, uint32_t round, void *stream) {
-    hipEvent_t e;
-    if (!st.spare.empty()) { e = st.spare.back(); st.spare.pop_back(); }
-    else ESGD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    // ESGD_STREAM_NULL names the legacy default stream (records on stream 0)
-    hipStream_t ps = stream == ESGD_STREAM_NULL ? nullptr : static_cast<hipStream_t>(stream);
-    ESGD_HIP(hipEventRecord(e, ps));
-    st.producer[round] = e;
+    std::shared_ptr<hipEvent_t> ev;
+    if (int rc = note_event(0, stream, &ev)) return rc;
+    st.producer[round] = std::move(ev);
     return ESGD_SUCCESS;
 }
 
 static int base_note_consumer(BaseState &st, void *stream) {
-    if (!st.consumer) ESGD_HIP(hipEventCreateWithFlags(&st.consumer, hipEventDisableTiming));
-    hipStream_t cs = stream == ESGD_STREAM_NULL ? nullptr : static_cast<hipStream_t>(stream);
-    ESGD_HIP(hipEventRecord(st.consumer, cs));
+    if (int rc = note_event(1, stream, &st.consumer)) return rc;
     st.consumer_pending = true;
     return ESGD_SUCCESS;
 }
@@ -655,7 +745,7 @@ static int base_note_consumer(BaseState &st, void *stream) {
 // previous round (and its zeroing of sb) has finished -- fresh round or not
 static int consumer_wait(BaseState &st, hipStream_t cs) {
     if (st.consumer_pending) {
-        ESGD_HIP(hipStreamWaitEvent(cs, st.consumer, 0));
+        if (int rc = stream_wait(cs, st.consumer)) return rc;
         st.consumer_pending = false;
     }
     return ESGD_SUCCESS;
@@ -754,8 +844,9 @@ static int base_prepare(Sched &s, BaseState &st, bool fresh) {
 // finished, then the move sb -> rb (host -> HBM for host buckets)
 static int producer_wait(BaseState &st, uint32_t round, bool fresh, hipStream_t cs) {
     for (auto it = st.producer.begin(); it != st.producer.end();) {
-        if (it->first == round && fresh) ESGD_HIP(hipStreamWaitEvent(cs, it->second, 0));
-        if (it->first <= round) { st.spare.push_back(it->second); it = st.producer.erase(it); }
+        if (it->first == round && fresh)
+            if (int rc = stream_wait(cs, it->second)) return rc;
+        if (it->first <= round) it = st.producer.erase(it);
         else ++it;
     }
     return ESGD_SUCCESS;
@@ -887,9 +978,8 @@ static void base_teardown(Sched &s, BaseState &st) {
     if (st.owns_rb) free_bucket(st.rb_dev);
     if (st.reg_rb) hip_ignore(hipHostUnregister(s.rb));
     if (st.reg_sb) hip_ignore(hipHostUnregister(s.sb));
-    for (auto &kv : st.producer) hip_ignore(hipEventDestroy(kv.second));
-    for (hipEvent_t e : st.spare) hip_ignore(hipEventDestroy(e));
-    if (st.consumer) hip_ignore(hipEventDestroy(st.consumer));
+    st.producer.clear();   // pooled events go back to the pool
+    st.consumer.reset();
     if (st.pin) hip_ignore(hipHostFree(st.pin));
     for (char *p : st.retired) free_bucket(p);
     if (st.ev) hip_ignore(hipEventDestroy(st.ev));
@@ -901,7 +991,7 @@ static void base_teardown(Sched &s, BaseState &st) {
 // stream and appends the round here; the engine flushes at the end of every pump of the
 // issue ring, and every other launch on the round stream flushes first, so the stream
 // still holds the rounds in ring order (the deadlock argument of DESIGN.md §5).
-static std::mutex g_batch_mu, g_evfree_mu;
+static std::mutex g_batch_mu;
 static BatchDesc *g_desc_dev = nullptr, *g_desc_host = nullptr;   // [kMaxSched], by schedule id
 struct BatchEntry {
     Sched *s;
@@ -909,7 +999,7 @@ struct BatchEntry {
     uint32_t round;
 };
 static std::vector<BatchEntry> g_pend;
-static std::vector<hipEvent_t> g_evfree;   // events of launches no round refers to any more
+static CopySet g_copy;   // the pending launch's snapshots (nseg 0: none)
 
 // this schedule's BatchDesc: built at its first batched round and uploaded on the round
 // stream (ahead of the launch that reads it); its buckets, peers' mappings and flags never
@@ -1002,25 +1092,19 @@ static int batch_flush_locked() {
     const int cap = round_batch_capacity(g_pend[0].s->dtype, g_pend[0].s->world) / ranks_on_my_device() - 1;
     workers = std::max(1u, std::min<unsigned>(workers, unsigned(std::max(1, cap))));
     hipStream_t cs = g_pend[0].st->stream;
-    int rc = round_batch(g_pend[0].s->dtype, g_pend[0].s->world, a, workers, cs);
-    hipEvent_t ev = nullptr;
-    if (!rc) {
-        {
-            std::lock_guard<std::mutex> lk(g_evfree_mu);
-            if (!g_evfree.empty()) { ev = g_evfree.back(); g_evfree.pop_back(); }
-        }
-        if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
-            rc = hip_fail(hipGetLastError(), "hipEventCreateWithFlags", __FILE__, __LINE__);
-        if (!rc && hipEventRecord(ev, cs) != hipSuccess)
-            rc = hip_fail(hipGetLastError(), "hipEventRecord", __FILE__, __LINE__);
+    int rc = ESGD_SUCCESS;
+    if (g_copy.nseg) {   // every entry's snapshot, before the launch that publishes its ready
+        rc = copy_many(g_copy, cs);
+        g_copy.nseg = 0;
+        if (!rc) ++g_launches;
     }
+    if (!rc) rc = round_batch(g_pend[0].s->dtype, g_pend[0].s->world, a, workers, cs);
     std::shared_ptr<hipEvent_t> sp;
-    if (!rc)
-        sp = std::shared_ptr<hipEvent_t>(new hipEvent_t(ev), [](hipEvent_t *p) {
-            std::lock_guard<std::mutex> lk(g_evfree_mu);
-            g_evfree.push_back(*p);
-            delete p;
-        });
+    if (!rc) {
+        sp = pooled_event();
+        if (!sp) rc = ESGD_ERROR;
+        else if (hipEventRecord(*sp, cs) != hipSuccess) rc = hip_fail(hipGetLastError(), "hipEventRecord", __FILE__, __LINE__);
+    }
     for (BatchEntry &b : g_pend) {
         b.st->batch_ev = sp;
         b.st->batch_rc = rc;
@@ -1046,13 +1130,53 @@ void dataplane_profile(uint64_t *launches, uint64_t *flush_ns) {
     *flush_ns = g_flush_ns.load(std::memory_order_relaxed);
 }
 
-// The round joins the pending launch (its snapshot is already queued on `cs`).
+// The snapshot of a round that goes out in a shared launch: the caller's producer and
+// consumer events are waited for now, on the round stream; the copy itself (rb = sb, or
+// rb = 0 for a FRESH_ONLY round this rank had not posted) joins the launch's k_copy_many
+// when the buckets are 16-B aligned and the copy fits the 32-bit descriptor range (else
+// it is queued now, as base_copy_in would).
+static int batch_snapshot(Sched &s, IpcState &st, uint32_t round, bool fresh, hipStream_t cs) {
+    if (int rc = consumer_wait(st, cs)) return rc;
+    if (int rc = producer_wait(st, round, fresh, cs)) return rc;
+    st.snap = false;
+    const size_t bytes = s.count * s.esize;
+    if (!bytes || s.zero_sb) return s.zero_sb && bytes ? move_zero(st.rb_dev, s.sb, bytes, cs) : ESGD_SUCCESS;
+    const void *src = nullptr;
+    if (s.fresh_only && !fresh) src = nullptr;            // contributes zeros, sb unread
+    else if (!s.in_place) src = s.sb;
+    else return ESGD_SUCCESS;                              // in place: nothing to move
+    const uintptr_t al = reinterpret_cast<uintptr_t>(st.rb_dev) | reinterpret_cast<uintptr_t>(src);
+    if ((al & 15) || bytes >= (size_t(1) << 31)) {   // (a launch holds as many copies as rounds: <= kBatchMax)
+        if (!src) ESGD_HIP(hipMemsetAsync(st.rb_dev, 0, bytes, cs));
+        else ESGD_HIP(hipMemcpyAsync(st.rb_dev, src, bytes, hipMemcpyDeviceToDevice, cs));
+        return ESGD_SUCCESS;
+    }
+    st.snap = true;
+    st.snap_src = src;
+    st.snap_bytes = bytes;
+    return ESGD_SUCCESS;
+}
+
+// The round joins the pending launch (its snapshot is queued on `cs` or deferred into the
+// launch's copy kernel).
 static int batch_append(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) {
     std::lock_guard<std::mutex> lk(g_batch_mu);
     if (!g_pend.empty() && (g_pend[0].s->dtype != s.dtype || g_pend[0].s->world != s.world ||
                             int64_t(g_pend.size()) >= batch_rounds()))
         batch_flush_locked();   // a failure is recorded in the rounds of that launch
     if (int rc = batch_desc(s, st, cs)) return rc;
+    if (st.snap) {
+        CopySet &c = g_copy;
+        if (c.nseg == 0) c.tile0[0] = 0;
+        const int i = c.nseg++;
+        c.src[i] = st.snap_src;
+        c.dst[i] = st.rb_dev;
+        c.nvec[i] = uint32_t(st.snap_bytes / 16);
+        c.tail[i] = uint32_t(st.snap_bytes % 16);
+        const uint32_t tiles = (c.nvec[i] + 1023) / 1024 + (c.nvec[i] == 0 && c.tail[i] ? 1 : 0);
+        c.tile0[i + 1] = c.tile0[i] + tiles;
+        st.snap = false;
+    }
     st.pub_round = round;
     st.fin_mode = true;
     st.batch_rc = 0;
@@ -1063,6 +1187,10 @@ static int batch_append(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) 
 static void batch_shutdown() {
     std::lock_guard<std::mutex> lk(g_batch_mu);
     (void)batch_flush_locked();
+    for (auto &w : g_waited) {   // their events go back to the pool before it is emptied
+        w.s = nullptr;
+        w.ev.reset();
+    }
     if (g_desc_dev) { hip_ignore(hipFree(g_desc_dev)); g_desc_dev = nullptr; }
     if (g_desc_host) { hip_ignore(hipHostFree(g_desc_host)); g_desc_host = nullptr; }
     std::lock_guard<std::mutex> ek(g_evfree_mu);
@@ -1296,6 +1424,8 @@ struct IpcTransport final : Transport {
             // in place, -> wire copy); rb is entirely rewritten by the two phases
             if (int rc = consumer_wait(st, cs)) return rc;
             if (int rc = producer_wait(st, round, fresh, cs)) return rc;
+        } else if (batch) {
+            if (int rc = batch_snapshot(s, st, round, fresh, cs)) return rc;
         } else if (int rc = base_copy_in(s, st, round, fresh, cs)) {
             return rc;
         }

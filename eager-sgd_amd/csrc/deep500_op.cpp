@@ -33,6 +33,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 #include <mutex>
 #include <string>
 
@@ -353,6 +354,67 @@ int allreducef_forward_cuda_wait(void *handle, float *output, void *stream) {
     op->pending = false;
     hipStream_t s = static_cast<hipStream_t>(stream);
     return op->finish_round(s, [&]() -> int { return cuda_copy_out(op, output, s); });
+}
+
+int allreducef_forward_cuda_post_many(void *const *handles, int n, const float *const *inputs, float divisor,
+                                      void *stream) {
+    ESGD_ARG(n >= 0 && (n == 0 || (handles && inputs)), "allreducef_forward_cuda_post_many: bad arguments");
+    ESGD_ARG(divisor == divisor && divisor != 0.0f, "allreducef_forward_cuda_post_many: bad divisor");
+    if (n == 0) return ESGD_SUCCESS;
+    std::vector<AllreduceOp *> ops(static_cast<size_t>(n));
+    std::vector<float *> sbs(static_cast<size_t>(n));
+    std::vector<uint64_t> counts(static_cast<size_t>(n));
+    std::vector<esgd_sched_h> hs(static_cast<size_t>(n));
+    for (int i = 0; i < n; ++i) {
+        AllreduceOp *op = ops[i] = static_cast<AllreduceOp *>(handles[i]);
+        ESGD_ARG(op, "allreducef_forward_cuda_post_many: op %d is null", i);
+        ESGD_ARG(!op->pending, "allreducef_forward_cuda_post_many: op %d's previous round was not waited", i);
+        if (int rc = op->ensure(true)) return rc;   // collective, in the callers' common order
+        sbs[i] = op->sb;
+        counts[i] = op->len;
+        hs[i] = op->sched;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    void *ps = caller_stream(s);
+    if (int rc = esgd::pack_scatter(n, inputs, sbs.data(), counts.data(), divisor, ps)) return rc;
+    std::vector<int> roles(static_cast<size_t>(n), -1);
+    const int rc = esgd_schedule_post_group(hs.data(), n, ps, roles.data());
+    for (int i = 0; i < n; ++i) ops[i]->pending = roles[i] >= 0;   // posted (a role was written)
+    return rc;
+}
+
+int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const *outputs, void *stream) {
+    ESGD_ARG(n >= 0 && (n == 0 || (handles && outputs)), "allreducef_forward_cuda_wait_many: bad arguments");
+    std::vector<float *> outs, rbs;
+    std::vector<uint64_t> counts;
+    std::vector<esgd_sched_h> hs;
+    std::vector<AllreduceOp *> done;
+    int first = ESGD_SUCCESS;
+    for (int i = 0; i < n; ++i) {
+        AllreduceOp *op = static_cast<AllreduceOp *>(handles[i]);
+        if (!op || !op->pending) continue;
+        op->pending = false;
+        if (int rc = esgd_schedule_wait(op->sched)) {
+            if (!first) first = rc;
+            continue;
+        }
+        outs.push_back(outputs[i]);
+        rbs.push_back(op->rb);
+        counts.push_back(op->len);
+        hs.push_back(op->sched);
+        done.push_back(op);
+    }
+    if (!done.empty()) {
+        void *ps = caller_stream(static_cast<hipStream_t>(stream));
+        int rc = esgd::unpack_gather(int(done.size()), outs.data(), rbs.data(), counts.data(), ps);
+        // released even when the copy-out could not be queued: no round stays held
+        const int rr = esgd_schedule_release_group(hs.data(), int(hs.size()), ps);
+        if (!rc) rc = rr;
+        if (rc && !first) first = rc;
+        if (!rc)
+            for (AllreduceOp *op : done) op->bytes += int64_t(op->len) * int64_t(sizeof(float));
+    }
+    return first;
 }
 
 bool is_cuda_supported(void *) { return true; }

@@ -227,6 +227,10 @@ void dataplane_shutdown();
 // launch the rounds appended to the pending shared launch (k_round_batch); the engine calls
 // it after every pump of the issue ring, transports before queuing anything else
 int dataplane_flush();
+// esgd_schedule_post_group / _release_group: until the end call, this thread's posts
+// (which 0) or releases (1) on `stream` share ONE event recording
+int dataplane_group_begin(int which, void *stream);
+void dataplane_group_end(int which);
 // a finalized job of this process had mapped peers' buckets (no new job with peers then)
 bool dataplane_mappings_closed();
 // settings new schedules capture (esgd_set_config; ESGD_SMALL_ROUND_BYTES / ESGD_DEVICE_FLAGS)

@@ -71,6 +71,11 @@ void arena_trim();
 // a multi-process job's first export: one chunk exported (or quarantined if refused)
 // before its buckets are allocated
 void arena_warm();
+// deep500 group entry points (reduce_kernels.hip): copy-in of n tensors (/ divisor) into
+// n buckets, copy-out of n buckets into n tensors -- one launch per 48
+int pack_scatter(int n, const float *const *src, float *const *dst, const uint64_t *count, float divisor,
+                 void *stream);
+int unpack_gather(int n, float *const *dst, const float *const *src, const uint64_t *count, void *stream);
 
 }  // namespace esgd
 

@@ -249,20 +249,20 @@ __global__ __launch_bounds__(256) void k_move_zero_bytes(uint8_t *dst, uint8_t *
 constexpr int kPackSeg = 48;
 struct PackSet {
     float *a[kPackSeg];          // pack: sources; unpack: destinations
-    uint64_t off[kPackSeg];      // element offset of tensor i in the bucket
+    float *b[kPackSeg];          // tensor i's place in the bucket (or its own bucket: scatter)
     uint64_t n[kPackSeg];
     uint32_t tile0[kPackSeg + 1];
     int nseg;
 };
 
 template <bool PACK, bool DIV>
-__global__ __launch_bounds__(256) void k_pack(PackSet p, float *bucket, float divisor) {
+__global__ __launch_bounds__(256) void k_pack(PackSet p, float divisor) {
     const uint32_t b = blockIdx.x;
     int i = 0;
     while (i + 1 < p.nseg && p.tile0[i + 1] <= b) ++i;
     const uint64_t e0 = uint64_t(b - p.tile0[i]) * 1024;
     float *t = p.a[i];
-    float *bk = bucket + p.off[i];
+    float *bk = p.b[i];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const uint64_t e = e0 + u * 256 + threadIdx.x;
@@ -453,10 +453,13 @@ int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s) {
     return ESGD_SUCCESS;
 }
 
+// pack: tensors[i] (/ divisor) -> buckets[i]; unpack: buckets[i] -> tensors[i].  One
+// launch per kPackSeg tensors.  `bucket` != nullptr: buckets[i] are consecutive places in
+// that one bucket (esgd_pack_div / esgd_unpack); else `buckets` names each tensor's own.
 static int pack_impl(bool pack, int n, float *const *tensors, const uint64_t *count, float *bucket,
-                     float divisor, void *stream) {
+                     float divisor, void *stream, float *const *buckets = nullptr) {
     ESGD_ARG(n >= 0 && n <= 4096, "esgd_pack: %d tensors outside [0, 4096]", n);
-    ESGD_ARG(n == 0 || (tensors && count && bucket), "esgd_pack: null argument");
+    ESGD_ARG(n == 0 || (tensors && count && (bucket || buckets)), "esgd_pack: null argument");
     ESGD_ARG(divisor == divisor && divisor != 0.0f, "esgd_pack: divisor must be a non-zero number");
     if (n == 0) return ESGD_SUCCESS;
     if (int rc = require_device()) return rc;
@@ -471,7 +474,8 @@ static int pack_impl(bool pack, int n, float *const *tensors, const uint64_t *co
             const uint64_t c = count[i0 + j];
             ESGD_ARG(c == 0 || tensors[i0 + j], "esgd_pack: tensor %d is null", i0 + j);
             p.a[j] = tensors[i0 + j];
-            p.off[j] = off;
+            p.b[j] = bucket ? bucket + off : buckets[i0 + j];
+            ESGD_ARG(c == 0 || p.b[j], "esgd_pack: bucket %d is null", i0 + j);
             p.n[j] = c;
             p.tile0[j] = uint32_t(tiles);
             tiles += (c + 1023) / 1024;
@@ -480,17 +484,27 @@ static int pack_impl(bool pack, int n, float *const *tensors, const uint64_t *co
         ESGD_ARG(tiles < (1ull << 31), "esgd_pack: too many elements in one launch");
         p.tile0[p.nseg] = uint32_t(tiles);
         if (!tiles) continue;
-        float *base = bucket;
         if (pack) {
-            if (divisor == 1.0f) hipLaunchKernelGGL((k_pack<true, false>), dim3(unsigned(tiles)), dim3(256), 0, s, p, base, divisor);
-            else hipLaunchKernelGGL((k_pack<true, true>), dim3(unsigned(tiles)), dim3(256), 0, s, p, base, divisor);
+            if (divisor == 1.0f) hipLaunchKernelGGL((k_pack<true, false>), dim3(unsigned(tiles)), dim3(256), 0, s, p, divisor);
+            else hipLaunchKernelGGL((k_pack<true, true>), dim3(unsigned(tiles)), dim3(256), 0, s, p, divisor);
         } else {
-            hipLaunchKernelGGL((k_pack<false, false>), dim3(unsigned(tiles)), dim3(256), 0, s, p, base, divisor);
+            hipLaunchKernelGGL((k_pack<false, false>), dim3(unsigned(tiles)), dim3(256), 0, s, p, divisor);
         }
         ESGD_HIP(hipGetLastError());
     }
     return ESGD_SUCCESS;
 }
+// the deep500 op's group entry points: every op's copy-in (/ divisor) into its own send
+// bucket, or every op's copy-out from its own receive bucket, in one launch per 48 ops
+int pack_scatter(int n, const float *const *src, float *const *dst, const uint64_t *count, float divisor,
+                 void *stream) {
+    return pack_impl(true, n, const_cast<float *const *>(src), count, nullptr, divisor, stream, dst);
+}
+
+int unpack_gather(int n, float *const *dst, const float *const *src, const uint64_t *count, void *stream) {
+    return pack_impl(false, n, dst, count, nullptr, 1.0f, stream, const_cast<float *const *>(src));
+}
+
 int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64_t count,
                   float scale, hipStream_t s) {
     return reduce_impl(dtype, k, inputs, out, count, scale, scale != 1.0f, s, true);

@@ -69,6 +69,19 @@ struct BatchArgs {
     long long timeout;                 // wall-clock ticks any flag wait may take
 };
 
+// The snapshots of a shared launch's rounds (rb = sb, or rb = 0 for a FRESH_ONLY round
+// this rank had not posted), all in one launch queued right before k_round_batch: up to
+// kBatchMax segments, 16-B aligned, write-through stores.
+struct CopySet {
+    const void *src[kBatchMax];        // nullptr: zero-fill
+    void *dst[kBatchMax];
+    uint32_t nvec[kBatchMax];          // 16-B vectors
+    uint32_t tail[kBatchMax];          // bytes after the last full vector
+    uint32_t tile0[kBatchMax + 1];     // 1024-vector tiles before segment i (prefix)
+    int nseg;
+};
+int copy_many(const CopySet &c, hipStream_t s);
+
 // world: ranks (2..ESGD_MAX_FANIN); grid = workers + 1 (the agent)
 int round_batch(int dtype, int world, const BatchArgs &a, unsigned workers, hipStream_t s);
 // workgroups of the batch kernel for (dtype, world) resident on this GPU at once

@@ -259,6 +259,47 @@ int round_batch_capacity(int dtype, int world) {
     return c;
 }
 
+// The shared launch's snapshots: tile g (1024 16-B vectors of one segment) on block
+// g mod grid; nt loads, write-through stores (peers read these buckets over xGMI once
+// the kernel boundary and the agent's ready have passed); ragged tails byte by byte.
+__global__ __launch_bounds__(256) void k_copy_many(CopySet c) {
+    const uint32_t total = c.tile0[c.nseg];
+    int i = 0;
+    for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
+        while (g >= c.tile0[i + 1]) ++i;
+        const uint32_t nv = c.nvec[i];
+        const uint32_t v0 = (g - c.tile0[i]) * 1024u;
+        const __amdgpu_buffer_rsrc_t wd = __builtin_amdgcn_make_buffer_rsrc(c.dst[i], (short)0, int(nv * 16u), 0x00020000);
+        raw16 r[4];
+        if (c.src[i]) {
+            const __amdgpu_buffer_rsrc_t rd =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(c.src[i]), (short)0, int(nv * 16u), 0x00020000);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b128(rd, (v0 + u * 256 + threadIdx.x) * 16, 0, 2);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r[u] = raw16{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(r[u], wd, (v0 + u * 256 + threadIdx.x) * 16, 0, 17);
+        if (v0 == 0 && threadIdx.x < c.tail[i]) {
+            uint8_t *d = static_cast<uint8_t *>(c.dst[i]) + size_t(nv) * 16;
+            const uint8_t *src = static_cast<const uint8_t *>(c.src[i]);
+            d[threadIdx.x] = src ? src[size_t(nv) * 16 + threadIdx.x] : uint8_t(0);
+        }
+    }
+}
+
+int copy_many(const CopySet &c, hipStream_t s) {
+    ESGD_ARG(c.nseg >= 1 && c.nseg <= kBatchMax, "copy_many: %d segments", c.nseg);
+    const uint32_t total = c.tile0[c.nseg];
+    if (!total) return ESGD_SUCCESS;
+    const unsigned grid = std::min<unsigned>(total, unsigned(cu_count()) * 4u);
+    hipLaunchKernelGGL(k_copy_many, dim3(grid), dim3(256), 0, s, c);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
 template <class Tr>
 static int launch_batch_t(int world, const BatchArgs &a, unsigned grid, hipStream_t s) {
     switch (world) {

@@ -59,6 +59,8 @@ def _bind(h):
         "esgd_get_config": (i, [C.c_char_p, C.POINTER(C.c_int64)]),
         "esgd_comm_issue_log": (i, [C.POINTER(u32), C.POINTER(u32), u32, C.POINTER(u32)]),
         "esgd_comm_profile": (i, [C.POINTER(u64), i]),
+        "esgd_schedule_post_group": (i, [C.POINTER(u64), i, vp, C.POINTER(i)]),
+        "esgd_schedule_release_group": (i, [C.POINTER(u64), i, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(h, name)
@@ -174,6 +176,28 @@ def _buf_arg(x, buf):
         return x.ctypes.data
     from .device import as_ptr
     return as_ptr(x)
+
+
+def _stream_arg(stream):
+    s = None if stream is None else (stream.handle if hasattr(stream, "handle") else int(stream))
+    return 1 if s == 0 else s   # 0: the legacy default stream (ESGD_STREAM_NULL)
+
+
+def post_group(scheds, stream=None) -> list:
+    """Post every schedule in this order with ONE producer event (esgd_schedule_post_group);
+    returns the roles (1 activated, 0 passive, 2 synchronous)."""
+    n = len(scheds)
+    hs = (C.c_uint64 * n)(*[s.handle for s in scheds])
+    roles = (C.c_int * n)(*([-1] * n))
+    check(lib().esgd_schedule_post_group(hs, n, _stream_arg(stream), roles), "esgd_schedule_post_group")
+    return list(roles)
+
+
+def release_group(scheds, stream=None):
+    """Release every HOLD schedule with ONE consumer event (esgd_schedule_release_group)."""
+    n = len(scheds)
+    hs = (C.c_uint64 * n)(*[s.handle for s in scheds])
+    check(lib().esgd_schedule_release_group(hs, n, _stream_arg(stream)), "esgd_schedule_release_group")
 
 
 class Schedule:

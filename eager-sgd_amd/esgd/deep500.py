@@ -55,6 +55,10 @@ def _bind(h):
     h.allreducef_forward_cuda_post.argtypes = [vp, vp, C.c_float, vp]
     h.allreducef_forward_cuda_wait.restype = C.c_int
     h.allreducef_forward_cuda_wait.argtypes = [vp, vp, vp]
+    h.allreducef_forward_cuda_post_many.restype = C.c_int
+    h.allreducef_forward_cuda_post_many.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), C.c_float, vp]
+    h.allreducef_forward_cuda_wait_many.restype = C.c_int
+    h.allreducef_forward_cuda_wait_many.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), vp]
     h.is_cuda_supported.restype, h.is_cuda_supported.argtypes = C.c_bool, [vp]
     h.report.restype, h.report.argtypes = C.c_int64, [vp, vp]
     h.delete_op.restype, h.delete_op.argtypes = None, [vp]
@@ -151,6 +155,30 @@ class AllreduceOp:
         _lib.check(lib().allreducef_forward_cuda_wait(self.handle, as_ptr(out), stream),
                    "allreducef_forward_cuda_wait")
         return out
+
+    @staticmethod
+    def post_many(ops, grads, divisor: float = 1.0, stream: int | None = None):
+        """post_cuda for many ops in one call (allreducef_forward_cuda_post_many): every
+        copy-in in one launch per 48 ops, the posts with one producer event.  Raises
+        EsgdError; the ops before a failed post stay posted (wait_many drains them)."""
+        from .device import as_ptr
+        n = len(ops)
+        hs = (C.c_void_p * n)(*[op.handle for op in ops])
+        gs = (C.c_void_p * n)(*[as_ptr(g) for g in grads])
+        _lib.check(lib().allreducef_forward_cuda_post_many(hs, n, gs, float(divisor), stream),
+                   "allreducef_forward_cuda_post_many")
+
+    @staticmethod
+    def wait_many(ops, outs, stream: int | None = None):
+        """wait_cuda for many ops in one call: every posted op's round waited for in order,
+        every copy-out in one launch per 48 ops, one release event; ops not posted are
+        skipped.  Raises EsgdError (the first failure) after every round was waited for."""
+        from .device import as_ptr
+        n = len(ops)
+        hs = (C.c_void_p * n)(*[op.handle for op in ops])
+        os_ = (C.c_void_p * n)(*[as_ptr(o) for o in outs])
+        _lib.check(lib().allreducef_forward_cuda_wait_many(hs, n, os_, stream),
+                   "allreducef_forward_cuda_wait_many")
 
     def forward_void(self, grad: np.ndarray) -> np.ndarray:
         """The reference ABI's void allreducef_forward verbatim (host buffers): on a failed

@@ -17,9 +17,12 @@ of the gradient (copy-in with the divide; the move with the zeroing fused; copy-
 instead of 5 (divide, copy-in, move, copy-out, memset).
 
 pipeline=True (the per-tensor default): every tensor's round is posted before the first
-is waited for (allreducef_forward_cuda_post / _wait), so the 161 host round trips overlap
-instead of running one after another as the reference's blocking ops do (:304-307); the
-same rounds over the same operands, so the same bits.  pipeline=False keeps the blocking
+is waited for, so the 161 host round trips overlap instead of running one after another as
+the reference's blocking ops do (:304-307); the same rounds over the same operands, so the
+same bits.  The posts and the waits each go through ONE call
+(allreducef_forward_cuda_post_many / _wait_many: one copy-in launch per 48 tensors, one
+producer event, one copy-out launch per 48, one release event), and the data plane runs
+the rounds that come due together in shared launches.  pipeline=False keeps the blocking
 chain.
 
 fuse=True (SURVEY.md §8(f) "bucket fusion"): the reference runs one schedule per tensor,
@@ -82,37 +85,31 @@ class EagerSGDOptimizer:
                 g = grad if (grad.dtype == torch.float32 and grad.is_contiguous()) \
                     else grad.float().contiguous()
                 if self.pipeline:
-                    try:
-                        op.post_cuda(g, self.comm_size, stream)            # :40 fused
-                    except Exception:
-                        self._drain(posted, stream)   # no op is left with a round posted
-                        raise
                     posted.append((op, g, grad, var))
                 else:
                     op.forward_cuda_div(g, g, self.comm_size, stream)      # :40 fused, in place
                     if g is not grad:
                         var.grad = g.to(grad.dtype).view_as(grad)
-            err = self._drain(posted, stream)
-            if err is not None:
-                raise err
+            if posted:
+                ops, gs = [p[0] for p in posted], [p[1] for p in posted]
+                err = None
+                try:
+                    deep500.AllreduceOp.post_many(ops, gs, self.comm_size, stream)   # :40 fused
+                except Exception as e:   # noqa: BLE001 -- re-raised below
+                    err = e
+                try:   # every posted round is waited for, even after a failed post
+                    deep500.AllreduceOp.wait_many(ops, gs, stream)   # results land in place
+                except Exception as e:   # noqa: BLE001
+                    err = err or e
+                if err is not None:
+                    raise err
+                for op, g, grad, var in posted:
+                    if g is not grad:
+                        var.grad = g.to(grad.dtype).view_as(grad)
         r = self.optimizer.step()
         if global_step is not None and hasattr(global_step, "add_"):
             global_step.add_(1)
         return r
-
-    @staticmethod
-    def _drain(posted, stream):
-        """Wait every posted round (a failure does not skip the rest); the first error."""
-        err = None
-        for op, g, grad, var in posted:
-            try:
-                op.wait_cuda(g, stream)
-            except Exception as e:   # noqa: BLE001 -- re-raised by the caller
-                err = err or e
-                continue
-            if g is not grad:
-                var.grad = g.to(grad.dtype).view_as(grad)
-        return err
 
     def _apply_fused(self, gvs, stream):
         import torch

@@ -251,6 +251,12 @@ int esgd_schedule_wait_ex(esgd_sched_h h, int *fresh);
  * `stream` so far (copy-out of rb, zeroing sb; NULL = nothing queued) is waited for by
  * the next round's snapshot on the GPU. */
 int esgd_schedule_release(esgd_sched_h h, void *stream);
+/* n posts (releases) in this order with ONE event recorded on the stream for all of them
+ * -- the per-tensor call pattern (opt_esgd_solo_imagenet_imbalance.py:24-44, one op per
+ * gradient) in one call: the same rounds, draws and activations as n single calls.
+ * roles may be NULL.  Stops at the first failure and returns its status. */
+int esgd_schedule_post_group(const esgd_sched_h *h, int n, void *producer_stream, int *roles);
+int esgd_schedule_release_group(const esgd_sched_h *h, int n, void *stream);
 int esgd_schedule_test(esgd_sched_h h, int *flag);
 int esgd_schedule_delete(esgd_sched_h h);
 int esgd_schedule_stats(esgd_sched_h h, esgd_sched_stats_t *out);

@@ -80,6 +80,17 @@ int allreducef_forward_cuda_packed(void *handle, int n, const float *const *grad
  * between them is ESGD_INVALID_ARG.  Every rank must post its ops in the same order. */
 int allreducef_forward_cuda_post(void *handle, const float *input, float divisor, void *stream);
 int allreducef_forward_cuda_wait(void *handle, float *output, void *stream);
+/* Extension: the same for n ops in one call each way (EagerSGDOptimizer's per-tensor step):
+ * _post_many queues every op's copy-in (inputs[i] / divisor into op i's send bucket; one
+ * launch per 48 ops) on stream, then posts the n rounds in this order with ONE producer
+ * event -- the same rounds, draws and activations as n _post calls.  It stops at the first
+ * failure (its status); the ops before it stay posted.  _wait_many waits for the rounds of
+ * the ops that are posted, in order, queues every copy-out (one launch per 48 ops) and
+ * releases the rounds with ONE consumer event; ops that are not posted are skipped; the
+ * first failure's status is returned after every round was waited for. */
+int allreducef_forward_cuda_post_many(void *const *handles, int n, const float *const *inputs, float divisor,
+                                      void *stream);
+int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const *outputs, void *stream);
 /* Extension: what the void entry points above (allreducef_forward, allreducef_forward_cuda)
  * do when their round fails (a peer timeout, an allocation failure).  ESGD_OP_ON_ERROR_ABORT
  * (default; env ESGD_OP_ON_ERROR=abort): print the error and abort the process, as their

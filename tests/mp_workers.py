@@ -532,7 +532,7 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp3
         dist.all_gather_object(allg, local)
         comm.barrier()
         late = t > 0 and rank in late_ranks(mode, world, t)
-        names = ("forward_cuda_div", "forward_cuda_packed", "post_cuda")
+        names = ("forward_cuda_div", "forward_cuda_packed", "post_cuda", "post_many")
         orig = {n: getattr(deep500.AllreduceOp, n) for n in names}
         if late:   # every op call (or post) of this step comes LATE_S after the peers'
             def delayed(fn):
@@ -561,6 +561,57 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp3
     nbytes = opt.bytes_reduced()
     comm.finalize()
     return {"ok": ok, "params_digest": params.tobytes().hex()[:64] + str(params.sum()), "bytes": nbytes}
+
+
+def op_group(rank, world, steps=3, sizes=(1, 17, 1000, 4099, 262147, (2 << 20) + 5, 64, 300007)):
+    """allreducef_forward_cuda_post_many / _wait_many against the single-op path: one set
+    of ops driven by the group calls, a second set by forward_cuda_div one op at a time
+    (allreduce mode: every rank posts every round, so both must give the same bits, and
+    the oracle tree of grad_r / P); plus the misuse rules: a group post over an op still
+    posted fails with ESGD_INVALID_ARG and leaves it posted, wait_many skips ops not posted."""
+    import numpy as np
+    import torch
+
+    from esgd import deep500
+    from esgd._lib import EsgdError
+    from oracle import ffref
+    comm = _comm()
+    dev = torch.device("cuda", local_device())
+    torch.cuda.set_device(dev)
+    deep500.configure("allreduce", 32, 6545343)
+    grp = [deep500.AllreduceOp((n,)) for n in sizes]
+    one = [deep500.AllreduceOp((n,)) for n in sizes]
+    ok, errs = [], {}
+    for t in range(steps):
+        xs = [[ffref.fill_uniform(0xA11 + 13 * t + i, r, n) for r in range(world)] for i, n in enumerate(sizes)]
+        g = [torch.from_numpy(x[rank]).to(dev) for x in xs]
+        h = [gi.clone() for gi in g]
+        comm.barrier()
+        deep500.AllreduceOp.post_many(grp, g, float(world))
+        deep500.AllreduceOp.wait_many(grp, g)
+        for op, hi in zip(one, h):
+            op.forward_cuda_div(hi, hi, float(world))
+        torch.cuda.synchronize()
+        for i, x in enumerate(xs):
+            want = ffref.tree_sum([np.float32(xr) / np.float32(world) for xr in x])
+            a, b = g[i].cpu().numpy(), h[i].cpu().numpy()
+            ok.append(bool(np.array_equal(a.view(np.uint32), want.view(np.uint32)) and
+                           np.array_equal(a.view(np.uint32), b.view(np.uint32))))
+    # misuse: op 0 posted alone, then a group post naming it fails and leaves it posted
+    x = [torch.ones(n, device=dev) for n in sizes]
+    grp[0].post_cuda(x[0], float(world))
+    try:
+        deep500.AllreduceOp.post_many(grp, x, float(world))
+        errs["post_many_over_posted"] = None
+    except EsgdError as e:
+        errs["post_many_over_posted"] = e.rc
+    deep500.AllreduceOp.wait_many(grp, x)   # waits op 0 only (the others are not posted)
+    torch.cuda.synchronize()
+    want0 = ffref.tree_sum([np.ones(sizes[0], np.float32) / np.float32(world)] * world)
+    errs["drained_op0"] = bool(np.array_equal(x[0].cpu().numpy(), want0))
+    comm.barrier()
+    comm.finalize()
+    return {"ok": ok, "errs": errs}
 
 
 def cp_ordered(rank, world, nsched=3, rounds=6, seed=7):
@@ -1625,6 +1676,27 @@ def cp_pipelined_steps(rank, world, steps=50, kind=2, n=161):
         s.delete()
     comm.finalize()
     return {"step_us_median": round(statistics.median(ts[2:]) * 1e6, 1), "last_step": rel, "per_sched": per}
+
+
+def cp_post_group(rank, world, n=12, rounds=20, kind=2):
+    """esgd_schedule_post_group on the control plane: `n` schedules, every round posted as
+    one group on half the steps and one by one on the others; the roles, the round logs and
+    the activators must be those of single posts (the same draws in the same order)."""
+    comm = _comm()
+    scheds = [comm.Schedule(kind, None, None, 0, seed=6545343 + i, async_=3, buf=comm.BUF_NONE)
+              for i in range(n)]
+    roles = []
+    for t in range(rounds):
+        comm.barrier()
+        roles.append(comm.post_group(scheds) if t % 2 == 0 else [s.post() for s in scheds])
+        for s in scheds:
+            s.wait()
+    comm.barrier()
+    logs = [s.log() for s in scheds]
+    for s in scheds:
+        s.delete()
+    comm.finalize()
+    return {"roles": roles, "logs": logs}
 
 
 def cp_create_many(rank, world, n=161, rounds=1):

@@ -96,3 +96,15 @@ def test_op_result_ordered_on_the_callers_default_stream(packed, host):
         assert outs[0][t]["contributors"] is not None and outs[1][t]["contributors"] is not None, (t, outs)
         assert outs[0][t]["contributors"] == outs[1][t]["contributors"], (t, outs)
         assert outs[0][t]["digest"] == outs[1][t]["digest"], t
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_group_post_wait_same_bits_as_single_ops(world):
+    # the optimizer's per-tensor step through ONE post and ONE wait call
+    # (allreducef_forward_cuda_post_many / _wait_many) against one forward_cuda_div per op:
+    # the oracle's bits, ragged and tiny tensors and a five-launch size among them
+    outs = run("op_group", world)
+    for o in outs:
+        assert all(o["ok"]) and o["ok"], o["ok"]
+        assert o["errs"]["post_many_over_posted"] == -2, o["errs"]   # ESGD_INVALID_ARG
+        assert o["errs"]["drained_op0"], o["errs"]

@@ -272,3 +272,22 @@ def test_creation_cost_161_schedules():
     outs = run("cp_create_many", 4, n=161)
     worst = max(o["create_ms_per_schedule"] for o in outs)
     assert worst < 20, worst
+
+
+@pytest.mark.parametrize("kind", [1, 2])
+def test_post_group_same_rounds_as_single_posts(kind):
+    # esgd_schedule_post_group (the per-tensor optimizer's one call for all its ops): the
+    # same roles, rounds and activators as posting the schedules one by one in that order
+    world, n, rounds = 3, 12, 20
+    outs = run("cp_post_group", world, n=n, rounds=rounds, kind=kind)
+    for o in outs:
+        for i, log in enumerate(o["logs"]):
+            assert [e["round"] for e in log] == list(range(1, rounds + 1))
+            if kind == 2:   # majority: the libc draw of each schedule's seed
+                assert [e["activator"] for e in log] == ffref.activators(6545343 + i, world, rounds)
+    if kind == 2:
+        for t in range(rounds):
+            for i in range(n):
+                act = ffref.activators(6545343 + i, world, rounds)[t]
+                for r, o in enumerate(outs):
+                    assert o["roles"][t][i] == (1 if act == r else 0), (t, i, r)
