@@ -1699,6 +1699,23 @@ def cp_post_group(rank, world, n=12, rounds=20, kind=2):
     return {"roles": roles, "logs": logs}
 
 
+def cp_profile(rank, world, n=5, rounds=10):
+    """esgd_comm_profile counts what the progress thread did: every round joined once."""
+    comm = _comm()
+    p0 = comm.profile()
+    scheds = [comm.Schedule(comm.ALLREDUCE, None, None, 0, buf=comm.BUF_NONE) for _ in range(n)]
+    for _ in range(rounds):
+        comm.post_group(scheds)
+        for s in scheds:
+            s.wait()
+    p1 = comm.profile()
+    comm.barrier()
+    for s in scheds:
+        s.delete()
+    comm.finalize()
+    return {k: p1[k] - p0[k] for k in p0}
+
+
 def cp_create_many(rank, world, n=161, rounds=1):
     """`n` schedules created back to back (the per-tensor wrapper's 161 buckets,
     opt_esgd_solo_imagenet_imbalance.py:85-248), each run for `rounds` rounds, then deleted:

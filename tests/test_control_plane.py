@@ -291,3 +291,13 @@ def test_post_group_same_rounds_as_single_posts(kind):
                 act = ffref.activators(6545343 + i, world, rounds)[t]
                 for r, o in enumerate(outs):
                     assert o["roles"][t][i] == (1 if act == r else 0), (t, i, r)
+
+
+def test_progress_thread_profile_counts_joins():
+    # esgd_comm_profile (the bench's per-step host breakdown): 5 schedules x 10 rounds
+    # joined once each, time spent inside busy passes, no data-plane launches (BUF_NONE)
+    outs = run("cp_profile", 2, n=5, rounds=10)
+    for o in outs:
+        assert o["joins"] == 50, o
+        assert o["passes"] >= 1 and o["pass_ns"] > 0 and o["join_ns"] > 0, o
+        assert o["launches"] == 0 and o["flush_ns"] == 0, o
