@@ -174,7 +174,7 @@ def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0
 def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0, buf="device",
                   in_place=False, transport="ipc", shadow_ranks=(), small_bytes=None,
                   piece_bytes=None, host_chunk=None, device_flags=None, wire=False, chunk_kernel=None,
-                  fail_exports=None, batch=None):
+                  fail_exports=None, batch=None, detail=False):
     """Data plane on the GPU: every rank reduces its splitmix bucket; returns the
     result bytes' digest per round plus a bit-exactness verdict against the oracle.
     shadow_ranks: ranks whose device buckets go through the owned shadow bucket.
@@ -255,7 +255,13 @@ def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0
             assert np.array_equal(want, exact)
         else:
             want = ffref.allreduce_rd(xs)[0]
-        verdicts.append(bool(np.array_equal(got.view(np.uint8), want.view(np.uint8))))
+        same = bool(np.array_equal(got.view(np.uint8), want.view(np.uint8)))
+        if detail and not same:   # diagnostics: the first wrong element, got vs want, every input
+            i = int(np.nonzero(got.view(np.uint8) != want.view(np.uint8))[0][0]) // got.itemsize
+            verdicts.append({"round": t, "index": i, "got": float(got[i]), "want": float(want[i]),
+                             "inputs": [float(x[i]) for x in xs], "stats": s.stats()})
+        else:
+            verdicts.append(same)
         comm.barrier()
     s.delete()
     comm.finalize()
