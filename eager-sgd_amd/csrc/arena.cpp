@@ -53,7 +53,8 @@ constexpr size_t kMinBlock = 4096;
 
 struct Chunk {
     char *base = nullptr;
-    size_t bytes = 0;
+    size_t bytes = 0;                // usable; the seal (kSealBytes) follows
+    uint64_t nonce = 0;              // the seal's, once exported
     int device = -1;
     bool exported = false;
     bool unexportable = false;   // the runtime refused its export: no new blocks from it
@@ -137,11 +138,11 @@ void release_idle(int dev) {
 int new_chunk(size_t bytes, int dev, bool release, Chunk **out) {
     if (release) release_idle(dev);
     char *p = nullptr;
-    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), bytes);
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), bytes + kSealBytes);
     if (e == hipErrorOutOfMemory && !release) {
         (void)hipGetLastError();
         release_idle(dev);
-        e = hipMalloc(reinterpret_cast<void **>(&p), bytes);
+        e = hipMalloc(reinterpret_cast<void **>(&p), bytes + kSealBytes);
     }
     if (e != hipSuccess) return hip_fail(e, "hipMalloc (bucket arena)", __FILE__, __LINE__);
     auto *c = new Chunk();
@@ -305,8 +306,29 @@ static std::mutex g_export_mu;
 // sim: ESGD_FAIL_EXPORTS may fail this export (not the warm-up's, arena_warm)
 static int export_impl(const void *p, size_t bytes, void **base, uint64_t *off, uint8_t handle[64], bool sim);
 
-int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_t handle[64]) {
-    return export_impl(p, bytes, base, off, handle, true);
+int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_t handle[64], SealInfo *seal) {
+    const int rc = export_impl(p, bytes, base, off, handle, true);
+    if (!rc && seal) {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_by_base.find(reinterpret_cast<uintptr_t>(*base));
+        seal->chunk_bytes = it != g_by_base.end() ? it->second->bytes : 0;
+        seal->chunk_base = reinterpret_cast<uintptr_t>(*base);
+        seal->nonce = it != g_by_base.end() ? it->second->nonce : 0;
+    }
+    return rc;
+}
+
+// the seal of chunk c, written (synchronously: creation time) before its first export
+static int write_seal(Chunk *c) {
+    static std::atomic<uint64_t> ctr{0};
+    uint64_t x = (uint64_t(getpid()) << 32) ^ uint64_t(reinterpret_cast<uintptr_t>(c->base)) ^
+                 (ctr.fetch_add(1) * 0x9E3779B97F4A7C15ull) ^ uint64_t(std::chrono::steady_clock::now().time_since_epoch().count());
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    ChunkSeal seal{kSealMagic, uint64_t(reinterpret_cast<uintptr_t>(c->base)), x ^ (x >> 31), uint32_t(getpid()), 0};
+    ESGD_HIP(hipMemcpy(c->base + c->bytes, &seal, sizeof(seal), hipMemcpyHostToDevice));
+    c->nonce = seal.nonce;
+    return ESGD_SUCCESS;
 }
 
 static int export_impl(const void *p, size_t bytes, void **base, uint64_t *off, uint8_t handle[64], bool sim) {
@@ -359,6 +381,8 @@ static int export_impl(const void *p, size_t bytes, void **base, uint64_t *off, 
         std::fprintf(stderr, "esgd: export of %p (%zu B chunk) fails by ESGD_FAIL_EXPORTS\n",
                      static_cast<void *>(c->base), c->bytes);
     }
+    if (!simulate && !c->nonce)
+        if (int rc = write_seal(c)) return rc;
     for (int attempt = 0; !simulate && attempt < 2; ++attempt) {
         e = hipIpcGetMemHandle(&h, c->base);
         if (e == hipSuccess) break;

@@ -17,6 +17,7 @@
 // limiter, majority draw, round protocol) can be exercised by multi-process CPU tests;
 // it is reachable only through ESGD_BUF_NONE and computes nothing.
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -199,7 +200,11 @@ struct IpcKey {
 static std::mutex g_ipc_mu;
 static std::map<IpcKey, void *> g_ipc;
 
-static int ipc_open(int peer, const uint8_t *h, void **base) {
+// Map a peer's exported chunk (once per (peer, chunk)).  `slot` (may be null: flag pages)
+// carries the chunk's seal: a fresh mapping is only kept if the seal read through it is
+// the exporter's -- a mapping that shows other memory fails the creation loudly instead
+// of feeding another process's bytes into the sums.
+static int ipc_open(int peer, const uint8_t *h, void **base, const IpcSlot *slot = nullptr) {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
     IpcKey k;
     k.peer = peer;
@@ -214,6 +219,22 @@ static int ipc_open(int peer, const uint8_t *h, void **base) {
     void *p = nullptr;
     ESGD_HIP(hipIpcOpenMemHandle(&p, hh, hipIpcMemLazyEnablePeerAccess));
     ipc_trace("open", peer, p, 0, h);
+    if (slot && slot->seal_nonce) {
+        ChunkSeal got;
+        std::memset(&got, 0, sizeof(got));
+        ESGD_HIP(hipMemcpy(&got, static_cast<char *>(p) + slot->chunk_bytes, sizeof(got), hipMemcpyDeviceToHost));
+        if (got.magic != kSealMagic || got.nonce != slot->seal_nonce || got.base != slot->chunk_base) {
+            ipc_trace("import-seal-mismatch", peer, p, slot->chunk_bytes, h);
+            std::fprintf(stderr, "esgd: pid %d: rank %d's chunk %#llx (%llu B) mapped at %p shows other memory: seal "
+                         "magic %#llx base %#llx nonce %#llx pid %u, expected base %#llx nonce %#llx\n", int(getpid()),
+                         peer, (unsigned long long)slot->chunk_base, (unsigned long long)slot->chunk_bytes, p,
+                         (unsigned long long)got.magic, (unsigned long long)got.base, (unsigned long long)got.nonce,
+                         got.pid, (unsigned long long)slot->chunk_base, (unsigned long long)slot->seal_nonce);
+            set_error("the runtime mapped rank %d's exported chunk to other memory (its seal does not match; "
+                      "DESIGN.md §5)", peer);
+            return ESGD_ERROR;   // not cached; the mapping is left open (closing is unsafe)
+        }
+    }
     g_ipc[k] = p;
     *base = p;
     return ESGD_SUCCESS;
@@ -369,6 +390,7 @@ static int flags_publish(int rank, int mode) {
     ESGD_HIP(hipIpcGetMemHandle(&h, fp.page));
     IpcSlot &mine = seg->flagpage[mode - 1][rank];
     std::memcpy(mine.handle, &h, 64);
+    mine.seal_nonce = 0;   // not arena memory: no seal
     mine.offset = 0;
     mine.bytes = kPageWords * sizeof(uint32_t);
     mine.gen.store(1, std::memory_order_release);
@@ -1219,10 +1241,14 @@ struct IpcTransport final : Transport {
         void *base = nullptr;
         uint64_t off = 0;
         uint8_t hb[64];
-        if (int rc = arena_export(p, bytes, &base, &off, hb)) return rc;
+        SealInfo seal{0, 0, 0};
+        if (int rc = arena_export(p, bytes, &base, &off, hb, &seal)) return rc;
         std::memcpy(mine.handle, hb, 64);
         mine.offset = off;
         mine.bytes = bytes;
+        mine.chunk_bytes = seal.chunk_bytes;
+        mine.chunk_base = seal.chunk_base;
+        mine.seal_nonce = seal.nonce;
         mine.gen.store(s.gen, std::memory_order_release);
         mine.ver.fetch_add(1, std::memory_order_acq_rel);
         ESGD_TRACE("r%d publish sched %d %s %p chunk %p + %llu\n", s.rank, s.id, what, (void *)p, base,
@@ -1297,7 +1323,7 @@ struct IpcTransport final : Transport {
         // mappings are cached per (peer, chunk) and never closed before shutdown
         if (!(m.base && std::memcmp(m.handle, ps.handle, 64) == 0)) {
             void *pb = nullptr;
-            if (int rc = ipc_open(q, ps.handle, &pb)) return rc;
+            if (int rc = ipc_open(q, ps.handle, &pb, &ps)) return rc;
             m.base = pb;
             std::memcpy(m.handle, ps.handle, 64);
         }

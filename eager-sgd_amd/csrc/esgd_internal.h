@@ -66,7 +66,26 @@ bool arena_free(void *p);
 int arena_device(const void *p);   // device of an arena block, -1 if p is not one
 bool arena_unexportable(const void *p);   // p's chunk: the runtime refused its IPC export
 void arena_stats(uint64_t *reserved, uint64_t *live, uint64_t *exported);
-int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_t handle[64]);
+// export p's chunk: its base, p's offset, the handle; seal (may be null): the chunk's
+// usable bytes and seal nonce (ChunkSeal, below)
+struct SealInfo {
+    uint64_t chunk_bytes, chunk_base, nonce;
+};
+int arena_export(const void *p, size_t bytes, void **base, uint64_t *off, uint8_t handle[64],
+                 SealInfo *seal = nullptr);
+// The seal: 32 bytes written right behind an exported chunk's usable bytes before its
+// first export.  Read back through a peer's fresh mapping, it proves the mapping shows
+// the exporter's chunk (round 4: a suite's job came out wrong with the runtime mapping
+// a peer's chunk to other memory).
+struct ChunkSeal {
+    uint64_t magic;
+    uint64_t base;    // the exporter's VA of the chunk
+    uint64_t nonce;
+    uint32_t pid;
+    uint32_t pad;
+};
+constexpr uint64_t kSealMagic = 0x4c41455344475345ull;   // "ESGDSEAL"
+constexpr size_t kSealBytes = 4096;                      // allocated behind every chunk
 void arena_trim();
 // a multi-process job's first export: one chunk exported (or quarantined if refused)
 // before its buckets are allocated

@@ -27,6 +27,12 @@ struct alignas(64) IpcSlot {
     uint64_t bytes;
     std::atomic<uint32_t> gen;    // 1 once this rank published its bucket for this id
     std::atomic<uint32_t> ver;    // bumped at every (re)publication (buffers that grow)
+    // the exported arena chunk's seal (arena.cpp, ChunkSeal): its usable bytes (the seal
+    // sits right behind them), the exporter's VA of the chunk and the seal's nonce -- an
+    // importer checks them through its fresh mapping (0: no seal, e.g. flag pages)
+    uint64_t chunk_bytes;
+    uint64_t chunk_base;
+    uint64_t seal_nonce;
 };
 
 struct alignas(64) SchedShm {
