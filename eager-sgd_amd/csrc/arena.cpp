@@ -49,6 +49,10 @@ namespace esgd {
 namespace {
 
 constexpr size_t kSlab = size_t(2) << 20;
+size_t alloc_bytes(size_t usable);
+bool seal_on();
+// what a small-class slab hands out: its last 4 KiB hold the seal (2 MiB allocations)
+size_t slab_usable() { return seal_on() ? kSlab - kSealBytes : kSlab; }
 constexpr size_t kMinBlock = 4096;
 
 struct Chunk {
@@ -130,6 +134,23 @@ void release_idle(int dev) {
     for (Chunk *c : idle) release_chunk(c);
 }
 
+// ESGD_SEAL=0 (an A/B switch): chunks without the seal and its room
+bool seal_on() {
+    static const bool on = !(getenv("ESGD_SEAL") && *getenv("ESGD_SEAL") == '0');
+    return on;
+}
+
+// A chunk of `usable` bytes is one hipMalloc of whole 2 MiB granules with room for the
+// seal right behind the usable bytes: an allocation that is not a multiple of 2 MiB
+// (2 MiB + 4 KiB) was seen to make the whole job 2-3x slower (round 4, r04j: every
+// peer-reading round; large pages lost, the likely mechanism).  Slabs keep 2 MiB
+// allocations by giving up their last 4 KiB (kSlabUsable); a large chunk gets a granule
+// more than its blocks.
+size_t alloc_bytes(size_t usable) {
+    if (!seal_on()) return usable;
+    return (usable + kSealBytes + kSlab - 1) / kSlab * kSlab;
+}
+
 // Nothing free fits.  Idle chunks no peer ever mapped go back to the driver first only
 // when the caller allows it (`release`: esgd_malloc and the op's buckets, on the caller's
 // thread) -- hipFree synchronises the whole device, which must never happen on the progress
@@ -138,11 +159,12 @@ void release_idle(int dev) {
 int new_chunk(size_t bytes, int dev, bool release, Chunk **out) {
     if (release) release_idle(dev);
     char *p = nullptr;
-    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), bytes + kSealBytes);
+    const size_t alloc = alloc_bytes(bytes);
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), alloc);
     if (e == hipErrorOutOfMemory && !release) {
         (void)hipGetLastError();
         release_idle(dev);
-        e = hipMalloc(reinterpret_cast<void **>(&p), bytes + kSealBytes);
+        e = hipMalloc(reinterpret_cast<void **>(&p), alloc);
     }
     if (e != hipSuccess) return hip_fail(e, "hipMalloc (bucket arena)", __FILE__, __LINE__);
     auto *c = new Chunk();
@@ -187,8 +209,9 @@ int arena_alloc(size_t bytes, void **out, bool release_idle_chunks) {
         auto &fl = g_small[{dev, cls}];
         if (fl.empty()) {
             Chunk *c = nullptr;
-            if (int rc = new_chunk(kSlab, dev, release_idle_chunks, &c)) return rc;
-            for (size_t o = kSlab; o >= cls; o -= cls) fl.push_back(c->base + o - cls);
+            const size_t usable = slab_usable();
+            if (int rc = new_chunk(usable, dev, release_idle_chunks, &c)) return rc;
+            for (size_t o = usable / cls * cls; o >= cls; o -= cls) fl.push_back(c->base + o - cls);
         }
         char *p = fl.back();
         fl.pop_back();
@@ -381,7 +404,7 @@ static int export_impl(const void *p, size_t bytes, void **base, uint64_t *off, 
         std::fprintf(stderr, "esgd: export of %p (%zu B chunk) fails by ESGD_FAIL_EXPORTS\n",
                      static_cast<void *>(c->base), c->bytes);
     }
-    if (!simulate && !c->nonce)
+    if (!simulate && !c->nonce && seal_on())
         if (int rc = write_seal(c)) return rc;
     for (int attempt = 0; !simulate && attempt < 2; ++attempt) {
         e = hipIpcGetMemHandle(&h, c->base);
