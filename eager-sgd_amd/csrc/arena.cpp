@@ -349,7 +349,9 @@ static int write_seal(Chunk *c) {
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
     x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
     ChunkSeal seal{kSealMagic, uint64_t(reinterpret_cast<uintptr_t>(c->base)), x ^ (x >> 31), uint32_t(getpid()), 0};
-    ESGD_HIP(hipMemcpy(c->base + c->bytes, &seal, sizeof(seal), hipMemcpyHostToDevice));
+    uint64_t w[4];
+    std::memcpy(w, &seal, sizeof(w));
+    if (int rc = seal_write(c->base + c->bytes, w)) return rc;
     c->nonce = seal.nonce;
     return ESGD_SUCCESS;
 }

@@ -221,8 +221,9 @@ static int ipc_open(int peer, const uint8_t *h, void **base, const IpcSlot *slot
     ipc_trace("open", peer, p, 0, h);
     if (slot && slot->seal_nonce) {
         ChunkSeal got;
-        std::memset(&got, 0, sizeof(got));
-        ESGD_HIP(hipMemcpy(&got, static_cast<char *>(p) + slot->chunk_bytes, sizeof(got), hipMemcpyDeviceToHost));
+        uint64_t w[4];
+        if (int rc = seal_read(static_cast<char *>(p) + slot->chunk_bytes, w)) return rc;
+        std::memcpy(&got, w, sizeof(got));
         if (got.magic != kSealMagic || got.nonce != slot->seal_nonce || got.base != slot->chunk_base) {
             ipc_trace("import-seal-mismatch", peer, p, slot->chunk_bytes, h);
             std::fprintf(stderr, "esgd: pid %d: rank %d's chunk %#llx (%llu B) mapped at %p shows other memory: seal "
