@@ -293,9 +293,20 @@ static Segment *g_seg_reg = nullptr;
 static char *g_seg_dev = nullptr;
 static long long g_ticks_per_s = 0;
 
+// ESGD_ROUND_PRIORITY = high | normal | low (A/B): the round stream's priority, i.e. the
+// runtime's pool of hardware queues it is placed in.
+static int round_priority() {
+    const char *e = getenv("ESGD_ROUND_PRIORITY");
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
+    if (e && !std::strcmp(e, "low")) return least;
+    if (e && !std::strcmp(e, "high")) return greatest;
+    return 0;
+}
+
 static int round_stream(hipStream_t *out) {
     std::lock_guard<std::mutex> lk(g_dp_mu);
-    if (!g_rs) ESGD_HIP(hipStreamCreateWithFlags(&g_rs, hipStreamNonBlocking));
+    if (!g_rs) ESGD_HIP(hipStreamCreateWithPriority(&g_rs, hipStreamNonBlocking, round_priority()));
     *out = g_rs;
     return ESGD_SUCCESS;
 }
