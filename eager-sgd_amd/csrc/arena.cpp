@@ -140,16 +140,9 @@ bool seal_on() {
     return on;
 }
 
-// ESGD_SEAL=3 (A/B): the seal's room and allocation layout, nothing written or checked
-bool seal_layout_only() {
-    static const bool on = getenv("ESGD_SEAL") && *getenv("ESGD_SEAL") == '3';
-    return on;
-}
-
 // A chunk of `usable` bytes is one hipMalloc of whole 2 MiB granules with room for the
-// seal right behind the usable bytes: an allocation that is not a multiple of 2 MiB
-// (2 MiB + 4 KiB) was seen to make the whole job 2-3x slower (round 4, r04j: every
-// peer-reading round; large pages lost, the likely mechanism).  Slabs keep 2 MiB
+// seal right behind the usable bytes: whole granules keep the arena's layout
+// what it is without the seal (measured the same, round 4 r04m).  Slabs keep 2 MiB
 // allocations by giving up their last 4 KiB (kSlabUsable); a large chunk gets a granule
 // more than its blocks.
 size_t alloc_bytes(size_t usable) {
@@ -412,7 +405,7 @@ static int export_impl(const void *p, size_t bytes, void **base, uint64_t *off, 
         std::fprintf(stderr, "esgd: export of %p (%zu B chunk) fails by ESGD_FAIL_EXPORTS\n",
                      static_cast<void *>(c->base), c->bytes);
     }
-    if (!simulate && !c->nonce && seal_on() && !seal_layout_only())
+    if (!simulate && !c->nonce && seal_on())
         if (int rc = write_seal(c)) return rc;
     for (int attempt = 0; !simulate && attempt < 2; ++attempt) {
         e = hipIpcGetMemHandle(&h, c->base);

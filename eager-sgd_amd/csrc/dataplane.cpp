@@ -293,22 +293,26 @@ static Segment *g_seg_reg = nullptr;
 static char *g_seg_dev = nullptr;
 static long long g_ticks_per_s = 0;
 
-// ESGD_ROUND_PRIORITY = high | normal | low (A/B): the round stream's priority, i.e. the
-// runtime's pool of hardware queues it is placed in.
-static int round_priority() {
-    const char *e = getenv("ESGD_ROUND_PRIORITY");
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 0;
-    if (e && !std::strcmp(e, "low")) return least;
-    if (e && !std::strcmp(e, "high")) return greatest;
-    return 0;
-}
-
 static int round_stream(hipStream_t *out) {
     std::lock_guard<std::mutex> lk(g_dp_mu);
-    if (!g_rs) ESGD_HIP(hipStreamCreateWithPriority(&g_rs, hipStreamNonBlocking, round_priority()));
+    if (!g_rs) ESGD_HIP(hipStreamCreateWithFlags(&g_rs, hipStreamNonBlocking));
     *out = g_rs;
     return ESGD_SUCCESS;
+}
+
+// The arena seal's kernels (reduce_kernels.hip) run on the round stream, synchronously, at
+// an export or a first mapping -- never on a stream of their own (one more hardware queue
+// per process slowed shared-GPU rounds 1.7x).  Waiting for the round stream
+// cannot deadlock: every rank launches rounds in the node's one issue order, so the
+// earliest round in flight anywhere has been launched by every rank and completes.
+// ESGD_SEAL_STREAM=library (A/B): the library's default stream instead.
+int seal_stream(hipStream_t *out) {
+    static const bool lib = getenv("ESGD_SEAL_STREAM") && !std::strcmp(getenv("ESGD_SEAL_STREAM"), "library");
+    if (lib) {
+        *out = default_stream();
+        return *out ? ESGD_SUCCESS : ESGD_ERROR;
+    }
+    return round_stream(out);
 }
 
 // Copy streams of the chunked host-bucket rounds (one per direction, so a chunk's D2H

@@ -88,6 +88,8 @@ constexpr uint64_t kSealMagic = 0x4c41455344475345ull;   // "ESGDSEAL"
 // written / read by kernels (reduce_kernels.hip), synchronously: 4 words
 int seal_write(void *dst, const uint64_t w[4]);
 int seal_read(const void *src, uint64_t w[4]);
+// the stream they run on (dataplane.cpp)
+int seal_stream(hipStream_t *out);
 constexpr size_t kSealBytes = 4096;                      // allocated behind every chunk
 void arena_trim();
 // a multi-process job's first export: one chunk exported (or quarantined if refused)

@@ -612,28 +612,15 @@ __global__ void k_seal_read(const uint64_t *src, uint64_t *dst) {
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// One stream per seal operation, destroyed right after it: a stream the process keeps
-// holds a hardware queue for its lifetime, and one more (idle) queue per process made the
-// peer rounds of two processes sharing a GPU 1.7x slower (round 4, r04m/r04n).
+// The seal kernels run on a stream the process already has (seal_stream, dataplane.cpp):
+// a stream of their own -- kept, or created per operation (the runtime pools its idle
+// hardware queue) -- left one more hardware queue per process, and with it the peer rounds
+// of two processes sharing a GPU ran 1.7x slower (round 4, r04m-r04o).
 static std::mutex g_seal_mu;
 static uint64_t *g_seal_host = nullptr, *g_seal_view = nullptr;   // pinned, mapped
 
-struct SealStream {
-    hipStream_t s = nullptr;
-    ~SealStream() {
-        if (s && !keep()) (void)hipStreamDestroy(s);
-    }
-    static bool keep() {   // ESGD_SEAL=5 (A/B): one persistent stream, round 4's first form
-        static const bool k = getenv("ESGD_SEAL") && *getenv("ESGD_SEAL") == '5';
-        return k;
-    }
-};
-
-static int seal_io_begin(SealStream &st) {   // g_seal_mu held
-    static hipStream_t kept = nullptr;
-    if (SealStream::keep() && kept) st.s = kept;
-    else ESGD_HIP(hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking));
-    if (SealStream::keep()) kept = st.s;
+static int seal_io_begin(hipStream_t *s) {   // g_seal_mu held
+    if (int rc = seal_stream(s)) return rc;
     if (!g_seal_host) {
         ESGD_HIP(hipHostMalloc(reinterpret_cast<void **>(&g_seal_host), 64, hipHostMallocMapped));
         ESGD_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&g_seal_view), g_seal_host, 0));
@@ -644,24 +631,23 @@ static int seal_io_begin(SealStream &st) {   // g_seal_mu held
 // the 32-B seal into this process's chunk memory at dst, synchronously
 int seal_write(void *dst, const uint64_t w[4]) {
     std::lock_guard<std::mutex> lk(g_seal_mu);
-    SealStream st;
-    if (int rc = seal_io_begin(st)) return rc;
-    hipLaunchKernelGGL(k_seal_write, dim3(1), dim3(64), 0, st.s, static_cast<uint64_t *>(dst), w[0], w[1], w[2],
-                       w[3]);
+    hipStream_t s = nullptr;
+    if (int rc = seal_io_begin(&s)) return rc;
+    hipLaunchKernelGGL(k_seal_write, dim3(1), dim3(64), 0, s, static_cast<uint64_t *>(dst), w[0], w[1], w[2], w[3]);
     ESGD_HIP(hipGetLastError());
-    ESGD_HIP(hipStreamSynchronize(st.s));
+    ESGD_HIP(hipStreamSynchronize(s));
     return ESGD_SUCCESS;
 }
 
 // the 32 B at src (a peer's chunk, through this process's mapping), synchronously
 int seal_read(const void *src, uint64_t w[4]) {
     std::lock_guard<std::mutex> lk(g_seal_mu);
-    SealStream st;
-    if (int rc = seal_io_begin(st)) return rc;
+    hipStream_t s = nullptr;
+    if (int rc = seal_io_begin(&s)) return rc;
     for (int i = 0; i < 4; ++i) g_seal_host[i] = 0;
-    hipLaunchKernelGGL(k_seal_read, dim3(1), dim3(64), 0, st.s, static_cast<const uint64_t *>(src), g_seal_view);
+    hipLaunchKernelGGL(k_seal_read, dim3(1), dim3(64), 0, s, static_cast<const uint64_t *>(src), g_seal_view);
     ESGD_HIP(hipGetLastError());
-    ESGD_HIP(hipStreamSynchronize(st.s));
+    ESGD_HIP(hipStreamSynchronize(s));
     for (int i = 0; i < 4; ++i) w[i] = reinterpret_cast<volatile uint64_t *>(g_seal_host)[i];
     return ESGD_SUCCESS;
 }
