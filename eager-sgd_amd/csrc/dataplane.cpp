@@ -133,6 +133,9 @@ bool config_strict_handoffs() {
 // five-launch rounds' first pairing): esgd_get_config("launches"), for the bench's
 // per-step breakdown
 static std::atomic<uint64_t> g_launches{0};
+// worker workgroups of the last shared launch: esgd_get_config("batch_workers"), so a test
+// can see that the grid is sized by the residency figure and not a fallback
+static std::atomic<int64_t> g_batch_workers{0};
 
 uint64_t config_small_round_bytes() {
     const int64_t v = g_cfg_small.load();
@@ -175,9 +178,10 @@ int config_get(const char *key, int64_t *value) {
     else if (!std::strcmp(key, "strict_handoffs")) *value = config_strict_handoffs() ? 1 : 0;
     else if (!std::strcmp(key, "batch_rounds")) *value = batch_rounds();
     else if (!std::strcmp(key, "launches")) *value = int64_t(g_launches.load());
+    else if (!std::strcmp(key, "batch_workers")) *value = g_batch_workers.load();
     else {
         set_error("esgd_get_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
-                  "batch_rounds, launches)", key);
+                  "batch_rounds, launches, batch_workers)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -1127,16 +1131,24 @@ static int batch_flush_locked() {
     // every workgroup of every rank sharing this GPU must be resident at once (the
     // workers of one launch wait on each other through the peers): with 8 ranks on one
     // GPU, 8 x 65 workgroups of the fan-in-8 kernel (2 per CU) did not fit and hung
-    const int cap = round_batch_capacity(g_pend[0].s->dtype, g_pend[0].s->world) / ranks_on_my_device() - 1;
+    const int capacity = round_batch_capacity(g_pend[0].s->dtype, g_pend[0].s->world);
+    const int cap = capacity / ranks_on_my_device() - 1;
     workers = std::max(1u, std::min<unsigned>(workers, unsigned(std::max(1, cap))));
     hipStream_t cs = g_pend[0].st->stream;
     int rc = ESGD_SUCCESS;
-    if (g_copy.nseg) {   // every entry's snapshot, before the launch that publishes its ready
+    if (capacity <= 0) {   // every entry of the launch fails (never a silent single worker)
+        set_error("batched rounds: no residency figure for dtype %d at %d ranks", g_pend[0].s->dtype,
+                  g_pend[0].s->world);
+        rc = ESGD_ERROR;
+        g_copy.nseg = 0;
+    }
+    if (!rc && g_copy.nseg) {   // every entry's snapshot, before the launch that publishes its ready
         rc = copy_many(g_copy, cs);
         g_copy.nseg = 0;
         if (!rc) ++g_launches;
     }
     if (!rc) rc = round_batch(g_pend[0].s->dtype, g_pend[0].s->world, a, workers, cs);
+    if (!rc) g_batch_workers.store(int64_t(workers), std::memory_order_relaxed);
     std::shared_ptr<hipEvent_t> sp;
     if (!rc) {
         sp = pooled_event();

@@ -594,9 +594,7 @@ int gather_widen(int n, const void *const *src, void *const *dst, const uint64_t
 }
 
 // ---- the arena chunk seal (arena.cpp, dataplane.cpp ipc_open) ----
-// Written and read by kernels, never by hipMemcpy: a host-side copy through a peer's IPC
-// mapping left every later peer-reading kernel of the job 2-3x slower (round 4, r04k:
-// C3 at P = 2 2.12 -> 1.25 TB/s with the seal read by hipMemcpy).
+// Written and read by one-wave kernels on the round stream, synchronously.
 __global__ void k_seal_write(uint64_t *dst, uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3) {
     if (threadIdx.x == 0) {
         const uint64_t w[4] = {w0, w1, w2, w3};

@@ -30,6 +30,8 @@
 // peer lines from its CU's L1 and its XCD's L2 once, at the start of the launch (every
 // read of peer memory in this launch follows its gate, and no entry's buffers are touched
 // by an earlier launch's reads after that point).
+#include <atomic>
+
 #include "reduce_core.h"
 #include "round_batch.h"
 
@@ -242,19 +244,30 @@ static int capacity_t(int world) {
     return nb * cu_count();
 }
 
+// cached per (dtype, world); 0 for a dtype or world the kernel does not take (the caller
+// fails the flush: a silent single worker once made every bf16 round 10-20x slower)
 int round_batch_capacity(int dtype, int world) {
-    static int cache[8][ESGD_MAX_FANIN + 1] = {};
-    if (dtype < 0 || dtype >= 8 || world < 2 || world > ESGD_MAX_FANIN) return 0;
-    int &c = cache[dtype][world];
+    static std::atomic<int> cache[5][ESGD_MAX_FANIN + 1] = {};
+    if (world < 2 || world > ESGD_MAX_FANIN) return 0;
+    int slot = -1;
+    switch (dtype) {   // dtype codes are not dense (ESGD_BF16 = 16)
+    case ESGD_FLOAT: slot = 0; break;
+    case ESGD_BF16: slot = 1; break;
+    case ESGD_DOUBLE: slot = 2; break;
+    case ESGD_INT32: slot = 3; break;
+    case ESGD_INT64: slot = 4; break;
+    default: return 0;
+    }
+    int c = cache[slot][world].load(std::memory_order_relaxed);
     if (!c) {
-        switch (dtype) {
-        case ESGD_FLOAT: c = capacity_t<F32>(world); break;
-        case ESGD_BF16: c = capacity_t<BF16>(world); break;
-        case ESGD_DOUBLE: c = capacity_t<F64>(world); break;
-        case ESGD_INT32: c = capacity_t<I32>(world); break;
-        case ESGD_INT64: c = capacity_t<I64>(world); break;
-        default: return 0;
+        switch (slot) {
+        case 0: c = capacity_t<F32>(world); break;
+        case 1: c = capacity_t<BF16>(world); break;
+        case 2: c = capacity_t<F64>(world); break;
+        case 3: c = capacity_t<I32>(world); break;
+        default: c = capacity_t<I64>(world); break;
         }
+        cache[slot][world].store(c, std::memory_order_relaxed);
     }
     return c;
 }

@@ -1473,6 +1473,7 @@ def gpu_many(rank, world, specs, rounds=3, batch=None, small_bytes=None, strict=
               for b, (d, c) in zip(bufs, specs)]
     rng = np.random.default_rng(1000 + rank)
     bad = []
+    workers = []   # pipelined=False: the last shared launch's workers after each round
     l0 = comm.get_config("launches")
     for t in range(rounds):
         wants = []
@@ -1492,6 +1493,7 @@ def gpu_many(rank, world, specs, rounds=3, batch=None, small_bytes=None, strict=
             for s in scheds:
                 s.post()
                 s.wait()
+                workers.append(comm.get_config("batch_workers"))
         for i, (b, want) in enumerate(zip(bufs, wants)):
             got = b.download()
             diff = np.nonzero(got.view(np.uint8) != want.view(np.uint8))[0]
@@ -1505,7 +1507,7 @@ def gpu_many(rank, world, specs, rounds=3, batch=None, small_bytes=None, strict=
     for k in ("batch_rounds", "small_round_bytes", "strict_handoffs"):
         comm.set_config(k, -1)
     comm.finalize()
-    return {"bad": bad, "launches": launches, "rounds": rounds * len(specs)}
+    return {"bad": bad, "launches": launches, "rounds": rounds * len(specs), "workers": workers}
 
 
 def gpu_va_reuse(rank, world, value, count=4099, ready_file=None, hold_file=None, rounds=2):

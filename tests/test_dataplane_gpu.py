@@ -90,6 +90,19 @@ def test_batched_rounds_mixed_dtypes_and_five_launch_rounds():
         assert not o["bad"], o["bad"]
 
 
+def test_batched_launch_grid_for_every_dtype():
+    # every dtype's shared launch gets the workers its tiles ask for: bf16's dtype code (16)
+    # once fell outside the residency cache, every bf16 launch ran ONE worker and bf16
+    # rounds were 10-20x slower (bench sweep_c5_majority_bf16, round 4)
+    specs = [(d, 1 << 18) for d in ("fp32", "bf16", "fp64", "int32", "int64")]
+    outs = run("gpu_many", 2, specs=specs, rounds=1, pipelined=False)
+    for o in outs:
+        assert not o["bad"], o["bad"]
+        assert len(o["workers"]) == len(specs)
+        for (d, _), w in zip(specs, o["workers"]):
+            assert w >= 8, (d, o["workers"])
+
+
 def test_batched_rounds_cut_differently_per_rank():
     # rank 0 batches up to 64 rounds, rank 1 one round per launch (k_round_small), rank 2
     # three, rank 3 two; random delays between posts: no deadlock, every round bit-exact
