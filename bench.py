@@ -675,6 +675,7 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
     finally:
         comm.set_config("batch_rounds", -1)
     t1 = _timed_steps(comm, fused_step, steps)
+    variants = _op_like_variants(comm, dev, lengths, steps)
     for s, b in zip(scheds, bufs):
         _defer(s, b)
     _defer(one, fused)
@@ -688,7 +689,46 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
             "rank0_progress_thread_per_step": prof,
             "step_ms_161_buckets_pipelined_one_launch_per_round": round(t161u * 1e3, 3),
             "rank0_pipelined_step_us_one_launch_per_round": breakdown_u,
-            "rank0_progress_thread_per_step_one_launch_per_round": prof_u}
+            "rank0_progress_thread_per_step_one_launch_per_round": prof_u,
+            "op_like_pipelined_variants": variants}
+
+
+def _op_like_variants(comm, dev, lengths, steps):
+    """The pipelined 161-bucket step with the deep500 op's schedule properties added one at
+    a time (what separates this leg's step from the optimizer's): HOLD | FRESH_ONLY with
+    group post / release; a separate send bucket (the snapshot copies it into rb); both.
+    Per variant: ms per step and rank 0's timeline breakdown."""
+    out = {}
+    for name, sep, flags in (("hold_fresh_group", False, comm.HOLD | comm.FRESH_ONLY),
+                             ("separate_sb", True, 0),
+                             ("separate_sb_hold_fresh_group", True, comm.HOLD | comm.FRESH_ONLY)):
+        rbs = [dev.DeviceBuffer(n) for n in lengths]
+        sbs = [dev.DeviceBuffer(n) for n in lengths] if sep else [None] * len(lengths)
+        for b in (sbs if sep else rbs):
+            dev.fill_uniform(b, SEED, comm.rank())
+        dev.synchronize()
+        scheds = [comm.Schedule(comm.MAJORITY, sb, rb, rb.count, seed=6545343, buf=comm.BUF_DEVICE, flags=flags)
+                  for sb, rb in zip(sbs, rbs)]
+        hold = bool(flags & comm.HOLD)
+
+        def step():
+            if hold:
+                comm.post_group(scheds)
+            else:
+                for sc in scheds:
+                    sc.post()
+            for sc in scheds:
+                sc.wait()
+            if hold:
+                comm.release_group(scheds)
+
+        for _ in range(2):
+            step()
+        t = _timed_steps(comm, step, steps)
+        out[name] = {"step_ms": round(t * 1e3, 3), "rank0_step_us": _step_breakdown_us(scheds)}
+        for sc, rb, sb in zip(scheds, rbs, sbs):
+            _defer(sc, *([rb] if sb is None else [rb, sb]))
+    return out
 
 
 def _profile_per_step(p0, p1, steps):
@@ -701,6 +741,21 @@ def _profile_per_step(p0, p1, steps):
             "flush_us": round(d["flush_ns"] / 1e3, 1)}
 
 
+def _timeline_of(handle):
+    """esgd_schedule_timeline of a raw schedule handle (a deep500 op's, esgd_op_schedule)."""
+    import ctypes as C
+
+    import numpy as np
+
+    from esgd._lib import check, lib
+    n = C.c_uint32()
+    check(lib().esgd_schedule_timeline(C.c_uint64(handle), None, 0, C.byref(n)))
+    out = np.zeros((max(1, n.value), 12), np.uint64)
+    check(lib().esgd_schedule_timeline(C.c_uint64(handle), out.ctypes.data_as(C.POINTER(C.c_uint64)), n.value,
+                                       C.byref(n)))
+    return out[: n.value]
+
+
 def _step_breakdown_us(scheds):
     """Where the last pipelined step's time went on this rank, from every schedule's host
     timeline (esgd_schedule_timeline) of its last round: stamps relative to the first post,
@@ -709,7 +764,7 @@ def _step_breakdown_us(scheds):
     import numpy as np
     rows = []
     for s in scheds:
-        tl = s.timeline().astype(np.int64)
+        tl = (s.timeline() if hasattr(s, "timeline") else _timeline_of(s)).astype(np.int64)
         tl = tl[(tl[:, 0] > 0) & (tl[:, 5] > 0)]
         if len(tl):
             rows.append(tl[-1])
@@ -763,6 +818,9 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
         step()   # creates the ops' schedules (collective, first step)
         step()
         out[name + "_ms"] = round(_timed_steps(comm, step, steps) * 1e3, 3)
+        if name != "fused":
+            out[name + "_breakdown_us"] = _optimizer_breakdown(opt, step, steps)
+            out[name + "_rank0_step_us"] = _step_breakdown_us([op.schedule() for op in opt._ops.values()])
         if name == "per_tensor_pipelined":
             comm.set_config("batch_rounds", 0)
             try:
@@ -777,6 +835,53 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
 
 
 _OPTS = []
+
+
+def _optimizer_breakdown(opt, step, steps):
+    """Median host time per step inside apply_gradients (rank 0's view, untimed steps):
+    the wrapper's Python loop over the tensors, post_many, wait_many (or the blocking
+    per-tensor forward calls), the wrapped SGD step and the closing synchronize."""
+    import statistics
+
+    import torch
+
+    from esgd import deep500
+    Op = deep500.AllreduceOp
+    acc = {}
+
+    def timed(key, f):
+        def g(*a, **k):
+            t0 = time.perf_counter()
+            try:
+                return f(*a, **k)
+            finally:
+                acc[key] = acc.get(key, 0.0) + time.perf_counter() - t0
+        return g
+
+    saved = (Op.post_many, Op.wait_many, Op.forward_cuda_div, opt.optimizer.step)
+    Op.post_many = staticmethod(timed("post_many", saved[0]))
+    Op.wait_many = staticmethod(timed("wait_many", saved[1]))
+    Op.forward_cuda_div = timed("forward_cuda_div", saved[2])
+    opt.optimizer.step = timed("sgd_step", saved[3])
+    rows = []
+    try:
+        for _ in range(steps):
+            acc.clear()
+            t0 = time.perf_counter()
+            opt.step()
+            t1 = time.perf_counter()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            row = dict(acc)
+            row["apply_gradients"] = t1 - t0
+            row["python_loop"] = row["apply_gradients"] - sum(v for k, v in acc.items())
+            row["synchronize"] = t2 - t1
+            rows.append(row)
+    finally:
+        Op.post_many, Op.wait_many = staticmethod(saved[0]), staticmethod(saved[1])
+        Op.forward_cuda_div = saved[2]
+        del opt.optimizer.step   # the instance attribute; the class method shows again
+    return {k: round(statistics.median(r[k] for r in rows) * 1e6, 1) for k in rows[0]}
 
 
 def c3_over_rccl(comm, dev, rank, world, count, steps=20):

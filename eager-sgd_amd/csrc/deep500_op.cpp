@@ -264,6 +264,8 @@ int esgd_op_status(void *handle) {
     return handle ? static_cast<AllreduceOp *>(handle)->status : ESGD_INVALID_ARG;
 }
 
+uint64_t esgd_op_schedule(void *handle) { return handle ? static_cast<AllreduceOp *>(handle)->sched : 0; }
+
 int esgd_op_configure(int mode, int async, unsigned seed) {
     ESGD_ARG(mode == ESGD_OP_SOLO || mode == ESGD_OP_MAJORITY || mode == ESGD_OP_ALLREDUCE,
              "esgd_op_configure: bad mode %d", mode);

@@ -39,6 +39,7 @@ def _bind(h):
     h.esgd_op_configure_wire.restype, h.esgd_op_configure_wire.argtypes = C.c_int, [C.c_int]
     h.esgd_op_on_error.restype, h.esgd_op_on_error.argtypes = C.c_int, [C.c_int]
     h.esgd_op_status.restype, h.esgd_op_status.argtypes = C.c_int, [C.c_void_p]
+    h.esgd_op_schedule.restype, h.esgd_op_schedule.argtypes = C.c_uint64, [C.c_void_p]
     h.create_new_op.restype = vp
     h.create_new_op.argtypes = [C.POINTER(tensor_t), C.c_int, C.POINTER(tensor_t), C.c_int]
     h.allreducef_forward.restype, h.allreducef_forward.argtypes = None, [vp, vp, vp, vp]
@@ -191,6 +192,10 @@ class AllreduceOp:
     def status(self) -> int:
         """First failure of a void entry point under on_error("local"), 0 while none."""
         return int(lib().esgd_op_status(self.handle))
+
+    def schedule(self) -> int:
+        """The op's esgd schedule handle (esgd_op_schedule), 0 before its first round."""
+        return int(lib().esgd_op_schedule(self.handle))
 
     def supports_cuda(self) -> bool:
         return bool(lib().is_cuda_supported(self.handle))

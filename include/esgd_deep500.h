@@ -102,6 +102,9 @@ int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const 
 #define ESGD_OP_ON_ERROR_LOCAL 1
 int esgd_op_on_error(int policy);
 int esgd_op_status(void *handle);
+/* extension: the op's schedule (an esgd_sched_h of esgd.h, e.g. for esgd_schedule_timeline);
+ * 0 before its first device or host round created it */
+uint64_t esgd_op_schedule(void *handle);
 bool is_cuda_supported(void *handle);
 int64_t report(void *handle, void *data);   /* bytes of gradient reduced so far */
 void delete_op(void *handle);

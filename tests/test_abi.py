@@ -94,6 +94,7 @@ def test_op_error_policy_argument_checks():
     lib = _lib.lib()
     assert lib.esgd_op_on_error(5) == _lib.INVALID_ARG
     assert lib.esgd_op_status(None) == _lib.INVALID_ARG
+    assert lib.esgd_op_schedule(None) == 0
     deep500.on_error("local")
     deep500.on_error("default")
 
