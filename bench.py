@@ -698,10 +698,15 @@ def _op_like_variants(comm, dev, lengths, steps):
     a time (what separates this leg's step from the optimizer's): HOLD | FRESH_ONLY with
     group post / release; a separate send bucket (the snapshot copies it into rb); both.
     Per variant: ms per step and rank 0's timeline breakdown."""
+    import torch
     out = {}
-    for name, sep, flags in (("hold_fresh_group", False, comm.HOLD | comm.FRESH_ONLY),
-                             ("separate_sb", True, 0),
-                             ("separate_sb_hold_fresh_group", True, comm.HOLD | comm.FRESH_ONLY)):
+    side = torch.cuda.Stream()
+    hf = comm.HOLD | comm.FRESH_ONLY
+    for name, sep, flags, stream in (("hold_fresh_group", False, hf, None),
+                                     ("separate_sb", True, 0, None),
+                                     ("separate_sb_hold_fresh_group", True, hf, None),
+                                     ("separate_sb_hold_fresh_group_null_stream", True, hf, 0),
+                                     ("separate_sb_hold_fresh_group_side_stream", True, hf, side.cuda_stream)):
         rbs = [dev.DeviceBuffer(n) for n in lengths]
         sbs = [dev.DeviceBuffer(n) for n in lengths] if sep else [None] * len(lengths)
         for b in (sbs if sep else rbs):
@@ -713,19 +718,23 @@ def _op_like_variants(comm, dev, lengths, steps):
 
         def step():
             if hold:
-                comm.post_group(scheds)
+                comm.post_group(scheds, stream)
             else:
                 for sc in scheds:
                     sc.post()
             for sc in scheds:
                 sc.wait()
             if hold:
-                comm.release_group(scheds)
+                comm.release_group(scheds, stream)
+            if stream is not None:
+                torch.cuda.synchronize()
 
         for _ in range(2):
             step()
+        p0 = comm.profile()
         t = _timed_steps(comm, step, steps)
-        out[name] = {"step_ms": round(t * 1e3, 3), "rank0_step_us": _step_breakdown_us(scheds)}
+        out[name] = {"step_ms": round(t * 1e3, 3), "rank0_step_us": _step_breakdown_us(scheds),
+                     "rank0_progress_thread_per_step": _profile_per_step(p0, comm.profile(), steps)}
         for sc, rb, sb in zip(scheds, rbs, sbs):
             _defer(sc, *([rb] if sb is None else [rb, sb]))
     return out
@@ -817,7 +826,9 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
 
         step()   # creates the ops' schedules (collective, first step)
         step()
+        p0 = comm.profile()
         out[name + "_ms"] = round(_timed_steps(comm, step, steps) * 1e3, 3)
+        out[name + "_progress_thread_per_step"] = _profile_per_step(p0, comm.profile(), steps)
         if name != "fused":
             out[name + "_breakdown_us"] = _optimizer_breakdown(opt, step, steps)
             out[name + "_rank0_step_us"] = _step_breakdown_us([op.schedule() for op in opt._ops.values()])
