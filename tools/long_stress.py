@@ -20,7 +20,15 @@ def main():
     ap.add_argument("--rounds", type=int, default=5000)
     ap.add_argument("--device-flags", default=None, help="ESGD_DEVICE_FLAGS for every rank (1 or 2)")
     ap.add_argument("--configs", default=None, help="world:count:buf,... (default: the four of the suite)")
+    ap.add_argument("--pipelined", default=None,
+                    help="world:batch,... -- the batched per-tensor stress (mp_workers.gpu_stress_pipelined: "
+                         "8 HOLD | FRESH_ONLY schedules posted at once every step; batch: rounds per shared "
+                         "launch, 'mix' = 64/0/5/2 by rank) instead of the one-schedule stress")
+    ap.add_argument("--strict", type=int, default=0, help="ESGD_STRICT_HANDOFFS for every rank")
     a = ap.parse_args()
+    os.environ["ESGD_STRICT_HANDOFFS"] = str(a.strict)
+    if a.pipelined:
+        return pipelined(a)
     if a.device_flags:
         os.environ["ESGD_DEVICE_FLAGS"] = a.device_flags   # inherited by the spawned ranks
     configs = ((3, 65536, "device"), (3, (1 << 20) + 3, "device"), (8, 65536, "device"), (3, 65536, "host"))
@@ -41,6 +49,28 @@ def main():
                               "device_flags": a.device_flags or "0 (host flags)",
                               "bad": int(bad), "auto_rounds": sum(o["stats"]["auto_rounds"] for o in outs),
                               "fresh_rounds": sum(o["stats"]["fresh_rounds"] for o in outs),
+                              "wall_s": round(time.time() - t0, 1)}), flush=True)
+
+
+def pipelined(a):
+    for cfg in a.pipelined.split(","):
+        w, b = cfg.split(":")
+        world = int(w)
+        batch = None if b == "default" else ([64, 0, 5, 2] * 2)[:world] if b == "mix" else int(b)
+        for kind, kname in ((1, "solo"), (2, "majority")):
+            t0 = time.time()
+            outs = run("gpu_stress_pipelined", world, kind=kind, rounds=a.rounds, batch=batch, timeout=900)
+            bits = outs[0]["bits"]
+            bad = sum(len(o["torn"]) for o in outs) + sum(o["vals"] != outs[0]["vals"] for o in outs)
+            for i in range(len(outs[0]["vals"])):
+                for t in range(1, len(outs[0]["vals"][i]) + 1):
+                    v = outs[0]["vals"][i][t - 1]
+                    for q in range(world):
+                        want = t % (1 << bits) if outs[q]["fresh"][i][t - 1] else 0
+                        bad += ((v >> (bits * q)) & ((1 << bits) - 1)) != want
+            print(json.dumps({"stress": "pipelined", "world": world, "batch": b, "kind": kname,
+                              "steps": a.rounds, "rounds": a.rounds * len(outs[0]["vals"]),
+                              "strict": a.strict, "bad": int(bad), "auto_rounds": sum(o["auto_rounds"] for o in outs),
                               "wall_s": round(time.time() - t0, 1)}), flush=True)
 
 
