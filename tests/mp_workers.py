@@ -33,6 +33,13 @@ def _entry(fn_name, rank, world, port, kw, q, env=None):
             os.environ.clear()   # are forked from a server started earlier)
             os.environ.update(env)
         os.environ.setdefault("ESGD_TIMEOUT_S", "60")
+        if os.environ.get("ESGD_HANG_DUMP_DIR"):   # diagnostics: every rank's Python stacks
+            import faulthandler   # after ESGD_HANG_DUMP_S seconds, and again every period
+            d = os.environ["ESGD_HANG_DUMP_DIR"]
+            os.makedirs(d, exist_ok=True)
+            _entry.dump = open(os.path.join(d, f"stacks_rank{rank}.txt"), "w")
+            faulthandler.dump_traceback_later(float(os.environ.get("ESGD_HANG_DUMP_S", "60")), repeat=True,
+                                              file=_entry.dump)
         # one GPU per rank where the box has them (device = rank % device_count, set in
         # _comm()): on a full node the data plane then crosses xGMI; on a 1-GPU box every
         # rank shares device 0
@@ -1176,8 +1183,12 @@ def gpu_stress_pipelined(rank, world, kind, counts=(4096, 65536, 17, (1 << 20) +
     vals = [[] for _ in scheds]
     fresh = [[] for _ in scheds]
     torn = []
+    progress = os.environ.get("ESGD_PROGRESS_FILE")   # diagnostics: rank, step every 50 steps
     comm.barrier()
     for t in range(1, rounds + 1):
+        if progress and t % 50 == 0:
+            with open(progress, "a") as f:
+                f.write(f"{time.time():.3f} rank {rank} step {t}\n")
         v = (t % (1 << bits)) << (bits * rank)
         for s, sb, rb, n in scheds:
             if rng.random() < 0.3:
