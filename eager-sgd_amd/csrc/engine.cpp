@@ -580,6 +580,17 @@ static bool step(Sched &s) {
     return false;
 }
 
+// An idle schedule whose next round is neither posted here nor activated by a peer has
+// nothing to do: the pass skips it without taking its mutex (step() would return false).
+// With hundreds of schedules (one per gradient tensor) most are quiet in any pass.
+static bool quiet(const Sched &s) {
+    static const bool off = getenv("ESGD_PASS_SKIP") && *getenv("ESGD_PASS_SKIP") == '0';   // A/B
+    if (off) return false;
+    if (s.stage.load(std::memory_order_acquire) != ST_IDLE || s.awaiting) return false;
+    const uint32_t next = s.joined.load(std::memory_order_acquire) + 1;
+    return s.posted.load(std::memory_order_acquire) < next && s.sh->activated.load(std::memory_order_acquire) < next;
+}
+
 // Launch rounds strictly in ring order (the same sequence on every rank).
 static bool pump_tickets(const std::vector<Sched *> &snap) {
     if (!g_seg) return false;
@@ -657,6 +668,7 @@ bool engine_progress_once() {
     if (any) g_prof_pump_ns.fetch_add(p1 - p0, std::memory_order_relaxed);
     int active = 0;
     for (Sched *s : snap) {
+        if (quiet(*s)) continue;
         while (step(*s)) any = true;   // run a schedule until it has to wait
         // in flight, or posted and waiting for its activation (majority: the drawn
         // activator's post; solo: a sync round's last poster): the join is imminent and

@@ -106,9 +106,12 @@ struct Sched {
     std::mutex mu;
     std::condition_variable cv;
     std::atomic<uint32_t> posted{0};
-    uint32_t joined = 0, completed = 0, waited = 0;
+    // joined and stage change only under mu; atomic so that the progress pass can skip a
+    // quiet idle schedule without taking mu (engine_progress_once)
+    std::atomic<uint32_t> joined{0};
+    uint32_t completed = 0, waited = 0;
     std::atomic<uint32_t> completed_a{0};   // = completed, for wait()'s lock-free spin
-    Stage stage = ST_IDLE;
+    std::atomic<Stage> stage{ST_IDLE};
     uint32_t cur = 0;
     bool cur_fresh = false;
     double stage_t0 = 0;
