@@ -700,13 +700,11 @@ def _op_like_variants(comm, dev, lengths, steps):
     Per variant: ms per step and rank 0's timeline breakdown."""
     import torch
     out = {}
-    side = torch.cuda.Stream()
     hf = comm.HOLD | comm.FRESH_ONLY
     for name, sep, flags, stream in (("hold_fresh_group", False, hf, None),
                                      ("separate_sb", True, 0, None),
                                      ("separate_sb_hold_fresh_group", True, hf, None),
-                                     ("separate_sb_hold_fresh_group_null_stream", True, hf, 0),
-                                     ("separate_sb_hold_fresh_group_side_stream", True, hf, side.cuda_stream)):
+                                     ("separate_sb_hold_fresh_group_null_stream", True, hf, 0)):
         rbs = [dev.DeviceBuffer(n) for n in lengths]
         sbs = [dev.DeviceBuffer(n) for n in lengths] if sep else [None] * len(lengths)
         for b in (sbs if sep else rbs):
@@ -812,16 +810,24 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
     gen.manual_seed(SEED + rank)
     out = {}
     opts = []
+    side = None   # created for its variant only: one more stream is one more hardware queue,
+    #               which on a GPU shared by the ranks changes the timings
     for name, kw in (("per_tensor_pipelined", dict(fuse=False)), ("per_tensor_blocking", dict(pipeline=False)),
-                     ("fused", dict(fuse=True))):
+                     ("fused", dict(fuse=True)), ("per_tensor_blocking_side_stream", dict(pipeline=False))):
+        if name.endswith("_side_stream") and side is None:
+            side = torch.cuda.Stream()
         params = [torch.zeros(n, device=dev_t, requires_grad=True) for n in lengths]
         for p in params:
             p.grad = torch.rand(p.numel(), device=dev_t, generator=gen) - 0.5
         opt = EagerSGDOptimizer(torch.optim.SGD(params, lr=1e-3), world, mode="majority", **kw)
         opts.append(opt)
 
-        def step():
-            opt.step()
+        def step(opt=opt, stream=side if name.endswith("_side_stream") else None):
+            if stream is None:
+                opt.step()
+            else:   # the caller's work on a non-default stream instead of the legacy NULL stream
+                with torch.cuda.stream(stream):
+                    opt.step()
             torch.cuda.synchronize()
 
         step()   # creates the ops' schedules (collective, first step)
@@ -830,7 +836,7 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
         out[name + "_ms"] = round(_timed_steps(comm, step, steps) * 1e3, 3)
         out[name + "_progress_thread_per_step"] = _profile_per_step(p0, comm.profile(), steps)
         if name != "fused":
-            out[name + "_breakdown_us"] = _optimizer_breakdown(opt, step, steps)
+            out[name + "_breakdown_us"] = _optimizer_breakdown(opt, steps, side if name.endswith("_side_stream") else None)
             out[name + "_rank0_step_us"] = _step_breakdown_us([op.schedule() for op in opt._ops.values()])
         if name == "per_tensor_pipelined":
             comm.set_config("batch_rounds", 0)
@@ -848,10 +854,11 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
 _OPTS = []
 
 
-def _optimizer_breakdown(opt, step, steps):
+def _optimizer_breakdown(opt, steps, stream=None):
     """Median host time per step inside apply_gradients (rank 0's view, untimed steps):
     the wrapper's Python loop over the tensors, post_many, wait_many (or the blocking
     per-tensor forward calls), the wrapped SGD step and the closing synchronize."""
+    import contextlib
     import statistics
 
     import torch
@@ -879,7 +886,8 @@ def _optimizer_breakdown(opt, step, steps):
         for _ in range(steps):
             acc.clear()
             t0 = time.perf_counter()
-            opt.step()
+            with (torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()):
+                opt.step()
             t1 = time.perf_counter()
             torch.cuda.synchronize()
             t2 = time.perf_counter()
