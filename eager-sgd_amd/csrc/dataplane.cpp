@@ -309,15 +309,7 @@ static int round_stream(hipStream_t *out) {
 // per process slowed shared-GPU rounds 1.7x).  Waiting for the round stream
 // cannot deadlock: every rank launches rounds in the node's one issue order, so the
 // earliest round in flight anywhere has been launched by every rank and completes.
-// ESGD_SEAL_STREAM=library (A/B): the library's default stream instead.
-int seal_stream(hipStream_t *out) {
-    static const bool lib = getenv("ESGD_SEAL_STREAM") && !std::strcmp(getenv("ESGD_SEAL_STREAM"), "library");
-    if (lib) {
-        *out = default_stream();
-        return *out ? ESGD_SUCCESS : ESGD_ERROR;
-    }
-    return round_stream(out);
-}
+int seal_stream(hipStream_t *out) { return round_stream(out); }
 
 // Copy streams of the chunked host-bucket rounds (one per direction, so a chunk's D2H
 // runs while the next chunk's H2D does: PCIe is full duplex).  Created on first use.
