@@ -1791,3 +1791,33 @@ def op_split_misuse(rank, world, count=4096):
     comm.barrier()
     comm.finalize()
     return {"errs": errs, "same": same}
+
+
+def op_queue_probe(rank, world, side=False, steps=3, sizes=(4099, 100003, 1 << 20)):
+    """Diagnostics (tools/queue_probe.py): deep500 ops driven the blocking way on torch's
+    current stream (the legacy NULL stream), optionally after creating one more torch
+    stream, under AMD_LOG_LEVEL so the runtime names the hardware queue of every dispatch.
+    Returns the time per blocking round."""
+    import torch
+
+    from esgd import deep500
+    _comm()
+    dev = torch.device("cuda", local_device())
+    torch.cuda.set_device(dev)
+    extra = torch.cuda.Stream() if side else None   # noqa: F841 -- kept alive: one more queue
+    deep500.configure("allreduce")
+    ops = [deep500.AllreduceOp((n,)) for n in sizes]
+    gs = [torch.rand(n, device=dev) for n in sizes]
+    stream = torch.cuda.current_stream().cuda_stream
+    for op, g in zip(ops, gs):   # creation (collective), untimed
+        op.forward_cuda_div(g, g, world, stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        for op, g in zip(ops, gs):
+            op.forward_cuda_div(g, g, world, stream)
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / (steps * len(ops)) * 1e6
+    for op in ops:
+        op.close()
+    return {"us_per_round": round(us, 1), "side": side}
