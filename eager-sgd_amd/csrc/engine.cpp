@@ -631,9 +631,12 @@ static bool pump_tickets(const std::vector<Sched *> &snap) {
         ++g_cursor;
         any = true;
     }
-    // the one-launch rounds this pump appended go out now, in one launch; a failure is
-    // recorded in every round of that launch (the transport reports it at its query)
-    if (any) (void)dataplane_flush();
+    // the one-launch rounds this pump appended go out in one launch (now, or once a
+    // queued shared launch has finished); a failure is recorded in every round of that
+    // launch (the transport reports it at its query)
+    // (every pass: a launch held back behind ESGD_BATCH_DEPTH queued ones goes out as soon
+    // as one of them has finished)
+    (void)dataplane_flush_soft();
     return any;
 }
 
