@@ -701,10 +701,13 @@ def _op_like_variants(comm, dev, lengths, steps):
     import torch
     out = {}
     hf = comm.HOLD | comm.FRESH_ONLY
-    for name, sep, flags, stream in (("hold_fresh_group", False, hf, None),
-                                     ("separate_sb", True, 0, None),
-                                     ("separate_sb_hold_fresh_group", True, hf, None),
-                                     ("separate_sb_hold_fresh_group_null_stream", True, hf, 0)):
+    for name, sep, flags, stream, rstream in (
+            ("hold_fresh_group", False, hf, None, None),
+            ("separate_sb", True, 0, None, None),
+            ("separate_sb_hold_fresh_group", True, hf, None, None),
+            ("separate_sb_hold_fresh_group_null_stream", True, hf, 0, 0),
+            ("separate_sb_hold_fresh_group_null_producer_only", True, hf, 0, None),
+            ("separate_sb_hold_fresh_group_null_consumer_only", True, hf, None, 0)):
         rbs = [dev.DeviceBuffer(n) for n in lengths]
         sbs = [dev.DeviceBuffer(n) for n in lengths] if sep else [None] * len(lengths)
         for b in (sbs if sep else rbs):
@@ -723,8 +726,8 @@ def _op_like_variants(comm, dev, lengths, steps):
             for sc in scheds:
                 sc.wait()
             if hold:
-                comm.release_group(scheds, stream)
-            if stream is not None:
+                comm.release_group(scheds, rstream)
+            if stream is not None or rstream is not None:
                 torch.cuda.synchronize()
 
         for _ in range(2):

@@ -1204,6 +1204,19 @@ int dataplane_flush_soft() {
     return rc;
 }
 
+void dataplane_extra_queues(int n) {
+    static std::vector<hipStream_t> keep;
+    static uint32_t *word = nullptr;
+    if (n <= 0 || (!word && hipMalloc(reinterpret_cast<void **>(&word), 64) != hipSuccess)) return;
+    for (int i = 0; i < n; ++i) {
+        hipStream_t st = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) break;
+        hip_ignore(hipMemsetAsync(word, 0, 4, st));   // the first command creates the queue
+        hip_ignore(hipStreamSynchronize(st));
+        keep.push_back(st);
+    }
+}
+
 void dataplane_profile(uint64_t *launches, uint64_t *flush_ns) {
     *launches = g_launches.load(std::memory_order_relaxed);
     *flush_ns = g_flush_ns.load(std::memory_order_relaxed);

@@ -133,6 +133,11 @@ int engine_init(const char *job, int rank, int world, bool start_progress) {
         g_thread = std::thread(progress_main);
     }
     if (world > 1 && g_device >= 0) arena_warm();   // before any bucket of the job is exported
+    // diagnostics (on a GPU shared by the ranks, the number of hardware
+    // queues each rank process holds changes round times 2-3x): ESGD_EXTRA_QUEUES=n makes
+    // this process hold n more, each created by a stream's first command
+    if (const char *e = getenv("ESGD_EXTRA_QUEUES"))
+        if (g_device >= 0) dataplane_extra_queues(atoi(e));
     return ESGD_SUCCESS;
 }
 

@@ -230,7 +230,8 @@ void dataplane_shutdown();
 // launch the rounds appended to the pending shared launch (k_round_batch); the engine calls
 // it after every pump of the issue ring, transports before queuing anything else
 int dataplane_flush();
-int dataplane_flush_soft();   // the end of a pump: flush unless ESGD_BATCH_DEPTH launches are queued
+int dataplane_flush_soft();
+void dataplane_extra_queues(int n);   // diagnostics: n more streams, each with a queue   // the end of a pump: flush unless ESGD_BATCH_DEPTH launches are queued
 // esgd_schedule_post_group / _release_group: until the end call, this thread's posts
 // (which 0) or releases (1) on `stream` share ONE event recording
 int dataplane_group_begin(int which, void *stream);
