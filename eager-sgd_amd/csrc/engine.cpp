@@ -21,6 +21,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <unordered_set>
 #include <ctime>
 
 #include "esgd_internal.h"
@@ -33,6 +34,7 @@ static std::string g_job;
 static double g_timeout = 600.0;
 static std::mutex g_reg_mu;
 static std::vector<Sched *> g_reg;
+static std::unordered_set<const Sched *> g_reg_set;   // = g_reg, for O(1) handle checks
 static std::mutex g_create_mu;
 static int g_next_id = 0;
 static std::thread g_thread;
@@ -154,6 +156,7 @@ int engine_finalize() {
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         left.swap(g_reg);
+        g_reg_set.clear();
     }
     for (Sched *s : left) {
         if (s->tp) s->tp->teardown(*s);
@@ -292,6 +295,7 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         g_reg.push_back(s);
+        g_reg_set.insert(s);
     }
     *out = s;
     return ESGD_SUCCESS;
@@ -455,6 +459,7 @@ int sched_delete(Sched *s) {
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         g_reg.erase(std::remove(g_reg.begin(), g_reg.end(), s), g_reg.end());
+        g_reg_set.erase(s);
     }
     // The progress thread may be inside a pass over a registry copy that still holds s:
     // wait until a pass that began after the erase has finished (two epochs).
@@ -476,9 +481,7 @@ int sched_delete(Sched *s) {
 Sched *sched_lookup(uint64_t handle) {
     Sched *p = reinterpret_cast<Sched *>(handle);
     std::lock_guard<std::mutex> lk(g_reg_mu);
-    for (Sched *s : g_reg)
-        if (s == p) return s;
-    return nullptr;
+    return g_reg_set.count(p) ? p : nullptr;
 }
 
 // ---- the progress step -------------------------------------------------------------
