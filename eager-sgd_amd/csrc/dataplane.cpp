@@ -608,6 +608,8 @@ struct IpcState : BaseState {
     bool snap = false;
     const void *snap_src = nullptr;
     size_t snap_bytes = 0;
+    // ... or done by the launch's own workers (ESGD_SNAPSHOT_IN_BATCH): 1 rb = sb, 2 rb = 0
+    uint8_t snap_kind = 0;
     uint32_t t1 = 0, t2 = 0;          // its phase-1 / phase-2 tiles
 };
 
@@ -1032,7 +1034,22 @@ struct BatchEntry {
     Sched *s;
     IpcState *st;
     uint32_t round;
+    uint8_t snap;   // the snapshot the launch's workers do (0: none, or queued before it)
 };
+
+// ESGD_SNAPSHOT_IN_BATCH (default 1): a batched round's snapshot is phase 0 of the shared
+// launch itself instead of a k_copy_many launch queued before it (one launch per flush)
+static bool snapshot_in_batch() {
+    static const bool on = !(getenv("ESGD_SNAPSHOT_IN_BATCH") && *getenv("ESGD_SNAPSHOT_IN_BATCH") == '0');
+    return on;
+}
+
+// the whole-bucket snapshot fits the kernel's 32-bit buffer ranges and 16-B vectors
+static bool snap_eligible(const Sched &s, const IpcState &st) {
+    const size_t bytes = s.count * s.esize;
+    const uintptr_t al = reinterpret_cast<uintptr_t>(st.rb_dev) | (s.in_place ? 0 : reinterpret_cast<uintptr_t>(s.sb));
+    return bytes && bytes < (size_t(1) << 31) && (al & 15) == 0;
+}
 static std::vector<BatchEntry> g_pend;
 static CopySet g_copy;   // the pending launch's snapshots (nseg 0: none)
 // shared launches queued and not yet seen complete, oldest first (their events)
@@ -1096,7 +1113,14 @@ static int batch_desc(Sched &s, IpcState &st, hipStream_t cs) {
     d.reduced = pair_flags(s, s.sh->reduced, 1);
     d.fin = dev_flag(&s.sh->fin[r]);
     d.err = dev_flag(&s.sh->gpu_err[r]);
-    d.ctr = st.ctr + 6;   // words 6..9 of the schedule's device counters
+    d.ctr = st.ctr + 6;   // words 6..10 of the schedule's device counters
+    if (snap_eligible(s, st)) {
+        const size_t bytes = s.count * es;
+        d.ssrc = s.in_place ? nullptr : s.sb;
+        d.sdst = st.rb_dev;
+        d.svec = uint32_t(bytes / 16);
+        d.stail = uint32_t(bytes % 16);
+    }
     st.t1 = d.t1;
     st.t2 = std::max<uint32_t>(1, d.t2pre[m]);   // at least one tile: it writes fin
     g_desc_host[s.id] = d;
@@ -1125,18 +1149,25 @@ static int batch_flush_locked() {
     a.table = g_desc_dev;
     a.nent = uint32_t(n);
     a.timeout = (long long)(engine_timeout() * double(g_ticks_per_s));
-    uint32_t t1 = 0, t2 = 0;
+    uint32_t t0 = 0, t1 = 0, t2 = 0;
     for (int e = 0; e < n; ++e) {
         a.sid[e] = uint16_t(g_pend[e].s->id);
         a.value[e] = g_pend[e].round;
+        a.tile0[e] = t0;
         a.tile1[e] = t1;
         a.tile2[e] = t2;
+        if (const uint8_t k = g_pend[e].snap) {
+            const BatchDesc &d = g_desc_host[g_pend[e].s->id];
+            a.snap[e] = k;
+            t0 += (d.svec + 1023) / 1024 + (d.svec == 0 && d.stail ? 1 : 0);
+        }
         t1 += g_pend[e].st->t1;
         t2 += g_pend[e].st->t2;
     }
+    a.tile0[n] = t0;
     a.tile1[n] = t1;
     a.tile2[n] = t2;
-    unsigned workers = std::min<unsigned>(kBatchWorkers, std::max<unsigned>(1, std::max(t1, t2)));
+    unsigned workers = std::min<unsigned>(kBatchWorkers, std::max<unsigned>(1, std::max(t0, std::max(t1, t2))));
     // every workgroup of every rank sharing this GPU must be resident at once (the
     // workers of one launch wait on each other through the peers): with 8 ranks on one
     // GPU, 8 x 65 workgroups of the fan-in-8 kernel (2 per CU) did not fit and hung
@@ -1231,12 +1262,17 @@ static int batch_snapshot(Sched &s, IpcState &st, uint32_t round, bool fresh, hi
     if (int rc = consumer_wait(st, cs)) return rc;
     if (int rc = producer_wait(st, round, fresh, cs)) return rc;
     st.snap = false;
+    st.snap_kind = 0;
     const size_t bytes = s.count * s.esize;
     if (!bytes || s.zero_sb) return s.zero_sb && bytes ? move_zero(st.rb_dev, s.sb, bytes, cs) : ESGD_SUCCESS;
     const void *src = nullptr;
     if (s.fresh_only && !fresh) src = nullptr;            // contributes zeros, sb unread
     else if (!s.in_place) src = s.sb;
     else return ESGD_SUCCESS;                              // in place: nothing to move
+    if (snapshot_in_batch() && snap_eligible(s, st)) {    // phase 0 of the shared launch
+        st.snap_kind = src ? 1 : 2;
+        return ESGD_SUCCESS;
+    }
     const uintptr_t al = reinterpret_cast<uintptr_t>(st.rb_dev) | reinterpret_cast<uintptr_t>(src);
     if ((al & 15) || bytes >= (size_t(1) << 31)) {   // (a launch holds as many copies as rounds: <= kBatchMax)
         if (!src) ESGD_HIP(hipMemsetAsync(st.rb_dev, 0, bytes, cs));
@@ -1272,7 +1308,8 @@ static int batch_append(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) 
     st.pub_round = round;
     st.fin_mode = true;
     st.batch_rc = 0;
-    g_pend.push_back({&s, &st, round});
+    g_pend.push_back({&s, &st, round, st.snap_kind});
+    st.snap_kind = 0;
     return ESGD_SUCCESS;
 }
 

@@ -55,7 +55,13 @@ struct BatchDesc {
     PairFlags ready, reduced;
     uint32_t *fin, *err;               // SchedShm::fin[rank], gpu_err[rank] (device views)
     uint32_t *ctr;                     // device words: [0] phase-1 arrivals, [1] phase-2
-                                       // arrivals, [2] ready gate, [3] reduced gate
+                                       // arrivals, [2] ready gate, [3] reduced gate,
+                                       // [4] snapshot arrivals
+    // the snapshot inside the launch (BatchArgs::snap): rb = sb, or rb = 0, whole bucket
+    const void *ssrc;                  // sb (nullptr: in place)
+    void *sdst;                        // rb
+    uint32_t svec, stail;              // 16-B vectors, bytes after them (svec 0 and stail 0:
+                                       // not eligible -- the host queues such snapshots)
 };
 
 // Kernel arguments: the entries of one launch, in issue-ring order.
@@ -67,6 +73,11 @@ struct BatchArgs {
     uint16_t sid[kBatchMax];
     uint32_t value[kBatchMax];         // the round of entry e
     long long timeout;                 // wall-clock ticks any flag wait may take
+    // snapshots done by the launch's own workers before the phases (ESGD_SNAPSHOT_IN_BATCH):
+    // entry e's kind (0 none / queued before the launch, 1 rb = sb, 2 rb = 0) and its
+    // 1024-vector tiles (prefix); the agent publishes e's ready once they have all landed
+    uint32_t tile0[kBatchMax + 1];
+    uint8_t snap[kBatchMax];
 };
 
 // The snapshots of a shared launch's rounds (rb = sb, or rb = 0 for a FRESH_ONLY round

@@ -5,14 +5,18 @@
 // worker that is not yet dispatched while the others spin would deadlock the launch.  The
 // host caps the grid so that every rank sharing this GPU fits (round_batch_capacity).
 //
-// Agent (wave 0 of the last block; lane e owns entry e):
+// Agent (wave 0 of block 0; lane e owns entry e):
 //   * publishes `ready` of every entry at once -- everything the entries' snapshots
 //     wrote was queued on the stream before this launch -- behind one system-scope
-//     release (L2 write-back) and a drain;
+//     release (L2 write-back) and a drain; an entry whose snapshot the workers do in this
+//     launch (phase 0) publishes once all its snapshot tiles have counted themselves;
 //   * polls every rank's ready / reduced flag of its entry (one system-scope load per rank,
 //     all lanes' loads in flight together) and raises the entry's device gates.
-// Workers walk a global tile list in ring order -- every entry's phase-1 tiles, then every
-// entry's phase-2 tiles -- tile g on worker 1 + g % workers:
+// Workers walk a global tile list in ring order -- every entry's snapshot tiles, then its
+// phase-1 tiles, then its phase-2 tiles -- tile g on worker 1 + g % workers:
+//   * phase 0 (snapshot, ESGD_SNAPSHOT_IN_BATCH): 1024 vectors of rb = sb or rb = 0,
+//     write-through, drained, counted -- no gate, so no worker waits before its own
+//     snapshot tiles are done;
 //   * phase 1 (reduce-scatter): wait for the entry's ready gate; fold one tile (tv1 16-B
 //     vectors) of shard `rank` of every rank's rb in the reference's tree order
 //     (ffallreduce.c:138-171 via tree_fold) into the local rb and the published shard;
@@ -66,12 +70,35 @@ __device__ void agent(const BatchArgs &a, long long t0) {
     const bool act = lane < int(a.nent);
     const BatchDesc *d = act ? &a.table[a.sid[lane]] : nullptr;
     const uint32_t v = act ? a.value[lane] : 0u;
+    // entries whose snapshot the workers do first wait for it (-1) before their ready
+    const uint32_t snaps = act && a.snap[lane] ? a.tile0[lane + 1] - a.tile0[lane] : 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: what the snapshots wrote
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (act) put_flags(d->ready, v);
-    int st = act ? 0 : 2;   // 0: waiting for every ready, 1: for every reduced, 2: done
+    if (act && !snaps) put_flags(d->ready, v);
+    int st = act ? (snaps ? -1 : 0) : 2;   // 0: waiting for every ready, 1: for every reduced, 2: done
     for (;;) {
-        if (st < 2) {
+        bool pub = false;   // this entry's snapshot has just landed
+        if (st == -1) {
+            // the snapshot tiles stored write-through and drained before counting: once all
+            // are counted the bucket is in memory, and the ready below follows a release
+            const uint32_t n = __hip_atomic_load(d->ctr + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (n >= snaps) {
+                __hip_atomic_store(d->ctr + 4, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                st = 0;
+                pub = true;
+            } else if (wall_clock64() - t0 > a.timeout) {
+                store_sys(d->err, v);
+                store_gate(d->ctr + 2, v, false);
+                store_gate(d->ctr + 3, v, false);
+                st = 2;
+            }
+        }
+        if (__any(pub)) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (pub) put_flags(d->ready, v);
+        if (st >= 0 && st < 2) {
             const uint32_t *f = st == 0 ? d->ready.mine : d->reduced.mine;
             uint32_t got[K];
 #pragma unroll
@@ -138,6 +165,30 @@ __device__ __forceinline__ void tile_reduce(const BatchDesc &d, uint32_t local) 
     }
 }
 
+// phase 0, tile `local` of an entry's snapshot: 1024 16-B vectors of rb = sb (kind 1) or
+// rb = 0 (kind 2), write-through; the ragged tail byte by byte in tile 0
+__device__ __forceinline__ void tile_snapshot(const BatchDesc &d, uint32_t local, uint8_t kind) {
+    const uint32_t nv = d.svec, v0 = local * 1024u;
+    const __amdgpu_buffer_rsrc_t wd = __builtin_amdgcn_make_buffer_rsrc(d.sdst, (short)0, int(nv * 16u), 0x00020000);
+    raw16 r[4];
+    if (kind == 1) {
+        const __amdgpu_buffer_rsrc_t rd =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(d.ssrc), (short)0, int(nv * 16u), 0x00020000);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b128(rd, (v0 + u * 256 + threadIdx.x) * 16, 0, 2);
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) r[u] = raw16{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(r[u], wd, (v0 + u * 256 + threadIdx.x) * 16, 0, 17);
+    if (local == 0 && threadIdx.x < d.stail) {
+        uint8_t *dst = static_cast<uint8_t *>(d.sdst) + size_t(nv) * 16;
+        const uint8_t b = kind == 1 ? static_cast<const uint8_t *>(d.ssrc)[size_t(nv) * 16 + threadIdx.x] : uint8_t(0);
+        __hip_atomic_store(dst + threadIdx.x, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // phase 2, tile `local` of an entry: tvg[sg] vectors of one peer's published shard
 __device__ __forceinline__ void tile_gather(const BatchDesc &d, uint32_t local) {
     uint32_t sg = 0;
@@ -176,16 +227,30 @@ __global__ __launch_bounds__(256) void k_round_batch(BatchArgs a) {
     // stale peer lines of earlier launches out of this CU's L1 and this XCD's L2
     if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     const uint32_t workers = gridDim.x - 1;
-    const uint32_t T1 = a.tile1[a.nent], T = T1 + a.tile2[a.nent];
+    // the tile list: every entry's snapshot tiles (phase 0), its phase-1 tiles, its phase-2
+    // tiles, each in ring order; a worker meets no gate before its snapshot tiles are done
+    const uint32_t T0 = a.tile0[a.nent], T1 = T0 + a.tile1[a.nent], T = T1 + a.tile2[a.nent];
     uint32_t e = 0;
-    bool gather = false;
+    int phase = 0;
     for (uint32_t g = blockIdx.x - 1; g < T; g += workers) {
-        if (!gather && g >= T1) { gather = true; e = 0; }
-        const uint32_t t = gather ? g - T1 : g;
-        const uint32_t *pre = gather ? a.tile2 : a.tile1;
+        const int ph = g < T0 ? 0 : g < T1 ? 1 : 2;
+        if (ph != phase) { phase = ph; e = 0; }
+        const uint32_t t = ph == 0 ? g : ph == 1 ? g - T0 : g - T1;
+        const uint32_t *pre = ph == 0 ? a.tile0 : ph == 1 ? a.tile1 : a.tile2;
         while (t >= pre[e + 1]) ++e;
         const BatchDesc &d = a.table[a.sid[e]];
         const uint32_t v = a.value[e];
+        if (ph == 0) {
+            tile_snapshot(d, t - pre[e], a.snap[e]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are in memory
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                if (d.strict) __hip_atomic_fetch_add(d.ctr + 4, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                else __hip_atomic_fetch_add(d.ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            continue;
+        }
+        const bool gather = ph == 2;
         if (threadIdx.x == 0) {
             const uint32_t *gate = d.ctr + (gather ? 3 : 2);
             while (!reached(__hip_atomic_load(const_cast<uint32_t *>(gate), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),

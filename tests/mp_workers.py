@@ -1151,7 +1151,7 @@ def gpu_stress_fresh(rank, world, kind, count, rounds=600, async_=3, seed=344956
 
 def gpu_stress_pipelined(rank, world, kind, counts=(4096, 65536, 17, (1 << 20) + 3, 300007, 1025, 65536 * 3,
                                                   (5 << 20) + 1), rounds=150, async_=3, seed=34495645,
-                         jitter_us=200, batch=None):
+                         jitter_us=200, batch=None, fail_exports=None):
     """The optimizer's pipelined per-tensor order under the activation stress: HOLD |
     FRESH_ONLY schedules (how the deep500 op drives them), every step writes each
     schedule's send bucket in the wrapper's racy order (after the release, right before
@@ -1160,13 +1160,16 @@ def gpu_stress_pipelined(rank, world, kind, counts=(4096, 65536, 17, (1 << 20) +
     differently on every rank, one five-launch size among them) while peers' activations
     carry ranks through rounds they have not posted.  A rank's share of every round must
     be its tag iff it had posted the round before joining it, never torn.  batch: rounds
-    per shared launch for this rank (a list: one value per rank)."""
+    per shared launch for this rank (a list: one value per rank).  fail_exports: per rank,
+    how many of its first chunk exports fail (ESGD_FAIL_EXPORTS, the runtime's refusals)."""
     import random
 
     import numpy as np
 
     from esgd import _lib
     from esgd import device as dev
+    if fail_exports is not None and fail_exports[rank]:
+        os.environ["ESGD_FAIL_EXPORTS"] = str(fail_exports[rank])
     comm = _comm()
     if batch is not None:
         comm.set_config("batch_rounds", batch[rank] if isinstance(batch, (list, tuple)) else batch)

@@ -25,6 +25,9 @@ def main():
                          "8 HOLD | FRESH_ONLY schedules posted at once every step; batch: rounds per shared "
                          "launch, 'mix' = 64/0/5/2 by rank) instead of the one-schedule stress")
     ap.add_argument("--strict", type=int, default=0, help="ESGD_STRICT_HANDOFFS for every rank")
+    ap.add_argument("--fail-exports", default=None,
+                    help="per rank, comma-separated: that many of its first chunk exports fail (the runtime's refusals)")
+    ap.add_argument("--kinds", default="solo,majority")
     a = ap.parse_args()
     os.environ["ESGD_STRICT_HANDOFFS"] = str(a.strict)
     if a.pipelined:
@@ -57,9 +60,13 @@ def pipelined(a):
         w, b = cfg.split(":")
         world = int(w)
         batch = None if b == "default" else ([64, 0, 5, 2] * 2)[:world] if b == "mix" else int(b)
+        fails = [int(x) for x in a.fail_exports.split(",")][:world] if a.fail_exports else None
         for kind, kname in ((1, "solo"), (2, "majority")):
+            if kname not in a.kinds.split(","):
+                continue
             t0 = time.time()
-            outs = run("gpu_stress_pipelined", world, kind=kind, rounds=a.rounds, batch=batch, timeout=900)
+            outs = run("gpu_stress_pipelined", world, kind=kind, rounds=a.rounds, batch=batch, timeout=900,
+                       fail_exports=fails)
             bits = outs[0]["bits"]
             bad = sum(len(o["torn"]) for o in outs) + sum(o["vals"] != outs[0]["vals"] for o in outs)
             for i in range(len(outs[0]["vals"])):
@@ -70,7 +77,7 @@ def pipelined(a):
                         bad += ((v >> (bits * q)) & ((1 << bits) - 1)) != want
             print(json.dumps({"stress": "pipelined", "world": world, "batch": b, "kind": kname,
                               "steps": a.rounds, "rounds": a.rounds * len(outs[0]["vals"]),
-                              "strict": a.strict, "bad": int(bad), "auto_rounds": sum(o["auto_rounds"] for o in outs),
+                              "strict": a.strict, "fail_exports": a.fail_exports, "bad": int(bad), "auto_rounds": sum(o["auto_rounds"] for o in outs),
                               "wall_s": round(time.time() - t0, 1)}), flush=True)
 
 
