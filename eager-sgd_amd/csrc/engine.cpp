@@ -327,6 +327,13 @@ static int activator_of(SchedShm *sh, uint32_t round) {
     return (v >> 32) == round ? int(v & 0xffffffffu) - 1 : -1;
 }
 
+static bool step(Sched &s, bool join_only);
+
+static bool inline_join() {
+    static const bool on = !(getenv("ESGD_INLINE_JOIN") && *getenv("ESGD_INLINE_JOIN") == '0');
+    return on;
+}
+
 int sched_post(Sched *s, void *producer_stream, int *role) {
     ESGD_ARG(s, "schedule post: null schedule");
     int r = 0;
@@ -371,6 +378,13 @@ int sched_post(Sched *s, void *producer_stream, int *role) {
             if (won) ++s->n_activated;
         }
     }
+    // the round this post makes due is joined right here, on the caller's thread, instead
+    // of at the progress thread's next pass (ESGD_INLINE_JOIN=0: always there): the join is
+    // per-schedule work under its mutex plus the issue-ring append (atomics), and joining at
+    // the post takes it off the progress thread, which then only launches.  Device buckets
+    // without FFCOLL_BUFFERS only (a host bucket's join stages the bucket; a resolve
+    // schedule's re-resolves it).
+    if (inline_join() && !s->resolve && !s->host_mode) (void)step(*s, true);
     seg_wake(g_seg);
     if (role) *role = r;
     return ESGD_SUCCESS;
@@ -486,9 +500,12 @@ Sched *sched_lookup(uint64_t handle) {
 
 // ---- the progress step -------------------------------------------------------------
 
-static bool step(Sched &s) {
+// join_only: only the IDLE -> joined transition (a caller's thread joining the round it
+// has just posted, sched_post); every other stage is left to the progress thread
+static bool step(Sched &s, bool join_only = false) {
     std::lock_guard<std::mutex> lk(s.mu);
     if (s.error || !s.live.load()) { s.awaiting = false; return false; }
+    if (join_only && s.stage != ST_IDLE) return false;
     SchedShm *sh = s.sh;
     auto enter = [&](Stage st) { s.stage = st; s.stage_t0 = now_s(); };
     auto check = [&](int rc, const char *what) {

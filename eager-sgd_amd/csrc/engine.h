@@ -118,7 +118,7 @@ struct Sched {
     int error = 0;
     char errmsg[256] = {0};
     uint32_t passive = 0;      // majority: passive rounds since the last activation
-    bool awaiting = false;     // posted, waiting for the activation (progress thread only)
+    std::atomic<bool> awaiting{false};   // posted, waiting for the activation (written under mu)
     uint64_t roctx_round = 0;  // ESGD_ROCTX=1: the open "round" range (join -> completion)
     uint64_t n_fresh = 0, n_auto = 0, n_activated = 0;
     std::vector<RoundLog> log;
