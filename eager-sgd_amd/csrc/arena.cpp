@@ -48,10 +48,15 @@ namespace esgd {
 
 namespace {
 
-constexpr size_t kSlab = size_t(2) << 20;
+// Large blocks come in 2 MiB granules; small-class blocks (4 KiB - 1 MiB) are carved from
+// 4 MiB slabs.  Every runtime refusal of an export seen so far (rounds 3-4) was of an
+// allocation of exactly 2 MiB, so with the seal on no chunk is that size: a slab is 4 MiB,
+// a large chunk has its seal granule on top.
+constexpr size_t kGranule = size_t(2) << 20;
+constexpr size_t kSlab = size_t(4) << 20;
 size_t alloc_bytes(size_t usable);
 bool seal_on();
-// what a small-class slab hands out: its last 4 KiB hold the seal (2 MiB allocations)
+// what a small-class slab hands out: its last 4 KiB hold the seal
 size_t slab_usable() { return seal_on() ? kSlab - kSealBytes : kSlab; }
 constexpr size_t kMinBlock = 4096;
 
@@ -141,13 +146,12 @@ bool seal_on() {
 }
 
 // A chunk of `usable` bytes is one hipMalloc of whole 2 MiB granules with room for the
-// seal right behind the usable bytes: whole granules keep the arena's layout
-// what it is without the seal (measured the same, round 4 r04m).  Slabs keep 2 MiB
-// allocations by giving up their last 4 KiB (kSlabUsable); a large chunk gets a granule
-// more than its blocks.
+// seal right behind the usable bytes (whole granules: measured the same as without the
+// seal, round 4 r04m).  A slab gives up its last 4 KiB (slab_usable); a large chunk gets a
+// granule more than its blocks.
 size_t alloc_bytes(size_t usable) {
     if (!seal_on()) return usable;
-    return (usable + kSealBytes + kSlab - 1) / kSlab * kSlab;
+    return (usable + kSealBytes + kGranule - 1) / kGranule * kGranule;
 }
 
 // Nothing free fits.  Idle chunks no peer ever mapped go back to the driver first only
@@ -203,7 +207,7 @@ int arena_alloc(size_t bytes, void **out, bool release_idle_chunks) {
         *out = c->base;
         return ESGD_SUCCESS;
     }
-    if (bytes <= kSlab / 2) {
+    if (bytes <= kGranule / 2) {
         const size_t cls = small_class(bytes);
         auto &fl = g_small[{dev, cls}];
         if (fl.empty()) {
@@ -223,7 +227,7 @@ int arena_alloc(size_t bytes, void **out, bool release_idle_chunks) {
         *out = p;
         return ESGD_SUCCESS;
     }
-    const size_t need = (bytes + kSlab - 1) / kSlab * kSlab;
+    const size_t need = (bytes + kGranule - 1) / kGranule * kGranule;
     char *p = nullptr;
     Chunk *c = nullptr;
     auto it = g_large.lower_bound({dev, need});
@@ -261,7 +265,7 @@ bool arena_free(void *p) {
         if (!b.chunk->live) release_chunk(b.chunk);
         return true;
     }
-    if (b.cls <= kSlab / 2) {
+    if (b.cls <= kGranule / 2) {
         g_small[{b.chunk->device, b.cls}].push_back(static_cast<char *>(p));
         return true;
     }
@@ -459,14 +463,14 @@ void arena_warm() {
     static std::atomic<bool> done{false};
     if (done.exchange(true)) return;
     void *p = nullptr;
-    if (arena_alloc(kSlab, &p) != ESGD_SUCCESS) {
+    if (arena_alloc(kGranule, &p) != ESGD_SUCCESS) {
         clear_error();
         return;
     }
     void *base = nullptr;
     uint64_t off = 0;
     uint8_t h[64];
-    if (export_impl(p, kSlab, &base, &off, h, false) == ESGD_SUCCESS) {
+    if (export_impl(p, kGranule, &base, &off, h, false) == ESGD_SUCCESS) {
         arena_free(p);
         return;
     }
