@@ -1151,7 +1151,7 @@ def gpu_stress_fresh(rank, world, kind, count, rounds=600, async_=3, seed=344956
 
 def gpu_stress_pipelined(rank, world, kind, counts=(4096, 65536, 17, (1 << 20) + 3, 300007, 1025, 65536 * 3,
                                                   (5 << 20) + 1), rounds=150, async_=3, seed=34495645,
-                         jitter_us=200, batch=None, fail_exports=None):
+                         jitter_us=200, batch=None, fail_exports=None, env=None):
     """The optimizer's pipelined per-tensor order under the activation stress: HOLD |
     FRESH_ONLY schedules (how the deep500 op drives them), every step writes each
     schedule's send bucket in the wrapper's racy order (after the release, right before
@@ -1170,6 +1170,7 @@ def gpu_stress_pipelined(rank, world, kind, counts=(4096, 65536, 17, (1 << 20) +
     from esgd import device as dev
     if fail_exports is not None and fail_exports[rank]:
         os.environ["ESGD_FAIL_EXPORTS"] = str(fail_exports[rank])
+    os.environ.update(env or {})   # data-plane switches, read at their first use
     comm = _comm()
     if batch is not None:
         comm.set_config("batch_rounds", batch[rank] if isinstance(batch, (list, tuple)) else batch)

@@ -527,6 +527,27 @@ def test_pipelined_stress_batched(kind, world, batch):
     assert sum(o["auto_rounds"] for o in outs) > 0
 
 
+@pytest.mark.parametrize("env", [{"ESGD_BATCH_DEPTH": "0"}, {"ESGD_BATCH_DEPTH": "3"},
+                                 {"ESGD_SNAPSHOT_IN_BATCH": "0"}, {"ESGD_INLINE_JOIN": "0"}],
+                         ids=["depth0", "depth3", "copy_kernel_snapshots", "progress_thread_joins"])
+def test_pipelined_stress_switches(env):
+    # the batched stress under each data-plane switch's other setting (the defaults run in
+    # test_pipelined_stress_batched): launches never held / held behind three, snapshots by
+    # a k_copy_many launch, every join on the progress thread
+    world = 4
+    outs = run("gpu_stress_pipelined", world, kind=SOLO, rounds=60, batch=[64, 0, 5, 2], env=env, timeout=300)
+    bits = outs[0]["bits"]
+    for o in outs:
+        assert not o["torn"], o["torn"]
+        assert o["vals"] == outs[0]["vals"]
+    for i in range(len(outs[0]["vals"])):
+        for t in range(1, len(outs[0]["vals"][i]) + 1):
+            v = outs[0]["vals"][i][t - 1]
+            for q in range(world):
+                want = t % (1 << bits) if outs[q]["fresh"][i][t - 1] else 0
+                assert (v >> (bits * q)) & ((1 << bits) - 1) == want, (i, t, q)
+
+
 @pytest.mark.parametrize("kind", [SOLO, MAJORITY])
 def test_schedule_churn_under_stress(kind):
     # temporary schedules (16 KiB .. 64 MiB) created, used and deleted every 20 steps
