@@ -49,9 +49,8 @@ namespace esgd {
 namespace {
 
 // Large blocks come in 2 MiB granules; small-class blocks (4 KiB - 1 MiB) are carved from
-// 4 MiB slabs.  Every runtime refusal of an export seen so far (rounds 3-4) was of an
-// allocation of exactly 2 MiB, so with the seal on no chunk is that size: a slab is 4 MiB,
-// a large chunk has its seal granule on top.
+// 4 MiB slabs (fewer chunks to export and map; the runtime's export refusals, first seen on
+// 2 MiB allocations, hit 4 MiB slabs too -- round 4, r04soak -- so size is not their cause).
 constexpr size_t kGranule = size_t(2) << 20;
 constexpr size_t kSlab = size_t(4) << 20;
 size_t alloc_bytes(size_t usable);
