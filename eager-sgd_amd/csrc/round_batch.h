@@ -6,9 +6,9 @@
 // Run one kernel launch and two rank pairings per round, that call pattern pays a host
 // launch and two flag round trips per bucket.  The data plane instead gathers the
 // one-launch rounds that are due in the node's issue order (engine.cpp) into one launch:
-// a flag-agent wave publishes every entry's `ready` at once and turns peers' flags into
-// device gates, while worker workgroups walk the entries' phase-1 tiles, then their
-// phase-2 tiles, in ring order.  Per-entry semantics are those of k_round_small: the same
+// a flag-agent wave publishes each entry's `ready` (once the entry's snapshot has landed)
+// and turns peers' flags into device gates, while worker workgroups walk the entries'
+// snapshot tiles, phase-1 tiles, then phase-2 tiles, in ring order.  Per-entry semantics are those of k_round_small: the same
 // flags, counters, published shard, fin word and tree order -- only the launch is shared.
 #pragma once
 
