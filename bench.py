@@ -675,6 +675,17 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
     finally:
         comm.set_config("batch_rounds", -1)
     t1 = _timed_steps(comm, fused_step, steps)
+    # A/B of the host path's switches, each against the defaults above
+    ab = {}
+    for key, val, what, fn in (("batch_depth", 0, "pipelined_batch_depth0_ms", pipelined),
+                               ("inline_join", 0, "pipelined_progress_thread_joins_ms", pipelined),
+                               ("inline_join", 0, "chain_progress_thread_joins_ms", chain)):
+        comm.set_config(key, val)
+        try:
+            fn()
+            ab[what] = round(_timed_steps(comm, fn, steps) * 1e3, 3)
+        finally:
+            comm.set_config(key, -1)
     variants = _op_like_variants(comm, dev, lengths, steps)
     for s, b in zip(scheds, bufs):
         _defer(s, b)
@@ -690,6 +701,7 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
             "step_ms_161_buckets_pipelined_one_launch_per_round": round(t161u * 1e3, 3),
             "rank0_pipelined_step_us_one_launch_per_round": breakdown_u,
             "rank0_progress_thread_per_step_one_launch_per_round": prof_u,
+            "ab_host_path_switches": ab,
             "op_like_pipelined_variants": variants}
 
 

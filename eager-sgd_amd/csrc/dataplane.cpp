@@ -111,6 +111,16 @@ static int device_flags_env() {
 // All ranks must set the same values before the same creations (the creation signature
 // checks it), so a benchmark can A/B them inside one job.
 static std::atomic<int64_t> g_cfg_small{-1}, g_cfg_flags{-1}, g_cfg_strict{-1}, g_cfg_batch{-1};
+// process-local switches of the host path (-1 = the env default), read where they act:
+// batch_depth (ESGD_BATCH_DEPTH), snapshot_in_batch (ESGD_SNAPSHOT_IN_BATCH), inline_join
+// (ESGD_INLINE_JOIN, engine.cpp)
+static std::atomic<int64_t> g_cfg_depth{-1}, g_cfg_snap{-1}, g_cfg_inline{-1};
+
+bool config_inline_join() {
+    static const bool env = !(getenv("ESGD_INLINE_JOIN") && *getenv("ESGD_INLINE_JOIN") == '0');
+    const int64_t v = g_cfg_inline.load(std::memory_order_relaxed);
+    return v >= 0 ? v != 0 : env;
+}
 
 // One-launch rounds due together in issue order share one launch of at most this many
 // rounds (k_round_batch, round_batch.hip); 0 or 1 = one k_round_small launch per round.
@@ -164,13 +174,25 @@ int config_set(const char *key, int64_t value) {
         ESGD_ARG(value >= -1 && value <= kBatchMax, "batch_rounds: 0..%d rounds per launch (-1: the default)",
                  kBatchMax);
         g_cfg_batch.store(value);
+    } else if (!std::strcmp(key, "batch_depth")) {
+        ESGD_ARG(value >= -1, "batch_depth: >= 0 shared launches queued before one is held (-1: the default)");
+        g_cfg_depth.store(value);
+    } else if (!std::strcmp(key, "snapshot_in_batch")) {
+        ESGD_ARG(value >= -1 && value <= 1, "snapshot_in_batch: 0 or 1 (-1: the default)");
+        g_cfg_snap.store(value);
+    } else if (!std::strcmp(key, "inline_join")) {
+        ESGD_ARG(value >= -1 && value <= 1, "inline_join: 0 or 1 (-1: the default)");
+        g_cfg_inline.store(value);
     } else {
         set_error("esgd_set_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
-                  "batch_rounds)", key);
+                  "batch_rounds, batch_depth, snapshot_in_batch, inline_join)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
 }
+
+static int batch_depth();
+static bool snapshot_in_batch();
 
 int config_get(const char *key, int64_t *value) {
     ESGD_ARG(key && value, "esgd_get_config: null argument");
@@ -180,9 +202,12 @@ int config_get(const char *key, int64_t *value) {
     else if (!std::strcmp(key, "batch_rounds")) *value = batch_rounds();
     else if (!std::strcmp(key, "launches")) *value = int64_t(g_launches.load());
     else if (!std::strcmp(key, "batch_workers")) *value = g_batch_workers.load();
+    else if (!std::strcmp(key, "batch_depth")) *value = batch_depth();
+    else if (!std::strcmp(key, "snapshot_in_batch")) *value = snapshot_in_batch() ? 1 : 0;
+    else if (!std::strcmp(key, "inline_join")) *value = config_inline_join() ? 1 : 0;
     else {
         set_error("esgd_get_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
-                  "batch_rounds, launches, batch_workers)", key);
+                  "batch_rounds, launches, batch_workers, batch_depth, snapshot_in_batch, inline_join)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -1040,8 +1065,9 @@ struct BatchEntry {
 // ESGD_SNAPSHOT_IN_BATCH (default 1): a batched round's snapshot is phase 0 of the shared
 // launch itself instead of a k_copy_many launch queued before it (one launch per flush)
 static bool snapshot_in_batch() {
-    static const bool on = !(getenv("ESGD_SNAPSHOT_IN_BATCH") && *getenv("ESGD_SNAPSHOT_IN_BATCH") == '0');
-    return on;
+    static const bool env = !(getenv("ESGD_SNAPSHOT_IN_BATCH") && *getenv("ESGD_SNAPSHOT_IN_BATCH") == '0');
+    const int64_t v = g_cfg_snap.load(std::memory_order_relaxed);
+    return v >= 0 ? v != 0 : env;
 }
 
 // the whole-bucket snapshot fits the kernel's 32-bit buffer ranges and 16-B vectors
@@ -1062,11 +1088,12 @@ static std::deque<std::shared_ptr<hipEvent_t>> g_outstanding;
 // pipelined step 0.75-0.83 -> 0.66-0.71 ms at P = 2, 1.26-1.52 -> 0.97-0.99 ms at P = 4;
 // the optimizer's per-tensor step unchanged within noise; depth 2 and 3 slowed it at P = 4).
 static int batch_depth() {
-    static const int v = [] {
+    static const int env = [] {
         const char *e = getenv("ESGD_BATCH_DEPTH");
         return e ? std::max(0, atoi(e)) : 1;
     }();
-    return v;
+    const int64_t v = g_cfg_depth.load(std::memory_order_relaxed);
+    return v >= 0 ? int(v) : env;
 }
 
 // this schedule's BatchDesc: built at its first batched round and uploaded on the round

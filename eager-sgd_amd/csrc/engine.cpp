@@ -329,10 +329,7 @@ static int activator_of(SchedShm *sh, uint32_t round) {
 
 static bool step(Sched &s, bool join_only);
 
-static bool inline_join() {
-    static const bool on = !(getenv("ESGD_INLINE_JOIN") && *getenv("ESGD_INLINE_JOIN") == '0');
-    return on;
-}
+static bool inline_join() { return config_inline_join(); }
 
 int sched_post(Sched *s, void *producer_stream, int *role) {
     ESGD_ARG(s, "schedule post: null schedule");

@@ -231,6 +231,7 @@ void dataplane_shutdown();
 // it after every pump of the issue ring, transports before queuing anything else
 int dataplane_flush();
 int dataplane_flush_soft();
+bool config_inline_join();   // esgd_set_config("inline_join") / ESGD_INLINE_JOIN
 void dataplane_extra_queues(int n);   // diagnostics: n more streams, each with a queue   // the end of a pump: flush unless ESGD_BATCH_DEPTH launches are queued
 // esgd_schedule_post_group / _release_group: until the end call, this thread's posts
 // (which 0) or releases (1) on `stream` share ONE event recording

@@ -89,6 +89,25 @@ def test_data_plane_config_keys():
     assert comm.get_config("device_flags") == int(os.environ.get("ESGD_DEVICE_FLAGS", 0))
 
 
+def test_host_path_switches():
+    # the process-local switches of the host path: settable at run time (the bench A/Bs
+    # them inside one job), -1 restores the env default
+    from esgd import _lib, comm  # noqa: F401
+    lib = _lib.lib()
+    defaults = {"batch_depth": 1, "snapshot_in_batch": 1, "inline_join": 1}
+    for key, bad in (("batch_depth", -2), ("snapshot_in_batch", 2), ("inline_join", 2)):
+        assert lib.esgd_set_config(key.encode(), bad) == _lib.INVALID_ARG
+    try:
+        for key, v in (("batch_depth", 3), ("snapshot_in_batch", 0), ("inline_join", 0)):
+            comm.set_config(key, v)
+            assert comm.get_config(key) == v
+    finally:
+        for key in defaults:
+            comm.set_config(key, -1)
+    for key, v in defaults.items():
+        assert comm.get_config(key) == v
+
+
 def test_op_error_policy_argument_checks():
     from esgd import _lib, deep500
     lib = _lib.lib()
