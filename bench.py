@@ -717,9 +717,9 @@ def _op_like_variants(comm, dev, lengths, steps):
             ("hold_fresh_group", False, hf, None, None),
             ("separate_sb", True, 0, None, None),
             ("separate_sb_hold_fresh_group", True, hf, None, None),
-            ("separate_sb_hold_fresh_group_null_stream", True, hf, 0, 0),
-            ("separate_sb_hold_fresh_group_null_producer_only", True, hf, 0, None),
-            ("separate_sb_hold_fresh_group_null_consumer_only", True, hf, None, 0)):
+            ("separate_sb_hold_fresh_group_null_stream", True, hf, 0, 0)):
+        # (producer-only / consumer-only NULL-stream variants: profiles/r04/extra_queues_ab/;
+        # every variant is 161 more schedules of the job's 2048)
         rbs = [dev.DeviceBuffer(n) for n in lengths]
         sbs = [dev.DeviceBuffer(n) for n in lengths] if sep else [None] * len(lengths)
         for b in (sbs if sep else rbs):
