@@ -708,8 +708,9 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
 def _op_like_variants(comm, dev, lengths, steps):
     """The pipelined 161-bucket step with the deep500 op's schedule properties added one at
     a time (what separates this leg's step from the optimizer's): HOLD | FRESH_ONLY with
-    group post / release; a separate send bucket (the snapshot copies it into rb); both.
-    Per variant: ms per step and rank 0's timeline breakdown."""
+    group post / release; a separate send bucket (the snapshot copies it into rb); both;
+    both with the legacy NULL stream as the producer and consumer stream (torch's default).
+    Per variant: ms per step, rank 0's timeline breakdown and progress-thread profile."""
     import torch
     out = {}
     hf = comm.HOLD | comm.FRESH_ONLY
