@@ -60,8 +60,20 @@ def emit(line: dict) -> None:
         os.write(_LINE_FD, text.encode())
 
 
+LEGS_HELP = """N > 1 extra legs (after the C3 headline, under a watchdog; ESGD_BENCH_LEGS=a,b picks a
+subset in that order): sweep_c5_majority, sweep_c5_majority_bf16, ab_one_launch_threshold,
+c3_wire_bf16, c1_host_majority, small_round_after_idle, straggler_c4_majority,
+c4_resnet50_161_vs_fused, optimizer_resnet50_161, c3_host_buckets, c3_rccl_transport,
+rccl_as_default_c3_c4, ab_flag_pages.  rccl_as_default_c3_c4 is the one-shot head-to-head of
+the north star's named data plane: RCCL P2P (grouped ncclSend/ncclRecv + the tree kernel on
+a side stream) set as the transport of C3 (solo, 256 MiB per GPU) and C4 (majority, the
+ResNet-50 fused gradient, one rank 0.2 T late), against the IPC-pull numbers of the same job
+(the headline and straggler_c4_majority).  It needs one GPU per rank: with ranks sharing a
+GPU (a 1-GPU rehearsal) it is skipped and says why.  ESGD_BENCH_RCCL=0 skips both RCCL legs."""
+
+
 def parse():
-    ap = argparse.ArgumentParser()
+    ap = argparse.ArgumentParser(epilog=LEGS_HELP, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
@@ -113,17 +125,26 @@ def _cpu_model():
 
 
 def cpu_baseline(k: int, count: int):
-    """fflib2's recursive doubling restated (oracle/ffref.c), one pthread per simulated
-    rank, on this host: the reference's CPU path for the same k x bucket workload."""
+    """fflib2 restated (oracle/ffref.c) on this host for the same k x bucket workload, with
+    the core budget SURVEY.md §8(d) gives the reference: 2 cores per rank -- each simulated
+    rank a main thread (the wrapper's copy-in, post, spin-wait, copy-out, zeroing of the
+    send bucket) and a progress thread (the move + recursive doubling with VSUM; ff.c:72's
+    pthread), 2k threads in all.  Also reported: the recursive doubling alone, one pthread
+    per rank (the round-4 figure)."""
     from oracle import ffref
-    threads = k
-    t1 = ffref.time_allreduce(k, count, threads, 1)          # warm + size the sample
-    reps = max(1, min(250, int(10.0 / max(t1, 1e-3))))   # ~10 s of CPU work
-    t = ffref.time_allreduce(k, count, threads, reps)
-    gbs = k * count * 4 / t / 1e9
-    return {"value": round(gbs, 3), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"full workload: {k}-rank recursive-doubling allreduce of {count*4/MiB:.0f} MiB "
-                      f"fp32 (oracle/ffref.c, 1 pthread/rank, best of {reps}; {t*1e3:.1f} ms each)",
+    t1, _ = ffref.time_c1(k, count, 2)                       # warm + size the sample
+    reps = max(3, min(250, int(10.0 / max(t1, 1e-3))))   # ~10 s of CPU work
+    t, ok = ffref.time_c1(k, count, reps)
+    t_rd1 = ffref.time_allreduce(k, count, k, max(1, reps // 2))
+    return {"value": round(k * count * 4 / t / 1e9, 3), "unit": "GB/s", "cores": 2 * k, "kind": "port",
+            "sample": f"full workload: {k} ranks x {count * 4 / MiB:.0f} MiB fp32, each a main thread (copy-in, "
+                      f"post, wait, copy-out, zero) + a progress thread (move + recursive doubling, VSUM) = "
+                      f"{2 * k} threads (oracle/ffref.c ffref_time_c1), median step of {reps}: {t * 1e3:.1f} ms",
+            "correct": ok,
+            "recursive_doubling_only_1_thread_per_rank": {
+                "value": round(k * count * 4 / t_rd1 / 1e9, 3), "cores": k,
+                "sample": f"{k}-rank recursive doubling alone (1 pthread/rank), best of {max(1, reps // 2)}: "
+                          f"{t_rd1 * 1e3:.1f} ms"},
             "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
 
 
@@ -828,7 +849,11 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
     opts = []
     side = None   # created for its variant only: one more stream is one more hardware queue,
     #               which on a GPU shared by the ranks changes the timings
-    for name, kw in (("per_tensor_pipelined", dict(fuse=False)), ("per_tensor_blocking", dict(pipeline=False)),
+    for name, kw in (("per_tensor_pipelined", dict(fuse=False)),
+                     # the same with copy-in / copy-out kernels on the caller's stream instead of
+                     # the rounds' own I/O (esgd_schedule_post_io): the A/B of the fused path
+                     ("per_tensor_pipelined_copy_kernels", dict(fuse=False, fused_io=False)),
+                     ("per_tensor_blocking", dict(pipeline=False)),
                      ("fused", dict(fuse=True)), ("per_tensor_blocking_side_stream", dict(pipeline=False))):
         if name.endswith("_side_stream") and side is None:
             side = torch.cuda.Stream()
@@ -854,6 +879,8 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
         if name != "fused":
             out[name + "_breakdown_us"] = _optimizer_breakdown(opt, steps, side if name.endswith("_side_stream") else None)
             out[name + "_rank0_step_us"] = _step_breakdown_us([op.schedule() for op in opt._ops.values()])
+        else:
+            out["fused_breakdown_us"] = _fused_breakdown(comm, opt, params, steps)
         if name == "per_tensor_pipelined":
             comm.set_config("batch_rounds", 0)
             try:
@@ -868,6 +895,63 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
 
 
 _OPTS = []
+
+
+def _fused_breakdown(comm, opt, params, steps):
+    """Where the fused optimizer step's time goes (EagerSGDOptimizer(fuse=True)): each part
+    timed alone on this rank, median over `steps`, against the whole step -- the pack of the
+    161 gradients (divided by P) into the bucket and the unpack back (torch events on the
+    caller's stream around one launch group each), the fused bucket's round alone (post ->
+    wait on its schedule, wall, max over ranks), the wrapped SGD step (events), and
+    apply_gradients + synchronize (wall, max over ranks).  The parts' sum against the step
+    is the host / launch overhead between them."""
+    import statistics
+
+    import torch
+
+    from esgd import _lib
+    from esgd import device as dev
+    from esgd._lib import check, lib
+    layout, op = opt._fused
+    total = sum(n for _, n in layout)
+    grads = [p.grad for p in reversed(params)]
+    bucket = torch.empty(total, device=grads[0].device)
+    counts = [g.numel() for g in grads]
+    stream = torch.cuda.current_stream()
+
+    def gpu_ms(fn):
+        ts = []
+        for _ in range(steps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            fn()
+            b.record(stream)
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b))
+        return statistics.median(ts)
+
+    pack = gpu_ms(lambda: dev.pack_div(grads, counts, bucket, float(comm.world()), stream.cuda_stream or 1))
+    unpack = gpu_ms(lambda: dev.unpack(grads, counts, bucket, stream.cuda_stream or 1))
+    sgd = gpu_ms(lambda: opt.optimizer.step())
+    h = C_u64(op.schedule())
+
+    def one_round():
+        check(lib().esgd_schedule_post(h, None, None), "post")
+        check(lib().esgd_schedule_wait(h), "wait")
+        check(lib().esgd_schedule_release(h, None), "release")
+
+    rnd = _timed_steps(comm, one_round, steps)
+    whole = _timed_steps(comm, lambda: (opt.step(), torch.cuda.synchronize()), steps)
+    parts = pack + unpack + sgd + rnd * 1e3
+    return {"pack_div_gpu": round(pack * 1e3, 1), "round_wall": round(rnd * 1e6, 1),
+            "unpack_gpu": round(unpack * 1e3, 1), "sgd_step_gpu": round(sgd * 1e3, 1),
+            "step_wall": round(whole * 1e6, 1), "parts_sum": round(parts * 1e3, 1),
+            "overhead": round((whole * 1e3 - parts) * 1e3, 1), "fp32_elements": total}
+
+
+def C_u64(v):
+    import ctypes as C
+    return C.c_uint64(v)
 
 
 def _optimizer_breakdown(opt, steps, stream=None):
@@ -984,6 +1068,58 @@ def c3_over_rccl(comm, dev, rank, world, count, steps=20):
             "wire_bf16": {"round_ms_median": round(tw * 1e3, 4), "value_GBs": round(world * S / tw / 1e9, 2),
                           "xgmi_frac": round(t_min / 2 / tw, 4),
                           "parity_rank_slice": "bitwise" if okw else "MISMATCH"}}
+
+
+def rccl_as_default_c3_c4(comm, dev, rank, world, count, ipc_c3_ms, ipc_c4, steps=10):
+    """C3 and C4 with RCCL P2P as the transport every schedule of the leg is created with
+    (esgd_set_transport("rccl")) -- the data plane the north star names -- head to head with
+    the IPC pull numbers of this job: C3 = solo rounds of one 256 MiB fp32 bucket per GPU
+    (the headline's shape), C4 = majority rounds of the ResNet-50 fused gradient with the
+    last rank 0.2 T late (straggler_c4's shape and contributor check).  One GPU per rank."""
+    import numpy as np
+
+    from oracle import ffref
+    if SHARED_GPU:
+        return {"skipped": "ranks share a GPU (a 1-GPU rehearsal): RCCL refuses two ranks on one device, so "
+                           "RCCL cannot be any schedule's transport here; the leg runs with one GPU per rank"}
+    comm.set_transport("rccl")
+    try:
+        rb = dev.DeviceBuffer(count)
+        dev.fill_uniform(rb, SEED, rank)
+        dev.synchronize()
+        sch = comm.Schedule(comm.SOLO, None, rb, count, async_=32, seed=6545343, buf=comm.BUF_DEVICE)
+
+        def step():
+            sch.post()
+            sch.wait()
+
+        for _ in range(3):
+            step()
+        t = _timed_steps(comm, step, steps)
+        dev.fill_uniform(rb, SEED + 3, rank)
+        dev.synchronize()
+        comm.barrier()
+        step()
+        m = min(count, 1 << 18)
+        got = rb.download()[:m]
+        ok = bool(np.array_equal(got.view(np.uint32),
+                                 ffref.tree_sum([ffref.fill_uniform(SEED + 3, r, m) for r in range(world)]).view(
+                                     np.uint32)))
+        sch.delete()
+        rb.close()
+        c4 = straggler_c4(comm, dev, rank, world, rounds=8, delay_fracs=(0.2,))
+    finally:
+        comm.set_transport("ipc")
+    S = count * 4
+    t_min = 2 * S / (world * XGMI_LINK_GBS * 1e9)
+    ipc4 = (ipc_c4 or {}).get("delay_0.2T", {})
+    return {"c3": {"round_ms_median": round(t * 1e3, 4), "value_GBs": round(world * S / t / 1e9, 2),
+                   "xgmi_frac": round(t_min / t, 4), "parity_head_slice": "bitwise" if ok else "MISMATCH",
+                   "ipc_pull_round_ms": ipc_c3_ms,
+                   "rccl_over_ipc_time": round(t * 1e3 / ipc_c3_ms, 3) if ipc_c3_ms else None},
+            "c4": {"T_no_straggler_ms": c4["T_no_straggler_ms"], "delay_0.2T": c4["delay_0.2T"],
+                   "ipc_pull_T_no_straggler_ms": (ipc_c4 or {}).get("T_no_straggler_ms"),
+                   "ipc_pull_on_time_ranks_median_ms": ipc4.get("on_time_ranks_median_ms")}}
 
 
 def c3_wire_bf16(comm, dev, rank, world, count, steps=20):
@@ -1422,6 +1558,8 @@ def run_allreduce(args, rank, world):
                                                                   int(args.bucket_mib * MiB) // 4))]
         if os.environ.get("ESGD_BENCH_RCCL", "1") == "1":
             legs.append(("c3_rccl_transport", lambda: c3_over_rccl(comm, dev, rank, world, count)))
+            legs.append(("rccl_as_default_c3_c4", lambda: rccl_as_default_c3_c4(
+                comm, dev, rank, world, count, round(t_step * 1e3, 4), extras.get("straggler_c4_majority"))))
         # last: device flag pages have never run across GPUs; a hang there costs the
         # round timeout, and no other leg is lost to it
         legs.append(("ab_flag_pages", lambda: ab_flag_pages(comm, dev, world)))

@@ -24,7 +24,8 @@
 // fragmentation), not by the number of distinct sizes ever used.  Chunks that were never
 // exported and hold no live block go back to the driver when a caller's allocation needs
 // a new chunk (never on the progress thread: new_chunk), on out-of-memory, and at finalize
-// (arena_trim).  Exported chunks stay until the process exits, so their
+// (arena_trim).  Exported chunks -- and chunks whose export the runtime refused, which are
+// quarantined -- stay until the process exits, so their
 // total is the sum of the successive record bucket sizes (below 2x the largest bucket for
 // C5's doubling sweep; one 8 GiB bucket reserves 8 GiB for good).
 #include <hip/hip_runtime.h>
@@ -130,11 +131,14 @@ void release_chunk(Chunk *c) {
     delete c;
 }
 
-// chunks never exported and holding no live block (dev < 0: every device)
+// chunks never offered for export and holding no live block (dev < 0: every device).  A
+// chunk the runtime refused to export stays too (quarantine): the runtime has seen an
+// export of that range, and a later hipMalloc handing the same VA to a chunk that IS
+// exported is the reuse pattern that mapped peers to the wrong memory.
 void release_idle(int dev) {
     std::vector<Chunk *> idle;
     for (Chunk *c : g_chunks)
-        if (!c->exported && !c->live && (dev < 0 || c->device == dev)) idle.push_back(c);
+        if (!c->exported && !c->unexportable && !c->live && (dev < 0 || c->device == dev)) idle.push_back(c);
     for (Chunk *c : idle) release_chunk(c);
 }
 
@@ -260,8 +264,7 @@ bool arena_free(void *p) {
         release_chunk(b.chunk);
         return true;
     }
-    if (b.chunk->unexportable) {   // never exported: back to the driver with its last block
-        if (!b.chunk->live) release_chunk(b.chunk);
+    if (b.chunk->unexportable) {   // quarantined for good: never handed out, never freed
         return true;
     }
     if (b.cls <= kGranule / 2) {
@@ -396,20 +399,23 @@ static int export_impl(const void *p, size_t bytes, void **base, uint64_t *off, 
     hipIpcMemHandle_t h;
     hipError_t e = hipSuccess;
     // ESGD_FAIL_EXPORTS=N (tests): the process's first N chunk exports fail as the
-    // runtime's did, without calling it, so the fallbacks can be exercised anywhere
+    // runtime's did.  The simulation walks the real path up to the runtime call -- the
+    // seal is written into the chunk (on the round stream, synchronously) -- and then the
+    // call is refused instead of made, so everything after it (quarantine, the buffers
+    // moved, peers mapping the new chunk and reading its seal) is what a real refusal runs.
     static int simulated = [] {
         const char *v = getenv("ESGD_FAIL_EXPORTS");
         return (v && *v) ? std::max(0, atoi(v)) : 0;
     }();
     const bool simulate = sim && simulated > 0;
-    if (simulate) {
-        --simulated;
-        e = hipErrorInvalidValue;
-        std::fprintf(stderr, "esgd: export of %p (%zu B chunk) fails by ESGD_FAIL_EXPORTS\n",
-                     static_cast<void *>(c->base), c->bytes);
-    }
-    if (!simulate && !c->nonce && seal_on())
+    if (simulate) --simulated;
+    if (!c->nonce && seal_on())
         if (int rc = write_seal(c)) return rc;
+    if (simulate) {
+        e = hipErrorInvalidValue;
+        std::fprintf(stderr, "esgd: pid %d: export of %p (%zu B chunk, sealed) fails by ESGD_FAIL_EXPORTS\n",
+                     int(getpid()), static_cast<void *>(c->base), c->bytes);
+    }
     for (int attempt = 0; !simulate && attempt < 2; ++attempt) {
         e = hipIpcGetMemHandle(&h, c->base);
         if (e == hipSuccess) break;

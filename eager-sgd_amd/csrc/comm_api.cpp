@@ -139,6 +139,28 @@ int esgd_schedule_post_group(const esgd_sched_h *hs, int n, void *producer_strea
     return rc;
 }
 
+int esgd_schedule_post_io(esgd_sched_h h, const void *src, void *dst, float divisor, void *producer_stream,
+                          int *role) {
+    Sched *s = handle_to_sched(h);
+    if (!s) return ESGD_INVALID_ARG;
+    const RoundIO io{src, dst, divisor};
+    return sched_post(s, producer_stream, role, &io);
+}
+
+int esgd_schedule_post_group_io(const esgd_sched_h *hs, int n, const void *const *srcs, void *const *dsts,
+                                float divisor, void *producer_stream, int *roles) {
+    ESGD_ARG(n >= 0 && (n == 0 || (hs && srcs && dsts)), "esgd_schedule_post_group_io: bad arguments");
+    dataplane_group_begin(0, producer_stream);
+    int rc = ESGD_SUCCESS;
+    for (int i = 0; i < n && !rc; ++i) {
+        Sched *s = handle_to_sched(hs[i]);
+        const RoundIO io{srcs[i], dsts[i], divisor};
+        rc = s ? sched_post(s, producer_stream, roles ? &roles[i] : nullptr, &io) : ESGD_INVALID_ARG;
+    }
+    dataplane_group_end(0);
+    return rc;
+}
+
 int esgd_schedule_release_group(const esgd_sched_h *hs, int n, void *stream) {
     ESGD_ARG(n >= 0 && (n == 0 || hs), "esgd_schedule_release_group: bad arguments");
     dataplane_group_begin(1, stream);

@@ -115,6 +115,10 @@ static std::atomic<int64_t> g_cfg_small{-1}, g_cfg_flags{-1}, g_cfg_strict{-1}, 
 // batch_depth (ESGD_BATCH_DEPTH), snapshot_in_batch (ESGD_SNAPSHOT_IN_BATCH), inline_join
 // (ESGD_INLINE_JOIN, engine.cpp)
 static std::atomic<int64_t> g_cfg_depth{-1}, g_cfg_snap{-1}, g_cfg_inline{-1};
+// "batch_hold" (diagnostics / tests): 1 = the end of a pump never sends the pending shared
+// launch; only an explicit flush (another launch on the round stream, schedule deletion,
+// finalize) does -- so a test can finalize with rounds held
+static std::atomic<int64_t> g_cfg_hold{0};
 
 bool config_inline_join() {
     static const bool env = !(getenv("ESGD_INLINE_JOIN") && *getenv("ESGD_INLINE_JOIN") == '0');
@@ -183,9 +187,12 @@ int config_set(const char *key, int64_t value) {
     } else if (!std::strcmp(key, "inline_join")) {
         ESGD_ARG(value >= -1 && value <= 1, "inline_join: 0 or 1 (-1: the default)");
         g_cfg_inline.store(value);
+    } else if (!std::strcmp(key, "batch_hold")) {
+        ESGD_ARG(value >= -1 && value <= 1, "batch_hold: 0 or 1 (-1: the default, 0)");
+        g_cfg_hold.store(value < 0 ? 0 : value);
     } else {
         set_error("esgd_set_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
-                  "batch_rounds, batch_depth, snapshot_in_batch, inline_join)", key);
+                  "batch_rounds, batch_depth, snapshot_in_batch, inline_join, batch_hold)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -205,9 +212,10 @@ int config_get(const char *key, int64_t *value) {
     else if (!std::strcmp(key, "batch_depth")) *value = batch_depth();
     else if (!std::strcmp(key, "snapshot_in_batch")) *value = snapshot_in_batch() ? 1 : 0;
     else if (!std::strcmp(key, "inline_join")) *value = config_inline_join() ? 1 : 0;
+    else if (!std::strcmp(key, "batch_hold")) *value = g_cfg_hold.load();
     else {
         set_error("esgd_get_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
-                  "batch_rounds, launches, batch_workers, batch_depth, snapshot_in_batch, inline_join)", key);
+                  "batch_rounds, launches, batch_workers, batch_depth, snapshot_in_batch, inline_join, batch_hold)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -593,6 +601,11 @@ struct BaseState {
     // hold mode: the caller's last reads of rb / writes of sb (esgd_schedule_release)
     std::shared_ptr<hipEvent_t> consumer;
     bool consumer_pending = false;
+    // rounds posted with their own data (esgd_schedule_post_io), by round; io_on: the
+    // launched round takes cur_io (it was joined fresh, i.e. at or after that post)
+    std::map<uint32_t, RoundIO> io;
+    RoundIO cur_io{nullptr, nullptr, 1.0f};
+    bool io_on = false;
     virtual ~BaseState() {}
 };
 
@@ -803,6 +816,53 @@ static int base_note_consumer(BaseState &st, void *stream) {
     return ESGD_SUCCESS;
 }
 
+int Transport::note_io(Sched &, uint32_t, const RoundIO &) {
+    set_error("this transport does not take a round's own data (esgd_schedule_post_io)");
+    return ESGD_INVALID_ARG;
+}
+
+// esgd_schedule_post_io: checked at the post, used by the round it posts if that round
+// is joined fresh (take_io)
+static int base_note_io(Sched &s, BaseState &st, uint32_t round, const RoundIO &io) {
+    ESGD_ARG(!s.host_mode && !s.resolve && !s.wire_bf16,
+             "schedule %d: a round's own data needs a device schedule without FFCOLL_BUFFERS or WIRE_BF16", s.id);
+    ESGD_ARG(s.count == 0 || (io.src && io.dst), "schedule %d: post_io: null src or dst", s.id);
+    ESGD_ARG(((reinterpret_cast<uintptr_t>(io.src) | reinterpret_cast<uintptr_t>(io.dst)) & 15) == 0,
+             "schedule %d: post_io: src and dst must be 16-B aligned", s.id);
+    ESGD_ARG(io.div == io.div && io.div != 0.0f, "schedule %d: post_io: bad divisor", s.id);
+    ESGD_ARG(io.div == 1.0f || s.dtype == ESGD_FLOAT, "schedule %d: post_io: a divisor needs FLOAT buckets", s.id);
+    st.io[round] = io;
+    return ESGD_SUCCESS;
+}
+
+// at launch: the round's own data, if it was posted with some and joined fresh; entries
+// of this and earlier rounds are dropped (a round carried through before its post ran
+// with the send bucket)
+static void take_io(BaseState &st, uint32_t round, bool fresh) {
+    st.io_on = false;
+    for (auto it = st.io.begin(); it != st.io.end() && it->first <= round;) {
+        if (it->first == round && fresh) {
+            st.cur_io = it->second;
+            st.io_on = true;
+        }
+        it = st.io.erase(it);
+    }
+}
+
+// the copy-in of a round with its own data, queued on the round stream: rb = src / div
+static int io_copy_in(Sched &s, BaseState &st, hipStream_t cs) {
+    const size_t bytes = s.count * s.esize;
+    if (!bytes) return ESGD_SUCCESS;
+    if (st.cur_io.div == 1.0f) {
+        ESGD_HIP(hipMemcpyAsync(st.rb_dev, st.cur_io.src, bytes, hipMemcpyDeviceToDevice, cs));
+        return ESGD_SUCCESS;
+    }
+    const float *src = static_cast<const float *>(st.cur_io.src);
+    float *dst = reinterpret_cast<float *>(st.rb_dev);
+    const uint64_t n = s.count;
+    return pack_scatter(1, &src, &dst, &n, st.cur_io.div, cs);
+}
+
 // queued at launch, before anything touches the buckets: the caller's copy-out of the
 // previous round (and its zeroing of sb) has finished -- fresh round or not
 static int consumer_wait(BaseState &st, hipStream_t cs) {
@@ -919,6 +979,7 @@ static int base_copy_in(Sched &s, BaseState &st, uint32_t round, bool fresh, hip
     if (int rc = producer_wait(st, round, fresh, cs)) return rc;
     const size_t bytes = s.count * s.esize;
     if (!bytes) return ESGD_SUCCESS;
+    if (st.io_on) return io_copy_in(s, st, cs);   // the round's own data (post_io)
     if (s.fresh_only && !fresh) {
         // carried through a round it had not posted: this rank contributes zeros, and its
         // send bucket -- which the caller may be writing right now -- is not read
@@ -959,7 +1020,9 @@ static int finish_round(Sched &s, BaseState &st, hipStream_t cs) {
 
 static int base_copy_out(Sched &s, BaseState &st, hipStream_t cs) {
     const size_t bytes = s.count * s.esize;
-    if (s.host_mode && bytes) {
+    if (st.io_on && bytes) {   // the round's own output (post_io); rb is not the caller's then
+        ESGD_HIP(hipMemcpyAsync(st.cur_io.dst, st.rb_dev, bytes, hipMemcpyDeviceToDevice, cs));
+    } else if (s.host_mode && bytes) {
         if (staged(s, st)) {
             if (int rc = ensure_pin(st, bytes)) return rc;
             if (int rc = host_move(st.pin, st.rb_dev, st.view_pin, false, bytes, cs)) return rc;
@@ -981,13 +1044,21 @@ static int base_complete(Sched &s, BaseState &st) {
     return ESGD_SUCCESS;
 }
 
+// Why a round has not finished: every rank's flag words of this schedule (ready / reduced /
+// done / fin, the GPU error word, the last round it joined) and how this rank's round went
+// out (one launch of its own, a shared launch, shadowed).
 static std::string base_diagnose(Sched &s) {
-    if (s.flag_mode > 0) return "(pairing flags in device memory, device_flags mode " + std::to_string(s.flag_mode) + ")";
-    std::string m = "(flags ready/reduced/done per rank:";
-    char buf[64];
+    std::string m = "(per rank ready/reduced/done/fin/err/joined:";
+    char buf[96];
     for (int q = 0; q < s.world; ++q) {
-        snprintf(buf, sizeof(buf), " %u/%u/%u", s.sh->ready[q].load(), s.sh->reduced[q].load(),
-                 s.sh->done[q].load());
+        snprintf(buf, sizeof(buf), " r%d %u/%u/%u/%u/%u/%u", q, s.sh->ready[q].load(), s.sh->reduced[q].load(),
+                 s.sh->done[q].load(), s.sh->fin[q].load(), s.sh->gpu_err[q].load(), s.sh->joined[q].load());
+        m += buf;
+    }
+    if (s.flag_mode > 0) m += "; pairing flags in device memory, mode " + std::to_string(s.flag_mode) + " (not shown)";
+    if (auto *st = static_cast<BaseState *>(s.tstate)) {
+        snprintf(buf, sizeof(buf), "; this rank: %s%s%s", st->batch_ev ? "shared launch" : "own launch",
+                 st->shadow ? ", shadowed bucket" : "", st->fin_mode ? ", fin-polled" : ", event-polled");
         m += buf;
     }
     return m + ")";
@@ -997,13 +1068,17 @@ static int base_query(Sched &s, BaseState &st) {
     if (st.batch_rc) return st.batch_rc;   // error message set by the failed launch
     if (st.fin_mode) {   // the round's last kernel writes fin (finish_round, k_round_small, done pairing)
         // a timed-out flag wait of a batched round still lets its workers finish (and
-        // write fin): the error word is checked first
+        // write fin): fin is loaded first, then the error word -- the GPU stores the error
+        // (and releases it) before it opens the gates that let any worker write fin, so a
+        // fin seen here comes with the error of that round, if there was one (a timed-out
+        // k_round_small leaves without fin: the error alone fails the round then)
+        const bool finished = int32_t(s.sh->fin[s.rank].load(std::memory_order_acquire) - s.cur) >= 0;
         if (s.world > 1 && s.sh->gpu_err[s.rank].load(std::memory_order_acquire) == s.cur) {
             set_error("this rank's GPU waited more than %.0f s for its peers in round %u %s",
                       engine_timeout(), s.cur, base_diagnose(s).c_str());
             return ESGD_ERROR;
         }
-        if (int32_t(s.sh->fin[s.rank].load(std::memory_order_acquire) - s.cur) >= 0) {
+        if (finished) {
             // the kernel may still be retiring (not ready is fine); a fault is reported
             // against this round, not a later one
             const hipError_t e = hipEventQuery(st.batch_ev ? *st.batch_ev : st.ev);
@@ -1060,6 +1135,7 @@ struct BatchEntry {
     IpcState *st;
     uint32_t round;
     uint8_t snap;   // the snapshot the launch's workers do (0: none, or queued before it)
+    RoundIO io;     // the round's own data (src nullptr: none; dst nullptr: results in rb)
 };
 
 // ESGD_SNAPSHOT_IN_BATCH (default 1): a batched round's snapshot is phase 0 of the shared
@@ -1070,14 +1146,26 @@ static bool snapshot_in_batch() {
     return v >= 0 ? v != 0 : env;
 }
 
-// the whole-bucket snapshot fits the kernel's 32-bit buffer ranges and 16-B vectors
-static bool snap_eligible(const Sched &s, const IpcState &st) {
+// the whole-bucket snapshot (rb = src) fits the kernel's 32-bit buffer ranges and 16-B
+// vectors (src nullptr: rb alone)
+static bool snap_eligible(const Sched &s, const IpcState &st, const void *src) {
     const size_t bytes = s.count * s.esize;
-    const uintptr_t al = reinterpret_cast<uintptr_t>(st.rb_dev) | (s.in_place ? 0 : reinterpret_cast<uintptr_t>(s.sb));
+    const uintptr_t al = reinterpret_cast<uintptr_t>(st.rb_dev) | reinterpret_cast<uintptr_t>(src);
     return bytes && bytes < (size_t(1) << 31) && (al & 15) == 0;
 }
 static std::vector<BatchEntry> g_pend;
 static CopySet g_copy;   // the pending launch's snapshots (nseg 0: none)
+// the shared launches' tile counter (BatchArgs::queue; a device word behind the descriptor
+// table) and its value when the next launch starts
+static uint32_t *g_queue = nullptr;
+static uint32_t g_qnext = 0;
+
+// ESGD_BATCH_STATIC=1: static tile assignment in shared launches (an A/B of the dynamic
+// counter; needs every worker resident at once)
+static bool batch_static() {
+    static const bool on = getenv("ESGD_BATCH_STATIC") && *getenv("ESGD_BATCH_STATIC") == '1';
+    return on;
+}
 // shared launches queued and not yet seen complete, oldest first (their events)
 static std::deque<std::shared_ptr<hipEvent_t>> g_outstanding;
 
@@ -1102,9 +1190,12 @@ static int batch_depth() {
 static int batch_desc(Sched &s, IpcState &st, hipStream_t cs) {
     if (st.desc_built) return ESGD_SUCCESS;
     if (!g_desc_dev) {
-        ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&g_desc_dev), sizeof(BatchDesc) * kMaxSched));
+        ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&g_desc_dev), sizeof(BatchDesc) * kMaxSched + 256));
         ESGD_HIP(hipHostMalloc(reinterpret_cast<void **>(&g_desc_host), sizeof(BatchDesc) * kMaxSched,
                                hipHostMallocDefault));
+        g_queue = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(g_desc_dev) + sizeof(BatchDesc) * kMaxSched);
+        ESGD_HIP(hipMemsetAsync(g_queue, 0, 256, cs));   // ahead of every launch on this stream
+        g_qnext = 0;
     }
     if (!st.ctr)
         if (int rc = ctr_words(s.id, cs, &st.ctr)) return rc;
@@ -1141,13 +1232,14 @@ static int batch_desc(Sched &s, IpcState &st, hipStream_t cs) {
     d.fin = dev_flag(&s.sh->fin[r]);
     d.err = dev_flag(&s.sh->gpu_err[r]);
     d.ctr = st.ctr + 6;   // words 6..10 of the schedule's device counters
-    if (snap_eligible(s, st)) {
+    if (snap_eligible(s, st, nullptr)) {   // the in-launch snapshot's target (rb) fits it
         const size_t bytes = s.count * es;
         d.ssrc = s.in_place ? nullptr : s.sb;
         d.sdst = st.rb_dev;
         d.svec = uint32_t(bytes / 16);
         d.stail = uint32_t(bytes % 16);
     }
+    d.rbase = st.rb_dev;
     st.t1 = d.t1;
     st.t2 = std::max<uint32_t>(1, d.t2pre[m]);   // at least one tile: it writes fin
     g_desc_host[s.id] = d;
@@ -1157,14 +1249,17 @@ static int batch_desc(Sched &s, IpcState &st, hipStream_t cs) {
 }
 
 // ranks of this job whose GPU is this process's (1 with a GPU per rank; the rehearsal on
-// a 1-GPU box puts every rank there)
+// a 1-GPU box puts every rank there).  Compared by PCI location, not by ordinal: with
+// HIP_VISIBLE_DEVICES set per rank every process calls its GPU "device 0".
 static int ranks_on_my_device() {
     Segment *seg = engine_segment();
     const int me = engine_rank(), world = engine_world();
     if (!seg) return 1;
+    const uint64_t gid = seg->gpu_id[me].load();
     const int dev = seg->device[me].load();
     int n = 0;
-    for (int q = 0; q < world; ++q) n += seg->device[q].load() == dev;
+    for (int q = 0; q < world; ++q)
+        n += gid ? seg->gpu_id[q].load() == gid : seg->device[q].load() == dev;
     return std::max(1, n);
 }
 
@@ -1183,6 +1278,9 @@ static int batch_flush_locked() {
         a.tile0[e] = t0;
         a.tile1[e] = t1;
         a.tile2[e] = t2;
+        a.isrc[e] = g_pend[e].snap ? g_pend[e].io.src : nullptr;   // read by phase 0 only
+        a.iout[e] = g_pend[e].io.dst;
+        a.idiv[e] = g_pend[e].io.div;
         if (const uint8_t k = g_pend[e].snap) {
             const BatchDesc &d = g_desc_host[g_pend[e].s->id];
             a.snap[e] = k;
@@ -1214,8 +1312,16 @@ static int batch_flush_locked() {
         g_copy.nseg = 0;
         if (!rc) ++g_launches;
     }
+    // the tile counter: every worker's last grab finds the list done, so one launch moves
+    // it by (tiles + workers); a launch starts once the previous one on the stream ended
+    a.dynamic = batch_static() ? 0u : 1u;
+    a.queue = g_queue;
+    a.qbase = g_qnext;
     if (!rc) rc = round_batch(g_pend[0].s->dtype, g_pend[0].s->world, a, workers, cs);
-    if (!rc) g_batch_workers.store(int64_t(workers), std::memory_order_relaxed);
+    if (!rc) {
+        g_batch_workers.store(int64_t(workers), std::memory_order_relaxed);
+        if (a.dynamic) g_qnext += t0 + t1 + t2 + workers;
+    }
     std::shared_ptr<hipEvent_t> sp;
     if (!rc) {
         sp = pooled_event();
@@ -1250,7 +1356,7 @@ int dataplane_flush() {
 // the next pass sends the held rounds.
 int dataplane_flush_soft() {
     std::lock_guard<std::mutex> lk(g_batch_mu);
-    if (g_pend.empty()) return ESGD_SUCCESS;
+    if (g_pend.empty() || g_cfg_hold.load(std::memory_order_relaxed)) return ESGD_SUCCESS;
     if (const int depth = batch_depth()) {
         while (!g_outstanding.empty() && hipEventQuery(*g_outstanding.front()) != hipErrorNotReady)
             g_outstanding.pop_front();   // finished (a fault is reported by its rounds)
@@ -1275,6 +1381,31 @@ void dataplane_extra_queues(int n) {
     }
 }
 
+// diagnostics for a timed-out wait: the shared launch being filled (schedule:round of each
+// entry), shared launches queued and not yet seen finished, and a seal I/O in progress
+std::string dataplane_state() {
+    std::string m;
+    char buf[64];
+    {
+        std::lock_guard<std::mutex> lk(g_batch_mu);
+        snprintf(buf, sizeof(buf), "pending shared launch %zu rounds", g_pend.size());
+        m += buf;
+        for (size_t i = 0; i < g_pend.size() && i < 16; ++i) {
+            snprintf(buf, sizeof(buf), "%s%d:%u", i ? "," : " [", g_pend[i].s->id, g_pend[i].round);
+            m += buf;
+        }
+        if (!g_pend.empty()) m += g_pend.size() > 16 ? ",...]" : "]";
+        size_t busy = 0;
+        for (auto &e : g_outstanding) busy += hipEventQuery(*e) == hipErrorNotReady;
+        (void)hipGetLastError();
+        snprintf(buf, sizeof(buf), "; %zu shared launches unfinished", busy);
+        m += buf;
+        if (g_cfg_hold.load()) m += " (batch_hold)";
+    }
+    if (seal_io_busy()) m += "; a seal read/write is waiting for the round stream";
+    return m;
+}
+
 void dataplane_profile(uint64_t *launches, uint64_t *flush_ns) {
     *launches = g_launches.load(std::memory_order_relaxed);
     *flush_ns = g_flush_ns.load(std::memory_order_relaxed);
@@ -1291,12 +1422,23 @@ static int batch_snapshot(Sched &s, IpcState &st, uint32_t round, bool fresh, hi
     st.snap = false;
     st.snap_kind = 0;
     const size_t bytes = s.count * s.esize;
-    if (!bytes || s.zero_sb) return s.zero_sb && bytes ? move_zero(st.rb_dev, s.sb, bytes, cs) : ESGD_SUCCESS;
+    if (!bytes) return ESGD_SUCCESS;
+    if (st.io_on) {   // the round's own data (post_io): rb = src / div
+        if (snapshot_in_batch() && snap_eligible(s, st, st.cur_io.src)) {   // phase 0 of the shared launch
+            st.snap_kind = st.cur_io.div == 1.0f ? 1 : 3;
+            return ESGD_SUCCESS;
+        }
+        return io_copy_in(s, st, cs);
+    }
+    // the order of base_copy_in: a FRESH_ONLY round this rank had not posted contributes
+    // zeros and never reads (or zeroes) the send bucket the caller may be writing -- ahead
+    // of ZERO_SB's fused move
     const void *src = nullptr;
     if (s.fresh_only && !fresh) src = nullptr;            // contributes zeros, sb unread
+    else if (s.zero_sb) return move_zero(st.rb_dev, s.sb, bytes, cs);
     else if (!s.in_place) src = s.sb;
     else return ESGD_SUCCESS;                              // in place: nothing to move
-    if (snapshot_in_batch() && snap_eligible(s, st)) {    // phase 0 of the shared launch
+    if (snapshot_in_batch() && snap_eligible(s, st, src)) {   // phase 0 of the shared launch
         st.snap_kind = src ? 1 : 2;
         return ESGD_SUCCESS;
     }
@@ -1335,7 +1477,8 @@ static int batch_append(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) 
     st.pub_round = round;
     st.fin_mode = true;
     st.batch_rc = 0;
-    g_pend.push_back({&s, &st, round, st.snap_kind});
+    const RoundIO none{nullptr, nullptr, 1.0f};
+    g_pend.push_back({&s, &st, round, st.snap_kind, st.io_on ? st.cur_io : none});
     st.snap_kind = 0;
     return ESGD_SUCCESS;
 }
@@ -1348,7 +1491,7 @@ static void batch_shutdown() {
         w.ev.reset();
     }
     g_outstanding.clear();
-    if (g_desc_dev) { hip_ignore(hipFree(g_desc_dev)); g_desc_dev = nullptr; }
+    if (g_desc_dev) { hip_ignore(hipFree(g_desc_dev)); g_desc_dev = nullptr; g_queue = nullptr; }
     if (g_desc_host) { hip_ignore(hipHostFree(g_desc_host)); g_desc_host = nullptr; }
     std::lock_guard<std::mutex> ek(g_evfree_mu);
     for (hipEvent_t e : g_evfree) hip_ignore(hipEventDestroy(e));
@@ -1536,6 +1679,8 @@ struct IpcTransport final : Transport {
 
     int note_consumer(Sched &s, void *stream) override { return base_note_consumer(S(s), stream); }
 
+    int note_io(Sched &s, uint32_t round, const RoundIO &io) override { return base_note_io(s, S(s), round, io); }
+
     // join: a moved bucket is re-published before this rank's join counts (peers map it
     // when they launch the round); a size change alone only updates the published size
     int prepare(Sched &s, uint32_t round, bool fresh) override {
@@ -1573,6 +1718,7 @@ struct IpcTransport final : Transport {
         st.fin_mode = false;
         st.batch_ev.reset();
         st.batch_rc = 0;
+        take_io(st, round, fresh);
         const bool batch = batched(s, st);
         // anything else queued on the round stream goes behind the pending shared launch
         if (!batch)
@@ -1599,7 +1745,7 @@ struct IpcTransport final : Transport {
                 if (int rc = launch_small(s, st, round, cs)) return rc;
                 // device buckets: nothing follows the kernel, the host polls its fin flag
                 // (the event only reports faults)
-                if (!s.host_mode && !st.shadow) {
+                if (!s.host_mode && !st.shadow && !st.io_on) {
                     st.fin_mode = true;
                     ESGD_HIP(hipEventRecord(st.ev, cs));
                     return ESGD_SUCCESS;
@@ -1647,7 +1793,7 @@ struct IpcTransport final : Transport {
             }
             // device buckets: the done pairing ends the round and reports it in fin, which
             // the host polls (as for one-launch rounds; the event only reports faults)
-            const bool last = !s.host_mode && !st.shadow;
+            const bool last = !s.host_mode && !st.shadow && !st.io_on;
             if (int rc = pair_ranks(s, s.sh->done, 2, round, cs, 0, last ? &s.sh->fin[s.rank] : nullptr))
                 return rc;
             if (last) {
@@ -1833,7 +1979,7 @@ struct IpcTransport final : Transport {
         uint64_t *ts = gpu_trace_on() ? reinterpret_cast<uint64_t *>(dev_flag(&s.sh->gpu_ts[s.rank][0])) : nullptr;
         return round_small(s.dtype, in, st.rb_dev + st.off[s.rank] * s.esize, st.pub, st.len[s.rank], m, src,
                            dst, bytes, pair_flags(s, s.sh->ready, 0), pair_flags(s, s.sh->reduced, 1),
-                           (s.host_mode || st.shadow) ? nullptr : dev_flag(&s.sh->fin[s.rank]),
+                           (s.host_mode || st.shadow || st.io_on) ? nullptr : dev_flag(&s.sh->fin[s.rank]),
                            dev_flag(&s.sh->gpu_err[s.rank]), ts, st.ctr,
                            s.rank, s.world, round, ticks, s.strict ? 1 : 0, cs);
     }
@@ -1980,6 +2126,7 @@ struct RcclState : BaseState {
     hipStream_t red = nullptr;       // tree folds of arrived chunks
     char *stage = nullptr;           // P x L elements: every peer's copy of this rank's shard
     char *wire = nullptr;            // wire rounds: bf16 copy of rb (count elements)
+    size_t stage_cap = 0, wire_cap = 0;   // bytes of the arena blocks behind stage / wire
     uint64_t wire_n = 0;
     uint64_t L = 0;                  // shard pitch (elements)
     uint64_t chunk = 0;              // pipeline chunk (elements)
@@ -1995,20 +2142,35 @@ struct RcclTransport final : Transport {
     // bytes per element on the wire (and in the staging area)
     static size_t stage_esize(const Sched &s) { return s.wire_bf16 ? 2 : s.esize; }
 
+    // A buffer of at least `need` bytes in *buf (capacity *cap): grown geometrically from
+    // the arena, never shrunk.  Called at setup (caller's thread) and at every join of an
+    // FFCOLL_BUFFERS round (the progress thread): the arena hands out and takes back blocks
+    // without hipFree -- whose device-wide synchronisation would stall every schedule's
+    // rounds in flight -- and the old block is free to go: a join follows the schedule's
+    // previous round, which was the last user of it.
+    static int fit_buf(char **buf, size_t *cap, size_t need) {
+        if (need <= *cap) return ESGD_SUCCESS;
+        char *p = nullptr;
+        const size_t want = std::max(need, 2 * *cap);
+        if (int rc = arena_alloc(want, reinterpret_cast<void **>(&p))) return rc;
+        if (*buf) arena_free(*buf);
+        *buf = p;
+        *cap = want;
+        return ESGD_SUCCESS;
+    }
+
     static int fit_stage(Sched &s, RcclState &st) {
         if (s.wire_bf16 && s.world > 1 && st.wire_n != s.count) {
-            if (st.wire) { ESGD_HIP(hipFree(st.wire)); st.wire = nullptr; }
+            if (int rc = fit_buf(&st.wire, &st.wire_cap, size_t(s.count) * 2)) return rc;
             st.wire_n = s.count;
-            if (s.count) ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.wire), size_t(s.count) * 2));
         }
         // pitch rounded to 8 elements: every staged shard starts 16-B aligned (the wire
         // kernels' vectors) even when one ragged shard holds the whole bucket
         const uint64_t pitch = (st.len[0] + 7) / 8 * 8;
         if (st.stage && st.L == pitch) return ESGD_SUCCESS;
-        if (st.stage) { ESGD_HIP(hipFree(st.stage)); st.stage = nullptr; }
         st.L = pitch;
         if (s.world > 1 && st.L)
-            ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&st.stage), size_t(s.world) * st.L * stage_esize(s)));
+            if (int rc = fit_buf(&st.stage, &st.stage_cap, size_t(s.world) * st.L * stage_esize(s))) return rc;
         // ~8 chunks per shard, at least 1 MiB each, 1 KiB aligned
         const uint64_t align = 1024 / s.esize, minc = (1u << 20) / s.esize;
         const uint64_t c = std::max<uint64_t>(minc, (st.L + 7) / 8);
@@ -2037,6 +2199,8 @@ struct RcclTransport final : Transport {
 
     int note_consumer(Sched &s, void *stream) override { return base_note_consumer(S(s), stream); }
 
+    int note_io(Sched &s, uint32_t round, const RoundIO &io) override { return base_note_io(s, S(s), round, io); }
+
     int prepare(Sched &s, uint32_t, bool fresh) override {
         RcclState &st = S(s);
         const int moved = base_refit(s, st);
@@ -2059,6 +2223,7 @@ struct RcclTransport final : Transport {
         const int P = s.world, r = s.rank;
         const size_t es = s.esize;
         if (int rc = dataplane_flush()) return rc;   // ring order on the round stream
+        take_io(st, round, fresh);
         if (int rc = base_copy_in(s, st, round, fresh, cs)) return rc;
         if (P > 1 && st.L && s.wire_bf16) {
             if (int rc = wire_round(s, st)) return rc;
@@ -2183,8 +2348,8 @@ struct RcclTransport final : Transport {
         if (!st) return;
         if (st->stream) hip_ignore(hipStreamSynchronize(st->stream));
         if (st->red) { hip_ignore(hipStreamSynchronize(st->red)); hip_ignore(hipStreamDestroy(st->red)); }
-        if (st->stage) hip_ignore(hipFree(st->stage));
-        if (st->wire) hip_ignore(hipFree(st->wire));
+        if (st->stage) arena_free(st->stage);
+        if (st->wire) arena_free(st->wire);
         for (hipEvent_t e : st->ev_chunk) hip_ignore(hipEventDestroy(e));
         if (st->ev_red) hip_ignore(hipEventDestroy(st->ev_red));
         base_teardown(s, *st);

@@ -101,6 +101,16 @@ struct AllreduceOp {
     int status = 0;                       // first failure of a void entry point (ESGD_OP_ON_ERROR_LOCAL)
     bool warned = false;
     bool pending = false;                 // a split round posted and not yet waited
+    // the pending round was posted with its own data (esgd_schedule_post_io): the gradient
+    // is read by the round itself and, if the round takes it, the result lands in io_out
+    bool io_posted = false;
+    float *io_out = nullptr;
+
+    // the fused path fits: device op, fp32 wire, 16-B aligned tensors
+    bool io_ok(const float *in, const float *out) const {
+        return device && cfg.wire != ESGD_BF16 &&
+               ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+    }
 
     // Lazy creation of the buckets and the schedule (:288-298); an esgd status (the void
     // entry points abort on failure, the status-returning ones pass it on).
@@ -203,10 +213,27 @@ int cuda_copy_out(AllreduceOp *op, float *output, hipStream_t s) {
     return ESGD_SUCCESS;
 }
 
+// The round reads the gradient itself (rb = input / divisor in its snapshot) and writes the
+// result into output (esgd_schedule_post_io): no copy-in or copy-out on the caller's stream.
+// A round a peer's activation carried this rank through before the post (not fresh) ran
+// without the gradient (FRESH_ONLY zeros) and left its result in rb: copied out as before.
+int forward_cuda_io(AllreduceOp *op, const float *input, float *output, float divisor, hipStream_t s) {
+    void *ps = caller_stream(s);
+    if (int rc = esgd_schedule_post_io(op->sched, input, output, divisor, ps, nullptr)) return rc;
+    int fresh = 0;
+    if (int rc = esgd_schedule_wait_ex(op->sched, &fresh)) return rc;
+    if (!fresh)
+        if (int rc = cuda_copy_out(op, output, s)) return rc;
+    if (int rc = esgd_schedule_release(op->sched, fresh ? nullptr : ps)) return rc;
+    op->bytes += int64_t(op->len) * int64_t(sizeof(float));
+    return ESGD_SUCCESS;
+}
+
 int forward_cuda_impl(AllreduceOp *op, const float *input, float *output, float divisor, hipStream_t s) {
     ESGD_ARG(op, "allreducef: null handle");
     ESGD_ARG(!op->pending, "allreducef: a split round is posted and not yet waited");
     if (int rc = op->ensure(true)) return rc;
+    if (op->io_ok(input, output)) return forward_cuda_io(op, input, output, divisor, s);
     if (int rc = cuda_copy_in(op, input, divisor, s)) return rc;
     return op->device_round(s, [&]() -> int { return cuda_copy_out(op, output, s); });
 }
@@ -385,30 +412,80 @@ int allreducef_forward_cuda_post_many(void *const *handles, int n, const float *
     return rc;
 }
 
+int allreducef_forward_cuda_post_many_io(void *const *handles, int n, const float *const *inputs,
+                                         float *const *outputs, float divisor, void *stream) {
+    ESGD_ARG(n >= 0 && (n == 0 || (handles && inputs && outputs)),
+             "allreducef_forward_cuda_post_many_io: bad arguments");
+    ESGD_ARG(divisor == divisor && divisor != 0.0f, "allreducef_forward_cuda_post_many_io: bad divisor");
+    if (n == 0) return ESGD_SUCCESS;
+    std::vector<AllreduceOp *> ops(static_cast<size_t>(n));
+    std::vector<esgd_sched_h> hs(static_cast<size_t>(n));
+    bool fits = true;
+    for (int i = 0; i < n; ++i) {
+        AllreduceOp *op = ops[i] = static_cast<AllreduceOp *>(handles[i]);
+        ESGD_ARG(op, "allreducef_forward_cuda_post_many_io: op %d is null", i);
+        ESGD_ARG(!op->pending, "allreducef_forward_cuda_post_many_io: op %d's previous round was not waited", i);
+        if (int rc = op->ensure(true)) return rc;   // collective, in the callers' common order
+        fits = fits && op->io_ok(inputs[i], outputs[i]);
+        hs[i] = op->sched;
+    }
+    // a tensor the fused path cannot take (unaligned, bf16 wire): the whole group goes the
+    // copy-in way, and wait_many copies out
+    if (!fits) return allreducef_forward_cuda_post_many(handles, n, inputs, divisor, stream);
+    void *ps = caller_stream(static_cast<hipStream_t>(stream));
+    std::vector<int> roles(static_cast<size_t>(n), -1);
+    const int rc = esgd_schedule_post_group_io(hs.data(), n, reinterpret_cast<const void *const *>(inputs),
+                                               reinterpret_cast<void *const *>(outputs), divisor, ps, roles.data());
+    for (int i = 0; i < n; ++i) {
+        ops[i]->pending = roles[i] >= 0;   // posted (a role was written)
+        ops[i]->io_posted = ops[i]->pending;
+        ops[i]->io_out = outputs[i];
+    }
+    return rc;
+}
+
 int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const *outputs, void *stream) {
     ESGD_ARG(n >= 0 && (n == 0 || (handles && outputs)), "allreducef_forward_cuda_wait_many: bad arguments");
     std::vector<float *> outs, rbs;
     std::vector<uint64_t> counts;
-    std::vector<esgd_sched_h> hs;
-    std::vector<AllreduceOp *> done;
+    std::vector<esgd_sched_h> hs, hs_io;   // copied out from rb / results already in place
+    std::vector<AllreduceOp *> done, done_io;
     int first = ESGD_SUCCESS;
     for (int i = 0; i < n; ++i) {
         AllreduceOp *op = static_cast<AllreduceOp *>(handles[i]);
         if (!op || !op->pending) continue;
         op->pending = false;
-        if (int rc = esgd_schedule_wait(op->sched)) {
+        const bool io = op->io_posted;
+        op->io_posted = false;
+        int fresh = 0;
+        if (int rc = esgd_schedule_wait_ex(op->sched, &fresh)) {
             if (!first) first = rc;
             continue;
         }
+        // a round that took the gradient wrote its result into io_out itself; one a peer
+        // carried this rank through before the post left it in rb
+        const bool in_place = io && fresh;
         outs.push_back(outputs[i]);
-        rbs.push_back(op->rb);
+        rbs.push_back(in_place ? op->io_out : op->rb);
         counts.push_back(op->len);
-        hs.push_back(op->sched);
-        done.push_back(op);
+        if (in_place && outputs[i] == op->io_out) {
+            outs.pop_back(); rbs.pop_back(); counts.pop_back();   // nothing to move
+            hs_io.push_back(op->sched);
+            done_io.push_back(op);
+        } else {
+            hs.push_back(op->sched);
+            done.push_back(op);
+        }
+    }
+    void *ps = caller_stream(static_cast<hipStream_t>(stream));
+    if (!done_io.empty()) {   // the caller read nothing of rb: no consumer event
+        const int rc = esgd_schedule_release_group(hs_io.data(), int(hs_io.size()), nullptr);
+        if (rc && !first) first = rc;
+        if (!rc)
+            for (AllreduceOp *op : done_io) op->bytes += int64_t(op->len) * int64_t(sizeof(float));
     }
     if (!done.empty()) {
-        void *ps = caller_stream(static_cast<hipStream_t>(stream));
-        int rc = esgd::unpack_gather(int(done.size()), outs.data(), rbs.data(), counts.data(), ps);
+        int rc = esgd::unpack_gather(int(outs.size()), outs.data(), rbs.data(), counts.data(), ps);
         // released even when the copy-out could not be queued: no round stays held
         const int rr = esgd_schedule_release_group(hs.data(), int(hs.size()), ps);
         if (!rc) rc = rr;

@@ -40,7 +40,9 @@ static int g_next_id = 0;
 static std::thread g_thread;
 static std::atomic<bool> g_running{false};
 static std::atomic<uint64_t> g_epoch{0};             // progress passes completed
-static uint64_t g_cursor = 0;                       // next ticket this rank issues
+// next ticket this rank issues (written by the thread pumping the ring; atomic so that a
+// timed-out wait on another thread can report it)
+static std::atomic<uint64_t> g_cursor{0};
 static std::mutex g_issue_mu;
 static std::vector<std::pair<uint32_t, uint32_t>> g_issued;
 
@@ -127,6 +129,18 @@ int engine_init(const char *job, int rank, int world, bool start_progress) {
     int dev = -1;
     if (start_progress && hipGetDevice(&dev) == hipSuccess) g_device = dev;
     seg->device[rank].store(g_device);
+    uint64_t gid = 0;
+    if (g_device >= 0) {
+        int dom = 0, bus = 0, slot = 0;
+        if (hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainId, g_device) == hipSuccess &&
+            hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, g_device) == hipSuccess &&
+            hipDeviceGetAttribute(&slot, hipDeviceAttributePciDeviceId, g_device) == hipSuccess)
+            gid = ((uint64_t(uint32_t(dom)) << 32) | (uint64_t(uint32_t(bus) & 0xffff) << 16) |
+                   uint64_t(uint32_t(slot) & 0xffff)) + 1;
+        else
+            (void)hipGetLastError();
+    }
+    seg->gpu_id[rank].store(gid);
     if (int rc = shm_barrier(seg, world, g_timeout)) { g_seg = nullptr; shm_detach(seg, job, rank); return rc; }
     // every rank is attached: drop the name so nothing outlives the job in /dev/shm
     if (rank == 0) shm_unlink_name(job);
@@ -152,6 +166,10 @@ int engine_finalize() {
     if (!g_seg) return ESGD_SUCCESS;
     int rc = shm_barrier(g_seg, g_world, g_timeout);
     if (g_running.exchange(false)) g_thread.join();
+    // rounds held for the next shared launch (ESGD_BATCH_DEPTH) go out now, while their
+    // schedules are alive: every rank launched them in ring order, so they pair up, and the
+    // teardowns below wait for them on the round stream
+    (void)dataplane_flush();
     std::vector<Sched *> left;
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
@@ -166,7 +184,7 @@ int engine_finalize() {
     shm_detach(g_seg, nullptr, -1);
     g_seg = nullptr;
     g_next_id = 0;
-    g_cursor = 0;
+    g_cursor.store(0);
     {
         std::lock_guard<std::mutex> lk(g_issue_mu);
         g_issued.clear();
@@ -188,6 +206,29 @@ void Sched::mark(uint32_t round, int what) {   // caller holds mu
     if (round == 0 || round > 65536) return;
     if (tl.size() < round) tl.resize(std::max<size_t>(round, std::min<size_t>(65536, 2 * tl.size())));
     tl[round - 1][what] = mono_ns();
+}
+
+// What a schedule is doing, for the message of a timed-out wait or join (caller holds
+// s.mu): this rank's round counters and stage, the node's activation and join counts, how
+// far this rank has launched the node's issue ring, then the transport's flag words and
+// the data plane's pending launches -- so a stall names the stage and the rank it is in.
+static const char *stage_name(Stage st) {
+    return st == ST_IDLE ? "idle" : st == ST_WAIT_TICKET ? "joined, waiting for its issue-ring turn" : "launched";
+}
+
+static std::string sched_state(Sched &s) {
+    char buf[512];
+    snprintf(buf, sizeof(buf),
+             "[rank %d: posted %u joined %u completed %u waited %u released %u; round %u %s (%s) for %.1f s%s; "
+             "node: activated %u, joins %u; issue ring: %llu launched here of %llu]",
+             s.rank, s.posted.load(), s.joined.load(), s.completed, s.waited, s.released, s.cur,
+             stage_name(s.stage.load()), s.cur_fresh ? "posted" : "carried by a peer", now_s() - s.stage_t0,
+             s.hold_mode && s.released < s.joined ? ", held until release()" : "", s.sh->activated.load(),
+             s.sh->ready_count.load(), (unsigned long long)g_cursor.load(std::memory_order_relaxed),
+             (unsigned long long)(g_seg ? g_seg->ticket_next.load() : 0));
+    std::string m = buf;
+    if (s.tp) m += " " + s.tp->diagnose(s);
+    return m + " [" + dataplane_state() + "]";
 }
 
 static void fail_locked(Sched &s, int rc, const char *msg) {
@@ -331,7 +372,7 @@ static bool step(Sched &s, bool join_only);
 
 static bool inline_join() { return config_inline_join(); }
 
-int sched_post(Sched *s, void *producer_stream, int *role) {
+int sched_post(Sched *s, void *producer_stream, int *role, const RoundIO *io) {
     ESGD_ARG(s, "schedule post: null schedule");
     int r = 0;
     {
@@ -349,6 +390,8 @@ int sched_post(Sched *s, void *producer_stream, int *role) {
             }
             if (int rc = s->resolve(*s)) return rc;
         }
+        if (io)   // before the post counts: a join that sees it fresh finds its data
+            if (int rc = s->tp->note_io(*s, t, *io)) return rc;
         if (producer_stream)
             if (int rc = s->tp->note_producer(*s, t, producer_stream)) return rc;
         s->posted.store(t, std::memory_order_release);
@@ -411,7 +454,8 @@ int sched_wait_ex(Sched *s, int *fresh) {
     while (s->completed < target && !s->error) {
         s->cv.wait_for(lk, std::chrono::milliseconds(50));
         if (now_s() - t0 > g_timeout) {
-            fail_locked(*s, ESGD_ERROR, "wait timed out (a peer never posted / activated?)");
+            const std::string m = "wait timed out " + sched_state(*s);
+            fail_locked(*s, ESGD_ERROR, m.c_str());
             break;
         }
     }
@@ -459,6 +503,9 @@ int sched_test(Sched *s, int *flag) {
 int sched_delete(Sched *s) {
     ESGD_ARG(s, "schedule delete: null schedule");
     const double t0 = now_s();
+    // an in-flight round of this schedule may sit in the pending shared launch (held behind
+    // ESGD_BATCH_DEPTH launches, or by batch_hold): send it, so that it can finish
+    (void)dataplane_flush();
     for (;;) {   // let an in-flight round finish (peers may still need our flags)
         {
             std::lock_guard<std::mutex> lk(s->mu);
@@ -481,6 +528,10 @@ int sched_delete(Sched *s) {
             std::this_thread::yield();
         }
     }
+    // A round of this schedule may still wait in the pending shared launch (the loop above
+    // gave up on an error or the timeout): it goes out now, while the schedule is alive --
+    // peers launched it too -- and the teardown's stream synchronisation waits for it.
+    (void)dataplane_flush();
     // Local, like ffschedule_delete: every peer finished reading this rank's buckets for
     // the rounds it joined (the done pairing), and the buckets go back to the IPC arena,
     // which never unmaps them under a peer (arena.cpp).
@@ -568,8 +619,10 @@ static bool step(Sched &s, bool join_only = false) {
         return true;
     }
     case ST_WAIT_TICKET:
-        if (now_s() - s.stage_t0 > g_timeout)
-            fail_locked(s, ESGD_ERROR, "not every rank joined the round (a peer never posted / activated?)");
+        if (now_s() - s.stage_t0 > g_timeout) {
+            const std::string m = "not every rank joined the round (a peer never posted / activated?) " + sched_state(s);
+            fail_locked(s, ESGD_ERROR, m.c_str());
+        }
         return false;
     case ST_INFLIGHT: {
         const int q = s.tp->query(s);
@@ -578,7 +631,7 @@ static bool step(Sched &s, bool join_only = false) {
             // the GPU's flag waits give up after the timeout and complete the round with
             // an error flag; this is the host's backstop
             if (now_s() - s.stage_t0 > 1.5 * g_timeout + 5) {
-                std::string m = "round did not finish on the GPU " + s.tp->diagnose(s);
+                std::string m = "round did not finish on the GPU " + sched_state(s);
                 fail_locked(s, ESGD_ERROR, m.c_str());
                 return true;
             }
@@ -618,8 +671,9 @@ static bool pump_tickets(const std::vector<Sched *> &snap) {
     if (!g_seg) return false;
     bool any = false;
     for (;;) {
-        TicketSlot &slot = g_seg->ring[g_cursor % kRing];
-        if (slot.tag.load(std::memory_order_acquire) != g_cursor + 1) break;
+        const uint64_t cur = g_cursor.load(std::memory_order_relaxed);
+        TicketSlot &slot = g_seg->ring[cur % kRing];
+        if (slot.tag.load(std::memory_order_acquire) != cur + 1) break;
         Sched *target = nullptr;
         for (Sched *s : snap)
             if (uint32_t(s->id) == slot.sched) { target = s; break; }
@@ -650,7 +704,7 @@ static bool pump_tickets(const std::vector<Sched *> &snap) {
             std::lock_guard<std::mutex> lk(g_issue_mu);
             if (g_issued.size() < 65536) g_issued.emplace_back(slot.sched, slot.round);
         }
-        ++g_cursor;
+        g_cursor.store(cur + 1, std::memory_order_relaxed);
         any = true;
     }
     // the one-launch rounds this pump appended go out in one launch (now, or once a

@@ -48,6 +48,15 @@ enum Stage {
 
 struct Sched;
 
+// A round's own data (esgd_schedule_post_io): the snapshot reads src / div instead of the
+// send bucket, and the result lands in dst instead of rb -- if the round is joined at or
+// after that post (fresh).
+struct RoundIO {
+    const void *src;
+    void *dst;
+    float div;
+};
+
 // Data movement of one round.  A round is joined on the host (activation rules,
 // buffer re-resolution, host staging: prepare()), then queued on the GPU as a whole
 // (launch()), in one node-wide order: every rank launches the rounds of all schedules
@@ -63,6 +72,8 @@ struct Transport {
     virtual int setup(Sched &s) = 0;
     virtual int connect(Sched &) { return ESGD_SUCCESS; }
     virtual int note_producer(Sched &s, uint32_t round, void *stream) = 0;
+    // the post of `round` carries its own data (RoundIO); checked here, used at launch
+    virtual int note_io(Sched &s, uint32_t round, const RoundIO &io);   // default: refused
     // hold mode: the caller's reads of rb / writes of sb queued on `stream` (after
     // wait()) must finish before the next round's snapshot touches the buckets
     virtual int note_consumer(Sched &, void *) { return ESGD_SUCCESS; }
@@ -116,7 +127,7 @@ struct Sched {
     bool cur_fresh = false;
     double stage_t0 = 0;
     int error = 0;
-    char errmsg[256] = {0};
+    char errmsg[1024] = {0};
     uint32_t passive = 0;      // majority: passive rounds since the last activation
     std::atomic<bool> awaiting{false};   // posted, waiting for the activation (written under mu)
     uint64_t roctx_round = 0;  // ESGD_ROCTX=1: the open "round" range (join -> completion)
@@ -200,7 +211,7 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
                       int tag = kNoTag);
 // transport chosen by esgd_set_transport / ESGD_TRANSPORT (comm_api.cpp)
 Transport *default_transport(bool control_only);
-int sched_post(Sched *s, void *producer_stream, int *role);
+int sched_post(Sched *s, void *producer_stream, int *role, const RoundIO *io = nullptr);
 int sched_wait(Sched *s);
 // wait, and say whether this rank had posted the round it returns before joining it
 int sched_wait_ex(Sched *s, int *fresh);
@@ -219,6 +230,8 @@ int engine_issue_log(uint32_t *sched, uint32_t *round, uint32_t cap, uint32_t *n
 void engine_profile(uint64_t out[7]);
 // dataplane.cpp: kernel launches of rounds and ns spent flushing shared launches
 void dataplane_profile(uint64_t *launches, uint64_t *flush_ns);
+// the pending / unfinished shared launches and seal I/O, for a timed-out wait's message
+std::string dataplane_state();
 
 // One polling pass over all schedules (the progress thread calls it in a loop; tests
 // without a thread may call it directly).  Returns true if anything advanced.

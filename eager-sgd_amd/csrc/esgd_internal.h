@@ -90,6 +90,8 @@ int seal_write(void *dst, const uint64_t w[4]);
 int seal_read(const void *src, uint64_t w[4]);
 // the stream they run on (dataplane.cpp)
 int seal_stream(hipStream_t *out);
+// diagnostics: "yes" while a seal read / write waits for the round stream, else nullptr
+const char *seal_io_busy();
 constexpr size_t kSealBytes = 4096;                      // allocated behind every chunk
 void arena_trim();
 // a multi-process job's first export: one chunk exported (or quarantined if refused)

@@ -9,6 +9,7 @@
 // fused snapshot, bucket packing, the rank-pairing kernels and the one-launch round.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <mutex>
@@ -616,6 +617,14 @@ __global__ void k_seal_read(const uint64_t *src, uint64_t *dst) {
 // of two processes sharing a GPU ran 1.7x slower (round 4, r04m-r04o).
 static std::mutex g_seal_mu;
 static uint64_t *g_seal_host = nullptr, *g_seal_view = nullptr;   // pinned, mapped
+static std::atomic<int> g_seal_busy{0};   // a seal kernel is queued and waited for (diagnostics)
+
+const char *seal_io_busy() { return g_seal_busy.load(std::memory_order_relaxed) ? "yes" : nullptr; }
+
+struct SealBusy {
+    SealBusy() { g_seal_busy.fetch_add(1, std::memory_order_relaxed); }
+    ~SealBusy() { g_seal_busy.fetch_sub(1, std::memory_order_relaxed); }
+};
 
 static int seal_io_begin(hipStream_t *s) {   // g_seal_mu held
     if (int rc = seal_stream(s)) return rc;
@@ -631,6 +640,7 @@ int seal_write(void *dst, const uint64_t w[4]) {
     std::lock_guard<std::mutex> lk(g_seal_mu);
     hipStream_t s = nullptr;
     if (int rc = seal_io_begin(&s)) return rc;
+    SealBusy busy;
     hipLaunchKernelGGL(k_seal_write, dim3(1), dim3(64), 0, s, static_cast<uint64_t *>(dst), w[0], w[1], w[2], w[3]);
     ESGD_HIP(hipGetLastError());
     ESGD_HIP(hipStreamSynchronize(s));
@@ -642,6 +652,7 @@ int seal_read(const void *src, uint64_t w[4]) {
     std::lock_guard<std::mutex> lk(g_seal_mu);
     hipStream_t s = nullptr;
     if (int rc = seal_io_begin(&s)) return rc;
+    SealBusy busy;
     for (int i = 0; i < 4; ++i) g_seal_host[i] = 0;
     hipLaunchKernelGGL(k_seal_read, dim3(1), dim3(64), 0, s, static_cast<const uint64_t *>(src), g_seal_view);
     ESGD_HIP(hipGetLastError());

@@ -62,11 +62,23 @@ struct BatchDesc {
     void *sdst;                        // rb
     uint32_t svec, stail;              // 16-B vectors, bytes after them (svec 0 and stail 0:
                                        // not eligible -- the host queues such snapshots)
+    // rb itself: `out` and every `gdst` lie in it; a round with its own output
+    // (BatchArgs::iout) lands at the same offsets there instead
+    void *rbase;
 };
 
 // Kernel arguments: the entries of one launch, in issue-ring order.
 struct BatchArgs {
     const BatchDesc *table;            // device table, indexed by schedule id
+    // Tile assignment.  dynamic: every worker takes the next tile of the launch's list from
+    // the process's tile counter (*queue - qbase), in ring order, until the list is done --
+    // a tile is only started after every earlier tile was, so the launch completes with
+    // ANY number of its workers resident (one suffices; a concurrent kernel may hold the
+    // rest of the GPU).  Static (dynamic 0, ESGD_BATCH_STATIC=1, an A/B): tile g on worker
+    // 1 + g % workers -- every worker must then be resident at once.
+    uint32_t *queue;
+    uint32_t qbase;
+    uint32_t dynamic;
     uint32_t nent;
     uint32_t tile1[kBatchMax + 1];     // phase-1 tiles before entry e (prefix)
     uint32_t tile2[kBatchMax + 1];     // phase-2 tiles before entry e (prefix)
@@ -77,8 +89,14 @@ struct BatchArgs {
     // entry e's kind (0 none / queued before the launch, 1 rb = sb, 2 rb = 0) and its
     // 1024-vector tiles (prefix); the agent publishes e's ready once they have all landed
     uint32_t tile0[kBatchMax + 1];
-    uint8_t snap[kBatchMax];
+    uint8_t snap[kBatchMax];           // 3: rb = isrc / idiv (fp32), the op's copy-in fused
+    // the round's own send data and output (esgd_schedule_post_io): phase 0 reads isrc
+    // (nullptr: the schedule's send bucket), phases 1 and 2 write iout (nullptr: rb)
+    const void *isrc[kBatchMax];
+    void *iout[kBatchMax];
+    float idiv[kBatchMax];
 };
+static_assert(sizeof(BatchArgs) <= 4096, "k_round_batch's arguments must fit the kernel-argument segment");
 
 // The snapshots of a shared launch's rounds (rb = sb, or rb = 0 for a FRESH_ONLY round
 // this rank had not posted), all in one launch queued right before k_round_batch: up to

@@ -1,9 +1,15 @@
 // round_batch.hip — k_round_batch: the one-launch rounds due in issue order, in one kernel.
 //
 // Grid: ONE agent workgroup (block 0, dispatched first) plus `workers` workgroups of 256
-// threads, all resident at once: workers wait on each other's entries through peers, so a
-// worker that is not yet dispatched while the others spin would deadlock the launch.  The
-// host caps the grid so that every rank sharing this GPU fits (round_batch_capacity).
+// threads.  Residency contract: the agent and at least ONE worker must be resident; the
+// other workers may be kept out by concurrent kernels (a torch stream, an RCCL kernel,
+// other ranks sharing the GPU).  Workers take tiles from a per-process counter in list
+// order (BatchArgs::dynamic), so every tile a resident worker spins on depends only on
+// tiles already taken -- by workers that are running -- and on peers' flags of entries no
+// later in the ring.  (Static assignment, tile g on worker 1 + g % workers, needed every
+// worker resident at once: one not dispatched while the others spun on gates its own tiles
+// would open deadlocked the launch -- round 4, 8 ranks on one GPU.)  The host still sizes
+// the grid to what the ranks sharing this GPU leave free (round_batch_capacity), for speed.
 //
 // Agent (wave 0 of block 0; lane e owns entry e):
 //   * publishes `ready` of every entry at once -- everything the entries' snapshots
@@ -13,17 +19,19 @@
 //   * polls every rank's ready / reduced flag of its entry (one system-scope load per rank,
 //     all lanes' loads in flight together) and raises the entry's device gates.
 // Workers walk a global tile list in ring order -- every entry's snapshot tiles, then its
-// phase-1 tiles, then its phase-2 tiles -- tile g on worker 1 + g % workers:
-//   * phase 0 (snapshot, ESGD_SNAPSHOT_IN_BATCH): 1024 vectors of rb = sb or rb = 0,
-//     write-through, drained, counted -- no gate, so no worker waits before its own
-//     snapshot tiles are done;
+// phase-1 tiles, then its phase-2 tiles -- taking the next tile from the counter:
+//   * phase 0 (snapshot, ESGD_SNAPSHOT_IN_BATCH): 1024 vectors of rb = sb, rb = 0 or, for a
+//     round posted with its own send data (esgd_schedule_post_io), rb = src / divisor --
+//     write-through, drained, counted -- no gate: every snapshot tile is taken before any
+//     gated tile;
 //   * phase 1 (reduce-scatter): wait for the entry's ready gate; fold one tile (tv1 16-B
 //     vectors) of shard `rank` of every rank's rb in the reference's tree order
-//     (ffallreduce.c:138-171 via tree_fold) into the local rb and the published shard;
-//     the last tile of an entry to arrive publishes the entry's `reduced` flag;
+//     (ffallreduce.c:138-171 via tree_fold) into the local rb (or the round's own output)
+//     and the published shard; the last tile of an entry to arrive publishes the entry's
+//     `reduced` flag;
 //   * phase 2 (all-gather): wait for the entry's reduced gate; copy one tile of a peer's
-//     published shard into the local rb; the last tile to arrive stores the
-//     round in the entry's fin word (the host polls it).
+//     published shard into the local rb (or the round's own output); the last tile to
+//     arrive stores the round in the entry's fin word (the host polls it).
 // The agent never waits for one entry before serving another, and a worker's tiles come
 // in ring order, so a flag of entry i depends only on flags of entries <= i on every rank:
 // ranks that cut the issue ring into launches differently cannot deadlock.
@@ -64,6 +72,17 @@ __device__ __forceinline__ void put_flags(const PairFlags &f, uint32_t v) {
     for (int q = 0; q < f.ndst; ++q) store_sys(f.dst[q], v);
 }
 
+// A timed-out wait: the host fails the round (err) and no worker is left waiting (both
+// gates open).  err is released at system scope before the gates: a worker's fin can only
+// follow an open gate, and the host reads fin before err (dataplane.cpp base_query).
+__device__ __forceinline__ void fail_entry(const BatchDesc *d, uint32_t v) {
+    store_sys(d->err, v);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_gate(d->ctr + 2, v, false);
+    store_gate(d->ctr + 3, v, false);
+}
+
 template <int K>
 __device__ void agent(const BatchArgs &a, long long t0) {
     const int lane = int(threadIdx.x);
@@ -87,9 +106,7 @@ __device__ void agent(const BatchArgs &a, long long t0) {
                 st = 0;
                 pub = true;
             } else if (wall_clock64() - t0 > a.timeout) {
-                store_sys(d->err, v);
-                store_gate(d->ctr + 2, v, false);
-                store_gate(d->ctr + 3, v, false);
+                fail_entry(d, v);
                 st = 2;
             }
         }
@@ -110,9 +127,7 @@ __device__ void agent(const BatchArgs &a, long long t0) {
                 store_gate(d->ctr + 2 + st, v, d->strict != 0);
                 ++st;
             } else if (wall_clock64() - t0 > a.timeout) {
-                store_sys(d->err, v);              // the host fails the round
-                store_gate(d->ctr + 2, v, false);  // and no worker is left waiting
-                store_gate(d->ctr + 3, v, false);
+                fail_entry(d, v);
                 st = 2;
             }
         }
@@ -121,9 +136,10 @@ __device__ void agent(const BatchArgs &a, long long t0) {
     }
 }
 
-// phase 1, tile `local` of an entry: fold the shard's vectors [local * tv1, +tv1)
+// phase 1, tile `local` of an entry: fold the shard's vectors [local * tv1, +tv1) into
+// `out` (the shard in rb, or in the round's own output) and the published shard
 template <class Tr, int K>
-__device__ __forceinline__ void tile_reduce(const BatchDesc &d, uint32_t local) {
+__device__ __forceinline__ void tile_reduce(const BatchDesc &d, uint32_t local, void *out) {
     using T = typename Tr::T;
     using A = typename Tr::A;
     const uint32_t nvec = uint32_t(d.n / Tr::E);
@@ -132,7 +148,7 @@ __device__ __forceinline__ void tile_reduce(const BatchDesc &d, uint32_t local) 
 #pragma unroll
     for (int j = 0; j < K; ++j)
         rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(d.src[j]), (short)0, bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(d.out, (short)0, bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t wp = __builtin_amdgcn_make_buffer_rsrc(d.pub, (short)0, bytes, 0x00020000);
     constexpr int U = sizeof(T) == 2 ? 2 : 4;   // vectors per input per lane in flight
     const uint32_t v0 = local * d.tv1;
@@ -160,44 +176,65 @@ __device__ __forceinline__ void tile_reduce(const BatchDesc &d, uint32_t local) 
             v[j] = Tr::load(__hip_atomic_load(static_cast<const T *>(d.src[j]) + e, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_SYSTEM));
         tree_fold<Tr, K>(v);
-        __hip_atomic_store(static_cast<T *>(d.out) + e, Tr::store(v[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(static_cast<T *>(out) + e, Tr::store(v[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(static_cast<T *>(d.pub) + e, Tr::store(v[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
-// phase 0, tile `local` of an entry's snapshot: 1024 16-B vectors of rb = sb (kind 1) or
-// rb = 0 (kind 2), write-through; the ragged tail byte by byte in tile 0
-__device__ __forceinline__ void tile_snapshot(const BatchDesc &d, uint32_t local, uint8_t kind) {
+// phase 0, tile `local` of an entry's snapshot: 1024 16-B vectors of rb = src (kind 1),
+// rb = 0 (kind 2) or rb = src / div (kind 3, fp32: the deep500 op's copy-in with the
+// wrapper's division, opt_esgd_solo_imagenet_imbalance.py:40, correctly rounded like
+// k_pack<DIV>), write-through; src = the round's own send data or the send bucket; the
+// ragged tail in tile 0 (bytes, or 4-B elements for kind 3)
+__device__ __forceinline__ void tile_snapshot(const BatchDesc &d, uint32_t local, uint8_t kind, const void *isrc,
+                                              float div) {
     const uint32_t nv = d.svec, v0 = local * 1024u;
+    const void *src = isrc ? isrc : d.ssrc;
     const __amdgpu_buffer_rsrc_t wd = __builtin_amdgcn_make_buffer_rsrc(d.sdst, (short)0, int(nv * 16u), 0x00020000);
     raw16 r[4];
-    if (kind == 1) {
-        const __amdgpu_buffer_rsrc_t rd =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(d.ssrc), (short)0, int(nv * 16u), 0x00020000);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b128(rd, (v0 + u * 256 + threadIdx.x) * 16, 0, 2);
-    } else {
+    if (kind == 2) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) r[u] = raw16{0u, 0u, 0u, 0u};
+    } else {
+        const __amdgpu_buffer_rsrc_t rd =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(src), (short)0, int(nv * 16u), 0x00020000);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b128(rd, (v0 + u * 256 + threadIdx.x) * 16, 0, 2);
+        if (kind == 3) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) r[u][c] = __float_as_uint(__fdiv_rn(__uint_as_float(r[u][c]), div));
+        }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(r[u], wd, (v0 + u * 256 + threadIdx.x) * 16, 0, 17);
     if (local == 0 && threadIdx.x < d.stail) {
-        uint8_t *dst = static_cast<uint8_t *>(d.sdst) + size_t(nv) * 16;
-        const uint8_t b = kind == 1 ? static_cast<const uint8_t *>(d.ssrc)[size_t(nv) * 16 + threadIdx.x] : uint8_t(0);
-        __hip_atomic_store(dst + threadIdx.x, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (kind == 3) {   // fp32: the tail holds whole elements
+            if (threadIdx.x < d.stail / 4) {
+                const float x = static_cast<const float *>(src)[size_t(nv) * 4 + threadIdx.x];
+                __hip_atomic_store(static_cast<float *>(d.sdst) + size_t(nv) * 4 + threadIdx.x, __fdiv_rn(x, div),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        } else {
+            uint8_t *dst = static_cast<uint8_t *>(d.sdst) + size_t(nv) * 16;
+            const uint8_t b = kind == 1 ? static_cast<const uint8_t *>(src)[size_t(nv) * 16 + threadIdx.x] : uint8_t(0);
+            __hip_atomic_store(dst + threadIdx.x, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
-// phase 2, tile `local` of an entry: tvg[sg] vectors of one peer's published shard
-__device__ __forceinline__ void tile_gather(const BatchDesc &d, uint32_t local) {
+// phase 2, tile `local` of an entry: tvg[sg] vectors of one peer's published shard, into
+// rb or (shift != 0) the same place of the round's own output
+__device__ __forceinline__ void tile_gather(const BatchDesc &d, uint32_t local, ptrdiff_t shift) {
     uint32_t sg = 0;
     while (sg < d.nseg && local >= d.t2pre[sg + 1]) ++sg;
     if (sg >= d.nseg) return;   // an entry with nothing to gather (its one dummy tile)
     const uint32_t gv = d.gvec[sg], tv = d.tvg[sg], first = (local - d.t2pre[sg]) * tv;
     const __amdgpu_buffer_rsrc_t gs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(d.gsrc[sg]), (short)0, int(gv * 16u), 0x00020000);
-    const __amdgpu_buffer_rsrc_t gd = __builtin_amdgcn_make_buffer_rsrc(d.gdst[sg], (short)0, int(gv * 16u), 0x00020000);
+    char *gdst = static_cast<char *>(d.gdst[sg]) + shift;
+    const __amdgpu_buffer_rsrc_t gd = __builtin_amdgcn_make_buffer_rsrc(gdst, (short)0, int(gv * 16u), 0x00020000);
     for (uint32_t base = first; base < first + tv && base < gv; base += 1024u) {
         const uint32_t i = base + threadIdx.x;
         raw16 r[4];
@@ -208,7 +245,7 @@ __device__ __forceinline__ void tile_gather(const BatchDesc &d, uint32_t local) 
     }
     if (first == 0 && threadIdx.x < d.gtail[sg]) {   // bytes after the last full vector
         const uint8_t *src = static_cast<const uint8_t *>(d.gsrc[sg]) + size_t(gv) * 16;
-        uint8_t *dst = static_cast<uint8_t *>(d.gdst[sg]) + size_t(gv) * 16;
+        uint8_t *dst = reinterpret_cast<uint8_t *>(gdst) + size_t(gv) * 16;
         __hip_atomic_store(dst + threadIdx.x,
                            __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -224,15 +261,24 @@ __global__ __launch_bounds__(256) void k_round_batch(BatchArgs a) {
         if (threadIdx.x < 64) agent<K>(a, t0);
         return;
     }
-    // stale peer lines of earlier launches out of this CU's L1 and this XCD's L2
+    // stale peer lines of earlier launches out of this CU's L1 and this XCD's L2 (a worker
+    // that starts late still does this before its first tile)
     if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     const uint32_t workers = gridDim.x - 1;
     // the tile list: every entry's snapshot tiles (phase 0), its phase-1 tiles, its phase-2
     // tiles, each in ring order; a worker meets no gate before its snapshot tiles are done
-    const uint32_t T0 = a.tile0[a.nent], T1 = T0 + a.tile1[a.nent], T = T1 + a.tile2[a.nent];
+    const uint32_t T0 = a.tile0[a.nent], T1 = T0 + a.tile1[a.nent], T = T0 + a.tile1[a.nent] + a.tile2[a.nent];
+    __shared__ uint32_t s_next;
     uint32_t e = 0;
     int phase = 0;
-    for (uint32_t g = blockIdx.x - 1; g < T; g += workers) {
+    for (uint32_t g = blockIdx.x - 1;; g += workers) {
+        if (a.dynamic) {   // the next tile of the list, whichever worker is free (BatchArgs)
+            if (threadIdx.x == 0)
+                s_next = __hip_atomic_fetch_add(a.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.qbase;
+            __syncthreads();
+            g = s_next;   // read by every thread before the next write (a barrier follows in each path)
+        }
+        if (g >= T) break;
         const int ph = g < T0 ? 0 : g < T1 ? 1 : 2;
         if (ph != phase) { phase = ph; e = 0; }
         const uint32_t t = ph == 0 ? g : ph == 1 ? g - T0 : g - T1;
@@ -241,7 +287,7 @@ __global__ __launch_bounds__(256) void k_round_batch(BatchArgs a) {
         const BatchDesc &d = a.table[a.sid[e]];
         const uint32_t v = a.value[e];
         if (ph == 0) {
-            tile_snapshot(d, t - pre[e], a.snap[e]);
+            tile_snapshot(d, t - pre[e], a.snap[e], a.isrc[e], a.idiv[e]);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are in memory
             __syncthreads();
             if (threadIdx.x == 0) {
@@ -262,8 +308,10 @@ __global__ __launch_bounds__(256) void k_round_batch(BatchArgs a) {
         }
         __syncthreads();
         const uint32_t local = t - pre[e];
-        if (!gather) tile_reduce<Tr, K>(d, local);
-        else tile_gather(d, local);
+        // a round with its own output (esgd_schedule_post_io) lands there, at rb's offsets
+        const ptrdiff_t shift = a.iout[e] ? static_cast<char *>(a.iout[e]) - static_cast<char *>(d.rbase) : 0;
+        if (!gather) tile_reduce<Tr, K>(d, local, static_cast<char *>(d.out) + shift);
+        else tile_gather(d, local, shift);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are in memory
         __syncthreads();
         if (threadIdx.x == 0) {

@@ -91,6 +91,9 @@ struct Segment {
     std::atomic<uint64_t> beat_ns;
     std::atomic<int32_t> pid[kMaxRanks];
     std::atomic<int32_t> device[kMaxRanks];
+    // the physical GPU of rank r ((PCI domain, bus, device) + 1; 0: none): device ordinals
+    // are per process (HIP_VISIBLE_DEVICES may give every rank "device 0")
+    std::atomic<uint64_t> gpu_id[kMaxRanks];
     std::atomic<uint64_t> ticket_next;
     // device pairing flags: rank r's flag page of mode m + 1 (1 uncached, 2 fine-grained
     // HBM; dataplane.cpp)

@@ -61,6 +61,9 @@ def _bind(h):
         "esgd_comm_profile": (i, [C.POINTER(u64), i]),
         "esgd_schedule_post_group": (i, [C.POINTER(u64), i, vp, C.POINTER(i)]),
         "esgd_schedule_release_group": (i, [C.POINTER(u64), i, vp]),
+        "esgd_schedule_post_io": (i, [u64, vp, vp, C.c_float, vp, C.POINTER(i)]),
+        "esgd_schedule_post_group_io": (i, [C.POINTER(u64), i, C.POINTER(vp), C.POINTER(vp), C.c_float, vp,
+                                            C.POINTER(i)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(h, name)
@@ -223,6 +226,20 @@ class Schedule:
         if s == 0:
             s = 1   # ESGD_STREAM_NULL
         check(lib().esgd_schedule_post(self.handle, s, C.byref(role)), "esgd_schedule_post")
+        return role.value
+
+    def post_io(self, src, dst, divisor: float = 1.0, stream=None) -> int:
+        """esgd_schedule_post_io: the round reads src / divisor instead of the send bucket
+        and writes its result into dst (device pointers, 16-B aligned) -- if this rank joins
+        it at or after this post (wait() then returns True); otherwise dst is untouched and
+        the result is in rb."""
+        from .device import as_ptr
+        role = C.c_int()
+        s = None if stream is None else (stream.handle if hasattr(stream, "handle") else int(stream))
+        if s == 0:
+            s = 1   # ESGD_STREAM_NULL
+        check(lib().esgd_schedule_post_io(self.handle, as_ptr(src), as_ptr(dst), float(divisor), s, C.byref(role)),
+              "esgd_schedule_post_io")
         return role.value
 
     def wait(self) -> bool:

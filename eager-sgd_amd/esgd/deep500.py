@@ -60,6 +60,9 @@ def _bind(h):
     h.allreducef_forward_cuda_post_many.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), C.c_float, vp]
     h.allreducef_forward_cuda_wait_many.restype = C.c_int
     h.allreducef_forward_cuda_wait_many.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), vp]
+    h.allreducef_forward_cuda_post_many_io.restype = C.c_int
+    h.allreducef_forward_cuda_post_many_io.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), C.POINTER(vp),
+                                                       C.c_float, vp]
     h.is_cuda_supported.restype, h.is_cuda_supported.argtypes = C.c_bool, [vp]
     h.report.restype, h.report.argtypes = C.c_int64, [vp, vp]
     h.delete_op.restype, h.delete_op.argtypes = None, [vp]
@@ -168,6 +171,21 @@ class AllreduceOp:
         gs = (C.c_void_p * n)(*[as_ptr(g) for g in grads])
         _lib.check(lib().allreducef_forward_cuda_post_many(hs, n, gs, float(divisor), stream),
                    "allreducef_forward_cuda_post_many")
+
+    @staticmethod
+    def post_many_io(ops, grads, outs, divisor: float = 1.0, stream: int | None = None):
+        """post_many with the outputs named at the post (allreducef_forward_cuda_post_many_io):
+        each round reads grads[i] / divisor itself and writes its result into outs[i] (may be
+        grads[i]) -- no copy-in or copy-out launch on the caller's stream.  wait_many(ops,
+        outs) then copies out only the rounds a peer carried this rank through before the
+        post.  Unaligned tensors or a bf16 wire fall back to post_many.  Raises EsgdError."""
+        from .device import as_ptr
+        n = len(ops)
+        hs = (C.c_void_p * n)(*[op.handle for op in ops])
+        gs = (C.c_void_p * n)(*[as_ptr(g) for g in grads])
+        os_ = (C.c_void_p * n)(*[as_ptr(o) for o in outs])
+        _lib.check(lib().allreducef_forward_cuda_post_many_io(hs, n, gs, os_, float(divisor), stream),
+                   "allreducef_forward_cuda_post_many_io")
 
     @staticmethod
     def wait_many(ops, outs, stream: int | None = None):

@@ -14,16 +14,19 @@ reference's CPU-only TF kernel (deep500/frameworks/tensorflow/custom_operators/t
 The division is fused into the op's copy-in (same IEEE fp32 division, same bits) and the
 reduced gradient is written back into p.grad in place: per tensor and step 3 HBM passes
 of the gradient (copy-in with the divide; the move with the zeroing fused; copy-out)
-instead of 5 (divide, copy-in, move, copy-out, memset).
+instead of 5 (divide, copy-in, move, copy-out, memset); with the fused round I/O below, 1
+(the round's own snapshot reads the gradient; its phases write the result back).
 
 pipeline=True (the per-tensor default): every tensor's round is posted before the first
 is waited for, so the 161 host round trips overlap instead of running one after another as
 the reference's blocking ops do (:304-307); the same rounds over the same operands, so the
 same bits.  The posts and the waits each go through ONE call
-(allreducef_forward_cuda_post_many / _wait_many: one copy-in launch per 48 tensors, one
-producer event, one copy-out launch per 48, one release event), and the data plane runs
-the rounds that come due together in shared launches.  pipeline=False keeps the blocking
-chain.
+(allreducef_forward_cuda_post_many_io / _wait_many, one producer event), and the data plane
+runs the rounds that come due together in shared launches, each round reading grad /
+comm_size and writing the reduced gradient back into p.grad itself (fused_io; no copy-in or
+copy-out launch on the caller's stream, 2 HBM passes of the gradient fewer -- only a round a
+peer carried this rank through before its post is copied out of the op's bucket).
+pipeline=False keeps the blocking chain (each op fused the same way).
 
 fuse=True (SURVEY.md §8(f) "bucket fusion"): the reference runs one schedule per tensor,
 161 per ResNet-50 step (opt_esgd_solo_imagenet_imbalance.py:85-248), each a
@@ -42,7 +45,7 @@ from . import deep500
 class EagerSGDOptimizer:
     def __init__(self, optimizer, comm_size: int, mode: str = "solo", async_: int = 32,
                  seed: int = 6545343, fuse: bool = False, wire: str = "fp32",
-                 pipeline: bool = True):
+                 pipeline: bool = True, fused_io: bool = True):
         if mode not in deep500.MODES:
             raise ValueError(f"mode must be one of {sorted(deep500.MODES)}")
         if wire not in deep500.WIRES:
@@ -54,6 +57,10 @@ class EagerSGDOptimizer:
         self.mode, self.async_, self.seed = mode, int(async_), int(seed)
         self.fuse = bool(fuse)
         self.pipeline = bool(pipeline)
+        # per tensor: the rounds read grad / comm_size and write the result back themselves
+        # (allreducef_forward_cuda_post_many_io); False: copy-in / copy-out kernels on the
+        # caller's stream around them (an A/B)
+        self.fused_io = bool(fused_io)
         self.wire = wire        # "bf16": bf16 copies between ranks
         self._ops = {}          # parameter -> op instance (one bucket per tensor)
         self._fused = None      # (layout, op, packed bucket, reduced bucket)
@@ -93,8 +100,11 @@ class EagerSGDOptimizer:
             if posted:
                 ops, gs = [p[0] for p in posted], [p[1] for p in posted]
                 err = None
-                try:
-                    deep500.AllreduceOp.post_many(ops, gs, self.comm_size, stream)   # :40 fused
+                try:   # :40 and the copy-in / copy-out fused into the rounds themselves
+                    if self.fused_io:
+                        deep500.AllreduceOp.post_many_io(ops, gs, gs, self.comm_size, stream)
+                    else:
+                        deep500.AllreduceOp.post_many(ops, gs, self.comm_size, stream)
                 except Exception as e:   # noqa: BLE001 -- re-raised below
                     err = e
                 try:   # every posted round is waited for, even after a failed post

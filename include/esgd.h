@@ -257,6 +257,21 @@ int esgd_schedule_release(esgd_sched_h h, void *stream);
  * roles may be NULL.  Stops at the first failure and returns its status. */
 int esgd_schedule_post_group(const esgd_sched_h *h, int n, void *producer_stream, int *roles);
 int esgd_schedule_release_group(const esgd_sched_h *h, int n, void *stream);
+/* A post whose round carries its own data (device schedules, ipc or rccl transport, not
+ * WIRE_BF16 / FFCOLL_BUFFERS): instead of moving the send bucket, the round's snapshot
+ * reads src / divisor (divisor 1: src as it is; any other divisor: FLOAT only, IEEE
+ * division as the wrapper's grad / comm_size, opt_esgd_solo_imagenet_imbalance.py:40),
+ * and the result is written to dst (may be src) instead of rb -- the deep500 op's copy-in
+ * and copy-out fused into the round.  src and dst: count elements, 16-B aligned, untouched
+ * by the caller until wait returns.  Only a round this rank joins at or after this post
+ * (wait_ex's fresh = 1) takes src and writes dst; a round a peer's activation carried this
+ * rank through before the post (fresh = 0) ran with the send bucket as usual (zeros with
+ * ESGD_SCHED_FRESH_ONLY) and left its result in rb.  producer_stream: as for post (the
+ * work that writes src).  The group form posts n schedules with ONE producer event. */
+int esgd_schedule_post_io(esgd_sched_h h, const void *src, void *dst, float divisor, void *producer_stream,
+                          int *role);
+int esgd_schedule_post_group_io(const esgd_sched_h *h, int n, const void *const *srcs, void *const *dsts,
+                                float divisor, void *producer_stream, int *roles);
 int esgd_schedule_test(esgd_sched_h h, int *flag);
 int esgd_schedule_delete(esgd_sched_h h);
 int esgd_schedule_stats(esgd_sched_h h, esgd_sched_stats_t *out);

@@ -91,6 +91,15 @@ int allreducef_forward_cuda_wait(void *handle, float *output, void *stream);
 int allreducef_forward_cuda_post_many(void *const *handles, int n, const float *const *inputs, float divisor,
                                       void *stream);
 int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const *outputs, void *stream);
+/* Extension: _post_many with the outputs known at the post (EagerSGDOptimizer writes the
+ * reduced gradients back into the gradient tensors): each round reads inputs[i] / divisor
+ * itself in its snapshot and writes its result into outputs[i] (esgd_schedule_post_io) --
+ * no copy-in or copy-out launch on stream, no consumer event.  _wait_many (with the same
+ * outputs) then only copies out the rounds a peer's activation carried this rank through
+ * before the post (their results are in the op's bucket).  Tensors must be 16-B aligned
+ * and the ops fp32 on the wire; otherwise the group is posted as by _post_many. */
+int allreducef_forward_cuda_post_many_io(void *const *handles, int n, const float *const *inputs,
+                                         float *const *outputs, float divisor, void *stream);
 /* Extension: what the void entry points above (allreducef_forward, allreducef_forward_cuda)
  * do when their round fails (a peer timeout, an allocation failure).  ESGD_OP_ON_ERROR_ABORT
  * (default; env ESGD_OP_ON_ERROR=abort): print the error and abort the process, as their

@@ -178,10 +178,39 @@ def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0
     return out
 
 
+class Mismatch(dict):
+    """A failed round's verdict: falsy (so `all(verdicts)` still fails), and it says where --
+    the round, the first wrong element, got / want, how many elements are wrong, every
+    rank's input at that element, and this rank's schedule stats (fresh / carried rounds,
+    transport, whether its bucket was shadowed)."""
+
+    def __bool__(self):
+        return False
+
+
+def mismatch(t, got, want, xs, sched=None):
+    import numpy as np
+    gb, wb = got.view(np.uint8), want.view(np.uint8)
+    bad = np.nonzero(gb.reshape(len(got), -1) != wb.reshape(len(want), -1))[0]
+    i = int(bad[0]) if len(bad) else -1
+    m = Mismatch(round=t, index=i, bad_elements=int(len(np.unique(bad))), count=int(len(got)))
+    if i >= 0:
+        val = (lambda a: float(a[i]) if a.dtype.kind == "f" else int(a[i]))
+        m.update(got=val(got), want=val(want), inputs=[val(x) for x in xs])
+    if sched is not None:
+        try:
+            m["stats"] = sched.stats()
+        except Exception as e:   # noqa: BLE001 -- diagnostics only
+            m["stats"] = repr(e)
+    m["env"] = {k: v for k, v in os.environ.items()
+                if k in ("ESGD_FAIL_EXPORTS", "ESGD_SHADOW", "ESGD_BATCH_ROUNDS", "ESGD_SMALL_ROUND_BYTES")}
+    return m
+
+
 def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0, buf="device",
                   in_place=False, transport="ipc", shadow_ranks=(), small_bytes=None,
                   piece_bytes=None, host_chunk=None, device_flags=None, wire=False, chunk_kernel=None,
-                  fail_exports=None, batch=None, detail=False):
+                  fail_exports=None, batch=None):
     """Data plane on the GPU: every rank reduces its splitmix bucket; returns the
     result bytes' digest per round plus a bit-exactness verdict against the oracle.
     shadow_ranks: ranks whose device buckets go through the owned shadow bucket.
@@ -263,10 +292,8 @@ def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0
         else:
             want = ffref.allreduce_rd(xs)[0]
         same = bool(np.array_equal(got.view(np.uint8), want.view(np.uint8)))
-        if detail and not same:   # diagnostics: the first wrong element, got vs want, every input
-            i = int(np.nonzero(got.view(np.uint8) != want.view(np.uint8))[0][0]) // got.itemsize
-            verdicts.append({"round": t, "index": i, "got": float(got[i]), "want": float(want[i]),
-                             "inputs": [float(x[i]) for x in xs], "stats": s.stats()})
+        if not same:   # self-describing: a falsy verdict that says what came out wrong
+            verdicts.append(mismatch(t, got, want, xs, s))
         else:
             verdicts.append(same)
         comm.barrier()
@@ -512,7 +539,7 @@ def op_device_pattern(rank, world, count=25559081, steps=9, mode="solo", packed=
     return out
 
 
-def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp32", pipeline=True):
+def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp32", pipeline=True, fused_io=True):
     """EagerSGDOptimizer on PyTorch-ROCm: every rank's p.grad after apply_gradients must
     equal the oracle tree of (grad_r / P) over ranks, bit for bit (allreduce), or over
     expected_inputs' contributors when the ranks call every op in late_ranks' order
@@ -531,7 +558,7 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp3
     torch.cuda.set_device(dev)
     model = torch.nn.Sequential(torch.nn.Linear(64, 48), torch.nn.ReLU(), torch.nn.Linear(48, 10)).to(dev)
     opt = EagerSGDOptimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9), world, mode=mode,
-                            fuse=fuse, wire=wire, pipeline=pipeline)
+                            fuse=fuse, wire=wire, pipeline=pipeline, fused_io=fused_io)
     ok = []
     for t in range(steps):
         g = torch.Generator().manual_seed(100 * t + rank)
@@ -545,7 +572,7 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp3
         dist.all_gather_object(allg, local)
         comm.barrier()
         late = t > 0 and rank in late_ranks(mode, world, t)
-        names = ("forward_cuda_div", "forward_cuda_packed", "post_cuda", "post_many")
+        names = ("forward_cuda_div", "forward_cuda_packed", "post_cuda", "post_many", "post_many_io")
         orig = {n: getattr(deep500.AllreduceOp, n) for n in names}
         if late:   # every op call (or post) of this step comes LATE_S after the peers'
             def delayed(fn):
@@ -594,22 +621,27 @@ def op_group(rank, world, steps=3, sizes=(1, 17, 1000, 4099, 262147, (2 << 20) +
     deep500.configure("allreduce", 32, 6545343)
     grp = [deep500.AllreduceOp((n,)) for n in sizes]
     one = [deep500.AllreduceOp((n,)) for n in sizes]
+    fio = [deep500.AllreduceOp((n,)) for n in sizes]   # post_many_io: the rounds do the copies
     ok, errs = [], {}
     for t in range(steps):
         xs = [[ffref.fill_uniform(0xA11 + 13 * t + i, r, n) for r in range(world)] for i, n in enumerate(sizes)]
         g = [torch.from_numpy(x[rank]).to(dev) for x in xs]
         h = [gi.clone() for gi in g]
+        k = [gi.clone() for gi in g]
         comm.barrier()
         deep500.AllreduceOp.post_many(grp, g, float(world))
         deep500.AllreduceOp.wait_many(grp, g)
         for op, hi in zip(one, h):
             op.forward_cuda_div(hi, hi, float(world))
+        deep500.AllreduceOp.post_many_io(fio, k, k, float(world))
+        deep500.AllreduceOp.wait_many(fio, k)
         torch.cuda.synchronize()
         for i, x in enumerate(xs):
             want = ffref.tree_sum([np.float32(xr) / np.float32(world) for xr in x])
-            a, b = g[i].cpu().numpy(), h[i].cpu().numpy()
+            a, b, c = g[i].cpu().numpy(), h[i].cpu().numpy(), k[i].cpu().numpy()
             ok.append(bool(np.array_equal(a.view(np.uint32), want.view(np.uint32)) and
-                           np.array_equal(a.view(np.uint32), b.view(np.uint32))))
+                           np.array_equal(a.view(np.uint32), b.view(np.uint32)) and
+                           np.array_equal(a.view(np.uint32), c.view(np.uint32))))
     # misuse: op 0 posted alone, then a group post naming it fails and leaves it posted
     x = [torch.ones(n, device=dev) for n in sizes]
     grp[0].post_cuda(x[0], float(world))
@@ -1580,6 +1612,212 @@ def gpu_reinit(rank, world, count=4099):
     except EsgdError as e:
         err = str(e)
     return {"ok": ok, "err": err}
+
+
+def gpu_finalize_held(rank, world, n=4, count=1024, delete_first=False):
+    """Finalize (or delete) while rounds wait in the pending shared launch: with batch_hold
+    nothing but an explicit flush sends it, so after every rank has launched its rounds into
+    it (posted, pumped, held), fffinalize -- or each schedule's deletion -- must send them
+    while the schedules are alive (the launch used to be flushed after the
+    teardown, on freed schedules).  The rounds then pair up across ranks and land: every
+    bucket holds the int32 sum of allreduce.c's (i + 7 r) inputs."""
+    import numpy as np
+
+    from esgd import _lib
+    from esgd import device as dev
+    comm = _comm()
+    comm.set_config("batch_hold", 1)
+    rbs = [dev.DeviceBuffer(count, _lib.INT32) for _ in range(n)]
+    for k, rb in enumerate(rbs):
+        rb.upload((np.arange(count) + 7 * rank + k).astype(np.int32))
+    scheds = [comm.Schedule(comm.ALLREDUCE, None, rb, count, dtype=_lib.INT32, buf=comm.BUF_DEVICE)
+              for rb in rbs]
+    l0 = comm.get_config("launches")
+    comm.barrier()
+    for s in scheds:
+        s.post()
+    time.sleep(0.5)   # every rank's progress thread joins and launches them: held
+    import torch.distributed as dist
+    dist.barrier()
+    launched_before = comm.get_config("launches") - l0
+    if delete_first:
+        for s in scheds:
+            s.delete()
+    comm.finalize()
+    ok = []
+    for k, rb in enumerate(rbs):
+        want = sum((np.arange(count) + 7 * r + k) for r in range(world)).astype(np.int32)
+        ok.append(bool(np.array_equal(rb.download(), want)))
+    return {"ok": ok, "launched_before_finalize": launched_before}
+
+
+def gpu_post_io(rank, world, count=4099, rounds=3, small_bytes=None, batch=None, shadow_ranks=(),
+                plain_ranks=(), divisor=None, separate_dst=True, dtype_name="fp32"):
+    """esgd_schedule_post_io on the data plane: every round of an allreduce schedule reads
+    this rank's tensor src / divisor itself and writes the result into dst (a separate
+    buffer, or src itself), never the send bucket -- checked bit for bit against the
+    oracle tree of (x_r / divisor), with rb left to the round.  plain_ranks post their
+    share through the send bucket instead (a mixed job); shadow_ranks' buckets are
+    shadowed (one-launch rounds of their own beside peers' shared launches)."""
+    import numpy as np
+
+    from esgd import _lib
+    from esgd import device as dev
+    from oracle import ffref
+    if rank in shadow_ranks:
+        os.environ["ESGD_SHADOW"] = "1"
+    if batch is not None:
+        os.environ["ESGD_BATCH_ROUNDS"] = str(batch)
+    if small_bytes is not None:
+        os.environ["ESGD_SMALL_ROUND_BYTES"] = str(small_bytes)
+    comm = _comm()
+    dt = {"fp32": _lib.FLOAT, "int32": _lib.INT32}[dtype_name]
+    div = float(world if divisor is None else divisor) if dt == _lib.FLOAT else 1.0
+    sb, rb = dev.DeviceBuffer(count, dt), dev.DeviceBuffer(count, dt)
+    src, dst = dev.DeviceBuffer(count, dt), dev.DeviceBuffer(count, dt)
+    s = comm.Schedule(comm.ALLREDUCE, sb, rb, count, dtype=dt, buf=comm.BUF_DEVICE)
+    verdicts, fresh = [], []
+    for t in range(rounds):
+        if dt == _lib.FLOAT:
+            xs = [ffref.fill_uniform(0x10D + t, r, count) for r in range(world)]
+        else:
+            xs = [(np.arange(count) + t + 7 * r).astype(np.int32) for r in range(world)]
+        if rank in plain_ranks:
+            sb.upload(xs[rank] / np.float32(div) if dt == _lib.FLOAT else xs[rank])
+        else:
+            src.upload(xs[rank])
+        dst.upload(np.full(count, 7, dtype=xs[0].dtype))
+        comm.barrier()
+        if rank in plain_ranks:
+            s.post()
+        else:
+            s.post_io(src, dst if separate_dst else src, div)
+        fresh.append(s.wait())
+        out = rb if rank in plain_ranks else (dst if separate_dst else src)
+        got = out.download()
+        want = ffref.tree_sum([x / np.float32(div) for x in xs]) if dt == _lib.FLOAT else \
+            sum(x.astype(np.int64) for x in xs).astype(np.int32)
+        same = bool(np.array_equal(got.view(np.uint8), want.view(np.uint8)))
+        verdicts.append(same if same else mismatch(t, got, want, xs, s))
+        comm.barrier()
+    s.delete()
+    comm.finalize()
+    return {"verdicts": verdicts, "fresh": fresh}
+
+
+def gpu_post_io_late(rank, world, count=4099, steps=8, async_=3, late=1):
+    """post_io under solo's asynchronous rounds: HOLD | FRESH_ONLY (how the deep500 op runs
+    them), rank `late` posts LATE_S after its peers every step.  A round the early rank's
+    activation carries the late rank through before its post does not take its data: wait
+    says fresh = 0, its dst keeps what it held, and the round's result (its share zero) is
+    in rb; a round it posted in time takes src and writes dst.  Every rank's result must be
+    the oracle tree of (x_r / P if rank r's round was fresh else 0), the same bits on every
+    rank."""
+    import numpy as np
+    import torch.distributed as dist
+
+    from esgd import device as dev
+    from oracle import ffref
+    comm = _comm()
+    rb = dev.DeviceBuffer(count)
+    src, dst = dev.DeviceBuffer(count), dev.DeviceBuffer(count)
+    s = comm.Schedule(comm.SOLO, None, rb, count, async_=async_, seed=6545343, buf=comm.BUF_DEVICE,
+                      flags=comm.HOLD | comm.FRESH_ONLY)
+    out = []
+    for t in range(steps):
+        xs = [ffref.fill_uniform(0x1A7E + t, r, count) for r in range(world)]
+        src.upload(xs[rank])
+        dst.upload(np.full(count, 3.0, np.float32))
+        comm.barrier()
+        if rank == late and t > 0:
+            time.sleep(LATE_S)
+        s.post_io(src, dst, float(world))
+        f = s.wait()
+        res = (dst if f else rb).download()
+        untouched = f or bool(np.all(dst.download() == np.float32(3.0)))
+        s.release()
+        fr = [None] * world
+        dist.all_gather_object(fr, bool(f))
+        want = ffref.tree_sum([x / np.float32(world) if fr[r] else np.zeros_like(x) for r, x in enumerate(xs)])
+        out.append({"t": t, "fresh": fr, "untouched": untouched, "ok": bool(np.array_equal(res.view(np.uint32),
+                                                                                          want.view(np.uint32))),
+                    "digest": zlib.crc32(res.tobytes())})
+    comm.barrier()
+    s.delete()
+    comm.finalize()
+    return out
+
+
+def gpu_residency(rank, world, hog_ms=6000, free_cus=2, rounds=4, counts=(1 << 20, 65536, 17, 300007, 1025),
+                  static=False):
+    """Batched rounds while a concurrent kernel holds almost the whole GPU (verdict r04 item
+    3): rank 0 starts k_occupy (tools/bin/libesgd_sweeps.so) on a side stream -- 2 x CUs -
+    2 x free_cus workgroups of 16 waves, resident for hog_ms -- then every rank posts one
+    round of five one-launch schedules (one shared k_round_batch launch per rank) and waits.
+    Those rounds must complete on the few workgroup slots left, long before the hog ends:
+    workers take tiles from the launch's counter, so the resident ones do every tile
+    (first_round_s; the five are held -- batch_hold -- until all are in the pending launch,
+    then sent together: 64 + 1 + ... tiles per phase, more workers than fit).  The
+    launch's workgroups that did not fit are dispatched, find the list done and leave once
+    the hog does -- only then can the stream's next launch start, so the later rounds
+    (checked for their bits) wait for the hog.  int32 inputs of allreduce.c, (i + t + 7 r)."""
+    import ctypes as C
+
+    import numpy as np
+
+    from esgd import _lib
+    from esgd import device as dev
+    if static:
+        os.environ["ESGD_BATCH_STATIC"] = "1"
+    comm = _comm()
+    sw = C.CDLL(os.path.join(ROOT, "tools", "bin", "libesgd_sweeps.so"))
+    sw.esgd_sweep_occupy.restype, sw.esgd_sweep_occupy.argtypes = C.c_int, [C.c_int, C.c_uint64, C.c_void_p]
+    sw.esgd_sweep_cu_count.restype = C.c_int
+    bufs = [(dev.DeviceBuffer(n, _lib.INT32), dev.DeviceBuffer(n, _lib.INT32)) for n in counts]
+    scheds = [comm.Schedule(comm.ALLREDUCE, sb, rb, n, dtype=_lib.INT32, buf=comm.BUF_DEVICE)
+              for n, (sb, rb) in zip(counts, bufs)]
+    ok, times = [], []
+
+    def one_round(t, held=False):
+        for n, (sb, _) in zip(counts, bufs):
+            sb.upload((np.arange(n) + t + 7 * rank).astype(np.int32))
+        comm.barrier()
+        if held:   # every round joined and launched into the pending shared launch first
+            comm.set_config("batch_hold", 1)
+        t0 = time.perf_counter()
+        for s_ in scheds:
+            s_.post()
+        if held:
+            time.sleep(0.3)
+            t0 = time.perf_counter()
+            comm.set_config("batch_hold", 0)   # the next progress pass sends all of them
+        for s_ in scheds:
+            s_.wait()
+        times.append(time.perf_counter() - t0)
+        for n, (_, rb) in zip(counts, bufs):
+            want = sum((np.arange(n) + t + 7 * r) for r in range(world)).astype(np.int32)
+            ok.append(bool(np.array_equal(rb.download(), want)))
+
+    for t in range(2):   # warm: the descriptors exist before the hog
+        one_round(t)
+    side = dev.Stream()
+    comm.barrier()
+    t_hog = time.perf_counter()
+    if rank == 0:
+        blocks = 2 * sw.esgd_sweep_cu_count() - 2 * free_cus
+        assert sw.esgd_sweep_occupy(blocks, int(hog_ms * 1000), side.handle) == 0
+        time.sleep(0.2)   # resident before the round starts
+    comm.barrier()
+    for t in range(2, 2 + rounds):
+        one_round(t, held=t == 2)
+    side.synchronize()
+    hog_s = time.perf_counter() - t_hog
+    comm.barrier()
+    workers = comm.get_config("batch_workers")
+    for s_ in scheds:
+        s_.delete()
+    comm.finalize()
+    return {"first_round_s": times[2], "round_s": times, "hog_s": hog_s, "ok": ok, "workers": workers}
 
 
 def op_void_peer_lost(rank, world, count=5000):

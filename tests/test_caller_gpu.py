@@ -41,7 +41,10 @@ def test_deep500_op_device_late_gradient_dropped(on_time, count):
         assert o["sync_rounds"] == [r % 4 == 0 for r in range(2, 10)]
 
 
-VARIANTS = {"blocking": dict(pipeline=False), "pipelined": dict(pipeline=True), "fused": dict(fuse=True)}
+VARIANTS = {"blocking": dict(pipeline=False), "pipelined": dict(pipeline=True), "fused": dict(fuse=True),
+            # the per-tensor rounds with copy-in / copy-out kernels on the caller's stream
+            # instead of the fused round I/O (an A/B): the same bits
+            "pipelined_copy_kernels": dict(pipeline=True, fused_io=False)}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))

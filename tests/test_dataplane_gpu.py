@@ -514,6 +514,13 @@ def test_pipelined_stress_batched(kind, world, batch):
     # one five-launch size among them); a rank's share is its tag iff it had posted the
     # round, never torn, the same bits on every rank
     outs = run("gpu_stress_pipelined", world, kind=kind, rounds=120, batch=batch, timeout=400)
+    _check_pipelined(outs, world)
+    assert sum(o["auto_rounds"] for o in outs) > 0
+
+
+def _check_pipelined(outs, world):
+    # a rank's share of every round is its tag iff it had posted the round, never torn,
+    # the same bits on every rank
     bits = outs[0]["bits"]
     for o in outs:
         assert not o["torn"], o["torn"]
@@ -523,8 +530,19 @@ def test_pipelined_stress_batched(kind, world, batch):
             v = outs[0]["vals"][i][t - 1]
             for q in range(world):
                 want = t % (1 << bits) if outs[q]["fresh"][i][t - 1] else 0
-                assert (v >> (bits * q)) & ((1 << bits) - 1) == want, (i, t, q)
-    assert sum(o["auto_rounds"] for o in outs) > 0
+                assert (v >> (bits * q)) & ((1 << bits) - 1) == want, (i, t, q, v, want)
+
+
+@pytest.mark.parametrize("kind", [SOLO, MAJORITY])
+def test_pipelined_stress_refused_exports_p8(kind):
+    # round 4's r04zp configuration: 8 ranks, the batched per-tensor stress, the first
+    # chunk export of ranks 4-7 refused -- through the real path now (ESGD_FAIL_EXPORTS
+    # writes the seal, then refuses the runtime call): the refused chunks are quarantined,
+    # the published shards move, the peers map the moved chunks and read their seals
+    world = 8
+    outs = run("gpu_stress_pipelined", world, kind=kind, rounds=60, fail_exports=[0, 0, 0, 0, 1, 1, 1, 1],
+               timeout=400)
+    _check_pipelined(outs, world)
 
 
 @pytest.mark.parametrize("env", [{"ESGD_BATCH_DEPTH": "0"}, {"ESGD_BATCH_DEPTH": "3"},
@@ -536,16 +554,7 @@ def test_pipelined_stress_switches(env):
     # a k_copy_many launch, every join on the progress thread
     world = 4
     outs = run("gpu_stress_pipelined", world, kind=SOLO, rounds=60, batch=[64, 0, 5, 2], env=env, timeout=300)
-    bits = outs[0]["bits"]
-    for o in outs:
-        assert not o["torn"], o["torn"]
-        assert o["vals"] == outs[0]["vals"]
-    for i in range(len(outs[0]["vals"])):
-        for t in range(1, len(outs[0]["vals"][i]) + 1):
-            v = outs[0]["vals"][i][t - 1]
-            for q in range(world):
-                want = t % (1 << bits) if outs[q]["fresh"][i][t - 1] else 0
-                assert (v >> (bits * q)) & ((1 << bits) - 1) == want, (i, t, q)
+    _check_pipelined(outs, world)
 
 
 @pytest.mark.parametrize("kind", [SOLO, MAJORITY])
@@ -677,6 +686,83 @@ def test_schedules_survive_refused_exports(fails):
             os.environ.pop("ESGD_FAIL_EXPORTS", None)
         else:
             os.environ["ESGD_FAIL_EXPORTS"] = old
+
+
+POST_IO_CASES = {
+    "batched": dict(count=4099),
+    "batched_tiny": dict(count=17),
+    "one_launch_per_round": dict(count=4099, batch=0),
+    "five_launch": dict(count=300007, small_bytes=0),
+    "dst_is_src": dict(count=100003, separate_dst=False),
+    "mixed_with_plain_posts": dict(count=4099, plain_ranks=(1,)),
+    "shadowed_rank": dict(count=4099, shadow_ranks=(1,)),
+    "int32_no_divisor": dict(count=4099, dtype_name="int32"),
+}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("case", list(POST_IO_CASES))
+def test_post_io_rounds_read_src_and_write_dst(case, world):
+    # esgd_schedule_post_io: the round's snapshot reads src / divisor (the deep500 op's
+    # copy-in fused) and its phases write dst (the copy-out fused) -- in shared launches,
+    # one launch per round, five-launch rounds, beside a shadowed rank or a rank posting
+    # through its send bucket; the oracle's bits every round
+    outs = run("gpu_post_io", world, **POST_IO_CASES[case])
+    for o in outs:
+        assert all(o["verdicts"]), o["verdicts"]
+        assert all(o["fresh"]), o["fresh"]
+
+
+def test_post_io_round_carried_through_before_the_post():
+    # solo, rank 1 posts late: rounds rank 0's activation carries it through do not take
+    # rank 1's data (fresh 0, dst untouched, result in rb, its share zero); synchronous
+    # rounds do; every rank the oracle's bits of that contributor set
+    outs = run("gpu_post_io_late", 2, steps=9)
+    for o in outs:
+        for step in o:
+            assert step["ok"] and step["untouched"], step
+    for a, b in zip(outs[0], outs[1]):
+        assert a["digest"] == b["digest"], (a, b)
+    assert any(not st["fresh"][1] for st in outs[0][1:]), outs[0]   # the late path was taken
+
+
+SWEEPS_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "bin",
+                          "libesgd_sweeps.so")
+
+
+@pytest.mark.skipif(not os.path.exists(SWEEPS_LIB), reason="tools/bin/libesgd_sweeps.so not built (make sweeps)")
+def test_batched_rounds_progress_beside_a_kernel_holding_the_gpu():
+    # the residency contract of k_round_batch: a kernel on another stream
+    # holds all but two CUs' wave slots for 6 s; the shared launch of each rank must finish
+    # its 5 rounds on the workgroups that fit, bit for bit, well before the hog leaves
+    # (static tile assignment waited for it: test below); the later rounds, bit for bit
+    # too, start once the launch's last workgroups could be dispatched
+    outs = run("gpu_residency", 2, timeout=180)
+    for o in outs:
+        assert all(o["ok"]) and len(o["ok"]) == 30, o
+        assert o["first_round_s"] < 0.25 * o["hog_s"], o
+
+
+@pytest.mark.diagnostic
+@pytest.mark.skipif(not os.path.exists(SWEEPS_LIB), reason="tools/bin/libesgd_sweeps.so not built (make sweeps)")
+def test_static_tile_assignment_waits_for_the_kernel_holding_the_gpu():
+    # the contrast (ESGD_BATCH_STATIC=1): a tile owned by a worker that is not resident
+    # waits until the hog leaves -- the rounds take about as long as the hog (still
+    # bit-exact: nothing deadlocks here because the hog ends)
+    outs = run("gpu_residency", 2, static=True, timeout=180)
+    for o in outs:
+        assert all(o["ok"]), o
+        assert o["first_round_s"] > 0.5 * o["hog_s"], o
+
+
+@pytest.mark.parametrize("delete_first", [False, True])
+def test_finalize_with_rounds_held_in_the_shared_launch(delete_first):
+    # rounds every rank launched into a held shared launch (batch_hold) are sent by the
+    # schedule deletion / finalize while the schedules are alive, pair up and land
+    outs = run("gpu_finalize_held", 2, delete_first=delete_first, timeout=120)
+    for o in outs:
+        assert o["launched_before_finalize"] == 0, o   # they really were held
+        assert all(o["ok"]), o
 
 
 def test_second_job_after_ipc_mappings_closed_is_refused():

@@ -402,11 +402,36 @@ static int launch_windows_streams(const InputSet &in, void *out, uint64_t count,
     return ESGD_SUCCESS;
 }
 
+// A stand-in for a concurrent persistent kernel (an RCCL kernel, a long kernel on another
+// stream of the training loop): workgroups of 1024 threads (16 waves: two fill a CU's 32
+// wave slots) that stay resident for `ticks` of the constant wall clock, then leave.
+__global__ __launch_bounds__(1024) void k_occupy(long long ticks) {
+    const long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 }  // namespace esgd
 
 using namespace esgd;
 
 extern "C" {
+
+// `blocks` k_occupy workgroups on `stream` for `usec` microseconds each (the residency test
+// of batched rounds, tests/test_dataplane_gpu.py: 2 x CUs - 2k blocks leave k CUs' worth of
+// wave slots free); returns at once
+int esgd_sweep_occupy(int blocks, uint64_t usec, void *stream) {
+    if (blocks <= 0) { set_error("occupy: %d blocks", blocks); return ESGD_INVALID_ARG; }
+    int dev = 0, khz = 0;
+    ESGD_HIP(hipGetDevice(&dev));
+    ESGD_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+    const long long ticks = (long long)usec * khz / 1000;
+    hipLaunchKernelGGL(k_occupy, dim3(unsigned(blocks)), dim3(1024), 0, static_cast<hipStream_t>(stream), ticks);
+    ESGD_HIP(hipGetLastError());
+    return ESGD_SUCCESS;
+}
+
+// the device's compute units (sizing the occupying grid)
+int esgd_sweep_cu_count(void) { return cu_count(); }
 
 const char *esgd_sweep_last_error(void) { return g_err; }
 
