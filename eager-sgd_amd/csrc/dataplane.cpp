@@ -1293,11 +1293,16 @@ static int batch_flush_locked() {
     a.tile1[n] = t1;
     a.tile2[n] = t2;
     unsigned workers = std::min<unsigned>(kBatchWorkers, std::max<unsigned>(1, std::max(t0, std::max(t1, t2))));
-    // every workgroup of every rank sharing this GPU must be resident at once (the
-    // workers of one launch wait on each other through the peers): with 8 ranks on one
-    // GPU, 8 x 65 workgroups of the fan-in-8 kernel (2 per CU) did not fit and hung
+    // The launch's rounds complete with the agent and one worker resident (the tile
+    // counter), but the stream's next launch starts only once every workgroup of this one
+    // was dispatched and left -- so the grid is kept to what the GPU can hold beside the
+    // other ranks' launches: with 8 ranks on one GPU, 8 x 65 workgroups of the fan-in-8
+    // kernel (2 per CU) were all of it, and the five-launch rounds' spinning pairing
+    // kernels left some launch short (r04zp).  Ranks sharing a GPU get half
+    // their share; one rank per GPU keeps kBatchWorkers (far below the chip's capacity).
     const int capacity = round_batch_capacity(g_pend[0].s->dtype, g_pend[0].s->world);
-    const int cap = capacity / ranks_on_my_device() - 1;
+    const int sharing = ranks_on_my_device();
+    const int cap = capacity / (sharing > 1 ? 2 * sharing : 1) - 1;
     workers = std::max(1u, std::min<unsigned>(workers, unsigned(std::max(1, cap))));
     hipStream_t cs = g_pend[0].st->stream;
     int rc = ESGD_SUCCESS;
