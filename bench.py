@@ -770,6 +770,14 @@ def _op_like_variants(comm, dev, lengths, steps):
         t = _timed_steps(comm, step, steps)
         out[name] = {"step_ms": round(t * 1e3, 3), "rank0_step_us": _step_breakdown_us(scheds),
                      "rank0_progress_thread_per_step": _profile_per_step(p0, comm.profile(), steps)}
+        if stream is not None:   # the cross-stream waits on the legacy NULL stream, A/B'd
+            for key in ("event_device_scope", "producer_host_sync"):
+                comm.set_config(key, 1)
+                try:
+                    step()
+                    out[name][key + "_step_ms"] = round(_timed_steps(comm, step, steps) * 1e3, 3)
+                finally:
+                    comm.set_config(key, -1)
         for sc, rb, sb in zip(scheds, rbs, sbs):
             _defer(sc, *([rb] if sb is None else [rb, sb]))
     return out
@@ -882,12 +890,22 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
         else:
             out["fused_breakdown_us"] = _fused_breakdown(comm, opt, params, steps)
         if name == "per_tensor_pipelined":
-            comm.set_config("batch_rounds", 0)
-            try:
-                step()
-                out[name + "_one_launch_per_round_ms"] = round(_timed_steps(comm, step, steps) * 1e3, 3)
-            finally:
-                comm.set_config("batch_rounds", -1)
+            # A/B of the host path around the same step (esgd_set_config, process-local):
+            # one launch per round; the post / release events with a device-scope release;
+            # the producer (torch's stream) waited for on the host, no cross-stream wait
+            for key, vals, what in (("batch_rounds", {"batch_rounds": 0}, "_one_launch_per_round_ms"),
+                                    ("event_device_scope", {"event_device_scope": 1}, "_event_device_scope_ms"),
+                                    ("producer_host_sync", {"producer_host_sync": 1}, "_producer_host_sync_ms"),
+                                    ("both", {"event_device_scope": 1, "producer_host_sync": 1},
+                                     "_event_device_scope_and_producer_host_sync_ms")):
+                for k, v in vals.items():
+                    comm.set_config(k, v)
+                try:
+                    step()
+                    out[name + what] = round(_timed_steps(comm, step, steps) * 1e3, 3)
+                finally:
+                    for k in vals:
+                        comm.set_config(k, -1)
     _OPTS.extend(opts)   # their schedules stay alive until the end, like every leg's
     out["tensors"] = len(lengths)
     out["steps"] = steps
@@ -976,11 +994,12 @@ def _optimizer_breakdown(opt, steps, stream=None):
                 acc[key] = acc.get(key, 0.0) + time.perf_counter() - t0
         return g
 
-    saved = (Op.post_many, Op.wait_many, Op.forward_cuda_div, opt.optimizer.step)
+    saved = (Op.post_many, Op.wait_many, Op.forward_cuda_div, opt.optimizer.step, Op.post_many_io)
     Op.post_many = staticmethod(timed("post_many", saved[0]))
     Op.wait_many = staticmethod(timed("wait_many", saved[1]))
     Op.forward_cuda_div = timed("forward_cuda_div", saved[2])
     opt.optimizer.step = timed("sgd_step", saved[3])
+    Op.post_many_io = staticmethod(timed("post_many_io", saved[4]))
     rows = []
     try:
         for _ in range(steps):
@@ -999,6 +1018,7 @@ def _optimizer_breakdown(opt, steps, stream=None):
     finally:
         Op.post_many, Op.wait_many = staticmethod(saved[0]), staticmethod(saved[1])
         Op.forward_cuda_div = saved[2]
+        Op.post_many_io = staticmethod(saved[4])
         del opt.optimizer.step   # the instance attribute; the class method shows again
     return {k: round(statistics.median(r[k] for r in rows) * 1e6, 1) for k in rows[0]}
 

@@ -194,7 +194,7 @@ bool bypass() {   // 1: bypass; 2: also close peer mappings at schedule deletion
 
 }  // namespace
 
-int arena_alloc(size_t bytes, void **out, bool release_idle_chunks) {
+int arena_alloc(size_t bytes, void **out, bool release_idle_chunks, bool fresh_chunk) {
     ESGD_ARG(out, "arena: null output");
     if (int rc = require_device()) return rc;
     int dev = 0;
@@ -213,7 +213,7 @@ int arena_alloc(size_t bytes, void **out, bool release_idle_chunks) {
     if (bytes <= kGranule / 2) {
         const size_t cls = small_class(bytes);
         auto &fl = g_small[{dev, cls}];
-        if (fl.empty()) {
+        if (fl.empty() || fresh_chunk) {   // a new slab; its blocks join the free list
             Chunk *c = nullptr;
             const size_t usable = slab_usable();
             if (int rc = new_chunk(usable, dev, release_idle_chunks, &c)) return rc;
@@ -233,7 +233,7 @@ int arena_alloc(size_t bytes, void **out, bool release_idle_chunks) {
     const size_t need = (bytes + kGranule - 1) / kGranule * kGranule;
     char *p = nullptr;
     Chunk *c = nullptr;
-    auto it = g_large.lower_bound({dev, need});
+    auto it = fresh_chunk ? g_large.end() : g_large.lower_bound({dev, need});
     if (it != g_large.end() && it->first.first == dev) {   // best fit: the smallest run that holds it
         p = it->second;
         const size_t have = it->first.second;

@@ -119,6 +119,30 @@ static std::atomic<int64_t> g_cfg_depth{-1}, g_cfg_snap{-1}, g_cfg_inline{-1};
 // launch; only an explicit flush (another launch on the round stream, schedule deletion,
 // finalize) does -- so a test can finalize with rounds held
 static std::atomic<int64_t> g_cfg_hold{0};
+// "event_device_scope" (ESGD_EVENT_DEVICE_SCOPE, default 0): the producer / consumer events
+// of posts and releases record with a device-scope release (hipEventReleaseToDevice) instead
+// of HIP's system-scope fence -- they only order the caller's stream before the round stream
+// of the same GPU.  "producer_host_sync" (ESGD_PRODUCER_HOST_SYNC, default 0): a post waits on
+// the host for its producer stream's work instead of the round stream waiting on the GPU (no
+// cross-stream dependency; the posting thread blocks until the gradient is written).
+static std::atomic<int64_t> g_cfg_evscope{-1}, g_cfg_psync{-1};
+
+static bool env_flag(const char *name) {
+    const char *e = getenv(name);
+    return e && *e == '1';
+}
+
+static bool event_device_scope() {
+    static const bool env = env_flag("ESGD_EVENT_DEVICE_SCOPE");
+    const int64_t v = g_cfg_evscope.load(std::memory_order_relaxed);
+    return v >= 0 ? v != 0 : env;
+}
+
+static bool producer_host_sync() {
+    static const bool env = env_flag("ESGD_PRODUCER_HOST_SYNC");
+    const int64_t v = g_cfg_psync.load(std::memory_order_relaxed);
+    return v >= 0 ? v != 0 : env;
+}
 
 bool config_inline_join() {
     static const bool env = !(getenv("ESGD_INLINE_JOIN") && *getenv("ESGD_INLINE_JOIN") == '0');
@@ -190,9 +214,16 @@ int config_set(const char *key, int64_t value) {
     } else if (!std::strcmp(key, "batch_hold")) {
         ESGD_ARG(value >= -1 && value <= 1, "batch_hold: 0 or 1 (-1: the default, 0)");
         g_cfg_hold.store(value < 0 ? 0 : value);
+    } else if (!std::strcmp(key, "event_device_scope")) {
+        ESGD_ARG(value >= -1 && value <= 1, "event_device_scope: 0 or 1 (-1: the default)");
+        g_cfg_evscope.store(value);
+    } else if (!std::strcmp(key, "producer_host_sync")) {
+        ESGD_ARG(value >= -1 && value <= 1, "producer_host_sync: 0 or 1 (-1: the default)");
+        g_cfg_psync.store(value);
     } else {
         set_error("esgd_set_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
-                  "batch_rounds, batch_depth, snapshot_in_batch, inline_join, batch_hold)", key);
+                  "batch_rounds, batch_depth, snapshot_in_batch, inline_join, batch_hold, event_device_scope, "
+                  "producer_host_sync)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -213,9 +244,12 @@ int config_get(const char *key, int64_t *value) {
     else if (!std::strcmp(key, "snapshot_in_batch")) *value = snapshot_in_batch() ? 1 : 0;
     else if (!std::strcmp(key, "inline_join")) *value = config_inline_join() ? 1 : 0;
     else if (!std::strcmp(key, "batch_hold")) *value = g_cfg_hold.load();
+    else if (!std::strcmp(key, "event_device_scope")) *value = event_device_scope() ? 1 : 0;
+    else if (!std::strcmp(key, "producer_host_sync")) *value = producer_host_sync() ? 1 : 0;
     else {
         set_error("esgd_get_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
-                  "batch_rounds, launches, batch_workers, batch_depth, snapshot_in_batch, inline_join, batch_hold)", key);
+                  "batch_rounds, launches, batch_workers, batch_depth, snapshot_in_batch, inline_join, batch_hold, "
+                  "event_device_scope, producer_host_sync)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -237,6 +271,22 @@ struct IpcKey {
 };
 static std::mutex g_ipc_mu;
 static std::map<IpcKey, void *> g_ipc;
+// set by ipc_open when a fresh mapping's seal did not match (the caller asks the exporter to
+// move: SchedShm::remap); per thread, read right after the call
+static thread_local bool t_seal_mismatch = false;
+
+// ESGD_FAIL_MAPS=N (tests): this process's first N sealed mappings are treated as showing
+// other memory, so the re-publish-and-remap retry of schedule creation runs anywhere
+static bool simulated_map_failure() {
+    static std::atomic<int> left{[] {
+        const char *v = getenv("ESGD_FAIL_MAPS");
+        return (v && *v) ? std::max(0, atoi(v)) : 0;
+    }()};
+    int n = left.load();
+    while (n > 0 && !left.compare_exchange_weak(n, n - 1)) {
+    }
+    return n > 0;
+}
 
 // Map a peer's exported chunk (once per (peer, chunk)).  `slot` (may be null: flag pages)
 // carries the chunk's seal: a fresh mapping is only kept if the seal read through it is
@@ -244,6 +294,7 @@ static std::map<IpcKey, void *> g_ipc;
 // of feeding another process's bytes into the sums.
 static int ipc_open(int peer, const uint8_t *h, void **base, const IpcSlot *slot = nullptr) {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
+    t_seal_mismatch = false;
     IpcKey k;
     k.peer = peer;
     std::memcpy(k.h, h, 64);
@@ -262,9 +313,16 @@ static int ipc_open(int peer, const uint8_t *h, void **base, const IpcSlot *slot
         uint64_t w[4];
         if (int rc = seal_read(static_cast<char *>(p) + slot->chunk_bytes, w)) return rc;
         std::memcpy(&got, w, sizeof(got));
-        if (got.magic != kSealMagic || got.nonce != slot->seal_nonce || got.base != slot->chunk_base) {
-            ipc_trace("import-seal-mismatch", peer, p, slot->chunk_bytes, h);
-            std::fprintf(stderr, "esgd: pid %d: rank %d's chunk %#llx (%llu B) mapped at %p shows other memory: seal "
+        const bool simulated = simulated_map_failure();
+        if (simulated)
+            std::fprintf(stderr, "esgd: pid %d: mapping of rank %d's chunk %#llx treated as showing other memory "
+                         "(ESGD_FAIL_MAPS)\n", int(getpid()), peer, (unsigned long long)slot->chunk_base);
+        if (simulated || got.magic != kSealMagic || got.nonce != slot->seal_nonce || got.base != slot->chunk_base) {
+            t_seal_mismatch = true;
+            ipc_trace(simulated ? "import-seal-mismatch-simulated" : "import-seal-mismatch", peer, p,
+                      slot->chunk_bytes, h);
+            if (!simulated)
+                std::fprintf(stderr, "esgd: pid %d: rank %d's chunk %#llx (%llu B) mapped at %p shows other memory: seal "
                          "magic %#llx base %#llx nonce %#llx pid %u, expected base %#llx nonce %#llx\n", int(getpid()),
                          peer, (unsigned long long)slot->chunk_base, (unsigned long long)slot->chunk_bytes, p,
                          (unsigned long long)got.magic, (unsigned long long)got.base, (unsigned long long)got.nonce,
@@ -714,26 +772,28 @@ static int base_setup(Sched &s, BaseState &st) {
 }
 
 static std::mutex g_evfree_mu;
-static std::vector<hipEvent_t> g_evfree;   // pooled events no round refers to any more
+static std::vector<hipEvent_t> g_evfree[2];   // pooled events no round refers to any more [device scope]
 
 // ---- events: a process-wide pool, and recordings shared by a group of schedules ----
 // A producer (consumer) event marks where the caller's stream stands at a post (release).
 // esgd_schedule_post_group / _release_group record ONE event for all the schedules they
 // name (dataplane_group_begin/end: this thread's posts / releases on that stream use it),
 // and the round stream waits for a recording once however many rounds refer to it.
-static std::shared_ptr<hipEvent_t> pooled_event() {
+static std::shared_ptr<hipEvent_t> pooled_event(bool device_scope = false) {
     hipEvent_t e = nullptr;
+    const int k = device_scope ? 1 : 0;
     {
         std::lock_guard<std::mutex> lk(g_evfree_mu);
-        if (!g_evfree.empty()) { e = g_evfree.back(); g_evfree.pop_back(); }
+        if (!g_evfree[k].empty()) { e = g_evfree[k].back(); g_evfree[k].pop_back(); }
     }
-    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming | (device_scope ? hipEventReleaseToDevice : 0u)) !=
+                  hipSuccess) {
         (void)hip_fail(hipGetLastError(), "hipEventCreateWithFlags", __FILE__, __LINE__);
         return nullptr;
     }
-    return std::shared_ptr<hipEvent_t>(new hipEvent_t(e), [](hipEvent_t *p) {
+    return std::shared_ptr<hipEvent_t>(new hipEvent_t(e), [k](hipEvent_t *p) {
         std::lock_guard<std::mutex> lk(g_evfree_mu);
-        g_evfree.push_back(*p);
+        g_evfree[k].push_back(*p);
         delete p;
     });
 }
@@ -746,6 +806,7 @@ struct GroupEvent {   // this thread's open group: [0] posts, [1] releases
     bool open = false;
     void *stream = nullptr;
     std::shared_ptr<hipEvent_t> ev;
+    bool synced = false;   // producer_host_sync: the group's producer work was waited for
 };
 static thread_local GroupEvent g_group[2];
 
@@ -754,6 +815,7 @@ int dataplane_group_begin(int which, void *stream) {
     g.open = true;
     g.stream = stream;
     g.ev.reset();   // recorded by the group's first schedule that needs it
+    g.synced = false;
     return ESGD_SUCCESS;
 }
 
@@ -766,11 +828,22 @@ void dataplane_group_end(int which) {
 // or a new one
 static int note_event(int which, void *stream, std::shared_ptr<hipEvent_t> *out) {
     GroupEvent &g = g_group[which];
-    if (g.open && g.stream == stream && g.ev) {
+    const bool same = g.open && g.stream == stream;
+    if (which == 0 && producer_host_sync()) {   // wait here; nothing for the GPU to wait on
+        out->reset();
+        if (same && g.synced) return ESGD_SUCCESS;
+        std::shared_ptr<hipEvent_t> ev = pooled_event(event_device_scope());
+        if (!ev) return ESGD_ERROR;
+        ESGD_HIP(hipEventRecord(*ev, user_stream(stream)));
+        ESGD_HIP(hipEventSynchronize(*ev));
+        if (same) g.synced = true;
+        return ESGD_SUCCESS;
+    }
+    if (same && g.ev) {
         *out = g.ev;
         return ESGD_SUCCESS;
     }
-    std::shared_ptr<hipEvent_t> ev = pooled_event();
+    std::shared_ptr<hipEvent_t> ev = pooled_event(event_device_scope());
     if (!ev) return ESGD_ERROR;
     ESGD_HIP(hipEventRecord(*ev, user_stream(stream)));
     if (g.open && g.stream == stream) g.ev = ev;
@@ -806,7 +879,7 @@ static int stream_wait(hipStream_t cs, const std::shared_ptr<hipEvent_t> &ev) {
 static int base_note_producer(BaseState &st, uint32_t round, void *stream) {
     std::shared_ptr<hipEvent_t> ev;
     if (int rc = note_event(0, stream, &ev)) return rc;
-    st.producer[round] = std::move(ev);
+    if (ev) st.producer[round] = std::move(ev);   // none: waited for on the host already
     return ESGD_SUCCESS;
 }
 
@@ -1499,8 +1572,10 @@ static void batch_shutdown() {
     if (g_desc_dev) { hip_ignore(hipFree(g_desc_dev)); g_desc_dev = nullptr; g_queue = nullptr; }
     if (g_desc_host) { hip_ignore(hipHostFree(g_desc_host)); g_desc_host = nullptr; }
     std::lock_guard<std::mutex> ek(g_evfree_mu);
-    for (hipEvent_t e : g_evfree) hip_ignore(hipEventDestroy(e));
-    g_evfree.clear();
+    for (auto &pool : g_evfree) {
+        for (hipEvent_t e : pool) hip_ignore(hipEventDestroy(e));
+        pool.clear();
+    }
 }
 
 struct IpcTransport final : Transport {
@@ -1594,8 +1669,10 @@ struct IpcTransport final : Transport {
         return publish_owned(s, s.sh->pub[s.rank], &st.pub, &st.pub_cap, st.pub_cap, "pub");
     }
 
-    // (re)map one peer publication if it changed since we last mapped it
-    static int map_slot(Sched &s, int q, IpcSlot &ps, PeerMap &m, const char *what) {
+    // (re)map one peer publication if it changed since we last mapped it; a fresh mapping
+    // whose seal shows other memory asks peer q to move that publication (`bit` in
+    // SchedShm::remap of this connect attempt; schedule creation retries)
+    static int map_slot(Sched &s, int q, IpcSlot &ps, PeerMap &m, const char *what, uint32_t bit) {
         if (ps.gen.load(std::memory_order_acquire) != s.gen) {
             set_error("schedule %d: rank %d did not publish its %s", s.id, q, what);
             return ESGD_ERROR;
@@ -1606,7 +1683,11 @@ struct IpcTransport final : Transport {
         // mappings are cached per (peer, chunk) and never closed before shutdown
         if (!(m.base && std::memcmp(m.handle, ps.handle, 64) == 0)) {
             void *pb = nullptr;
-            if (int rc = ipc_open(q, ps.handle, &pb, &ps)) return rc;
+            if (int rc = ipc_open(q, ps.handle, &pb, &ps)) {
+                if (t_seal_mismatch && s.connect_attempt <= kRemapTries)
+                    s.sh->remap[s.connect_attempt][q].fetch_or(bit, std::memory_order_acq_rel);
+                return rc;
+            }
             m.base = pb;
             std::memcpy(m.handle, ps.handle, 64);
         }
@@ -1621,7 +1702,7 @@ struct IpcTransport final : Transport {
         for (int q = 0; q < s.world; ++q) {
             if (q == s.rank) continue;
             IpcSlot &ps = s.sh->slot[q];
-            if (int rc = map_slot(s, q, ps, st.rbmap[q], "bucket")) return rc;
+            if (int rc = map_slot(s, q, ps, st.rbmap[q], "bucket", 1)) return rc;
             if (ps.bytes != bytes) {
                 set_error("schedule %d: rank %d has %llu bytes, this rank %zu", s.id, q,
                           (unsigned long long)ps.bytes, bytes);
@@ -1629,7 +1710,7 @@ struct IpcTransport final : Transport {
             }
             st.peer[q] = st.rbmap[q].ptr;
             if (!one_launch(s)) continue;   // every rank has this size (checked above)
-            if (int rc = map_slot(s, q, s.sh->pub[q], st.pubmap[q], "published shard")) return rc;
+            if (int rc = map_slot(s, q, s.sh->pub[q], st.pubmap[q], "published shard", 2)) return rc;
             if (s.sh->pub[q].bytes < st.len[q] * s.esize) {
                 set_error("schedule %d: rank %d's published shard is too small", s.id, q);
                 return ESGD_ERROR;
@@ -1676,6 +1757,48 @@ struct IpcTransport final : Transport {
         if (s.flag_mode > 0)
             if (int rc = flags_connect(s.rank, s.world, s.flag_mode)) return rc;
         return map_peers(s, S(s));
+    }
+
+    // A peer's fresh mapping of this rank's publication showed other memory: whatever was
+    // published from that chunk moves to a chunk allocated now (a new handle), contents
+    // need not move (creation: no round has run).  The caller's own bucket cannot move --
+    // it is shadowed instead, as a bucket in a refused chunk is.  The old chunk stays
+    // exported (never freed), its blocks back on the free lists.
+    int remap(Sched &s, uint32_t which) override {
+        IpcState &st = S(s);
+        auto move = [&](IpcSlot &slot, char **buf, size_t *cap, size_t bytes, const char *what) -> int {
+            char *old = *buf;
+            if (int rc = arena_alloc(std::max<size_t>(*cap, 1), reinterpret_cast<void **>(buf), false, true)) return rc;
+            std::fprintf(stderr, "esgd: rank %d schedule %d: %s %p re-published from a new chunk at %p\n", s.rank, s.id,
+                         what, static_cast<void *>(old), static_cast<void *>(*buf));
+            free_bucket(old);
+            return publish_owned(s, slot, buf, cap, bytes, what);
+        };
+        // the published shard moves whichever was asked: it may share the suspect chunk
+        if (st.pub && which)
+            if (int rc = move(s.sh->pub[s.rank], &st.pub, &st.pub_cap, st.pub_cap, "pub")) return rc;
+        if (which & 1) {
+            IpcSlot &mine = s.sh->slot[s.rank];
+            if (s.wire_bf16) {
+                if (int rc = move(mine, &st.wire, &st.wire_cap, s.count * 2, "wire")) return rc;
+                st.peer[s.rank] = st.wire;
+            } else if (st.owns_rb) {
+                if (int rc = move(mine, &st.rb_dev, &st.cap, s.count * s.esize, "rb")) return rc;
+                st.peer[s.rank] = st.rb_dev;
+            } else {   // the caller's bucket: reduce through a shadow in a new chunk
+                if (int rc = arena_alloc(std::max<size_t>(s.count * s.esize, 1), reinterpret_cast<void **>(&st.rb_dev),
+                                         false, true))
+                    return rc;
+                st.cap = std::max<size_t>(s.count * s.esize, 1);
+                st.owns_rb = st.shadow = true;
+                st.peer[s.rank] = st.rb_dev;
+                std::fprintf(stderr, "esgd: rank %d schedule %d: bucket %p shadowed by %p in a new chunk\n", s.rank,
+                             s.id, s.rb, static_cast<void *>(st.rb_dev));
+                if (int rc = publish(s, st)) return rc;
+            }
+            st.desc_built = false;
+        }
+        return ESGD_SUCCESS;
     }
 
     int note_producer(Sched &s, uint32_t round, void *stream) override {

@@ -323,6 +323,31 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
         rc = tp->connect(*s);   // needs every peer's publication
         rc = vote(rc, s->sh->connect_err);
     }
+    // A fresh mapping of a peer's chunk that showed other memory (its seal: round 5 caught
+    // the runtime handing an importer its OWN exported chunk for a peer's handle, DESIGN.md
+    // §5) asked that peer to move the publication (SchedShm::remap): every rank sees the same
+    // requests after the vote, the asked ranks re-publish from chunks allocated anew, a vote,
+    // and every rank maps again -- up to kRemapTries times before the creation fails.
+    for (int a = 0; rc && a < kRemapTries; ++a) {
+        uint32_t any = 0;
+        for (int q = 0; q < g_world; ++q) any |= s->sh->remap[a][q].load(std::memory_order_acquire);
+        if (!any) break;
+        const uint32_t mine = s->sh->remap[a][g_rank].load(std::memory_order_acquire);
+        if (mine)
+            fprintf(stderr, "esgd: rank %d schedule %d: a peer's mapping of this rank's %s showed other memory; "
+                    "re-publishing from a new chunk (attempt %d)\n", g_rank, s->id,
+                    mine == 3 ? "bucket and shard" : mine == 1 ? "bucket" : "shard", a + 1);
+        clear_error();
+        int r2 = mine ? tp->remap(*s, mine) : ESGD_SUCCESS;
+        r2 = vote(r2, s->sh->retry_err[2 * a]);
+        if (!r2) {
+            s->connect_attempt = a + 1;
+            r2 = tp->connect(*s);
+            r2 = vote(r2, s->sh->retry_err[2 * a + 1]);
+        }
+        ++s->remaps;
+        rc = r2;
+    }
     if (dbg)
         fprintf(stderr, "[esgd] r%d create sched %d (%llu x %d B): setup %.1f ms, vote %.1f ms, connect %.1f ms\n",
                 g_rank, s->id, (unsigned long long)count, int(s->esize), (c1 - c0) * 1e3, (c2 - c1) * 1e3,

@@ -71,6 +71,9 @@ struct Transport {
     // peers, communicator bring-up).  A failure in either fails the creation on all ranks.
     virtual int setup(Sched &s) = 0;
     virtual int connect(Sched &) { return ESGD_SUCCESS; }
+    // a peer could not map this rank's publication (`which`: SchedShm::remap bits): move
+    // it to a chunk allocated anew and publish again (creation only, before any round)
+    virtual int remap(Sched &, uint32_t) { return ESGD_SUCCESS; }
     virtual int note_producer(Sched &s, uint32_t round, void *stream) = 0;
     // the post of `round` carries its own data (RoundIO); checked here, used at launch
     virtual int note_io(Sched &s, uint32_t round, const RoundIO &io);   // default: refused
@@ -102,6 +105,8 @@ struct Sched {
     int rank = 0, world = 1;
     SchedShm *sh = nullptr;
     uint32_t gen = 0;
+    int connect_attempt = 0;   // creation: which connect attempt maps peers now (SchedShm::remap)
+    int remaps = 0;            // creation retries this schedule needed (diagnostics)
     Transport *tp = nullptr;
     void *tstate = nullptr;
 

@@ -60,8 +60,9 @@ struct PairFlags {
 void ipc_trace(const char *what, int peer, const void *ptr, size_t bytes, const uint8_t handle[64]);
 
 // release_idle_chunks: a new chunk may first give idle never-exported chunks back to the
-// driver (hipFree synchronises the device: callers' threads only, never the progress thread)
-int arena_alloc(size_t bytes, void **out, bool release_idle_chunks = false);
+// driver (hipFree synchronises the device: callers' threads only, never the progress thread);
+// fresh_chunk: the block comes from a chunk allocated now (never one a peer has opened)
+int arena_alloc(size_t bytes, void **out, bool release_idle_chunks = false, bool fresh_chunk = false);
 bool arena_free(void *p);
 int arena_device(const void *p);   // device of an arena block, -1 if p is not one
 bool arena_unexportable(const void *p);   // p's chunk: the runtime refused its IPC export

@@ -16,6 +16,7 @@
 namespace esgd {
 
 constexpr int kMaxRanks = 16;     // ranks per node
+constexpr int kRemapTries = 3;    // creation retries after a peer's mapping showed other memory
 constexpr int kMaxSched = 2048;   // persistent schedules per job (the ResNet-50 wrapper uses 161)
 constexpr uint64_t kShmMagic = 0x314d4853444753ull;  // "ESGDSHM1"
 
@@ -58,6 +59,12 @@ struct alignas(64) SchedShm {
     std::atomic<uint64_t> sig[kMaxRanks];   // creation signature of rank r: kind, dtype, tag
     IpcSlot slot[kMaxRanks];   // rank r's receive bucket (peers read shard q of it in phase 1)
     IpcSlot pub[kMaxRanks];    // rank r's reduced shard, published for the all-gather
+    // A peer's fresh mapping of rank r's publication showed other memory (the chunk seal,
+    // dataplane.cpp ipc_open) at connect attempt a: remap[a][r] (bit 1 the bucket, bit 2
+    // the published shard) asks rank r to move it to a chunk allocated anew; every rank
+    // then re-maps (sched_create_with's retry votes, retry_err)
+    std::atomic<uint32_t> remap[kRemapTries + 1][kMaxRanks];
+    std::atomic<uint32_t> retry_err[2 * kRemapTries];
 };
 
 // Global issue order for transports whose collectives must be issued in the same

@@ -210,7 +210,7 @@ def mismatch(t, got, want, xs, sched=None):
 def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0, buf="device",
                   in_place=False, transport="ipc", shadow_ranks=(), small_bytes=None,
                   piece_bytes=None, host_chunk=None, device_flags=None, wire=False, chunk_kernel=None,
-                  fail_exports=None, batch=None):
+                  fail_exports=None, batch=None, fail_maps=None):
     """Data plane on the GPU: every rank reduces its splitmix bucket; returns the
     result bytes' digest per round plus a bit-exactness verdict against the oracle.
     shadow_ranks: ranks whose device buckets go through the owned shadow bucket.
@@ -224,6 +224,8 @@ def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0
         os.environ["ESGD_SHADOW"] = "1"
     if fail_exports is not None and fail_exports[rank]:   # this rank's first N chunk exports fail
         os.environ["ESGD_FAIL_EXPORTS"] = str(fail_exports[rank])
+    if fail_maps is not None and fail_maps[rank]:   # this rank's first N mappings "show other memory"
+        os.environ["ESGD_FAIL_MAPS"] = str(fail_maps[rank])
     if batch is not None:
         os.environ["ESGD_BATCH_ROUNDS"] = str(batch)
     if small_bytes is not None:

@@ -251,6 +251,24 @@ def test_refused_export_on_one_rank(count, batch):
         assert all(all(v) for v in verdicts), (fails, verdicts)
 
 
+@pytest.mark.parametrize("count,small", [(17, None), (4099, None), (300007, 0)])
+@pytest.mark.parametrize("fails", [(1, 0), (0, 2), (3, 0)])
+def test_wrong_mapping_is_remapped(fails, count, small):
+    # round 5 (r05b): a fresh mapping of a peer's chunk showed the importer's OWN exported
+    # chunk (the seal caught it).  ESGD_FAIL_MAPS makes a rank's first N sealed mappings
+    # count as such: the exporter moves the publication to a new chunk (its own bucket is
+    # shadowed), every rank maps again, up to kRemapTries (3) times -- then bit-exact rounds
+    verdicts = run("gpu_allreduce", 2, count=count, rounds=2, fail_maps=fails, small_bytes=small)
+    assert all(all(v) for v in verdicts), (fails, verdicts)
+
+
+def test_wrong_mapping_retries_exhausted_fails_every_rank():
+    # four wrong mappings in a row on rank 0 (initial connect + 3 retries): the creation
+    # fails on every rank, naming the mapping, instead of hanging or summing other memory
+    with pytest.raises(AssertionError, match="other memory|another rank failed"):
+        run("gpu_allreduce", 2, count=4099, rounds=1, fail_maps=(4, 0), timeout=120)
+
+
 # ---- BASELINE.json's workloads (C1, C3, C4, C5) at their full sizes -----------------
 # Every rank writes its bucket before a barrier and posts (the pattern of
 # evaluation/{solo,rand}_allreduce_correctness.c:76-97): solo / majority rounds then
