@@ -862,7 +862,10 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
                      # the rounds' own I/O (esgd_schedule_post_io): the A/B of the fused path
                      ("per_tensor_pipelined_copy_kernels", dict(fuse=False, fused_io=False)),
                      ("per_tensor_blocking", dict(pipeline=False)),
-                     ("fused", dict(fuse=True)), ("per_tensor_blocking_side_stream", dict(pipeline=False))):
+                     ("fused", dict(fuse=True)), ("per_tensor_blocking_side_stream", dict(pipeline=False)),
+                     # the pipelined step with the caller's work on a torch side stream instead
+                     # of the legacy NULL stream (the blocking pair above differs 1.6x)
+                     ("per_tensor_pipelined_side_stream", dict(fuse=False))):
         if name.endswith("_side_stream") and side is None:
             side = torch.cuda.Stream()
         params = [torch.zeros(n, device=dev_t, requires_grad=True) for n in lengths]
