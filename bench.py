@@ -858,6 +858,8 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
     side = None   # created for its variant only: one more stream is one more hardware queue,
     #               which on a GPU shared by the ranks changes the timings
     for name, kw in (("per_tensor_pipelined", dict(fuse=False)),
+                     # the ops on torch's legacy default stream itself (no internal stream)
+                     ("per_tensor_pipelined_legacy_stream", dict(fuse=False, side_stream=False)),
                      # the same with copy-in / copy-out kernels on the caller's stream instead of
                      # the rounds' own I/O (esgd_schedule_post_io): the A/B of the fused path
                      ("per_tensor_pipelined_copy_kernels", dict(fuse=False, fused_io=False)),

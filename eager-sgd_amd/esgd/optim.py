@@ -42,10 +42,15 @@ from typing import Iterable
 from . import deep500
 
 
+def _nullcontext():
+    import contextlib
+    return contextlib.nullcontext()
+
+
 class EagerSGDOptimizer:
     def __init__(self, optimizer, comm_size: int, mode: str = "solo", async_: int = 32,
                  seed: int = 6545343, fuse: bool = False, wire: str = "fp32",
-                 pipeline: bool = True, fused_io: bool = True):
+                 pipeline: bool = True, fused_io: bool = True, side_stream: bool = True):
         if mode not in deep500.MODES:
             raise ValueError(f"mode must be one of {sorted(deep500.MODES)}")
         if wire not in deep500.WIRES:
@@ -61,6 +66,12 @@ class EagerSGDOptimizer:
         # (allreducef_forward_cuda_post_many_io); False: copy-in / copy-out kernels on the
         # caller's stream around them (an A/B)
         self.fused_io = bool(fused_io)
+        # when the caller works on the legacy default stream (torch's default), the ops'
+        # posts, waits and copies go through a stream of the optimizer's own, ordered after
+        # the caller's stream on entry and before it on exit (the ops on the legacy stream
+        # cost 1.3-1.6x per step on the 1-GPU rehearsal: profiles/r05/README.md)
+        self.side_stream = bool(side_stream)
+        self._side = None
         self.wire = wire        # "bf16": bf16 copies between ranks
         self._ops = {}          # parameter -> op instance (one bucket per tensor)
         self._fused = None      # (layout, op, packed bucket, reduced bucket)
@@ -77,10 +88,31 @@ class EagerSGDOptimizer:
         if not self._configured:
             deep500.configure(self.mode, self.async_, self.seed, self.wire)
             self._configured = True
-        stream = torch.cuda.current_stream().cuda_stream
-        gvs = list(grads_and_vars)
+        caller = torch.cuda.current_stream()
+        side = None
+        if self.side_stream and caller.cuda_stream == 0:
+            if self._side is None or self._side.device != caller.device:
+                self._side = torch.cuda.Stream(device=caller.device)
+            side = self._side
+            side.wait_stream(caller)       # the gradients were written on the caller's stream
+        with (torch.cuda.stream(side) if side is not None else _nullcontext()):
+            made = self._reduce(list(grads_and_vars), torch.cuda.current_stream().cuda_stream)
+        if side is not None:
+            caller.wait_stream(side)       # the wrapped step reads what the ops wrote there
+            for t in made:                 # gradients converted on the side stream: the
+                t.record_stream(caller)    # caller's stream uses them too
+        r = self.optimizer.step()
+        if global_step is not None and hasattr(global_step, "add_"):
+            global_step.add_(1)
+        return r
+
+    def _reduce(self, gvs, stream):
+        """The ops' rounds over every gradient, results back in p.grad; returns the
+        gradients it had to replace (converted to contiguous fp32 and back)."""
+        import torch
+        made = []
         if self.fuse:
-            self._apply_fused(gvs, stream)
+            self._apply_fused(gvs, stream, made)
         else:
             posted = []
             for grad, var in reversed(gvs):
@@ -97,6 +129,7 @@ class EagerSGDOptimizer:
                     op.forward_cuda_div(g, g, self.comm_size, stream)      # :40 fused, in place
                     if g is not grad:
                         var.grad = g.to(grad.dtype).view_as(grad)
+                        made.append(var.grad)
             if posted:
                 ops, gs = [p[0] for p in posted], [p[1] for p in posted]
                 err = None
@@ -116,12 +149,10 @@ class EagerSGDOptimizer:
                 for op, g, grad, var in posted:
                     if g is not grad:
                         var.grad = g.to(grad.dtype).view_as(grad)
-        r = self.optimizer.step()
-        if global_step is not None and hasattr(global_step, "add_"):
-            global_step.add_(1)
-        return r
+                        made.append(var.grad)
+        return made
 
-    def _apply_fused(self, gvs, stream):
+    def _apply_fused(self, gvs, stream, made):
         import torch
         live = [(g, v) for g, v in reversed(gvs) if g is not None]
         if not live:
@@ -144,6 +175,7 @@ class EagerSGDOptimizer:
         for g32, (g, v) in zip(gs, live):
             if g32 is not g:
                 v.grad = g32.to(g.dtype).view_as(g)
+                made.append(v.grad)
 
     # -- torch.optim-style convenience ---------------------------------------------
     def step(self, closure=None):
