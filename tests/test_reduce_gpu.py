@@ -393,3 +393,28 @@ def test_sweep_variants_match_oracle():
             if not np.array_equal(out.download(stream=s).view(np.uint32), want.view(np.uint32)):
                 bad.append((pol, unroll, nt, grid))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("divisor", [1.0, 3.0, 8.0])
+def test_pack_div_and_unpack_bitwise(divisor):
+    # esgd_pack_div / esgd_unpack (the fused optimizer bucket): tensors of ragged sizes packed
+    # at arbitrary element offsets (4-B accesses), at 16-B aligned ones (vector path: sizes
+    # that are multiples of 4), tiles of 16 Ki elements and their ragged ends; the division
+    # is IEEE (x / divisor, numpy float32), unpack returns every tensor's slice bit for bit
+    from esgd.device import pack_div, unpack
+    sizes = [1, 3, 17, 1000, 16384, 16385, 70001, 8, 262147, 5, 4096, 49152, 7]
+    rng = np.random.default_rng(7)
+    xs = [(rng.standard_normal(n) * 10.0 ** rng.integers(-3, 4)).astype(np.float32) for n in sizes]
+    bufs = [DeviceBuffer(n) for n in sizes]
+    for b, x in zip(bufs, xs):
+        b.upload(x)
+    bucket = DeviceBuffer(sum(sizes))
+    pack_div(bufs, sizes, bucket, divisor)
+    synchronize()
+    want = np.concatenate([x / np.float32(divisor) for x in xs]).astype(np.float32)
+    bits_equal(bucket.download(), want)
+    outs = [DeviceBuffer(n) for n in sizes]
+    unpack(outs, sizes, bucket)
+    synchronize()
+    for o, x in zip(outs, xs):
+        bits_equal(o.download(), x / np.float32(divisor))
