@@ -858,6 +858,9 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
     side = None   # created for its variant only: one more stream is one more hardware queue,
     #               which on a GPU shared by the ranks changes the timings
     for name, kw in (("per_tensor_pipelined", dict(fuse=False)),
+                     # the rounds waited for on the host (every round seen finished before the
+                     # wrapped step is queued) instead of on the GPU (stream_wait): the A/B
+                     ("per_tensor_pipelined_host_wait", dict(fuse=False, stream_wait=False)),
                      # the ops on torch's legacy default stream itself (no internal stream)
                      ("per_tensor_pipelined_legacy_stream", dict(fuse=False, side_stream=False)),
                      # the same with copy-in / copy-out kernels on the caller's stream instead of
@@ -895,14 +898,10 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
         else:
             out["fused_breakdown_us"] = _fused_breakdown(comm, opt, params, steps)
         if name == "per_tensor_pipelined":
-            # A/B of the host path around the same step (esgd_set_config, process-local):
-            # one launch per round; the post / release events with a device-scope release;
-            # the producer (torch's stream) waited for on the host, no cross-stream wait
-            for key, vals, what in (("batch_rounds", {"batch_rounds": 0}, "_one_launch_per_round_ms"),
-                                    ("event_device_scope", {"event_device_scope": 1}, "_event_device_scope_ms"),
-                                    ("producer_host_sync", {"producer_host_sync": 1}, "_producer_host_sync_ms"),
-                                    ("both", {"event_device_scope": 1, "producer_host_sync": 1},
-                                     "_event_device_scope_and_producer_host_sync_ms")):
+            # A/B of the same step with one launch per round (esgd_set_config, process-local).
+            # (r05d-r05g also A/B'd a device-scope event release and a host-side producer
+            # sync here: within noise every time, profiles/r05/README.md; dropped)
+            for key, vals, what in (("batch_rounds", {"batch_rounds": 0}, "_one_launch_per_round_ms"),):
                 for k, v in vals.items():
                     comm.set_config(k, v)
                 try:

@@ -651,6 +651,7 @@ struct BaseState {
     bool copyout_pending = false;
     bool fin_mode = false;            // the round in flight reports through SchedShm::fin
     int batch_rc = 0;                 // the shared launch of this round failed (its status)
+    bool in_batch = false;            // the round in flight went into a shared launch
     std::vector<char *> retired;      // grown-out buckets: peers may still map them
     uint64_t off[kMaxRanks] = {}, len[kMaxRanks] = {};   // elements
     // events from the process-wide pool (pooled_event); one recording may be shared by a
@@ -1555,10 +1556,32 @@ static int batch_append(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) 
     st.pub_round = round;
     st.fin_mode = true;
     st.batch_rc = 0;
+    st.in_batch = true;
     const RoundIO none{nullptr, nullptr, 1.0f};
     g_pend.push_back({&s, &st, round, st.snap_kind, st.io_on ? st.cur_io : none});
     st.snap_kind = 0;
     return ESGD_SUCCESS;
+}
+
+// sched_wait_on: `stream` waits for the event after the round's last queued work -- its
+// shared launch's (once flushed) or its own (st.ev, recorded last by every device round).
+// Host buckets finish on the host (base_complete), a failed shared launch is reported by
+// the host wait.
+static int base_order_after(Sched &s, BaseState &st, void *stream) {
+    if (s.host_mode || st.copyout_pending) return 2;
+    hipEvent_t ev;
+    {
+        std::lock_guard<std::mutex> lk(g_batch_mu);
+        if (st.batch_rc) return 2;
+        if (st.in_batch) {
+            if (!st.batch_ev) return 0;   // still in the pending launch
+            ev = *st.batch_ev;
+        } else {
+            ev = st.ev;
+        }
+    }
+    ESGD_HIP(hipStreamWaitEvent(user_stream(stream), ev, 0));
+    return 1;
 }
 
 static void batch_shutdown() {
@@ -1846,6 +1869,7 @@ struct IpcTransport final : Transport {
         st.fin_mode = false;
         st.batch_ev.reset();
         st.batch_rc = 0;
+        st.in_batch = false;
         take_io(st, round, fresh);
         const bool batch = batched(s, st);
         // anything else queued on the round stream goes behind the pending shared launch
@@ -2113,6 +2137,7 @@ struct IpcTransport final : Transport {
     }
 
     int query(Sched &s) override { return base_query(s, S(s)); }
+    int order_after(Sched &s, uint32_t, void *stream) override { return base_order_after(s, S(s), stream); }
 
     int complete(Sched &s) override { return base_complete(s, S(s)); }
 
@@ -2469,6 +2494,7 @@ struct RcclTransport final : Transport {
     }
 
     int query(Sched &s) override { return base_query(s, S(s)); }
+    int order_after(Sched &s, uint32_t, void *stream) override { return base_order_after(s, S(s), stream); }
     int complete(Sched &s) override { return base_complete(s, S(s)); }
 
     void teardown(Sched &s) override {

@@ -444,8 +444,15 @@ int allreducef_forward_cuda_post_many_io(void *const *handles, int n, const floa
     return rc;
 }
 
-int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const *outputs, void *stream) {
+}  // extern "C"
+
+namespace {
+
+// on_stream: each round is waited for on the GPU (esgd_schedule_wait_on): stream waits for
+// it, and the call returns once every round is queued instead of finished
+int wait_many_impl(void *const *handles, int n, float *const *outputs, void *stream, bool on_stream) {
     ESGD_ARG(n >= 0 && (n == 0 || (handles && outputs)), "allreducef_forward_cuda_wait_many: bad arguments");
+    void *ps = caller_stream(static_cast<hipStream_t>(stream));
     std::vector<float *> outs, rbs;
     std::vector<uint64_t> counts;
     std::vector<esgd_sched_h> hs, hs_io;   // copied out from rb / results already in place
@@ -458,7 +465,7 @@ int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const 
         const bool io = op->io_posted;
         op->io_posted = false;
         int fresh = 0;
-        if (int rc = esgd_schedule_wait_ex(op->sched, &fresh)) {
+        if (int rc = on_stream ? esgd_schedule_wait_on(op->sched, ps, &fresh) : esgd_schedule_wait_ex(op->sched, &fresh)) {
             if (!first) first = rc;
             continue;
         }
@@ -477,7 +484,6 @@ int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const 
             done.push_back(op);
         }
     }
-    void *ps = caller_stream(static_cast<hipStream_t>(stream));
     if (!done_io.empty()) {   // the caller read nothing of rb: no consumer event
         const int rc = esgd_schedule_release_group(hs_io.data(), int(hs_io.size()), nullptr);
         if (rc && !first) first = rc;
@@ -494,6 +500,18 @@ int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const 
             for (AllreduceOp *op : done) op->bytes += int64_t(op->len) * int64_t(sizeof(float));
     }
     return first;
+}
+
+}  // namespace
+
+extern "C" {
+
+int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const *outputs, void *stream) {
+    return wait_many_impl(handles, n, outputs, stream, false);
+}
+
+int allreducef_forward_cuda_wait_many_on(void *const *handles, int n, float *const *outputs, void *stream) {
+    return wait_many_impl(handles, n, outputs, stream, true);
 }
 
 bool is_cuda_supported(void *) { return true; }

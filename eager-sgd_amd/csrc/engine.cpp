@@ -495,6 +495,57 @@ int sched_wait_ex(Sched *s, int *fresh) {
     return ESGD_SUCCESS;
 }
 
+// wait(), ordered on the GPU: returns once `stream` waits (hipStreamWaitEvent) for the
+// round's last queued work -- as soon as the progress thread has queued the round, not when
+// the host sees it finish -- or once the round has finished.  The caller's work on `stream`
+// (the wrapped optimizer reading the reduced gradient) is then queued behind the round
+// while the round still runs, as torch.distributed's Work.wait() orders the caller's
+// stream behind an RCCL collective.  The round's outcome is not known yet: a failure that
+// comes later is reported by the schedule's next post / wait (the error is sticky).
+// Transports or buckets without such an event (host buckets) wait on the host.
+int sched_wait_on(Sched *s, void *stream, int *fresh) {
+    ESGD_ARG(s && stream, "schedule wait_on: null schedule or stream (ESGD_STREAM_NULL names the legacy stream)");
+    uint32_t target;
+    {
+        std::lock_guard<std::mutex> lk(s->mu);
+        ESGD_ARG(!s->held, "schedule %d: release() the round wait() returned before waiting for the next", s->id);
+        target = s->waited + 1;
+    }
+    const double t0 = now_s();
+    unsigned polls = 0;
+    if (roctx_on()) roctxRangePushA("esgd wait_on");
+    struct Pop {
+        ~Pop() { if (roctx_on()) roctxRangePop(); }
+    } pop;
+    for (;;) {
+        {
+            std::lock_guard<std::mutex> lk(s->mu);
+            if (s->error) { set_error("%s", s->errmsg); return s->error; }
+            if (s->completed >= target) break;
+            if (s->stage == ST_INFLIGHT && s->cur == target) {
+                const int q = s->tp->order_after(*s, target, stream);
+                if (q < 0) return q;
+                if (q == 1) break;
+                if (q == 2) return sched_wait_ex(s, fresh);   // nothing taken yet
+            }
+            if (now_s() - t0 > g_timeout) {
+                const std::string m = "wait timed out " + sched_state(*s);
+                fail_locked(*s, ESGD_ERROR, m.c_str());
+                set_error("%s", s->errmsg);
+                return s->error;
+            }
+        }
+        backoff(polls);
+    }
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->waited = target;
+    s->mark(target, 5);
+    if (s->hold_mode) s->held = true;
+    const int f = s->fresh_take(target) ? 1 : 0;
+    if (fresh) *fresh = f;
+    return ESGD_SUCCESS;
+}
+
 int sched_release(Sched *s, void *stream) {
     ESGD_ARG(s, "schedule release: null schedule");
     {

@@ -83,6 +83,10 @@ struct Transport {
     virtual int prepare(Sched &s, uint32_t round, bool fresh) = 0;
     virtual int launch(Sched &s, uint32_t round, bool fresh) = 0;
     virtual int query(Sched &s) = 0;
+    // stream-ordered completion (sched_wait_on): make `stream` wait on the GPU for the
+    // launched round's last queued work.  1: done; 0: the round is not on the GPU yet (it
+    // sits in the pending shared launch); 2: no such event (host buckets: wait on the host)
+    virtual int order_after(Sched &, uint32_t, void *) { return 2; }
     // host-side work once the copy-out has landed (before wait() returns)
     virtual int complete(Sched &) { return ESGD_SUCCESS; }
     // why a launched round has not finished (timeouts), "" if unknown
@@ -220,6 +224,8 @@ int sched_post(Sched *s, void *producer_stream, int *role, const RoundIO *io = n
 int sched_wait(Sched *s);
 // wait, and say whether this rank had posted the round it returns before joining it
 int sched_wait_ex(Sched *s, int *fresh);
+// the same, ordered on the GPU: `stream` waits for the round (engine.cpp)
+int sched_wait_on(Sched *s, void *stream, int *fresh);
 // hold mode: the caller is done with the round wait() returned; work it queued on
 // `stream` (may be null) is waited for by the next round's snapshot
 int sched_release(Sched *s, void *stream);

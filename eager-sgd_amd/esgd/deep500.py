@@ -60,6 +60,8 @@ def _bind(h):
     h.allreducef_forward_cuda_post_many.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), C.c_float, vp]
     h.allreducef_forward_cuda_wait_many.restype = C.c_int
     h.allreducef_forward_cuda_wait_many.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), vp]
+    h.allreducef_forward_cuda_wait_many_on.restype = C.c_int
+    h.allreducef_forward_cuda_wait_many_on.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), vp]
     h.allreducef_forward_cuda_post_many_io.restype = C.c_int
     h.allreducef_forward_cuda_post_many_io.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), C.POINTER(vp),
                                                        C.c_float, vp]
@@ -188,16 +190,23 @@ class AllreduceOp:
                    "allreducef_forward_cuda_post_many_io")
 
     @staticmethod
-    def wait_many(ops, outs, stream: int | None = None):
+    def wait_many(ops, outs, stream: int | None = None, on_stream: bool = False):
         """wait_cuda for many ops in one call: every posted op's round waited for in order,
         every copy-out in one launch per 48 ops, one release event; ops not posted are
-        skipped.  Raises EsgdError (the first failure) after every round was waited for."""
+        skipped.  Raises EsgdError (the first failure) after every round was waited for.
+        on_stream=True (allreducef_forward_cuda_wait_many_on): the rounds are waited for on
+        the GPU -- `stream` waits for each, and the call returns once all are queued there;
+        a round that fails later fails its op's next post."""
         from .device import as_ptr
         n = len(ops)
         hs = (C.c_void_p * n)(*[op.handle for op in ops])
         os_ = (C.c_void_p * n)(*[as_ptr(o) for o in outs])
-        _lib.check(lib().allreducef_forward_cuda_wait_many(hs, n, os_, stream),
-                   "allreducef_forward_cuda_wait_many")
+        if on_stream:
+            _lib.check(lib().allreducef_forward_cuda_wait_many_on(hs, n, os_, stream),
+                       "allreducef_forward_cuda_wait_many_on")
+        else:
+            _lib.check(lib().allreducef_forward_cuda_wait_many(hs, n, os_, stream),
+                       "allreducef_forward_cuda_wait_many")
 
     def forward_void(self, grad: np.ndarray) -> np.ndarray:
         """The reference ABI's void allreducef_forward verbatim (host buffers): on a failed

@@ -26,6 +26,10 @@ runs the rounds that come due together in shared launches, each round reading gr
 comm_size and writing the reduced gradient back into p.grad itself (fused_io; no copy-in or
 copy-out launch on the caller's stream, 2 HBM passes of the gradient fewer -- only a round a
 peer carried this rank through before its post is copied out of the op's bucket).
+The waits are ordered on the GPU (stream_wait): the caller's stream waits for each round's
+launch event, so the wrapped optimizer's step is queued while the rounds still run -- the
+way torch.distributed's Work.wait() orders a stream behind an RCCL collective -- and a round
+that fails later fails the next step's post.
 pipeline=False keeps the blocking chain (each op fused the same way).
 
 fuse=True (SURVEY.md §8(f) "bucket fusion"): the reference runs one schedule per tensor,
@@ -50,7 +54,8 @@ def _nullcontext():
 class EagerSGDOptimizer:
     def __init__(self, optimizer, comm_size: int, mode: str = "solo", async_: int = 32,
                  seed: int = 6545343, fuse: bool = False, wire: str = "fp32",
-                 pipeline: bool = True, fused_io: bool = True, side_stream: bool = True):
+                 pipeline: bool = True, fused_io: bool = True, side_stream: bool = True,
+                 stream_wait: bool = True):
         if mode not in deep500.MODES:
             raise ValueError(f"mode must be one of {sorted(deep500.MODES)}")
         if wire not in deep500.WIRES:
@@ -71,6 +76,11 @@ class EagerSGDOptimizer:
         # the caller's stream on entry and before it on exit (the ops on the legacy stream
         # cost 1.3-1.6x per step on the 1-GPU rehearsal: profiles/r05/README.md)
         self.side_stream = bool(side_stream)
+        # pipelined per-tensor rounds are waited for on the GPU (allreducef_forward_cuda_
+        # wait_many_on): the wrapped step is queued behind the rounds while they still run,
+        # instead of after the host has seen the last one finish; a round that fails after
+        # that fails the next step's post.  False: the host waits for every round (an A/B)
+        self.stream_wait = bool(stream_wait)
         self._side = None
         self.wire = wire        # "bf16": bf16 copies between ranks
         self._ops = {}          # parameter -> op instance (one bucket per tensor)
@@ -141,7 +151,7 @@ class EagerSGDOptimizer:
                 except Exception as e:   # noqa: BLE001 -- re-raised below
                     err = e
                 try:   # every posted round is waited for, even after a failed post
-                    deep500.AllreduceOp.wait_many(ops, gs, stream)   # results land in place
+                    deep500.AllreduceOp.wait_many(ops, gs, stream, on_stream=self.stream_wait)
                 except Exception as e:   # noqa: BLE001
                     err = err or e
                 if err is not None:

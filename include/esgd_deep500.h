@@ -100,6 +100,12 @@ int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const 
  * and the ops fp32 on the wire; otherwise the group is posted as by _post_many. */
 int allreducef_forward_cuda_post_many_io(void *const *handles, int n, const float *const *inputs,
                                          float *const *outputs, float divisor, void *stream);
+/* Extension: _wait_many ordered on the GPU (esgd_schedule_wait_on): stream waits for each
+ * round on the GPU, and the call returns once every round is queued there, not finished --
+ * the wrapped optimizer's step is queued behind the rounds while they run, as after
+ * torch.distributed's Work.wait().  A round that fails after this returned fails its op's
+ * next post. */
+int allreducef_forward_cuda_wait_many_on(void *const *handles, int n, float *const *outputs, void *stream);
 /* Extension: what the void entry points above (allreducef_forward, allreducef_forward_cuda)
  * do when their round fails (a peer timeout, an allocation failure).  ESGD_OP_ON_ERROR_ABORT
  * (default; env ESGD_OP_ON_ERROR=abort): print the error and abort the process, as their

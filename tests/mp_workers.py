@@ -624,10 +624,15 @@ def op_group(rank, world, steps=3, sizes=(1, 17, 1000, 4099, 262147, (2 << 20) +
     grp = [deep500.AllreduceOp((n,)) for n in sizes]
     one = [deep500.AllreduceOp((n,)) for n in sizes]
     fio = [deep500.AllreduceOp((n,)) for n in sizes]   # post_many_io: the rounds do the copies
+    # the same two group paths waited for on the GPU (wait_many(on_stream=True)): clones
+    # queued right after the call read the results only if the stream waits for the rounds
+    fon = [deep500.AllreduceOp((n,)) for n in sizes]
+    gon = [deep500.AllreduceOp((n,)) for n in sizes]
     ok, errs = [], {}
     for t in range(steps):
         xs = [[ffref.fill_uniform(0xA11 + 13 * t + i, r, n) for r in range(world)] for i, n in enumerate(sizes)]
         g = [torch.from_numpy(x[rank]).to(dev) for x in xs]
+        g0 = [gi.clone() for gi in g]
         h = [gi.clone() for gi in g]
         k = [gi.clone() for gi in g]
         comm.barrier()
@@ -637,13 +642,23 @@ def op_group(rank, world, steps=3, sizes=(1, 17, 1000, 4099, 262147, (2 << 20) +
             op.forward_cuda_div(hi, hi, float(world))
         deep500.AllreduceOp.post_many_io(fio, k, k, float(world))
         deep500.AllreduceOp.wait_many(fio, k)
+        m = [gi.clone() for gi in g0]
+        q = [gi.clone() for gi in g0]
+        deep500.AllreduceOp.post_many_io(fon, m, m, float(world))
+        deep500.AllreduceOp.wait_many(fon, m, on_stream=True)
+        mc = [mi.clone() for mi in m]
+        deep500.AllreduceOp.post_many(gon, q, float(world))
+        deep500.AllreduceOp.wait_many(gon, q, on_stream=True)
+        qc = [qi.clone() for qi in q]
         torch.cuda.synchronize()
         for i, x in enumerate(xs):
             want = ffref.tree_sum([np.float32(xr) / np.float32(world) for xr in x])
             a, b, c = g[i].cpu().numpy(), h[i].cpu().numpy(), k[i].cpu().numpy()
             ok.append(bool(np.array_equal(a.view(np.uint32), want.view(np.uint32)) and
                            np.array_equal(a.view(np.uint32), b.view(np.uint32)) and
-                           np.array_equal(a.view(np.uint32), c.view(np.uint32))))
+                           np.array_equal(a.view(np.uint32), c.view(np.uint32)) and
+                           all(np.array_equal(a.view(np.uint32), y[i].cpu().numpy().view(np.uint32))
+                               for y in (m, mc, q, qc))))
     # misuse: op 0 posted alone, then a group post naming it fails and leaves it posted
     x = [torch.ones(n, device=dev) for n in sizes]
     grp[0].post_cuda(x[0], float(world))
@@ -1707,14 +1722,16 @@ def gpu_post_io(rank, world, count=4099, rounds=3, small_bytes=None, batch=None,
     return {"verdicts": verdicts, "fresh": fresh}
 
 
-def gpu_post_io_late(rank, world, count=4099, steps=8, async_=3, late=1):
+def gpu_post_io_late(rank, world, count=4099, steps=8, async_=3, late=1, on_stream=False):
     """post_io under solo's asynchronous rounds: HOLD | FRESH_ONLY (how the deep500 op runs
     them), rank `late` posts LATE_S after its peers every step.  A round the early rank's
     activation carries the late rank through before its post does not take its data: wait
     says fresh = 0, its dst keeps what it held, and the round's result (its share zero) is
     in rb; a round it posted in time takes src and writes dst.  Every rank's result must be
     the oracle tree of (x_r / P if rank r's round was fresh else 0), the same bits on every
-    rank."""
+    rank.  on_stream: waited for with wait_on(stream) (esgd_schedule_wait_on), the result
+    copied by a kernel queued on that stream right after it returns -- before the round has
+    necessarily finished -- so the copy holds the result only if the stream waits for it."""
     import numpy as np
     import torch.distributed as dist
 
@@ -1723,6 +1740,11 @@ def gpu_post_io_late(rank, world, count=4099, steps=8, async_=3, late=1):
     comm = _comm()
     rb = dev.DeviceBuffer(count)
     src, dst = dev.DeviceBuffer(count), dev.DeviceBuffer(count)
+    if on_stream:
+        import torch
+        torch.cuda.set_device(local_device())
+        stream = torch.cuda.Stream()
+        copy = torch.empty(count, dtype=torch.float32, device="cuda")
     s = comm.Schedule(comm.SOLO, None, rb, count, async_=async_, seed=6545343, buf=comm.BUF_DEVICE,
                       flags=comm.HOLD | comm.FRESH_ONLY)
     out = []
@@ -1734,10 +1756,18 @@ def gpu_post_io_late(rank, world, count=4099, steps=8, async_=3, late=1):
         if rank == late and t > 0:
             time.sleep(LATE_S)
         s.post_io(src, dst, float(world))
-        f = s.wait()
-        res = (dst if f else rb).download()
+        if on_stream:
+            f = s.wait_on(stream)
+            dev.pack_div([dst if f else rb], [count], copy, 1.0, stream.cuda_stream)
+            s.release(None if f else stream.cuda_stream)
+            stream.synchronize()
+            res = copy.cpu().numpy()
+        else:
+            f = s.wait()
+            res = (dst if f else rb).download()
         untouched = f or bool(np.all(dst.download() == np.float32(3.0)))
-        s.release()
+        if not on_stream:
+            s.release()
         fr = [None] * world
         dist.all_gather_object(fr, bool(f))
         want = ffref.tree_sum([x / np.float32(world) if fr[r] else np.zeros_like(x) for r, x in enumerate(xs)])

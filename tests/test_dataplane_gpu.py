@@ -731,11 +731,13 @@ def test_post_io_rounds_read_src_and_write_dst(case, world):
         assert all(o["fresh"]), o["fresh"]
 
 
-def test_post_io_round_carried_through_before_the_post():
+@pytest.mark.parametrize("on_stream", [False, True], ids=["host_wait", "wait_on"])
+def test_post_io_round_carried_through_before_the_post(on_stream):
     # solo, rank 1 posts late: rounds rank 0's activation carries it through do not take
     # rank 1's data (fresh 0, dst untouched, result in rb, its share zero); synchronous
-    # rounds do; every rank the oracle's bits of that contributor set
-    outs = run("gpu_post_io_late", 2, steps=9)
+    # rounds do; every rank the oracle's bits of that contributor set.  wait_on: the
+    # result is copied by a kernel queued right after esgd_schedule_wait_on returned
+    outs = run("gpu_post_io_late", 2, steps=9, on_stream=on_stream)
     for o in outs:
         for step in o:
             assert step["ok"] and step["untouched"], step
