@@ -652,6 +652,8 @@ struct BaseState {
     bool fin_mode = false;            // the round in flight reports through SchedShm::fin
     int batch_rc = 0;                 // the shared launch of this round failed (its status)
     bool in_batch = false;            // the round in flight went into a shared launch
+    std::atomic<uint32_t> flushed{0}; // the last round whose shared launch went out
+    uint64_t batch_seq = 0;           // that launch's number (g_batch_seq; g_batch_mu)
     std::vector<char *> retired;      // grown-out buckets: peers may still map them
     uint64_t off[kMaxRanks] = {}, len[kMaxRanks] = {};   // elements
     // events from the process-wide pool (pooled_event); one recording may be shared by a
@@ -1228,6 +1230,7 @@ static bool snap_eligible(const Sched &s, const IpcState &st, const void *src) {
     return bytes && bytes < (size_t(1) << 31) && (al & 15) == 0;
 }
 static std::vector<BatchEntry> g_pend;
+static uint64_t g_batch_seq = 0;   // shared launches sent so far (g_batch_mu)
 static CopySet g_copy;   // the pending launch's snapshots (nseg 0: none)
 // the shared launches' tile counter (BatchArgs::queue; a device word behind the descriptor
 // table) and its value when the next launch starts
@@ -1407,9 +1410,12 @@ static int batch_flush_locked() {
         if (!sp) rc = ESGD_ERROR;
         else if (hipEventRecord(*sp, cs) != hipSuccess) rc = hip_fail(hipGetLastError(), "hipEventRecord", __FILE__, __LINE__);
     }
+    ++g_batch_seq;
     for (BatchEntry &b : g_pend) {
         b.st->batch_ev = sp;
         b.st->batch_rc = rc;
+        b.st->batch_seq = g_batch_seq;
+        b.st->flushed.store(b.round, std::memory_order_release);
     }
     if (sp) g_outstanding.push_back(sp);
     g_pend.clear();
@@ -1564,21 +1570,24 @@ static int batch_append(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) 
 }
 
 // sched_wait_on: `stream` waits for the event after the round's last queued work -- its
-// shared launch's (once flushed) or its own (st.ev, recorded last by every device round).
-// Host buckets finish on the host (base_complete), a failed shared launch is reported by
-// the host wait.
-static int base_order_after(Sched &s, BaseState &st, void *stream) {
+// shared launch's (once sent) or its own (st.ev, recorded last by every device round).  All
+// of them are queued on the process's one round stream, so a shared launch at or before one
+// `stream` already waits for (`seen`) needs no second wait: the 161 waits of the optimizer's
+// step become one per shared launch (~13).  Host buckets finish on the host (base_complete),
+// a failed shared launch is reported by the host wait.  Caller holds s.mu (in_batch is
+// written under it; batch_ev / batch_seq under g_batch_mu, after `flushed`).
+static int base_order_after(Sched &s, BaseState &st, uint32_t round, void *stream, uint64_t *seen) {
     if (s.host_mode || st.copyout_pending) return 2;
     hipEvent_t ev;
-    {
+    if (st.in_batch) {
+        if (st.flushed.load(std::memory_order_acquire) != round) return 0;   // still pending
         std::lock_guard<std::mutex> lk(g_batch_mu);
-        if (st.batch_rc) return 2;
-        if (st.in_batch) {
-            if (!st.batch_ev) return 0;   // still in the pending launch
-            ev = *st.batch_ev;
-        } else {
-            ev = st.ev;
-        }
+        if (st.batch_rc || !st.batch_ev) return 2;
+        if (seen && *seen >= st.batch_seq) return 1;
+        ev = *st.batch_ev;
+        if (seen) *seen = st.batch_seq;
+    } else {
+        ev = st.ev;
     }
     ESGD_HIP(hipStreamWaitEvent(user_stream(stream), ev, 0));
     return 1;
@@ -2137,7 +2146,9 @@ struct IpcTransport final : Transport {
     }
 
     int query(Sched &s) override { return base_query(s, S(s)); }
-    int order_after(Sched &s, uint32_t, void *stream) override { return base_order_after(s, S(s), stream); }
+    int order_after(Sched &s, uint32_t round, void *stream, uint64_t *seen) override {
+        return base_order_after(s, S(s), round, stream, seen);
+    }
 
     int complete(Sched &s) override { return base_complete(s, S(s)); }
 
@@ -2494,7 +2505,9 @@ struct RcclTransport final : Transport {
     }
 
     int query(Sched &s) override { return base_query(s, S(s)); }
-    int order_after(Sched &s, uint32_t, void *stream) override { return base_order_after(s, S(s), stream); }
+    int order_after(Sched &s, uint32_t round, void *stream, uint64_t *seen) override {
+        return base_order_after(s, S(s), round, stream, seen);
+    }
     int complete(Sched &s) override { return base_complete(s, S(s)); }
 
     void teardown(Sched &s) override {

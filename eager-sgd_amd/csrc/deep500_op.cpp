@@ -450,9 +450,21 @@ namespace {
 
 // on_stream: each round is waited for on the GPU (esgd_schedule_wait_on): stream waits for
 // it, and the call returns once every round is queued instead of finished
+// esgd_schedule_wait_on, remembering across the group the latest shared launch the stream
+// already waits for (one stream wait per shared launch, not per round)
+int wait_on(uint64_t h, void *ps, int *fresh, uint64_t *seen) {
+    esgd::Sched *s = esgd::sched_lookup(h);
+    if (!s) {
+        esgd::set_error("allreducef_forward_cuda_wait_many_on: unknown schedule");
+        return ESGD_INVALID_ARG;
+    }
+    return esgd::sched_wait_on(s, ps, fresh, seen);
+}
+
 int wait_many_impl(void *const *handles, int n, float *const *outputs, void *stream, bool on_stream) {
     ESGD_ARG(n >= 0 && (n == 0 || (handles && outputs)), "allreducef_forward_cuda_wait_many: bad arguments");
     void *ps = caller_stream(static_cast<hipStream_t>(stream));
+    uint64_t seen = 0;
     std::vector<float *> outs, rbs;
     std::vector<uint64_t> counts;
     std::vector<esgd_sched_h> hs, hs_io;   // copied out from rb / results already in place
@@ -465,7 +477,7 @@ int wait_many_impl(void *const *handles, int n, float *const *outputs, void *str
         const bool io = op->io_posted;
         op->io_posted = false;
         int fresh = 0;
-        if (int rc = on_stream ? esgd_schedule_wait_on(op->sched, ps, &fresh) : esgd_schedule_wait_ex(op->sched, &fresh)) {
+        if (int rc = on_stream ? wait_on(op->sched, ps, &fresh, &seen) : esgd_schedule_wait_ex(op->sched, &fresh)) {
             if (!first) first = rc;
             continue;
         }

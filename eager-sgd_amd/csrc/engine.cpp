@@ -503,7 +503,7 @@ int sched_wait_ex(Sched *s, int *fresh) {
 // stream behind an RCCL collective.  The round's outcome is not known yet: a failure that
 // comes later is reported by the schedule's next post / wait (the error is sticky).
 // Transports or buckets without such an event (host buckets) wait on the host.
-int sched_wait_on(Sched *s, void *stream, int *fresh) {
+int sched_wait_on(Sched *s, void *stream, int *fresh, uint64_t *seen) {
     ESGD_ARG(s && stream, "schedule wait_on: null schedule or stream (ESGD_STREAM_NULL names the legacy stream)");
     uint32_t target;
     {
@@ -517,13 +517,18 @@ int sched_wait_on(Sched *s, void *stream, int *fresh) {
     struct Pop {
         ~Pop() { if (roctx_on()) roctxRangePop(); }
     } pop;
+    // spin on the lock-free counters; the schedule's mutex is taken only once the round is
+    // launched (or finished) and every 1024 polls (errors, the timeout): a waiter that
+    // took it every poll slowed the progress thread's launches and flushes 1.5x (r05h)
     for (;;) {
-        {
+        const bool due = int32_t(s->completed_a.load(std::memory_order_acquire) - target) >= 0 ||
+                         int32_t(s->launched_a.load(std::memory_order_acquire) - target) >= 0;
+        if (due || (polls & 1023) == 1023) {
             std::lock_guard<std::mutex> lk(s->mu);
             if (s->error) { set_error("%s", s->errmsg); return s->error; }
             if (s->completed >= target) break;
             if (s->stage == ST_INFLIGHT && s->cur == target) {
-                const int q = s->tp->order_after(*s, target, stream);
+                const int q = s->tp->order_after(*s, target, stream, seen);
                 if (q < 0) return q;
                 if (q == 1) break;
                 if (q == 2) return sched_wait_ex(s, fresh);   // nothing taken yet
@@ -773,6 +778,7 @@ static bool pump_tickets(const std::vector<Sched *> &snap) {
                 } else {
                     target->stage = ST_INFLIGHT;
                     target->stage_t0 = now_s();
+                    target->launched_a.store(target->cur, std::memory_order_release);
                 }
             }
         }

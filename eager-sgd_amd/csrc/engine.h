@@ -85,8 +85,11 @@ struct Transport {
     virtual int query(Sched &s) = 0;
     // stream-ordered completion (sched_wait_on): make `stream` wait on the GPU for the
     // launched round's last queued work.  1: done; 0: the round is not on the GPU yet (it
-    // sits in the pending shared launch); 2: no such event (host buckets: wait on the host)
-    virtual int order_after(Sched &, uint32_t, void *) { return 2; }
+    // sits in the pending shared launch); 2: no such event (host buckets: wait on the host).
+    // seen (may be null): the latest shared launch `stream` already waits for -- a round in
+    // that launch or an earlier one (one round stream: launches finish in order) needs no
+    // second wait; updated
+    virtual int order_after(Sched &, uint32_t, void *, uint64_t *) { return 2; }
     // host-side work once the copy-out has landed (before wait() returns)
     virtual int complete(Sched &) { return ESGD_SUCCESS; }
     // why a launched round has not finished (timeouts), "" if unknown
@@ -131,6 +134,7 @@ struct Sched {
     std::atomic<uint32_t> joined{0};
     uint32_t completed = 0, waited = 0;
     std::atomic<uint32_t> completed_a{0};   // = completed, for wait()'s lock-free spin
+    std::atomic<uint32_t> launched_a{0};    // last round launch() queued (wait_on's lock-free spin)
     std::atomic<Stage> stage{ST_IDLE};
     uint32_t cur = 0;
     bool cur_fresh = false;
@@ -225,7 +229,7 @@ int sched_wait(Sched *s);
 // wait, and say whether this rank had posted the round it returns before joining it
 int sched_wait_ex(Sched *s, int *fresh);
 // the same, ordered on the GPU: `stream` waits for the round (engine.cpp)
-int sched_wait_on(Sched *s, void *stream, int *fresh);
+int sched_wait_on(Sched *s, void *stream, int *fresh, uint64_t *seen = nullptr);
 // hold mode: the caller is done with the round wait() returned; work it queued on
 // `stream` (may be null) is waited for by the next round's snapshot
 int sched_release(Sched *s, void *stream);

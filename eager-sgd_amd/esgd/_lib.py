@@ -8,6 +8,7 @@ that copy through the shared soname).
 """
 from __future__ import annotations
 
+import array
 import ctypes as C
 import os
 
@@ -125,7 +126,10 @@ def dtype_size(dtype: int) -> int:
 
 
 def ptr_array(ptrs):
-    arr = (C.c_void_p * len(ptrs))()
-    for i, p in enumerate(ptrs):
-        arr[i] = int(p)
-    return arr
+    """A C array of pointers from Python ints, through array('Q') (about 3x cheaper than
+    ctypes' element-wise conversion: the optimizer passes 161-entry groups every step).  The
+    ctypes array keeps the buffer alive."""
+    buf = array.array("Q", ptrs)
+    if not buf:
+        return (C.c_void_p * 1)()
+    return (C.c_void_p * len(buf)).from_buffer(buf)

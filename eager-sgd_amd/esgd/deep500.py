@@ -169,8 +169,8 @@ class AllreduceOp:
         EsgdError; the ops before a failed post stay posted (wait_many drains them)."""
         from .device import as_ptr
         n = len(ops)
-        hs = (C.c_void_p * n)(*[op.handle for op in ops])
-        gs = (C.c_void_p * n)(*[as_ptr(g) for g in grads])
+        hs = _lib.ptr_array([op.handle for op in ops])
+        gs = _lib.ptr_array([as_ptr(g) for g in grads])
         _lib.check(lib().allreducef_forward_cuda_post_many(hs, n, gs, float(divisor), stream),
                    "allreducef_forward_cuda_post_many")
 
@@ -183,9 +183,9 @@ class AllreduceOp:
         post.  Unaligned tensors or a bf16 wire fall back to post_many.  Raises EsgdError."""
         from .device import as_ptr
         n = len(ops)
-        hs = (C.c_void_p * n)(*[op.handle for op in ops])
-        gs = (C.c_void_p * n)(*[as_ptr(g) for g in grads])
-        os_ = (C.c_void_p * n)(*[as_ptr(o) for o in outs])
+        hs = _lib.ptr_array([op.handle for op in ops])
+        gs = _lib.ptr_array([as_ptr(g) for g in grads])
+        os_ = _lib.ptr_array([as_ptr(o) for o in outs])
         _lib.check(lib().allreducef_forward_cuda_post_many_io(hs, n, gs, os_, float(divisor), stream),
                    "allreducef_forward_cuda_post_many_io")
 
@@ -199,8 +199,8 @@ class AllreduceOp:
         a round that fails later fails its op's next post."""
         from .device import as_ptr
         n = len(ops)
-        hs = (C.c_void_p * n)(*[op.handle for op in ops])
-        os_ = (C.c_void_p * n)(*[as_ptr(o) for o in outs])
+        hs = _lib.ptr_array([op.handle for op in ops])
+        os_ = _lib.ptr_array([as_ptr(o) for o in outs])
         if on_stream:
             _lib.check(lib().allreducef_forward_cuda_wait_many_on(hs, n, os_, stream),
                        "allreducef_forward_cuda_wait_many_on")

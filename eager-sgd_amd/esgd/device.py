@@ -23,12 +23,13 @@ NP_DTYPE = {
 
 
 def as_ptr(x) -> int:
+    dp = getattr(x, "data_ptr", None)   # torch tensors first: the per-step group calls
+    if dp is not None:
+        return int(dp())
     if isinstance(x, int):
         return x
     if hasattr(x, "ptr"):
         return int(x.ptr)
-    if hasattr(x, "data_ptr"):
-        return int(x.data_ptr())
     raise TypeError(f"cannot take a device pointer of {type(x)!r}")
 
 
