@@ -861,6 +861,11 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
                      # the rounds waited for on the host (every round seen finished before the
                      # wrapped step is queued) instead of on the GPU (stream_wait): the A/B
                      ("per_tensor_pipelined_host_wait", dict(fuse=False, stream_wait=False)),
+                     # the ops' work and the wrapped SGD step on the data plane's round stream
+                     # (esgd_round_stream): ordered behind the rounds by the stream itself
+                     ("per_tensor_pipelined_round_stream", dict(fuse=False, round_stream=True)),
+                     ("per_tensor_pipelined_round_stream_host_wait",
+                      dict(fuse=False, round_stream=True, stream_wait=False)),
                      # the ops on torch's legacy default stream itself (no internal stream)
                      ("per_tensor_pipelined_legacy_stream", dict(fuse=False, side_stream=False)),
                      # the same with copy-in / copy-out kernels on the caller's stream instead of

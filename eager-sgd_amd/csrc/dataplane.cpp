@@ -403,6 +403,15 @@ static int round_stream(hipStream_t *out) {
 // earliest round in flight anywhere has been launched by every rank and completes.
 int seal_stream(hipStream_t *out) { return round_stream(out); }
 
+// esgd_round_stream: a caller may queue work on the round stream itself, to be ordered
+// after the rounds launched so far by stream order alone (EagerSGDOptimizer's round_stream)
+int dataplane_round_stream(void **out) {
+    hipStream_t st = nullptr;
+    if (int rc = round_stream(&st)) return rc;
+    *out = st;
+    return ESGD_SUCCESS;
+}
+
 // Copy streams of the chunked host-bucket rounds (one per direction, so a chunk's D2H
 // runs while the next chunk's H2D does: PCIe is full duplex).  Created on first use.
 static hipStream_t g_h2d = nullptr, g_d2h = nullptr;
@@ -1581,12 +1590,14 @@ static int base_order_after(Sched &s, BaseState &st, uint32_t round, void *strea
     hipEvent_t ev;
     if (st.in_batch) {
         if (st.flushed.load(std::memory_order_acquire) != round) return 0;   // still pending
+        if (user_stream(stream) == st.stream) return 1;   // the round stream: in order already
         std::lock_guard<std::mutex> lk(g_batch_mu);
         if (st.batch_rc || !st.batch_ev) return 2;
         if (seen && *seen >= st.batch_seq) return 1;
         ev = *st.batch_ev;
         if (seen) *seen = st.batch_seq;
     } else {
+        if (user_stream(stream) == st.stream) return 1;
         ev = st.ev;
     }
     ESGD_HIP(hipStreamWaitEvent(user_stream(stream), ev, 0));

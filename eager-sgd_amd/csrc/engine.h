@@ -258,6 +258,7 @@ void dataplane_shutdown();
 // launch the rounds appended to the pending shared launch (k_round_batch); the engine calls
 // it after every pump of the issue ring, transports before queuing anything else
 int dataplane_flush();
+int dataplane_round_stream(void **out);   // esgd_round_stream
 int dataplane_flush_soft();
 bool config_inline_join();   // esgd_set_config("inline_join") / ESGD_INLINE_JOIN
 void dataplane_extra_queues(int n);   // diagnostics: n more streams, each with a queue   // the end of a pump: flush unless ESGD_BATCH_DEPTH launches are queued

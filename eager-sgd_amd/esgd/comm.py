@@ -45,6 +45,7 @@ def _bind(h):
         "esgd_schedule_create_ex": (i, [i, i, vp, vp, u64, i, i, C.c_uint, C.c_uint, C.POINTER(u64)]),
         "esgd_schedule_wait_ex": (i, [u64, C.POINTER(i)]),
         "esgd_schedule_wait_on": (i, [u64, vp, C.POINTER(i)]),
+        "esgd_round_stream": (i, [C.POINTER(vp)]),
         "esgd_schedule_release": (i, [u64, vp]),
         "esgd_schedule_post": (i, [u64, vp, C.POINTER(i)]),
         "esgd_schedule_wait": (i, [u64]),
@@ -170,6 +171,15 @@ def profile() -> dict:
 
 def barrier():
     check(lib().esgd_barrier(), "esgd_barrier")
+
+
+def round_stream() -> int:
+    """esgd_round_stream: the handle of the process's round stream (every round is queued
+    on it in issue order); work queued there runs after the rounds launched so far.  Wrap it
+    with torch.cuda.ExternalStream to queue torch work on it."""
+    h = C.c_void_p()
+    check(lib().esgd_round_stream(C.byref(h)), "esgd_round_stream")
+    return int(h.value or 0)
 
 
 def _buf_arg(x, buf):

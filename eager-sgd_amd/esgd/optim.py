@@ -55,7 +55,7 @@ class EagerSGDOptimizer:
     def __init__(self, optimizer, comm_size: int, mode: str = "solo", async_: int = 32,
                  seed: int = 6545343, fuse: bool = False, wire: str = "fp32",
                  pipeline: bool = True, fused_io: bool = True, side_stream: bool = True,
-                 stream_wait: bool = True):
+                 stream_wait: bool = True, round_stream: bool = False):
         if mode not in deep500.MODES:
             raise ValueError(f"mode must be one of {sorted(deep500.MODES)}")
         if wire not in deep500.WIRES:
@@ -81,6 +81,11 @@ class EagerSGDOptimizer:
         # instead of after the host has seen the last one finish; a round that fails after
         # that fails the next step's post.  False: the host waits for every round (an A/B)
         self.stream_wait = bool(stream_wait)
+        # the ops' work AND the wrapped step queued on the data plane's round stream itself
+        # (esgd_round_stream): the step follows the rounds by stream order, no event wait
+        # between queues, one hardware queue fewer per process than the side stream
+        self.round_stream = bool(round_stream)
+        self._rs = None
         self._side = None
         self.wire = wire        # "bf16": bf16 copies between ranks
         self._ops = {}          # parameter -> op instance (one bucket per tensor)
@@ -99,6 +104,8 @@ class EagerSGDOptimizer:
             deep500.configure(self.mode, self.async_, self.seed, self.wire)
             self._configured = True
         caller = torch.cuda.current_stream()
+        if self.round_stream and not self.fuse:
+            return self._apply_on_round_stream(grads_and_vars, caller, global_step)
         side = None
         if self.side_stream and caller.cuda_stream == 0:
             if self._side is None or self._side.device != caller.device:
@@ -112,6 +119,24 @@ class EagerSGDOptimizer:
             for t in made:                 # gradients converted on the side stream: the
                 t.record_stream(caller)    # caller's stream uses them too
         r = self.optimizer.step()
+        if global_step is not None and hasattr(global_step, "add_"):
+            global_step.add_(1)
+        return r
+
+    def _apply_on_round_stream(self, grads_and_vars, caller, global_step):
+        import torch
+
+        from . import comm
+        if self._rs is None or self._rs.device != caller.device:
+            self._rs = torch.cuda.ExternalStream(comm.round_stream(), device=caller.device)
+        rs = self._rs
+        rs.wait_stream(caller)            # the gradients were written on the caller's stream
+        with torch.cuda.stream(rs):
+            made = self._reduce(list(grads_and_vars), rs.cuda_stream)
+            r = self.optimizer.step()     # behind the rounds on the same stream
+        caller.wait_stream(rs)
+        for t in made:
+            t.record_stream(caller)
         if global_step is not None and hasattr(global_step, "add_"):
             global_step.add_(1)
         return r

@@ -255,6 +255,12 @@ int esgd_schedule_wait_ex(esgd_sched_h h, int *fresh);
  * failure that comes later fails the schedule's next post / wait.  Host buckets wait on the
  * host (as wait_ex). */
 int esgd_schedule_wait_on(esgd_sched_h h, void *stream, int *fresh);
+/* The process's round stream (a hipStream_t; created on first use on the current device):
+ * every round of every schedule is queued on it in the node's issue order.  Work a caller
+ * queues there runs after the rounds launched so far, by stream order alone -- e.g. the
+ * optimizer step that reads the reduced gradients (wait_on with this stream needs no event
+ * wait).  Never synchronise on it from inside a round's producer work. (extension) */
+int esgd_round_stream(void **stream);
 /* ESGD_SCHED_HOLD schedules: done with the round wait returned.  Work queued on
  * `stream` so far (copy-out of rb, zeroing sb; NULL = nothing queued) is waited for by
  * the next round's snapshot on the GPU. */

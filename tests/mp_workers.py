@@ -541,7 +541,8 @@ def op_device_pattern(rank, world, count=25559081, steps=9, mode="solo", packed=
     return out
 
 
-def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp32", pipeline=True, fused_io=True):
+def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp32", pipeline=True, fused_io=True,
+                   **opt_kw):
     """EagerSGDOptimizer on PyTorch-ROCm: every rank's p.grad after apply_gradients must
     equal the oracle tree of (grad_r / P) over ranks, bit for bit (allreduce), or over
     expected_inputs' contributors when the ranks call every op in late_ranks' order
@@ -560,7 +561,7 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp3
     torch.cuda.set_device(dev)
     model = torch.nn.Sequential(torch.nn.Linear(64, 48), torch.nn.ReLU(), torch.nn.Linear(48, 10)).to(dev)
     opt = EagerSGDOptimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9), world, mode=mode,
-                            fuse=fuse, wire=wire, pipeline=pipeline, fused_io=fused_io)
+                            fuse=fuse, wire=wire, pipeline=pipeline, fused_io=fused_io, **opt_kw)
     ok = []
     for t in range(steps):
         g = torch.Generator().manual_seed(100 * t + rank)

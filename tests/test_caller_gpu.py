@@ -44,7 +44,12 @@ def test_deep500_op_device_late_gradient_dropped(on_time, count):
 VARIANTS = {"blocking": dict(pipeline=False), "pipelined": dict(pipeline=True), "fused": dict(fuse=True),
             # the per-tensor rounds with copy-in / copy-out kernels on the caller's stream
             # instead of the fused round I/O (an A/B): the same bits
-            "pipelined_copy_kernels": dict(pipeline=True, fused_io=False)}
+            "pipelined_copy_kernels": dict(pipeline=True, fused_io=False),
+            # the rounds waited for on the host instead of on the GPU; the ops and the wrapped
+            # step on the data plane's round stream (esgd_round_stream), either wait
+            "pipelined_host_wait": dict(pipeline=True, stream_wait=False),
+            "pipelined_round_stream": dict(pipeline=True, round_stream=True),
+            "pipelined_round_stream_host_wait": dict(pipeline=True, round_stream=True, stream_wait=False)}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
