@@ -858,21 +858,19 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
     side = None   # created for its variant only: one more stream is one more hardware queue,
     #               which on a GPU shared by the ranks changes the timings
     for name, kw in (("per_tensor_pipelined", dict(fuse=False)),
-                     # the rounds waited for on the host (every round seen finished before the
-                     # wrapped step is queued) instead of on the GPU (stream_wait): the A/B
-                     ("per_tensor_pipelined_host_wait", dict(fuse=False, stream_wait=False)),
+                     # the rounds waited for on the GPU (allreducef_forward_cuda_wait_many_on:
+                     # the wrapped step queued behind them while they run) instead of the host
+                     ("per_tensor_pipelined_stream_wait", dict(fuse=False, stream_wait=True)),
                      # the ops' work and the wrapped SGD step on the data plane's round stream
                      # (esgd_round_stream): ordered behind the rounds by the stream itself
-                     ("per_tensor_pipelined_round_stream", dict(fuse=False, round_stream=True)),
-                     ("per_tensor_pipelined_round_stream_host_wait",
-                      dict(fuse=False, round_stream=True, stream_wait=False)),
+                     ("per_tensor_pipelined_round_stream", dict(fuse=False, round_stream=True, stream_wait=True)),
                      # the ops on torch's legacy default stream itself (no internal stream)
                      ("per_tensor_pipelined_legacy_stream", dict(fuse=False, side_stream=False)),
                      # the same with copy-in / copy-out kernels on the caller's stream instead of
                      # the rounds' own I/O (esgd_schedule_post_io): the A/B of the fused path
                      ("per_tensor_pipelined_copy_kernels", dict(fuse=False, fused_io=False)),
                      ("per_tensor_blocking", dict(pipeline=False)),
-                     ("fused", dict(fuse=True)), ("per_tensor_blocking_side_stream", dict(pipeline=False)),
+                     ("fused", dict(fuse=True)),
                      # the pipelined step with the caller's work on a torch side stream instead
                      # of the legacy NULL stream (the blocking pair above differs 1.6x)
                      ("per_tensor_pipelined_side_stream", dict(fuse=False))):

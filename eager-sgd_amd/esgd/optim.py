@@ -26,10 +26,12 @@ runs the rounds that come due together in shared launches, each round reading gr
 comm_size and writing the reduced gradient back into p.grad itself (fused_io; no copy-in or
 copy-out launch on the caller's stream, 2 HBM passes of the gradient fewer -- only a round a
 peer carried this rank through before its post is copied out of the op's bucket).
-The waits are ordered on the GPU (stream_wait): the caller's stream waits for each round's
-launch event, so the wrapped optimizer's step is queued while the rounds still run -- the
-way torch.distributed's Work.wait() orders a stream behind an RCCL collective -- and a round
-that fails later fails the next step's post.
+stream_wait=True orders the waits on the GPU instead: the ops' stream waits for each
+shared launch's event, so the wrapped optimizer's step is queued while the rounds still
+run -- the way torch.distributed's Work.wait() orders a stream behind an RCCL collective --
+and a round that fails later fails the next step's post; round_stream=True queues the ops'
+work and the wrapped step on the data plane's round stream itself (esgd_round_stream).  Both
+are opt-in A/Bs (measured no faster on the 1-GPU rehearsal).
 pipeline=False keeps the blocking chain (each op fused the same way).
 
 fuse=True (SURVEY.md §8(f) "bucket fusion"): the reference runs one schedule per tensor,
@@ -55,7 +57,7 @@ class EagerSGDOptimizer:
     def __init__(self, optimizer, comm_size: int, mode: str = "solo", async_: int = 32,
                  seed: int = 6545343, fuse: bool = False, wire: str = "fp32",
                  pipeline: bool = True, fused_io: bool = True, side_stream: bool = True,
-                 stream_wait: bool = True, round_stream: bool = False):
+                 stream_wait: bool = False, round_stream: bool = False):
         if mode not in deep500.MODES:
             raise ValueError(f"mode must be one of {sorted(deep500.MODES)}")
         if wire not in deep500.WIRES:
@@ -76,10 +78,12 @@ class EagerSGDOptimizer:
         # the caller's stream on entry and before it on exit (the ops on the legacy stream
         # cost 1.3-1.6x per step on the 1-GPU rehearsal: profiles/r05/README.md)
         self.side_stream = bool(side_stream)
-        # pipelined per-tensor rounds are waited for on the GPU (allreducef_forward_cuda_
-        # wait_many_on): the wrapped step is queued behind the rounds while they still run,
-        # instead of after the host has seen the last one finish; a round that fails after
-        # that fails the next step's post.  False: the host waits for every round (an A/B)
+        # stream_wait=True: pipelined per-tensor rounds are waited for on the GPU
+        # (allreducef_forward_cuda_wait_many_on): the wrapped step is queued behind the rounds
+        # while they still run; a round that fails after that fails the next step's post.
+        # Off by default: on the 1-GPU rehearsal the side stream's pending waits slowed the
+        # rounds' completion 1.4x, and on the round stream it gained nothing (the last shared
+        # launch goes out when the one before it finishes), profiles/r05/README.md
         self.stream_wait = bool(stream_wait)
         # the ops' work AND the wrapped step queued on the data plane's round stream itself
         # (esgd_round_stream): the step follows the rounds by stream order, no event wait

@@ -45,11 +45,11 @@ VARIANTS = {"blocking": dict(pipeline=False), "pipelined": dict(pipeline=True), 
             # the per-tensor rounds with copy-in / copy-out kernels on the caller's stream
             # instead of the fused round I/O (an A/B): the same bits
             "pipelined_copy_kernels": dict(pipeline=True, fused_io=False),
-            # the rounds waited for on the host instead of on the GPU; the ops and the wrapped
-            # step on the data plane's round stream (esgd_round_stream), either wait
-            "pipelined_host_wait": dict(pipeline=True, stream_wait=False),
-            "pipelined_round_stream": dict(pipeline=True, round_stream=True),
-            "pipelined_round_stream_host_wait": dict(pipeline=True, round_stream=True, stream_wait=False)}
+            # the rounds waited for on the GPU instead of the host (wait_many_on); the ops and
+            # the wrapped step on the data plane's round stream (esgd_round_stream), either wait
+            "pipelined_stream_wait": dict(pipeline=True, stream_wait=True),
+            "pipelined_round_stream": dict(pipeline=True, round_stream=True, stream_wait=True),
+            "pipelined_round_stream_host_wait": dict(pipeline=True, round_stream=True)}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
