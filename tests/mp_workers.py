@@ -2096,3 +2096,51 @@ def op_queue_probe(rank, world, side=False, steps=3, sizes=(4099, 100003, 1 << 2
     for op in ops:
         op.close()
     return {"us_per_round": round(us, 1), "side": side}
+
+
+def gpu_wait_on_paths(rank, world, rounds=3):
+    """esgd_schedule_wait_on on the round paths the optimizer test does not reach: a
+    five-launch round (4 MiB + 12 B: its own event, no shared launch), a one-launch round
+    (a shared launch of its own), and host buckets (no GPU event: the host wait instead).
+    Each result is read by a copy queued on the waited stream right after wait_on returned
+    (device buckets) or straight from host memory; the oracle tree of the ranks' inputs."""
+    import numpy as np
+
+    from esgd import device as dev
+    from oracle import ffref
+    comm = _comm()
+    stream = dev.Stream()
+    out = {}
+    big = (1 << 20) + 3
+    cases = {"five_launch": (big, False), "one_launch": (4099, False), "host": (4099, True)}
+    for name, (count, host) in cases.items():
+        if host:
+            sb, rb = np.zeros(count, np.float32), np.zeros(count, np.float32)
+            s = comm.Schedule(comm.ALLREDUCE, sb, rb, count, buf=comm.BUF_HOST)
+        else:
+            sb, rb = dev.DeviceBuffer(count), dev.DeviceBuffer(count)
+            s = comm.Schedule(comm.ALLREDUCE, sb, rb, count, buf=comm.BUF_DEVICE)
+            copy = dev.DeviceBuffer(count)
+        ok = []
+        for t in range(rounds):
+            xs = [ffref.fill_uniform(0x3A1 + 7 * t, r, count) for r in range(world)]
+            if host:
+                sb[:] = xs[rank]
+            else:
+                sb.upload(xs[rank])
+            comm.barrier()
+            s.post()
+            fresh = s.wait_on(stream)
+            if host:
+                got = rb.copy()
+            else:
+                dev.pack_div([rb], [count], copy, 1.0, stream.handle)
+                stream.synchronize()
+                got = copy.download()
+            want = ffref.tree_sum(xs)
+            ok.append(bool(fresh) and bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
+            comm.barrier()
+        s.delete()
+        out[name] = ok
+    comm.finalize()
+    return out

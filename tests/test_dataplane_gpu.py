@@ -746,6 +746,16 @@ def test_post_io_round_carried_through_before_the_post(on_stream):
     assert any(not st["fresh"][1] for st in outs[0][1:]), outs[0]   # the late path was taken
 
 
+def test_wait_on_five_launch_one_launch_and_host_buckets():
+    # esgd_schedule_wait_on beyond the shared launches: a five-launch round (its own
+    # event), a one-launch round, and host buckets (the host wait fallback); the oracle's
+    # bits read right behind the wait on the waited stream
+    outs = run("gpu_wait_on_paths", 2)
+    for o in outs:
+        for name, ok in o.items():
+            assert all(ok), (name, ok)
+
+
 SWEEPS_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "bin",
                           "libesgd_sweeps.so")
 
