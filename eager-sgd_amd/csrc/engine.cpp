@@ -520,6 +520,7 @@ int sched_wait_on(Sched *s, void *stream, int *fresh, uint64_t *seen) {
     // spin on the lock-free counters; the schedule's mutex is taken only once the round is
     // launched (or finished) and every 1024 polls (errors, the timeout): a waiter that
     // took it every poll slowed the progress thread's launches and flushes 1.5x (r05h)
+    bool host_wait = false;
     for (;;) {
         const bool due = int32_t(s->completed_a.load(std::memory_order_acquire) - target) >= 0 ||
                          int32_t(s->launched_a.load(std::memory_order_acquire) - target) >= 0;
@@ -531,7 +532,7 @@ int sched_wait_on(Sched *s, void *stream, int *fresh, uint64_t *seen) {
                 const int q = s->tp->order_after(*s, target, stream, seen);
                 if (q < 0) return q;
                 if (q == 1) break;
-                if (q == 2) return sched_wait_ex(s, fresh);   // nothing taken yet
+                if (q == 2) { host_wait = true; break; }   // wait_ex below, with mu released
             }
             if (now_s() - t0 > g_timeout) {
                 const std::string m = "wait timed out " + sched_state(*s);
@@ -542,6 +543,9 @@ int sched_wait_on(Sched *s, void *stream, int *fresh, uint64_t *seen) {
         }
         backoff(polls);
     }
+    // no GPU event for this round (host buckets): wait on the host -- outside the loop, whose
+    // guard of s->mu wait_ex would otherwise try to take a second time (r05k2: hung)
+    if (host_wait) return sched_wait_ex(s, fresh);
     std::lock_guard<std::mutex> lk(s->mu);
     s->waited = target;
     s->mark(target, 5);

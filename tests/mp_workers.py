@@ -145,7 +145,7 @@ def _comm():
 
 
 def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0.0,
-              first_poster_rotates=False, barrier_each=False, use_test=False):
+              first_poster_rotates=False, barrier_each=False, use_test=False, wait_on=False):
     """Control plane only (ESGD_BUF_NONE): drive `rounds` post/wait cycles and return
     this rank's per-round log, post roles and stats."""
     comm = _comm()
@@ -169,6 +169,8 @@ def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0
         if use_test:
             while not s.test():
                 time.sleep(0.0005)
+        elif wait_on:   # esgd_schedule_wait_on: no GPU event here, so the host wait runs
+            s.wait_on(0)
         else:
             s.wait()
     comm.barrier()
@@ -1831,8 +1833,14 @@ def gpu_residency(rank, world, hog_ms=6000, free_cus=2, rounds=4, counts=(1 << 2
             want = sum((np.arange(n) + t + 7 * r) for r in range(world)).astype(np.int32)
             ok.append(bool(np.array_equal(rb.download(), want)))
 
+    t_start = time.perf_counter()
+
+    def note(what):   # progress on stderr (shown with the failure if the test times out)
+        print(f"[gpu_residency r{rank} +{time.perf_counter() - t_start:.2f}s] {what}", file=sys.stderr, flush=True)
+
     for t in range(2):   # warm: the descriptors exist before the hog
         one_round(t)
+    note("warm rounds done")
     side = dev.Stream()
     comm.barrier()
     t_hog = time.perf_counter()
@@ -1841,14 +1849,18 @@ def gpu_residency(rank, world, hog_ms=6000, free_cus=2, rounds=4, counts=(1 << 2
         assert sw.esgd_sweep_occupy(blocks, int(hog_ms * 1000), side.handle) == 0
         time.sleep(0.2)   # resident before the round starts
     comm.barrier()
+    note("hog launched" if rank == 0 else "past the hog barrier")
     for t in range(2, 2 + rounds):
         one_round(t, held=t == 2)
+        note(f"round {t} done in {times[-1]:.3f}s")
     side.synchronize()
     hog_s = time.perf_counter() - t_hog
+    note(f"hog stream synchronized after {hog_s:.2f}s")
     comm.barrier()
     workers = comm.get_config("batch_workers")
     for s_ in scheds:
         s_.delete()
+    note("schedules deleted")
     comm.finalize()
     return {"first_round_s": times[2], "round_s": times, "hog_s": hog_s, "ok": ok, "workers": workers}
 

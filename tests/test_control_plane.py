@@ -79,6 +79,16 @@ def test_majority_activator_is_rand_r(world, seed):
                 assert e["fresh"]
 
 
+@pytest.mark.parametrize("kind", [ALLREDUCE, SOLO])
+def test_wait_on_without_a_gpu_event_falls_back_to_the_host_wait(kind):
+    # esgd_schedule_wait_on on a schedule whose rounds have no GPU event (control only, like
+    # host buckets): the host wait, taken after the poll loop let go of the schedule's mutex
+    # (r05k2: taken inside it, the wait locked the mutex twice and hung)
+    outs = run("cp_rounds", 2, kind=kind, rounds=6, async_=2, wait_on=True, timeout=60)
+    for o in outs:
+        assert o["stats"]["completed"] == 6 and o["stats"]["waited"] == 6, o["stats"]
+
+
 def test_test_polling_equivalent_to_wait():
     outs = run("cp_rounds", 2, kind=SOLO, rounds=6, async_=2, use_test=True)
     for o in outs:
