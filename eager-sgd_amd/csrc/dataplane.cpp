@@ -1326,6 +1326,14 @@ static int batch_desc(Sched &s, IpcState &st, hipStream_t cs) {
         d.stail = uint32_t(bytes % 16);
     }
     d.rbase = st.rb_dev;
+    d.rank = uint32_t(r);
+    {
+        const uint64_t b0 = st.off[r] * es, b1 = (st.off[r] + st.len[r]) * es, total = s.count * es;
+        d.own_v0 = uint32_t(b0 / 16);
+        d.own_v1 = uint32_t(b1 / 16);
+        d.own_tail = (st.len[r] && b1 == total && total % 16) ? 1u : 0u;
+        d.own_off = b0;
+    }
     st.t1 = d.t1;
     st.t2 = std::max<uint32_t>(1, d.t2pre[m]);   // at least one tile: it writes fin
     g_desc_host[s.id] = d;
@@ -1925,6 +1933,7 @@ struct IpcTransport final : Transport {
                 return base_copy_out(s, st, cs);
             }
             ++g_launches;
+            const bool io_direct = st.io_on && !s.host_mode && !st.shadow && !s.wire_bf16;
             if (s.wire_bf16) {
                 if (int rc = wire_phases(s, st, round, fresh, cs)) return rc;
             } else {
@@ -1944,15 +1953,18 @@ struct IpcTransport final : Transport {
                     return rc;
             }
             if (int rc = pair_ranks(s, s.sh->reduced, 1, round, cs)) return rc;
+            // a round with its own output (post_io) gathers straight into it, its own
+            // reduced shard too (one more segment of the same launch): no copy-out
+            char *gbase = io_direct ? static_cast<char *>(st.cur_io.dst) : st.rb_dev;
             const void *src[kMaxSegs];
             void *dst[kMaxSegs];
             uint64_t bytes[kMaxSegs];
             int m = 0;
             for (int j = 0; j < s.world; ++j) {
-                if (j == s.rank) continue;
+                if (j == s.rank && !io_direct) continue;
                 for (uint64_t o = 0; o < st.len[j]; o += piece) {
-                    src[m] = st.peer[j] + (st.off[j] + o) * es;
-                    dst[m] = st.rb_dev + (st.off[j] + o) * es;
+                    src[m] = (j == s.rank ? st.rb_dev : st.peer[j]) + (st.off[j] + o) * es;
+                    dst[m] = gbase + (st.off[j] + o) * es;
                     bytes[m] = std::min(piece, st.len[j] - o) * es;
                     if (++m == kMaxSegs) {
                         if (int rc = gather_remote(m, src, dst, bytes, cs)) return rc;
@@ -1965,7 +1977,7 @@ struct IpcTransport final : Transport {
             }
             // device buckets: the done pairing ends the round and reports it in fin, which
             // the host polls (as for one-launch rounds; the event only reports faults)
-            const bool last = !s.host_mode && !st.shadow && !st.io_on;
+            const bool last = !s.host_mode && !st.shadow && (!st.io_on || io_direct);
             if (int rc = pair_ranks(s, s.sh->done, 2, round, cs, 0, last ? &s.sh->fin[s.rank] : nullptr))
                 return rc;
             if (last) {

@@ -65,6 +65,13 @@ struct BatchDesc {
     // rb itself: `out` and every `gdst` lie in it; a round with its own output
     // (BatchArgs::iout) lands at the same offsets there instead
     void *rbase;
+    // this rank's own shard: only this rank reads it (phase 1), so a snapshot with a source
+    // (rb = src or src / div) skips it and phase 1 reads src there instead -- (P-1)/P of the
+    // snapshot's bytes.  Vectors [own_v0, own_v1) of the bucket, own_tail: the ragged bytes
+    // after the last vector are the own shard's; own_off: its byte offset
+    uint32_t rank;
+    uint32_t own_v0, own_v1, own_tail;
+    uint64_t own_off;
 };
 
 // Kernel arguments: the entries of one launch, in issue-ring order.

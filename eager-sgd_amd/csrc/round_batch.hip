@@ -138,8 +138,11 @@ __device__ void agent(const BatchArgs &a, long long t0) {
 
 // phase 1, tile `local` of an entry: fold the shard's vectors [local * tv1, +tv1) into
 // `out` (the shard in rb, or in the round's own output) and the published shard
+// own: this rank's operand read from the snapshot's source instead of rb (nullptr: rb),
+// divided by div (fp32 kind 3; 1: as it is) -- the value the snapshot would have stored
 template <class Tr, int K>
-__device__ __forceinline__ void tile_reduce(const BatchDesc &d, uint32_t local, void *out) {
+__device__ __forceinline__ void tile_reduce(const BatchDesc &d, uint32_t local, void *out, const void *own,
+                                            float div) {
     using T = typename Tr::T;
     using A = typename Tr::A;
     const uint32_t nvec = uint32_t(d.n / Tr::E);
@@ -147,7 +150,10 @@ __device__ __forceinline__ void tile_reduce(const BatchDesc &d, uint32_t local, 
     __amdgpu_buffer_rsrc_t rs[K];
 #pragma unroll
     for (int j = 0; j < K; ++j)
-        rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(d.src[j]), (short)0, bytes, 0x00020000);
+        rs[j] = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(own && j == int(d.rank) ? own : d.src[j]),
+                                                  (short)0, bytes, 0x00020000);
+    constexpr bool kF32 = sizeof(T) == 4 && Tr::E == 4 && __is_same(T, float);
+    const bool divide = kF32 && own && div != 1.0f;
     const __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t wp = __builtin_amdgcn_make_buffer_rsrc(d.pub, (short)0, bytes, 0x00020000);
     constexpr int U = sizeof(T) == 2 ? 2 : 4;   // vectors per input per lane in flight
@@ -160,6 +166,16 @@ __device__ __forceinline__ void tile_reduce(const BatchDesc &d, uint32_t local, 
 #pragma unroll
             for (int j = 0; j < K; ++j)
                 r[u][j] = __builtin_amdgcn_raw_buffer_load_b128(rs[j], (i + u * 256) * 16, 0, 17);
+        if (divide) {   // the own operand as the snapshot's kind 3 stores it (__fdiv_rn)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int j = 0; j < K; ++j)
+                    if (j == int(d.rank))
+#pragma unroll
+                        for (int c = 0; c < 4; ++c)
+                            r[u][j][c] = __float_as_uint(__fdiv_rn(__uint_as_float(r[u][j][c]), div));
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const raw16 o = fold16<Tr, K, false>(r[u], 1.0f);
@@ -172,9 +188,15 @@ __device__ __forceinline__ void tile_reduce(const BatchDesc &d, uint32_t local, 
         const uint64_t e = uint64_t(nvec) * Tr::E + threadIdx.x;
         A v[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j)
-            v[j] = Tr::load(__hip_atomic_load(static_cast<const T *>(d.src[j]) + e, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_SYSTEM));
+        for (int j = 0; j < K; ++j) {
+            const bool mine = own && j == int(d.rank);
+            T x = __hip_atomic_load(static_cast<const T *>(mine ? own : d.src[j]) + e, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_SYSTEM);
+            if constexpr (kF32) {
+                if (mine && divide) x = __fdiv_rn(x, div);
+            }
+            v[j] = Tr::load(x);
+        }
         tree_fold<Tr, K>(v);
         __hip_atomic_store(static_cast<T *>(out) + e, Tr::store(v[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(static_cast<T *>(d.pub) + e, Tr::store(v[0]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -191,7 +213,15 @@ __device__ __forceinline__ void tile_snapshot(const BatchDesc &d, uint32_t local
     const uint32_t nv = d.svec, v0 = local * 1024u;
     const void *src = isrc ? isrc : d.ssrc;
     const __amdgpu_buffer_rsrc_t wd = __builtin_amdgcn_make_buffer_rsrc(d.sdst, (short)0, int(nv * 16u), 0x00020000);
+    // a sourced snapshot leaves this rank's own shard out: phase 1 reads src there itself
+    const bool skip_own = kind != 2 && src;
     raw16 r[4];
+    bool mine[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t vi = v0 + u * 256 + threadIdx.x;
+        mine[u] = skip_own && vi >= d.own_v0 && vi < d.own_v1;
+    }
     if (kind == 2) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) r[u] = raw16{0u, 0u, 0u, 0u};
@@ -199,7 +229,8 @@ __device__ __forceinline__ void tile_snapshot(const BatchDesc &d, uint32_t local
         const __amdgpu_buffer_rsrc_t rd =
             __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(src), (short)0, int(nv * 16u), 0x00020000);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b128(rd, (v0 + u * 256 + threadIdx.x) * 16, 0, 2);
+        for (int u = 0; u < 4; ++u)
+            if (!mine[u]) r[u] = __builtin_amdgcn_raw_buffer_load_b128(rd, (v0 + u * 256 + threadIdx.x) * 16, 0, 2);
         if (kind == 3) {
 #pragma unroll
             for (int u = 0; u < 4; ++u)
@@ -208,8 +239,9 @@ __device__ __forceinline__ void tile_snapshot(const BatchDesc &d, uint32_t local
         }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(r[u], wd, (v0 + u * 256 + threadIdx.x) * 16, 0, 17);
-    if (local == 0 && threadIdx.x < d.stail) {
+    for (int u = 0; u < 4; ++u)
+        if (!mine[u]) __builtin_amdgcn_raw_buffer_store_b128(r[u], wd, (v0 + u * 256 + threadIdx.x) * 16, 0, 17);
+    if (local == 0 && threadIdx.x < d.stail && !(skip_own && d.own_tail)) {
         if (kind == 3) {   // fp32: the tail holds whole elements
             if (threadIdx.x < d.stail / 4) {
                 const float x = static_cast<const float *>(src)[size_t(nv) * 4 + threadIdx.x];
@@ -310,7 +342,11 @@ __global__ __launch_bounds__(256) void k_round_batch(BatchArgs a) {
         const uint32_t local = t - pre[e];
         // a round with its own output (esgd_schedule_post_io) lands there, at rb's offsets
         const ptrdiff_t shift = a.iout[e] ? static_cast<char *>(a.iout[e]) - static_cast<char *>(d.rbase) : 0;
-        if (!gather) tile_reduce<Tr, K>(d, local, static_cast<char *>(d.out) + shift);
+        // a sourced in-launch snapshot skipped the own shard: its operand comes from the source
+        const uint8_t kind = a.snap[e];
+        const void *ssrc = a.isrc[e] ? a.isrc[e] : d.ssrc;
+        const void *own = (kind == 1 || kind == 3) && ssrc ? static_cast<const char *>(ssrc) + d.own_off : nullptr;
+        if (!gather) tile_reduce<Tr, K>(d, local, static_cast<char *>(d.out) + shift, own, kind == 3 ? a.idiv[e] : 1.0f);
         else tile_gather(d, local, shift);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are in memory
         __syncthreads();

@@ -253,7 +253,8 @@ int esgd_schedule_wait_ex(esgd_sched_h h, int *fresh);
  * or once the round has finished.  Work queued on `stream` afterwards sees the result, as
  * after torch.distributed's Work.wait().  The round's outcome is not known at return: a
  * failure that comes later fails the schedule's next post / wait.  Host buckets wait on the
- * host (as wait_ex). */
+ * host (as wait_ex).  Until the round finishes, esgd_schedule_stats counts it as waited but
+ * not completed. */
 int esgd_schedule_wait_on(esgd_sched_h h, void *stream, int *fresh);
 /* The process's round stream (a hipStream_t; created on first use on the current device):
  * every round of every schedule is queued on it in the node's issue order.  Work a caller
