@@ -1248,6 +1248,15 @@ static uint32_t g_qnext = 0;
 
 // ESGD_BATCH_STATIC=1: static tile assignment in shared launches (an A/B of the dynamic
 // counter; needs every worker resident at once)
+uint32_t batch_workers_max() {
+    static const uint32_t v = [] {
+        const char *e = getenv("ESGD_BATCH_WORKERS");
+        const long n = (e && *e) ? atol(e) : long(kBatchWorkers);
+        return uint32_t(std::max<long>(1, std::min<long>(long(kBatchWorkersMax), n)));
+    }();
+    return v;
+}
+
 static bool batch_static() {
     static const bool on = getenv("ESGD_BATCH_STATIC") && *getenv("ESGD_BATCH_STATIC") == '1';
     return on;
@@ -1293,11 +1302,11 @@ static int batch_desc(Sched &s, IpcState &st, hipStream_t cs) {
     d.out = st.rb_dev + st.off[r] * es;
     d.pub = st.pub;
     d.n = st.len[r];
-    batch_tiling(st.len[r] * es / 16, kBatchWorkers, &d.t1, &d.tv1);
+    batch_tiling(st.len[r] * es / 16, batch_workers_max(), &d.t1, &d.tv1);
     uint32_t m = 0;
     for (int j = 0; j < s.world; ++j)
         if (j != r && st.len[j]) ++m;
-    const uint32_t per_seg = std::max<uint32_t>(1, kBatchWorkers / std::max<uint32_t>(1, m));
+    const uint32_t per_seg = std::max<uint32_t>(1, batch_workers_max() / std::max<uint32_t>(1, m));
     m = 0;
     for (int j = 0; j < s.world; ++j) {
         if (j == r || st.len[j] == 0) continue;
@@ -1386,7 +1395,7 @@ static int batch_flush_locked() {
     a.tile0[n] = t0;
     a.tile1[n] = t1;
     a.tile2[n] = t2;
-    unsigned workers = std::min<unsigned>(kBatchWorkers, std::max<unsigned>(1, std::max(t0, std::max(t1, t2))));
+    unsigned workers = std::min<unsigned>(batch_workers_max(), std::max<unsigned>(1, std::max(t0, std::max(t1, t2))));
     // The launch's rounds complete with the agent and one worker resident (the tile
     // counter), but the stream's next launch starts only once every workgroup of this one
     // was dispatched and left -- so the grid is kept to what the GPU can hold beside the

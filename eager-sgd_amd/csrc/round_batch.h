@@ -23,7 +23,11 @@
 namespace esgd {
 
 constexpr int kBatchMax = 64;          // rounds per launch: one agent lane each
-constexpr uint32_t kBatchWorkers = 64; // worker workgroups at most (k_round_small's grid)
+constexpr uint32_t kBatchWorkers = 64; // worker workgroups at most, by default (k_round_small's grid)
+constexpr uint32_t kBatchWorkersMax = 512;   // ... and with ESGD_BATCH_WORKERS (batch_workers_max())
+// ESGD_BATCH_WORKERS (1..512, default kBatchWorkers): the worker cap of shared launches and
+// of a phase's tiles per entry (dataplane.cpp; read once per process)
+uint32_t batch_workers_max();
 // A phase's tiles of one entry: at most kBatchWorkers (one arrival count each), at least
 // 1024 16-B vectors (one pass of a 256-lane workgroup, 4 vectors per lane) per tile -- a
 // lone entry gets k_round_small's parallelism, a large one few counts.

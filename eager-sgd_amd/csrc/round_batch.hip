@@ -479,7 +479,7 @@ static int launch_batch_t(int world, const BatchArgs &a, unsigned grid, hipStrea
 }
 
 int round_batch(int dtype, int world, const BatchArgs &a, unsigned workers, hipStream_t s) {
-    ESGD_ARG(a.nent >= 1 && a.nent <= uint32_t(kBatchMax) && a.table && workers >= 1 && workers <= kBatchWorkers,
+    ESGD_ARG(a.nent >= 1 && a.nent <= uint32_t(kBatchMax) && a.table && workers >= 1 && workers <= kBatchWorkersMax,
              "batched rounds: %u entries, %u workers", a.nent, workers);
     const unsigned grid = workers + 1;
     switch (dtype) {
