@@ -147,6 +147,20 @@ int esgd_schedule_post_io(esgd_sched_h h, const void *src, void *dst, float divi
     return sched_post(s, producer_stream, role, &io);
 }
 
+int esgd_schedule_post_iov(esgd_sched_h h, int n, const float *const *srcs, float *const *dsts,
+                           const uint64_t *counts, float divisor, void *producer_stream, int *role) {
+    ESGD_ARG(n >= 0 && (n == 0 || (srcs && dsts && counts)), "esgd_schedule_post_iov: bad arguments");
+    Sched *s = handle_to_sched(h);
+    if (!s) return ESGD_INVALID_ARG;
+    auto g = std::make_shared<RoundIOSegs>();
+    g->src.assign(srcs, srcs + n);
+    g->dst.assign(dsts, dsts + n);
+    g->count.assign(counts, counts + n);
+    RoundIO io{nullptr, nullptr, divisor};
+    io.segs = std::move(g);
+    return sched_post(s, producer_stream, role, &io);
+}
+
 int esgd_schedule_post_group_io(const esgd_sched_h *hs, int n, const void *const *srcs, void *const *dsts,
                                 float divisor, void *producer_stream, int *roles) {
     ESGD_ARG(n >= 0 && (n == 0 || (hs && srcs && dsts)), "esgd_schedule_post_group_io: bad arguments");

@@ -911,6 +911,20 @@ int Transport::note_io(Sched &, uint32_t, const RoundIO &) {
 static int base_note_io(Sched &s, BaseState &st, uint32_t round, const RoundIO &io) {
     ESGD_ARG(!s.host_mode && !s.resolve && !s.wire_bf16,
              "schedule %d: a round's own data needs a device schedule without FFCOLL_BUFFERS or WIRE_BF16", s.id);
+    if (io.segs) {   // post_iov: fp32 pieces, any alignment (the pack kernels take it)
+        ESGD_ARG(s.dtype == ESGD_FLOAT, "schedule %d: post_iov needs FLOAT buckets", s.id);
+        ESGD_ARG(io.div == io.div && io.div != 0.0f, "schedule %d: post_iov: bad divisor", s.id);
+        uint64_t total = 0;
+        for (size_t i = 0; i < io.segs->count.size(); ++i) {
+            ESGD_ARG(io.segs->count[i] == 0 || (io.segs->src[i] && io.segs->dst[i]),
+                     "schedule %d: post_iov: piece %zu has a null pointer", s.id, i);
+            total += io.segs->count[i];
+        }
+        ESGD_ARG(total == s.count, "schedule %d: post_iov: %llu elements in the pieces for a %llu-element schedule",
+                 s.id, (unsigned long long)total, (unsigned long long)s.count);
+        st.io[round] = io;
+        return ESGD_SUCCESS;
+    }
     ESGD_ARG(s.count == 0 || (io.src && io.dst), "schedule %d: post_io: null src or dst", s.id);
     ESGD_ARG(((reinterpret_cast<uintptr_t>(io.src) | reinterpret_cast<uintptr_t>(io.dst)) & 15) == 0,
              "schedule %d: post_io: src and dst must be 16-B aligned", s.id);
@@ -935,9 +949,24 @@ static void take_io(BaseState &st, uint32_t round, bool fresh) {
 }
 
 // the copy-in of a round with its own data, queued on the round stream: rb = src / div
+// rb's place of each piece of a post_iov round, in order
+static std::vector<float *> io_pieces_in_rb(const BaseState &st, const RoundIOSegs &g) {
+    std::vector<float *> at(g.count.size());
+    float *p = reinterpret_cast<float *>(st.rb_dev);
+    for (size_t i = 0; i < at.size(); ++i) {
+        at[i] = p;
+        p += g.count[i];
+    }
+    return at;
+}
+
 static int io_copy_in(Sched &s, BaseState &st, hipStream_t cs) {
     const size_t bytes = s.count * s.esize;
     if (!bytes) return ESGD_SUCCESS;
+    if (const RoundIOSegs *g = st.cur_io.segs.get()) {   // the pieces packed into rb (/ div)
+        const std::vector<float *> at = io_pieces_in_rb(st, *g);
+        return pack_scatter(int(at.size()), g->src.data(), at.data(), g->count.data(), st.cur_io.div, cs);
+    }
     if (st.cur_io.div == 1.0f) {
         ESGD_HIP(hipMemcpyAsync(st.rb_dev, st.cur_io.src, bytes, hipMemcpyDeviceToDevice, cs));
         return ESGD_SUCCESS;
@@ -1105,7 +1134,12 @@ static int finish_round(Sched &s, BaseState &st, hipStream_t cs) {
 
 static int base_copy_out(Sched &s, BaseState &st, hipStream_t cs) {
     const size_t bytes = s.count * s.esize;
-    if (st.io_on && bytes) {   // the round's own output (post_io); rb is not the caller's then
+    if (st.io_on && bytes && st.cur_io.segs) {   // post_iov: rb unpacked into the pieces
+        const RoundIOSegs &g = *st.cur_io.segs;
+        const std::vector<float *> at = io_pieces_in_rb(st, g);
+        std::vector<const float *> from(at.begin(), at.end());
+        if (int rc = unpack_gather(int(at.size()), g.dst.data(), from.data(), g.count.data(), cs)) return rc;
+    } else if (st.io_on && bytes) {   // the round's own output (post_io); rb is not the caller's then
         ESGD_HIP(hipMemcpyAsync(st.cur_io.dst, st.rb_dev, bytes, hipMemcpyDeviceToDevice, cs));
     } else if (s.host_mode && bytes) {
         if (staged(s, st)) {
@@ -1896,7 +1930,9 @@ struct IpcTransport final : Transport {
     // pairings, the gather reads the published shards).
     // rounds that go out in a shared k_round_batch launch
     static bool batched(const Sched &s, const IpcState &st) {
+        // (a post_iov round ends with its unpack on the round stream: a launch of its own)
         return one_launch(s) && !s.host_mode && !st.shadow && !s.resolve && batch_rounds() > 1 &&
+               !(st.io_on && st.cur_io.segs) &&
                !gpu_trace_on() && st.len[0] * s.esize <= (uint64_t(1) << 30);
     }
 
@@ -1942,7 +1978,7 @@ struct IpcTransport final : Transport {
                 return base_copy_out(s, st, cs);
             }
             ++g_launches;
-            const bool io_direct = st.io_on && !s.host_mode && !st.shadow && !s.wire_bf16;
+            const bool io_direct = st.io_on && !st.cur_io.segs && !s.host_mode && !st.shadow && !s.wire_bf16;
             if (s.wire_bf16) {
                 if (int rc = wire_phases(s, st, round, fresh, cs)) return rc;
             } else {

@@ -359,6 +359,20 @@ int allreducef_forward_cuda_packed(void *handle, int n, const float *const *grad
     ESGD_ARG(!op->pending, "allreducef_forward_cuda_packed: a split round is posted and not yet waited");
     if (int rc = op->ensure(true)) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (op->io_ok(nullptr, nullptr)) {
+        // the pack (/ divisor) and the unpack are the round's own copy-in and copy-out
+        // (esgd_schedule_post_iov, on the round stream): no send bucket, no kernels on s
+        void *ps = caller_stream(s);
+        if (int rc = esgd_schedule_post_iov(op->sched, n, grads, outs, counts, divisor, ps, nullptr)) return rc;
+        int fresh = 0;
+        if (int rc = esgd_schedule_wait_ex(op->sched, &fresh)) return rc;
+        // a round a peer carried this rank through before the post left its result in rb
+        if (!fresh)
+            if (int rc = esgd_unpack(n, outs, counts, op->rb, ps)) return rc;
+        if (int rc = esgd_schedule_release(op->sched, fresh ? nullptr : ps)) return rc;
+        op->bytes += int64_t(op->len) * int64_t(sizeof(float));
+        return ESGD_SUCCESS;
+    }
     if (int rc = esgd_pack_div(n, grads, counts, op->sb, divisor, caller_stream(s))) return rc;
     return op->device_round(s, [&]() -> int { return esgd_unpack(n, outs, counts, op->rb, caller_stream(s)); });
 }

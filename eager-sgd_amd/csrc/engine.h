@@ -24,6 +24,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -51,10 +52,16 @@ struct Sched;
 // A round's own data (esgd_schedule_post_io): the snapshot reads src / div instead of the
 // send bucket, and the result lands in dst instead of rb -- if the round is joined at or
 // after that post (fresh).
+struct RoundIOSegs {   // esgd_schedule_post_iov: the round's data in pieces (fp32)
+    std::vector<const float *> src;
+    std::vector<float *> dst;
+    std::vector<uint64_t> count;
+};
 struct RoundIO {
     const void *src;
     void *dst;
     float div;
+    std::shared_ptr<const RoundIOSegs> segs = nullptr;   // set: src / dst unused
 };
 
 // Data movement of one round.  A round is joined on the host (activation rules,

@@ -287,6 +287,13 @@ int esgd_schedule_post_io(esgd_sched_h h, const void *src, void *dst, float divi
                           int *role);
 int esgd_schedule_post_group_io(const esgd_sched_h *h, int n, const void *const *srcs, void *const *dsts,
                                 float divisor, void *producer_stream, int *roles);
+/* post_io with the round's data in n fp32 pieces (FLOAT device schedules; counts summing to
+ * the schedule's count; any alignment): a round this rank joins at or after the post packs
+ * srcs[i] / divisor into its bucket in order and, finished, unpacks the result into
+ * dsts[i] (may be srcs[i]) -- the fused optimizer's pack and unpack as part of the round,
+ * on the round stream, with no send bucket in between.  Otherwise as post_io. */
+int esgd_schedule_post_iov(esgd_sched_h h, int n, const float *const *srcs, float *const *dsts,
+                           const uint64_t *counts, float divisor, void *producer_stream, int *role);
 int esgd_schedule_test(esgd_sched_h h, int *flag);
 int esgd_schedule_delete(esgd_sched_h h);
 int esgd_schedule_stats(esgd_sched_h h, esgd_sched_stats_t *out);
