@@ -925,11 +925,12 @@ _OPTS = []
 def _fused_breakdown(comm, opt, params, steps):
     """Where the fused optimizer step's time goes (EagerSGDOptimizer(fuse=True)): each part
     timed alone on this rank, median over `steps`, against the whole step -- the pack of the
-    161 gradients (divided by P) into the bucket and the unpack back (torch events on the
-    caller's stream around one launch group each), the fused bucket's round alone (post ->
-    wait on its schedule, wall, max over ranks), the wrapped SGD step (events), and
-    apply_gradients + synchronize (wall, max over ranks).  The parts' sum against the step
-    is the host / launch overhead between them."""
+    161 gradients (divided by P) into a bucket and the unpack back (torch events on the
+    caller's stream around one launch group each: what the round's own copy-in / copy-out
+    cost), the fused bucket's round alone (post -> wait, wall, max over ranks), the round as
+    the step runs it (esgd_schedule_post_iov: pack + round + unpack on the round stream), the
+    wrapped SGD step (events), and apply_gradients + synchronize (wall, max over ranks).  The
+    step against (round with pack / unpack + SGD) is the host / launch overhead."""
     import statistics
 
     import torch
@@ -965,11 +966,24 @@ def _fused_breakdown(comm, opt, params, steps):
         check(lib().esgd_schedule_wait(h), "wait")
         check(lib().esgd_schedule_release(h, None), "release")
 
+    import ctypes as C
+    n = len(grads)
+    ptrs = _lib.ptr_array([g.data_ptr() for g in grads])
+    cnt = (C.c_uint64 * n)(*counts)
+    sh = stream.cuda_stream or 1   # ESGD_STREAM_NULL: torch's legacy stream
+
+    def one_round_iov():   # what the step's round is: pack (/ P) + round + unpack, on the round stream
+        check(lib().esgd_schedule_post_iov(h, n, ptrs, ptrs, cnt, float(comm.world()), sh, None), "post_iov")
+        check(lib().esgd_schedule_wait(h), "wait")
+        check(lib().esgd_schedule_release(h, None), "release")
+
     rnd = _timed_steps(comm, one_round, steps)
+    rnd_io = _timed_steps(comm, one_round_iov, steps)
     whole = _timed_steps(comm, lambda: (opt.step(), torch.cuda.synchronize()), steps)
-    parts = pack + unpack + sgd + rnd * 1e3
+    parts = sgd + rnd_io * 1e3
     return {"pack_div_gpu": round(pack * 1e3, 1), "round_wall": round(rnd * 1e6, 1),
-            "unpack_gpu": round(unpack * 1e3, 1), "sgd_step_gpu": round(sgd * 1e3, 1),
+            "unpack_gpu": round(unpack * 1e3, 1), "round_with_pack_unpack_wall": round(rnd_io * 1e6, 1),
+            "sgd_step_gpu": round(sgd * 1e3, 1),
             "step_wall": round(whole * 1e6, 1), "parts_sum": round(parts * 1e3, 1),
             "overhead": round((whole * 1e3 - parts) * 1e3, 1), "fp32_elements": total}
 

@@ -46,6 +46,8 @@ def _bind(h):
         "esgd_schedule_wait_ex": (i, [u64, C.POINTER(i)]),
         "esgd_schedule_wait_on": (i, [u64, vp, C.POINTER(i)]),
         "esgd_round_stream": (i, [C.POINTER(vp)]),
+        "esgd_schedule_post_iov": (i, [u64, i, C.POINTER(vp), C.POINTER(vp), C.POINTER(u64), C.c_float, vp,
+                                       C.POINTER(i)]),
         "esgd_schedule_release": (i, [u64, vp]),
         "esgd_schedule_post": (i, [u64, vp, C.POINTER(i)]),
         "esgd_schedule_wait": (i, [u64]),
@@ -251,6 +253,23 @@ class Schedule:
             s = 1   # ESGD_STREAM_NULL
         check(lib().esgd_schedule_post_io(self.handle, as_ptr(src), as_ptr(dst), float(divisor), s, C.byref(role)),
               "esgd_schedule_post_io")
+        return role.value
+
+    def post_iov(self, srcs, dsts, divisor: float = 1.0, stream=None) -> int:
+        """esgd_schedule_post_iov: the round's data in fp32 pieces (tensors / buffers whose
+        sizes sum to the schedule's count): packed (/ divisor) into the bucket and the result
+        unpacked into dsts by the round itself, if this rank joins it at or after this post."""
+        from .device import as_ptr
+        n = len(srcs)
+        counts = (C.c_uint64 * max(1, n))(*[int(x.numel()) if hasattr(x, "numel") else int(x.count)
+                                            for x in srcs])
+        role = C.c_int()
+        s = None if stream is None else (stream.handle if hasattr(stream, "handle") else int(stream))
+        if s == 0:
+            s = 1   # ESGD_STREAM_NULL
+        check(lib().esgd_schedule_post_iov(self.handle, n, _lib.ptr_array([as_ptr(x) for x in srcs]),
+                                           _lib.ptr_array([as_ptr(x) for x in dsts]), counts, float(divisor), s,
+                                           C.byref(role)), "esgd_schedule_post_iov")
         return role.value
 
     def wait(self) -> bool:

@@ -2156,3 +2156,39 @@ def gpu_wait_on_paths(rank, world, rounds=3):
         out[name] = ok
     comm.finalize()
     return out
+
+
+def gpu_post_iov(rank, world, count=4099, rounds=3, in_place=False):
+    """esgd_schedule_post_iov: the round's data in three fp32 pieces (sizes 1, 1000 and the
+    rest; the middle one starting off any 16-B boundary), packed / divisor into the bucket
+    and unpacked into the destinations by the round itself (one-launch rounds: a launch of
+    their own; larger: the five launches) -- the oracle tree of (x_r / P), bit for bit, in
+    every piece, every round."""
+    import numpy as np
+
+    from esgd import device as dev
+    from oracle import ffref
+    comm = _comm()
+    sizes = [1, 1000, count - 1001]
+    sb, rb = dev.DeviceBuffer(count), dev.DeviceBuffer(count)
+    s = comm.Schedule(comm.ALLREDUCE, sb, rb, count, buf=comm.BUF_DEVICE)
+    srcs = [dev.DeviceBuffer(n) for n in sizes]
+    dsts = srcs if in_place else [dev.DeviceBuffer(n) for n in sizes]
+    ok, fresh = [], []
+    for t in range(rounds):
+        xs = [ffref.fill_uniform(0x10F + t, r, count) for r in range(world)]
+        o = 0
+        for b, n in zip(srcs, sizes):
+            b.upload(xs[rank][o:o + n])
+            o += n
+        comm.barrier()
+        s.post_iov(srcs, dsts, float(world))
+        fresh.append(s.wait())
+        got = np.concatenate([b.download() for b in dsts])
+        want = ffref.tree_sum([x / np.float32(world) for x in xs])
+        same = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+        ok.append(same if same else mismatch(t, got, want, xs, s))
+        comm.barrier()
+    s.delete()
+    comm.finalize()
+    return {"ok": ok, "fresh": fresh}

@@ -746,6 +746,18 @@ def test_post_io_round_carried_through_before_the_post(on_stream):
     assert any(not st["fresh"][1] for st in outs[0][1:]), outs[0]   # the late path was taken
 
 
+@pytest.mark.parametrize("count,in_place", [(4099, False), (4099, True), ((1 << 21) + 7, False)],
+                         ids=["one_launch", "one_launch_in_place", "five_launch"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_post_iov_pieces_packed_and_unpacked_by_the_round(world, count, in_place):
+    # the fused optimizer's pack (/ P) and unpack as the round's own copy-in / copy-out
+    # (esgd_schedule_post_iov): the oracle's bits in every piece
+    outs = run("gpu_post_iov", world, count=count, in_place=in_place)
+    for o in outs:
+        assert all(o["ok"]), o["ok"]
+        assert all(o["fresh"]), o["fresh"]
+
+
 def test_wait_on_five_launch_one_launch_and_host_buckets():
     # esgd_schedule_wait_on beyond the shared launches: a five-launch round (its own
     # event), a one-launch round, and host buckets (the host wait fallback); the oracle's
