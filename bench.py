@@ -1630,6 +1630,19 @@ def run_allreduce(args, rank, world):
         _delete_deferred()
         comm.finalize()
     line.update(extras)
+    opt_leg, c4_leg = extras.get("optimizer_resnet50_161"), extras.get("c4_resnet50_161_vs_fused")
+    if isinstance(opt_leg, dict) and isinstance(c4_leg, dict) and c4_leg.get("step_ms_161_buckets_pipelined"):
+        # the drop-in caller path against the data plane beneath it, same job (VERDICT r04
+        # item 2): the bare in-place rounds, and the rounds with the op's schedule properties
+        # (separate send bucket, HOLD, FRESH_ONLY, group calls)
+        bare = c4_leg["step_ms_161_buckets_pipelined"]
+        op_like = (c4_leg.get("op_like_pipelined_variants", {}).get("separate_sb_hold_fresh_group") or {}).get("step_ms")
+        pt = opt_leg.get("per_tensor_pipelined_ms")
+        line["caller_vs_data_plane"] = {
+            "per_tensor_pipelined_ms": pt, "rounds_161_in_place_ms": bare, "rounds_161_op_like_ms": op_like,
+            "per_tensor_over_in_place": round(pt / bare, 3) if pt else None,
+            "per_tensor_over_op_like": round(pt / op_like, 3) if pt and op_like else None,
+            "fused_ms": opt_leg.get("fused_ms")}
     dist.destroy_process_group()
     return line
 
