@@ -948,7 +948,6 @@ static void take_io(BaseState &st, uint32_t round, bool fresh) {
     }
 }
 
-// the copy-in of a round with its own data, queued on the round stream: rb = src / div
 // rb's place of each piece of a post_iov round, in order
 static std::vector<float *> io_pieces_in_rb(const BaseState &st, const RoundIOSegs &g) {
     std::vector<float *> at(g.count.size());
@@ -960,6 +959,7 @@ static std::vector<float *> io_pieces_in_rb(const BaseState &st, const RoundIOSe
     return at;
 }
 
+// the copy-in of a round with its own data, queued on the round stream: rb = src / div
 static int io_copy_in(Sched &s, BaseState &st, hipStream_t cs) {
     const size_t bytes = s.count * s.esize;
     if (!bytes) return ESGD_SUCCESS;
@@ -1856,16 +1856,16 @@ struct IpcTransport final : Transport {
     // A peer's fresh mapping of this rank's publication showed other memory: whatever was
     // published from that chunk moves to a chunk allocated now (a new handle), contents
     // need not move (creation: no round has run).  The caller's own bucket cannot move --
-    // it is shadowed instead, as a bucket in a refused chunk is.  The old chunk stays
-    // exported (never freed), its blocks back on the free lists.
+    // it is shadowed instead, as a bucket in a refused chunk is.  The old block is left
+    // allocated (quarantined): back on the free lists it could carry a later publication
+    // of this rank through the same chunk handle, whose mapping went wrong once.
     int remap(Sched &s, uint32_t which) override {
         IpcState &st = S(s);
         auto move = [&](IpcSlot &slot, char **buf, size_t *cap, size_t bytes, const char *what) -> int {
             char *old = *buf;
             if (int rc = arena_alloc(std::max<size_t>(*cap, 1), reinterpret_cast<void **>(buf), false, true)) return rc;
-            std::fprintf(stderr, "esgd: rank %d schedule %d: %s %p re-published from a new chunk at %p\n", s.rank, s.id,
-                         what, static_cast<void *>(old), static_cast<void *>(*buf));
-            free_bucket(old);
+            std::fprintf(stderr, "esgd: rank %d schedule %d: %s %p re-published from a new chunk at %p (the old "
+                         "block quarantined)\n", s.rank, s.id, what, static_cast<void *>(old), static_cast<void *>(*buf));
             return publish_owned(s, slot, buf, cap, bytes, what);
         };
         // the published shard moves whichever was asked: it may share the suspect chunk
