@@ -462,8 +462,6 @@ int allreducef_forward_cuda_post_many_io(void *const *handles, int n, const floa
 
 namespace {
 
-// on_stream: each round is waited for on the GPU (esgd_schedule_wait_on): stream waits for
-// it, and the call returns once every round is queued instead of finished
 // esgd_schedule_wait_on, remembering across the group the latest shared launch the stream
 // already waits for (one stream wait per shared launch, not per round)
 int wait_on(uint64_t h, void *ps, int *fresh, uint64_t *seen) {
@@ -475,6 +473,8 @@ int wait_on(uint64_t h, void *ps, int *fresh, uint64_t *seen) {
     return esgd::sched_wait_on(s, ps, fresh, seen);
 }
 
+// on_stream: each round is waited for on the GPU (esgd_schedule_wait_on): stream waits for
+// it, and the call returns once every round is queued instead of finished
 int wait_many_impl(void *const *handles, int n, float *const *outputs, void *stream, bool on_stream) {
     ESGD_ARG(n >= 0 && (n == 0 || (handles && outputs)), "allreducef_forward_cuda_wait_many: bad arguments");
     void *ps = caller_stream(static_cast<hipStream_t>(stream));
