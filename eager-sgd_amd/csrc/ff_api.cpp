@@ -235,12 +235,27 @@ struct FFComp {
     bool device = false;
     hipEvent_t ev = nullptr;
     bool posted = false;
+    bool host_done = false;   // a user operator's post ran its function already
 };
 
+// user operators (ffcomp_operator_create): handle FFCUSTOM + slot, as the reference numbers
+// them (ffop_gcomp_operator.c:124-141); a deleted slot is reused
+constexpr int kMaxCustomOps = 64;
+std::mutex g_custom_mu;
+ffoperator_fun_t g_custom[kMaxCustomOps] = {};
+
+ffoperator_fun_t custom_fun(int op) {
+    if (op < FFCUSTOM || op >= FFCUSTOM + kMaxCustomOps) return nullptr;
+    std::lock_guard<std::mutex> lk(g_custom_mu);
+    return g_custom[op - FFCUSTOM];
+}
+
 int comp_make(FFComp *o, ffop_h *out) {
-    ESGD_ARG(o->op == FFSUM || o->op == FFIDENTITY,
-             "ffcomp: operator %d -- libesgd runs FFSUM and FFIDENTITY (custom operators are host "
-             "functions, not GPU code: DESIGN.md §8)", o->op);
+    const bool custom = custom_fun(o->op) != nullptr;
+    ESGD_ARG(o->op == FFSUM || o->op == FFIDENTITY || custom,
+             "ffcomp: operator %d -- FFSUM, FFIDENTITY or a handle from ffcomp_operator_create", o->op);
+    ESGD_ARG(!custom || !o->device,
+             "ffcomp: a user operator is a host function: host buffers only (not ESGD_FF_DEVICE_BUFFERS)");
     ESGD_ARG(esgd_dtype_size(o->dtype) > 0, "ffcomp: unsupported datatype %d", o->dtype);
     *out = reinterpret_cast<ffop_h>(o);
     return FFSUCCESS;
@@ -275,13 +290,26 @@ int ffcomp_b(ffbuffer_h b1, ffbuffer_h b2, ffoperator_h op, int options, ffbuffe
     return FFSUCCESS;
 }
 
-int ffcomp_operator_create(ffoperator_fun_t, int, ffoperator_h *) {
-    esgd::set_error("ffcomp_operator_create: custom operators are host functions and do not run on the GPU "
-                    "path (DESIGN.md §8)");
-    return FFINVALID_ARG;
+int ffcomp_operator_create(ffoperator_fun_t fun, int, ffoperator_h *handle) {
+    ESGD_ARG(fun && handle, "ffcomp_operator_create: null function or handle");
+    std::lock_guard<std::mutex> lk(g_custom_mu);
+    for (int i = 0; i < kMaxCustomOps; ++i)
+        if (!g_custom[i]) {
+            g_custom[i] = fun;
+            *handle = FFCUSTOM + i;
+            return FFSUCCESS;
+        }
+    esgd::set_error("ffcomp_operator_create: more than %d user operators", kMaxCustomOps);
+    return FFENOMEM;
 }
 
-int ffcomp_operator_delete(ffoperator_h) { return FFINVALID_ARG; }
+int ffcomp_operator_delete(ffoperator_h handle) {
+    std::lock_guard<std::mutex> lk(g_custom_mu);
+    ESGD_ARG(handle >= FFCUSTOM && handle < FFCUSTOM + kMaxCustomOps && g_custom[handle - FFCUSTOM],
+             "ffcomp_operator_delete: %d is not a user operator", handle);
+    g_custom[handle - FFCUSTOM] = nullptr;
+    return FFSUCCESS;
+}
 
 int ffop_post(ffop_h h) {
     auto *o = reinterpret_cast<FFComp *>(h);
@@ -291,6 +319,16 @@ int ffop_post(ffop_h h) {
     int64_t n = o->ba ? int64_t(o->ba->count) : int64_t(o->count);
     if (o->bb) n = std::min<int64_t>(n, o->bb->count);
     if (o->bc) n = std::min<int64_t>(n, o->bc->count);
+    if (const ffoperator_fun_t fun = custom_fun(o->op)) {
+        // the user's host function over the host buffers, now (ffop_gcomp.c:52-55): the op
+        // is complete when the post returns, and the function's status is the post's
+        const int rc = fun(a, b, c, uint32_t(std::max<int64_t>(n, 0)), o->dtype);
+        if (rc != FFSUCCESS) return rc;
+        o->posted = true;
+        o->host_done = true;
+        return FFSUCCESS;
+    }
+    o->host_done = false;
     if (!o->ev) ESGD_HIP(hipEventCreateWithFlags(&o->ev, hipEventDisableTiming));
     hipStream_t s = default_stream();
     if (n > 0) {
@@ -311,7 +349,7 @@ int ffop_post(ffop_h h) {
 int ffop_wait(ffop_h h) {
     auto *o = reinterpret_cast<FFComp *>(h);
     ESGD_ARG(o && o->posted, "ffop_wait: op not posted");
-    ESGD_HIP(hipEventSynchronize(o->ev));
+    if (!o->host_done) ESGD_HIP(hipEventSynchronize(o->ev));
     o->posted = false;
     return FFSUCCESS;
 }
@@ -319,7 +357,7 @@ int ffop_wait(ffop_h h) {
 int ffop_test(ffop_h h, int *flag) {
     auto *o = reinterpret_cast<FFComp *>(h);
     ESGD_ARG(o && flag, "ffop_test: null argument");
-    if (!o->posted) { *flag = 1; return FFSUCCESS; }
+    if (!o->posted || o->host_done) { *flag = 1; o->posted = false; return FFSUCCESS; }
     const hipError_t e = hipEventQuery(o->ev);
     if (e == hipErrorNotReady) { *flag = 0; return FFSUCCESS; }
     if (e != hipSuccess) return hip_fail(e, "ffop_test", __FILE__, __LINE__);

@@ -48,6 +48,8 @@ extern "C" {
 #define FFMAX 2
 #define FFMIN 3
 #define FFIDENTITY 4
+#define FFOPERATOR_SENTINEL 5
+#define FFCUSTOM 6                         /* first user operator handle (src/ff.h:41) */
 
 /* options used by collective callers (src/ff.h:43-58) */
 #define FFCOLL_BUFFERS (1 << 7)
@@ -101,8 +103,12 @@ int ffschedule_post_stream(ffschedule_h sched, void *stream);
  * once over MIN(count1, count2, count3) elements (src/components/gcomp/ffop_gcomp.c:29-64):
  * FFSUM c = a + b, FFIDENTITY c = a (b may be NULL).  Host buffers (the reference's); with
  * ESGD_FF_DEVICE_BUFFERS device buffers.  ffcomp_b takes ffbuffer_h descriptors and re-reads
- * them at every post.  Other operators and ffcomp_operator_create (user host functions)
- * return FFINVALID_ARG: no host compute path exists here. */
+ * them at every post.  User operators (ffcomp_operator_create: a host function, handles
+ * FFCUSTOM + i, src/components/gcomp/ffop_gcomp_operator.c:124-141) run as the reference runs
+ * them -- the function itself, on the host, over host buffers, once per post
+ * (ffop_gcomp.c:52-55; its status is the post's) -- and are refused with device buffers and
+ * by the allreduce schedules, whose GPU reductions are FFSUM.  FFPROD / FFMAX
+ * / FFMIN have no implementation in the reference either: FFINVALID_ARG. */
 int ffcomp(void *addr1, void *addr2, int count, ffdatatype_h datatype, ffoperator_h ffoperator, int options,
            void *addr3, ffop_h *op);
 int ffcomp_b(ffbuffer_h buffer1, ffbuffer_h buffer2, ffoperator_h ffoperator, int options, ffbuffer_h buffer3,

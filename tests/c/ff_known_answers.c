@@ -41,6 +41,15 @@ static int check_int(const int32_t *got, const int32_t *want, int n, const char 
 }
 
 /* simple_computation.c on the GPU kernel, every rank on its own */
+/* custom_computation.c:12-24 */
+static int plus_one(void *a, void *b, void *c, uint32_t count, ffdatatype_h type) {
+    const int32_t *ia = (const int32_t *)a, *ib = (const int32_t *)b;
+    int32_t *ic = (int32_t *)c;
+    (void)type;
+    for (uint32_t i = 0; i < count; ++i) ic[i] = (int32_t)((uint32_t)ia[i] + (uint32_t)ib[i] + 1u);   /* wraps */
+    return FFSUCCESS;
+}
+
 static int single_computations(int count) {
     int32_t *a = malloc(count * sizeof(int32_t)), *b = malloc(count * sizeof(int32_t)),
             *c = calloc(count, sizeof(int32_t)), *w = malloc(count * sizeof(int32_t));
@@ -84,8 +93,20 @@ static int single_computations(int count) {
     if (check_int(c, w, m, "ffcomp_b MIN(counts)", 0)) return 1;
     for (int i = m; i < count; ++i) if (c[i] != -7) { fprintf(stderr, "ffcomp_b wrote past MIN(counts)\n"); return 1; }
     ffbuffer_delete(ba); ffbuffer_delete(bb); ffbuffer_delete(bc);
+    /* evaluation/custom_computation.c: a user operator c = a + b + 1, run on the host
+     * buffers once per post; a null function is refused */
     ffoperator_h custom;
     if (ffcomp_operator_create(NULL, 1, &custom) != FFINVALID_ARG) return 1;
+    if (ffcomp_operator_create(plus_one, 1, &custom) != FFSUCCESS || custom < FFCUSTOM) return 1;
+    if (ffcomp(a, b, count, FFINT32, custom, 0, c, &op) != FFSUCCESS || ffop_post(op) != FFSUCCESS ||
+        ffop_wait(op) != FFSUCCESS) return 1;
+    ffop_free(op);
+    for (int i = 0; i < count; ++i)
+        if (c[i] != (int32_t)((uint32_t)a[i] + (uint32_t)b[i] + 1u)) {
+            fprintf(stderr, "custom operator: c[%d] = %d\n", i, c[i]);
+            return 1;
+        }
+    if (ffcomp_operator_delete(custom) != FFSUCCESS) return 1;
     free(a); free(b); free(c); free(w); free(fa); free(fb); free(fc);
     return 0;
 }
