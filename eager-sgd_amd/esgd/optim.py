@@ -57,7 +57,7 @@ class EagerSGDOptimizer:
     def __init__(self, optimizer, comm_size: int, mode: str = "solo", async_: int = 32,
                  seed: int = 6545343, fuse: bool = False, wire: str = "fp32",
                  pipeline: bool = True, fused_io: bool = True, side_stream: bool = True,
-                 stream_wait: bool = False, round_stream: bool = False):
+                 stream_wait: bool = False, round_stream: bool = False, overlap: bool = False):
         if mode not in deep500.MODES:
             raise ValueError(f"mode must be one of {sorted(deep500.MODES)}")
         if wire not in deep500.WIRES:
@@ -90,6 +90,15 @@ class EagerSGDOptimizer:
         # between queues, one hardware queue fewer per process than the side stream
         self.round_stream = bool(round_stream)
         self._rs = None
+        # overlap=True: every tensor's round is posted from a post-accumulate-grad hook, as
+        # soon as backward has written that gradient -- the way TF's dataflow runs the
+        # reference's ops as their inputs become ready -- and apply_gradients waits for them
+        # (one backward per step; not with fuse=True)
+        self.overlap = bool(overlap) and not self.fuse
+        self._bwd = []          # (op, grad, param) posted by the hooks since the last step
+        self._hooks = []
+        if self.overlap:
+            self._attach()
         self._side = None
         self.wire = wire        # "bf16": bf16 copies between ranks
         self._ops = {}          # parameter -> op instance (one bucket per tensor)
@@ -145,6 +154,36 @@ class EagerSGDOptimizer:
             global_step.add_(1)
         return r
 
+    def _attach(self):
+        for group in self.optimizer.param_groups:
+            for p in group["params"]:
+                if p.requires_grad:
+                    self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def _on_grad(self, p):
+        """Backward has accumulated p.grad: post its round now (read grad / P, result back
+        into grad), ordered after the backward's stream.  A gradient the fused round I/O cannot
+        take (not fp32 contiguous and 16-B aligned) waits for apply_gradients."""
+        import torch
+        g = p.grad
+        if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.data_ptr() % 16:
+            return
+        if not self._configured:
+            deep500.configure(self.mode, self.async_, self.seed, self.wire)
+            self._configured = True
+        op = self._ops.get(p)
+        if op is None:
+            op = self._ops[p] = deep500.AllreduceOp(tuple(g.shape))
+        deep500.AllreduceOp.post_many_io([op], [g], [g], self.comm_size, torch.cuda.current_stream().cuda_stream)
+        self._bwd.append((op, g, p))
+
+    def detach(self):
+        """Remove the overlap hooks (posts go back to apply_gradients)."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        self.overlap = False
+
     def _reduce(self, gvs, stream):
         """The ops' rounds over every gradient, results back in p.grad; returns the
         gradients it had to replace (converted to contiguous fp32 and back)."""
@@ -153,6 +192,18 @@ class EagerSGDOptimizer:
         if self.fuse:
             self._apply_fused(gvs, stream, made)
         else:
+            early, self._bwd = self._bwd, []
+            if early:   # posted by the backward hooks (overlap): wait for those first
+                done = {id(p) for _, _, p in early}
+                err = None
+                try:
+                    deep500.AllreduceOp.wait_many([o for o, _, _ in early], [g for _, g, _ in early], stream,
+                                                  on_stream=self.stream_wait)
+                except Exception as e:   # noqa: BLE001 -- re-raised after the rest
+                    err = e
+                gvs = [(g, v) for g, v in gvs if id(v) not in done]
+                if err is not None:
+                    raise err
             posted = []
             for grad, var in reversed(gvs):
                 if grad is None:      # the reference would still feed None (:35-42); skip

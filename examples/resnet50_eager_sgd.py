@@ -73,6 +73,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", choices=["solo", "majority", "allreduce", "ddp"], default="solo")
     ap.add_argument("--fuse", action="store_true", help="eager-SGD: one fused bucket per step")
+    ap.add_argument("--overlap", action="store_true",
+                    help="eager-SGD per tensor: post each tensor's round from its gradient hook during backward")
     ap.add_argument("--wire", choices=["fp32", "bf16"], default="fp32",
                     help="eager-SGD: what the ranks exchange (bf16: fp32 buckets, bf16 copies on the wire)")
     ap.add_argument("--steps", type=int, default=20)
@@ -124,7 +126,8 @@ def main():
     model = resnet50().to(dev)
     params = [p for p in model.parameters() if p.requires_grad]
     sgd = torch.optim.SGD(params, lr=0.1, momentum=0.9)
-    opt = sgd if a.mode == "ddp" else EagerSGDOptimizer(sgd, world, mode=a.mode, fuse=a.fuse, wire=a.wire)
+    opt = sgd if a.mode == "ddp" else EagerSGDOptimizer(sgd, world, mode=a.mode, fuse=a.fuse, wire=a.wire,
+                                                        overlap=a.overlap)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     x = torch.randn(a.batch, 3, a.image, a.image, device=dev, generator=g)
     y = torch.randint(0, 1001, (a.batch,), device=dev, generator=g)
@@ -186,6 +189,7 @@ def main():
         print(json.dumps({
             "model": "resnet50 (1001 classes)", "tensors": len(params),
             "parameters": sum(p.numel() for p in params), "mode": a.mode, "fuse": a.fuse, "wire": a.wire,
+            "overlap": a.overlap,
             "world": world, "batch_per_rank": a.batch, "image": a.image, "dtype": "f32",
             "data": "synthetic", "straggler_delay_s": a.delay, "steps": a.steps,
             "step_ms_median": round(statistics.median(times) * 1e3, 2),

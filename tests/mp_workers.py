@@ -562,6 +562,10 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp3
     dev = torch.device("cuda", local_device())
     torch.cuda.set_device(dev)
     model = torch.nn.Sequential(torch.nn.Linear(64, 48), torch.nn.ReLU(), torch.nn.Linear(48, 10)).to(dev)
+    captured = {}
+    if opt_kw.get("overlap"):   # the local gradients, taken before the optimizer's hooks post them
+        for prm in model.parameters():
+            prm.register_post_accumulate_grad_hook(lambda q: captured.__setitem__(id(q), q.grad.detach().clone()))
     opt = EagerSGDOptimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9), world, mode=mode,
                             fuse=fuse, wire=wire, pipeline=pipeline, fused_io=fused_io, **opt_kw)
     ok = []
@@ -572,7 +576,10 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp3
         opt.zero_grad()
         loss = torch.nn.functional.cross_entropy(model(x), y)
         gvs = opt.compute_gradients(loss)
-        local = [(gr.detach().float() / world).cpu().numpy().ravel() for gr, _ in gvs]
+        if captured:   # the rounds posted in backward may have written p.grad already
+            local = [(captured[id(p)].float() / world).cpu().numpy().ravel() for _, p in gvs]
+        else:
+            local = [(gr.detach().float() / world).cpu().numpy().ravel() for gr, _ in gvs]
         allg = [None] * world
         dist.all_gather_object(allg, local)
         comm.barrier()

@@ -66,6 +66,18 @@ def test_eager_sgd_optimizer(mode, variant):
         assert outs[0]["params_digest"] == outs[1]["params_digest"]
 
 
+@pytest.mark.parametrize("wait", ["host_wait", "stream_wait"])
+def test_eager_sgd_optimizer_rounds_posted_during_backward(wait):
+    # overlap=True: each tensor's round posted from its post-accumulate-grad hook while
+    # backward still runs (TF's dataflow order for the reference's ops), waited for in
+    # apply_gradients -- the same rounds, so the oracle's bits and identical replicas
+    outs = run("optimizer_step", 2, mode="allreduce", steps=3, overlap=True, stream_wait=wait == "stream_wait")
+    for o in outs:
+        assert all(o["ok"]) and o["ok"], o["ok"]
+        assert o["bytes"] > 0
+    assert outs[0]["params_digest"] == outs[1]["params_digest"]
+
+
 @pytest.mark.parametrize("fuse", [False, True])
 @pytest.mark.parametrize("mode", ["allreduce", "solo", "majority"])
 def test_eager_sgd_optimizer_wire_bf16(mode, fuse):

@@ -36,15 +36,20 @@ def _run(world, *args):
     return out
 
 
-def test_resnet50_synchronous_rounds_keep_ranks_identical():
-    out = _run(2, "--mode", "allreduce", "--steps", "3", "--delay", "0")
+@pytest.mark.parametrize("overlap", [False, True], ids=["after_backward", "during_backward"])
+def test_resnet50_synchronous_rounds_keep_ranks_identical(overlap):
+    # overlap: the 161 rounds posted from the gradient hooks while backward runs
+    out = _run(2, "--mode", "allreduce", "--steps", "3", "--delay", "0", *(["--overlap"] if overlap else []))
     assert out["weights_identical_on_every_rank"], out
 
 
-@pytest.mark.parametrize("mode,fuse", [("solo", True), ("majority", False)])
-def test_resnet50_eager_sgd_with_stragglers(mode, fuse):
+@pytest.mark.parametrize("mode,fuse,overlap", [("solo", True, False), ("majority", False, False),
+                                               ("solo", False, True)])
+def test_resnet50_eager_sgd_with_stragglers(mode, fuse, overlap):
     # up to two drawn ranks sleep before each forward pass; the job runs through, and the
-    # replicas stay identical: a partial round gives every rank the same sum
-    out = _run(2, "--mode", mode, "--steps", "4", "--delay", "0.05", *(["--fuse"] if fuse else []))
+    # replicas stay identical: a partial round gives every rank the same sum (overlap: the
+    # rounds posted from the gradient hooks during backward)
+    out = _run(2, "--mode", mode, "--steps", "4", "--delay", "0.05", *(["--fuse"] if fuse else []),
+               *(["--overlap"] if overlap else []))
     assert out["images_per_s"] > 0, out
     assert out["weights_identical_on_every_rank"], out
