@@ -57,7 +57,8 @@ class EagerSGDOptimizer:
     def __init__(self, optimizer, comm_size: int, mode: str = "solo", async_: int = 32,
                  seed: int = 6545343, fuse: bool = False, wire: str = "fp32",
                  pipeline: bool = True, fused_io: bool = True, side_stream: bool = True,
-                 stream_wait: bool = False, round_stream: bool = False, overlap: bool = False):
+                 stream_wait: bool = False, round_stream: bool = False, overlap: bool = False,
+                 overlap_group: int = 16):
         if mode not in deep500.MODES:
             raise ValueError(f"mode must be one of {sorted(deep500.MODES)}")
         if wire not in deep500.WIRES:
@@ -95,6 +96,11 @@ class EagerSGDOptimizer:
         # reference's ops as their inputs become ready -- and apply_gradients waits for them
         # (one backward per step; not with fuse=True)
         self.overlap = bool(overlap) and not self.fuse
+        # the hooks post in groups of this many tensors (one call, one producer event each):
+        # a post per tensor from Python cost ~15 us of host time apiece, on the backward's
+        # host path (r05t)
+        self.overlap_group = max(1, int(overlap_group))
+        self._ready = []        # (op, grad, param) whose gradient exists, not yet posted
         self._bwd = []          # (op, grad, param) posted by the hooks since the last step
         self._hooks = []
         if self.overlap:
@@ -174,8 +180,16 @@ class EagerSGDOptimizer:
         op = self._ops.get(p)
         if op is None:
             op = self._ops[p] = deep500.AllreduceOp(tuple(g.shape))
-        deep500.AllreduceOp.post_many_io([op], [g], [g], self.comm_size, torch.cuda.current_stream().cuda_stream)
-        self._bwd.append((op, g, p))
+        self._ready.append((op, g, p))
+        if len(self._ready) >= self.overlap_group:
+            self._post_ready(torch.cuda.current_stream().cuda_stream)
+
+    def _post_ready(self, stream):
+        group, self._ready = self._ready, []
+        if group:
+            self._bwd.extend(group)   # waited for in apply_gradients even if the post failed part-way
+            deep500.AllreduceOp.post_many_io([o for o, _, _ in group], [g for _, g, _ in group],
+                                             [g for _, g, _ in group], self.comm_size, stream)
 
     def detach(self):
         """Remove the overlap hooks (posts go back to apply_gradients)."""
@@ -192,6 +206,8 @@ class EagerSGDOptimizer:
         if self.fuse:
             self._apply_fused(gvs, stream, made)
         else:
+            if self._ready:   # the hooks' last, partial group
+                self._post_ready(stream)
             early, self._bwd = self._bwd, []
             if early:   # posted by the backward hooks (overlap): wait for those first
                 done = {id(p) for _, _, p in early}
