@@ -105,6 +105,10 @@ struct AllreduceOp {
     // is read by the round itself and, if the round takes it, the result lands in io_out
     bool io_posted = false;
     float *io_out = nullptr;
+    // a split packed round (allreducef_forward_cuda_packed_post): the pieces' outputs and
+    // counts, for the copy-out of a round that did not take them
+    std::vector<float *> pk_out;
+    std::vector<uint64_t> pk_count;
 
     // the fused path fits: device op, fp32 wire, 16-B aligned tensors
     bool io_ok(const float *in, const float *out) const {
@@ -375,6 +379,51 @@ int allreducef_forward_cuda_packed(void *handle, int n, const float *const *grad
     }
     if (int rc = esgd_pack_div(n, grads, counts, op->sb, divisor, caller_stream(s))) return rc;
     return op->device_round(s, [&]() -> int { return esgd_unpack(n, outs, counts, op->rb, caller_stream(s)); });
+}
+
+int allreducef_forward_cuda_packed_post(void *handle, int n, const float *const *grads, const uint64_t *counts,
+                                        float *const *outs, float divisor, void *stream) {
+    auto *op = static_cast<AllreduceOp *>(handle);
+    ESGD_ARG(op && n >= 0 && (n == 0 || (grads && counts && outs)), "allreducef_forward_cuda_packed_post: bad arguments");
+    ESGD_ARG(divisor == divisor && divisor != 0.0f, "allreducef_forward_cuda_packed_post: bad divisor");
+    ESGD_ARG(!op->pending, "allreducef_forward_cuda_packed_post: the previous round was not waited");
+    uint64_t total = 0;
+    for (int i = 0; i < n; ++i) total += counts[i];
+    ESGD_ARG(total == op->len, "allreducef_forward_cuda_packed_post: %llu elements for a %llu-element op",
+             (unsigned long long)total, (unsigned long long)op->len);
+    if (int rc = op->ensure(true)) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    void *ps = caller_stream(s);
+    op->pk_out.assign(outs, outs + n);
+    op->pk_count.assign(counts, counts + n);
+    if (op->io_ok(nullptr, nullptr)) {   // the round packs and unpacks the pieces itself
+        if (int rc = esgd_schedule_post_iov(op->sched, n, grads, outs, counts, divisor, ps, nullptr)) return rc;
+        op->io_posted = true;
+    } else {                             // bf16 wire: packed into the send bucket first
+        if (int rc = esgd_pack_div(n, grads, counts, op->sb, divisor, ps)) return rc;
+        if (int rc = op->post_round(s)) return rc;
+        op->io_posted = false;
+    }
+    op->pending = true;
+    return ESGD_SUCCESS;
+}
+
+int allreducef_forward_cuda_packed_wait(void *handle, void *stream) {
+    auto *op = static_cast<AllreduceOp *>(handle);
+    ESGD_ARG(op && op->pending, "allreducef_forward_cuda_packed_wait: no round posted");
+    op->pending = false;
+    void *ps = caller_stream(static_cast<hipStream_t>(stream));
+    int fresh = 0;
+    if (int rc = esgd_schedule_wait_ex(op->sched, &fresh)) return rc;
+    const bool in_place = op->io_posted && fresh;   // the round unpacked into the outputs itself
+    op->io_posted = false;
+    int rc = ESGD_SUCCESS;
+    if (!in_place)
+        rc = esgd_unpack(int(op->pk_out.size()), op->pk_out.data(), op->pk_count.data(), op->rb, ps);
+    const int rr = esgd_schedule_release(op->sched, in_place ? nullptr : ps);   // released even after a failure
+    if (!rc) rc = rr;
+    if (!rc) op->bytes += int64_t(op->len) * int64_t(sizeof(float));
+    return rc;
 }
 
 int allreducef_forward_cuda_post(void *handle, const float *input, float divisor, void *stream) {

@@ -60,6 +60,11 @@ def _bind(h):
     h.allreducef_forward_cuda_post_many.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), C.c_float, vp]
     h.allreducef_forward_cuda_wait_many.restype = C.c_int
     h.allreducef_forward_cuda_wait_many.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), vp]
+    h.allreducef_forward_cuda_packed_post.restype = C.c_int
+    h.allreducef_forward_cuda_packed_post.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(C.c_uint64),
+                                                      C.POINTER(vp), C.c_float, vp]
+    h.allreducef_forward_cuda_packed_wait.restype = C.c_int
+    h.allreducef_forward_cuda_packed_wait.argtypes = [vp, vp]
     h.allreducef_forward_cuda_wait_many_on.restype = C.c_int
     h.allreducef_forward_cuda_wait_many_on.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), vp]
     h.allreducef_forward_cuda_post_many_io.restype = C.c_int
@@ -146,6 +151,22 @@ class AllreduceOp:
         _lib.check(lib().allreducef_forward_cuda_packed(self.handle, n, src, counts, dst, float(divisor),
                                                         stream), "allreducef_forward_cuda_packed")
         return outs
+
+    def post_packed(self, grads, outs, divisor: float = 1.0, stream: int | None = None):
+        """First half of forward_cuda_packed (allreducef_forward_cuda_packed_post): the round
+        of the fused bucket posted with the pieces as its own data; wait_packed() finishes it.
+        The tensors must stay alive until then.  Raises EsgdError."""
+        from .device import as_ptr
+        n = len(grads)
+        counts = (C.c_uint64 * max(1, n))(*[int(g.numel()) for g in grads])
+        _lib.check(lib().allreducef_forward_cuda_packed_post(self.handle, n, _lib.ptr_array([as_ptr(g) for g in grads]),
+                                                             counts, _lib.ptr_array([as_ptr(o) for o in outs]),
+                                                             float(divisor), stream),
+                   "allreducef_forward_cuda_packed_post")
+
+    def wait_packed(self, stream: int | None = None):
+        """Second half: wait for the fused bucket's round (results in the outputs)."""
+        _lib.check(lib().allreducef_forward_cuda_packed_wait(self.handle, stream), "allreducef_forward_cuda_packed_wait")
 
     def post_cuda(self, grad, divisor: float = 1.0, stream: int | None = None):
         """First half of forward_cuda_div: queue the copy-in (divided) and post the round,

@@ -58,7 +58,7 @@ class EagerSGDOptimizer:
                  seed: int = 6545343, fuse: bool = False, wire: str = "fp32",
                  pipeline: bool = True, fused_io: bool = True, side_stream: bool = True,
                  stream_wait: bool = False, round_stream: bool = False, overlap: bool = False,
-                 overlap_group: int = 16):
+                 overlap_group: int = 16, bucket_mb: float = 25.0):
         if mode not in deep500.MODES:
             raise ValueError(f"mode must be one of {sorted(deep500.MODES)}")
         if wire not in deep500.WIRES:
@@ -94,8 +94,17 @@ class EagerSGDOptimizer:
         # overlap=True: every tensor's round is posted from a post-accumulate-grad hook, as
         # soon as backward has written that gradient -- the way TF's dataflow runs the
         # reference's ops as their inputs become ready -- and apply_gradients waits for them
-        # (one backward per step; not with fuse=True)
-        self.overlap = bool(overlap) and not self.fuse
+        # (one backward per step).  With fuse=True the gradients go in buckets of about
+        # bucket_mb MiB (reversed parameter order, the order backward produces them), one
+        # fused round per bucket, posted once its last gradient exists
+        self.overlap = bool(overlap)
+        self.bucket_mb = float(bucket_mb)
+        self._buckets = None    # fuse + overlap: [[param, ...], ...] in reversed order
+        self._bucket_of = {}    # id(param) -> bucket index
+        self._bucket_ops = []   # one AllreduceOp per bucket (created at its first post)
+        self._bucket_left = []  # gradients each bucket still waits for in this backward
+        self._bucket_posted = []
+        self._conv = []         # (param, its gradient, the fp32 copy the bucket reduces)
         # the hooks post in groups of this many tensors (one call, one producer event each):
         # a post per tensor from Python cost ~15 us of host time apiece, on the backward's
         # host path (r05t)
@@ -161,16 +170,65 @@ class EagerSGDOptimizer:
         return r
 
     def _attach(self):
-        for group in self.optimizer.param_groups:
-            for p in group["params"]:
-                if p.requires_grad:
-                    self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        params = [p for group in self.optimizer.param_groups for p in group["params"] if p.requires_grad]
+        if self.fuse:
+            cap = max(1.0, self.bucket_mb * (1 << 20))
+            self._buckets, cur, size = [], [], 0
+            for p in reversed(params):
+                cur.append(p)
+                size += p.numel() * 4
+                if size >= cap:
+                    self._buckets.append(cur)
+                    cur, size = [], 0
+            if cur:
+                self._buckets.append(cur)
+            self._bucket_of = {id(p): b for b, bk in enumerate(self._buckets) for p in bk}
+            self._bucket_ops = [None] * len(self._buckets)
+            self._bucket_posted = [False] * len(self._buckets)
+            self._bucket_left = [len(bk) for bk in self._buckets]
+        for p in params:
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def _post_bucket(self, b, stream, made=None):
+        """The fused round of bucket b, its pieces the parameters' gradients (converted to
+        contiguous fp32 if they are not: only from apply_gradients, `made` given)."""
+        import torch
+        bk = self._buckets[b]
+        gs = []
+        for p in bk:
+            g = p.grad
+            if g is None:
+                raise RuntimeError("EagerSGDOptimizer(fuse=True, overlap=True): a parameter of a bucket has no "
+                                   "gradient, but the bucket's schedule is persistent")
+            if g.dtype != torch.float32 or not g.is_contiguous():
+                if made is None:
+                    return False   # apply_gradients posts it
+                g32 = g.float().contiguous()
+                self._conv.append((p, g, g32))   # written back after the wait
+                g = g32
+            gs.append(g)
+        if not self._configured:
+            deep500.configure(self.mode, self.async_, self.seed, self.wire)
+            self._configured = True
+        if self._bucket_ops[b] is None:
+            self._bucket_ops[b] = deep500.AllreduceOp((sum(g.numel() for g in gs),))
+        self._bucket_ops[b].post_packed(gs, gs, self.comm_size, stream)
+        self._bucket_posted[b] = True
+        return True
 
     def _on_grad(self, p):
         """Backward has accumulated p.grad: post its round now (read grad / P, result back
         into grad), ordered after the backward's stream.  A gradient the fused round I/O cannot
-        take (not fp32 contiguous and 16-B aligned) waits for apply_gradients."""
+        take (not fp32 contiguous and 16-B aligned) waits for apply_gradients.  fuse=True: the
+        bucket's round once its last gradient is there."""
         import torch
+        if self.fuse:
+            b = self._bucket_of.get(id(p))
+            if b is not None and not self._bucket_posted[b]:
+                self._bucket_left[b] -= 1
+                if self._bucket_left[b] == 0:
+                    self._post_bucket(b, torch.cuda.current_stream().cuda_stream)
+            return
         g = p.grad
         if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.data_ptr() % 16:
             return
@@ -260,6 +318,29 @@ class EagerSGDOptimizer:
 
     def _apply_fused(self, gvs, stream, made):
         import torch
+        if self._buckets is not None:   # overlap: the buckets' rounds, posted by the hooks or now
+            err = None
+            for b in range(len(self._buckets)):
+                if not self._bucket_posted[b]:
+                    try:
+                        self._post_bucket(b, stream, made)
+                    except Exception as e:   # noqa: BLE001 -- the posted ones are waited for first
+                        err = err or e
+            for b, op in enumerate(self._bucket_ops):
+                if self._bucket_posted[b]:
+                    try:
+                        op.wait_packed(stream)
+                    except Exception as e:   # noqa: BLE001
+                        err = err or e
+            self._bucket_posted = [False] * len(self._buckets)
+            self._bucket_left = [len(bk) for bk in self._buckets]
+            conv, self._conv = self._conv, []
+            if err is not None:
+                raise err
+            for p, g, g32 in conv:
+                p.grad = g32.to(g.dtype).view_as(g)
+                made.append(p.grad)
+            return
         live = [(g, v) for g, v in reversed(gvs) if g is not None]
         if not live:
             return
@@ -301,4 +382,5 @@ class EagerSGDOptimizer:
         n = sum(op.report() for op in self._ops.values())
         if self._fused is not None:
             n += self._fused[1].report()
+        n += sum(op.report() for op in self._bucket_ops if op is not None)
         return n

@@ -74,7 +74,9 @@ def parse():
     ap.add_argument("--mode", choices=["solo", "majority", "allreduce", "ddp"], default="solo")
     ap.add_argument("--fuse", action="store_true", help="eager-SGD: one fused bucket per step")
     ap.add_argument("--overlap", action="store_true",
-                    help="eager-SGD per tensor: post each tensor's round from its gradient hook during backward")
+                    help="eager-SGD: post the rounds from the gradient hooks during backward (per tensor; "
+                         "with --fuse one fused round per bucket of --bucket-mb)")
+    ap.add_argument("--bucket-mb", type=float, default=25.0, help="--fuse --overlap: bucket size in MiB")
     ap.add_argument("--wire", choices=["fp32", "bf16"], default="fp32",
                     help="eager-SGD: what the ranks exchange (bf16: fp32 buckets, bf16 copies on the wire)")
     ap.add_argument("--steps", type=int, default=20)
@@ -127,7 +129,7 @@ def main():
     params = [p for p in model.parameters() if p.requires_grad]
     sgd = torch.optim.SGD(params, lr=0.1, momentum=0.9)
     opt = sgd if a.mode == "ddp" else EagerSGDOptimizer(sgd, world, mode=a.mode, fuse=a.fuse, wire=a.wire,
-                                                        overlap=a.overlap)
+                                                        overlap=a.overlap, bucket_mb=a.bucket_mb)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     x = torch.randn(a.batch, 3, a.image, a.image, device=dev, generator=g)
     y = torch.randint(0, 1001, (a.batch,), device=dev, generator=g)

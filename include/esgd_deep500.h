@@ -106,6 +106,15 @@ int allreducef_forward_cuda_post_many_io(void *const *handles, int n, const floa
  * torch.distributed's Work.wait().  A round that fails after this returned fails its op's
  * next post. */
 int allreducef_forward_cuda_wait_many_on(void *const *handles, int n, float *const *outputs, void *stream);
+/* Extension: allreducef_forward_cuda_packed split in two (posting a fused bucket while
+ * backward still runs): _packed_post hands the n pieces to the round (esgd_schedule_post_iov:
+ * packed / divisor into the op's bucket and unpacked into outs by the round; bf16 wire:
+ * packed into the send bucket on stream), _packed_wait waits for it and copies out a round
+ * that did not take them (a peer carried this rank through first).  One round in flight per
+ * op; the pieces and outputs must stay valid until _packed_wait. */
+int allreducef_forward_cuda_packed_post(void *handle, int n, const float *const *grads, const uint64_t *counts,
+                                        float *const *outs, float divisor, void *stream);
+int allreducef_forward_cuda_packed_wait(void *handle, void *stream);
 /* Extension: what the void entry points above (allreducef_forward, allreducef_forward_cuda)
  * do when their round fails (a peer timeout, an allocation failure).  ESGD_OP_ON_ERROR_ABORT
  * (default; env ESGD_OP_ON_ERROR=abort): print the error and abort the process, as their

@@ -66,12 +66,16 @@ def test_eager_sgd_optimizer(mode, variant):
         assert outs[0]["params_digest"] == outs[1]["params_digest"]
 
 
-@pytest.mark.parametrize("wait", ["host_wait", "stream_wait"])
-def test_eager_sgd_optimizer_rounds_posted_during_backward(wait):
+@pytest.mark.parametrize("variant", ["host_wait", "stream_wait", "fused_buckets"])
+def test_eager_sgd_optimizer_rounds_posted_during_backward(variant):
     # overlap=True: each tensor's round posted from its post-accumulate-grad hook while
     # backward still runs (TF's dataflow order for the reference's ops), waited for in
-    # apply_gradients -- the same rounds, so the oracle's bits and identical replicas
-    outs = run("optimizer_step", 2, mode="allreduce", steps=3, overlap=True, stream_wait=wait == "stream_wait")
+    # apply_gradients -- the same rounds, so the oracle's bits and identical replicas;
+    # fused_buckets: fuse=True in buckets of ~4 KiB (this model: several), each bucket's
+    # fused round posted once its last gradient exists
+    kw = dict(fuse=True, bucket_mb=4096 / (1 << 20)) if variant == "fused_buckets" else \
+        dict(stream_wait=variant == "stream_wait")
+    outs = run("optimizer_step", 2, mode="allreduce", steps=3, overlap=True, **kw)
     for o in outs:
         assert all(o["ok"]) and o["ok"], o["ok"]
         assert o["bytes"] > 0

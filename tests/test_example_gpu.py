@@ -44,7 +44,7 @@ def test_resnet50_synchronous_rounds_keep_ranks_identical(overlap):
 
 
 @pytest.mark.parametrize("mode,fuse,overlap", [("solo", True, False), ("majority", False, False),
-                                               ("solo", False, True)])
+                                               ("solo", False, True), ("majority", True, True)])
 def test_resnet50_eager_sgd_with_stragglers(mode, fuse, overlap):
     # up to two drawn ranks sleep before each forward pass; the job runs through, and the
     # replicas stay identical: a partial round gives every rank the same sum (overlap: the
