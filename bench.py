@@ -864,8 +864,6 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
                      # the ops' work and the wrapped SGD step on the data plane's round stream
                      # (esgd_round_stream): ordered behind the rounds by the stream itself
                      ("per_tensor_pipelined_round_stream", dict(fuse=False, round_stream=True, stream_wait=True)),
-                     # the ops on torch's legacy default stream itself (no internal stream)
-                     ("per_tensor_pipelined_legacy_stream", dict(fuse=False, side_stream=False)),
                      # the same with copy-in / copy-out kernels on the caller's stream instead of
                      # the rounds' own I/O (esgd_schedule_post_io): the A/B of the fused path
                      ("per_tensor_pipelined_copy_kernels", dict(fuse=False, fused_io=False)),
