@@ -237,7 +237,7 @@ int esgd_schedule_stats(esgd_sched_h h, esgd_sched_stats_t *out) {
     out->joined = s->joined;
     out->completed = s->completed;
     out->waited = s->waited;
-    out->activated = s->sh->activated.load();
+    out->activated = s->activated->load();
     out->last_activator = s->sh->last_activator.load();
     out->fresh_rounds = s->n_fresh;
     out->auto_rounds = s->n_auto;

@@ -35,6 +35,24 @@ static double g_timeout = 600.0;
 static std::mutex g_reg_mu;
 static std::vector<Sched *> g_reg;
 static std::unordered_set<const Sched *> g_reg_set;   // = g_reg, for O(1) handle checks
+// = g_reg by schedule id, for the issue-ring pump (written under g_reg_mu; a schedule is
+// freed only two progress epochs after its entry is cleared, like its g_reg entry)
+static std::atomic<Sched *> g_by_id[kMaxSched];
+static std::atomic<int> g_id_end{0};   // ids below this were handed out (the pass's scan range)
+// What the progress pass needs to skip a quiet schedule, packed by id: its posted and joined
+// counters and whether it is busy (stage != idle, or posted and awaiting its activation) --
+// written wherever the Sched's own fields change.  A pass reads these and the segment's
+// packed activation counters, and touches a Sched object only when there is work: with
+// ~1700 schedules alive (the bench's legs) the per-schedule Sched reads were most of a pass.
+struct alignas(16) HotState {
+    std::atomic<uint32_t> posted{0}, joined{0}, busy{0};
+};
+static HotState g_hot[kMaxSched];
+
+static void hot_busy(const Sched &s) {
+    g_hot[s.id].busy.store((s.stage.load(std::memory_order_relaxed) != ST_IDLE || s.awaiting.load(std::memory_order_relaxed))
+                               ? 1u : 0u, std::memory_order_release);
+}
 static std::mutex g_create_mu;
 static int g_next_id = 0;
 static std::thread g_thread;
@@ -175,6 +193,9 @@ int engine_finalize() {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         left.swap(g_reg);
         g_reg_set.clear();
+        for (auto &e : g_by_id) e.store(nullptr, std::memory_order_relaxed);
+        for (auto &h : g_hot) { h.posted.store(0); h.joined.store(0); h.busy.store(0); }
+        g_id_end.store(0);
     }
     for (Sched *s : left) {
         if (s->tp) s->tp->teardown(*s);
@@ -223,7 +244,7 @@ static std::string sched_state(Sched &s) {
              "node: activated %u, joins %u; issue ring: %llu launched here of %llu]",
              s.rank, s.posted.load(), s.joined.load(), s.completed, s.waited, s.released, s.cur,
              stage_name(s.stage.load()), s.cur_fresh ? "posted" : "carried by a peer", now_s() - s.stage_t0,
-             s.hold_mode && s.released < s.joined ? ", held until release()" : "", s.sh->activated.load(),
+             s.hold_mode && s.released < s.joined ? ", held until release()" : "", s.activated->load(),
              s.sh->ready_count.load(), (unsigned long long)g_cursor.load(std::memory_order_relaxed),
              (unsigned long long)(g_seg ? g_seg->ticket_next.load() : 0));
     std::string m = buf;
@@ -260,6 +281,7 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
     s->async = async; s->seed = seed;
     s->rank = g_rank; s->world = g_world;
     s->sh = &g_seg->sched[s->id];
+    s->activated = &g_seg->activated[s->id];
     s->tp = tp;
     s->resolve = resolve;
     s->resolve_ctx = ctx;
@@ -362,6 +384,11 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
         std::lock_guard<std::mutex> lk(g_reg_mu);
         g_reg.push_back(s);
         g_reg_set.insert(s);
+        g_hot[s->id].posted.store(0);
+        g_hot[s->id].joined.store(0);
+        g_hot[s->id].busy.store(0);
+        g_by_id[s->id].store(s, std::memory_order_release);
+        if (g_id_end.load() < s->id + 1) g_id_end.store(s->id + 1, std::memory_order_release);
     }
     *out = s;
     return ESGD_SUCCESS;
@@ -369,7 +396,8 @@ int sched_create_with(int kind, int dtype, uint64_t count, void *sb, void *rb, b
 
 // Activate `round` (the activation flood of colls/ffactivation.c): claim the round's
 // slot first (first claimant = activator), then raise the shared counter.
-static void activate(SchedShm *sh, uint32_t round, int rank, bool *won) {
+static void activate(Sched &s, uint32_t round, int rank, bool *won) {
+    SchedShm *sh = s.sh;
     std::atomic<uint64_t> &slot = sh->act_of[round % 256];
     uint64_t cur = slot.load(std::memory_order_acquire);
     const uint64_t mine = (uint64_t(round) << 32) | uint64_t(rank + 1);
@@ -382,8 +410,8 @@ static void activate(SchedShm *sh, uint32_t round, int rank, bool *won) {
             break;
         }
     }
-    uint32_t a = sh->activated.load(std::memory_order_acquire);
-    while (a < round && !sh->activated.compare_exchange_weak(a, round, std::memory_order_acq_rel)) {
+    uint32_t a = s.activated->load(std::memory_order_acquire);
+    while (a < round && !s.activated->compare_exchange_weak(a, round, std::memory_order_acq_rel)) {
     }
     seg_wake(g_seg);   // the flood: every idle progress thread joins now
 }
@@ -420,13 +448,14 @@ int sched_post(Sched *s, void *producer_stream, int *role, const RoundIO *io) {
         if (producer_stream)
             if (int rc = s->tp->note_producer(*s, t, producer_stream)) return rc;
         s->posted.store(t, std::memory_order_release);
+        g_hot[s->id].posted.store(t, std::memory_order_release);
         s->mark(t, 0);
         if (s->kind == KIND_MAJORITY) {
             // colls/ffrand_allreduce.c:88 — the same glibc draw on every rank
             const int act = int(unsigned(rand_r(&s->seed)) % unsigned(s->world));
             if (act == s->rank) {
                 bool won;
-                activate(s->sh, t, s->rank, &won);
+                activate(*s, t, s->rank, &won);
                 s->passive = 0;   // catch-up of :93-96 is implicit in the round counter
                 r = 1;
                 if (won) ++s->n_activated;
@@ -438,7 +467,7 @@ int sched_post(Sched *s, void *producer_stream, int *role, const RoundIO *io) {
             r = 2;
         } else {
             bool won;
-            activate(s->sh, t, s->rank, &won);   // the first poster activates the round
+            activate(*s, t, s->rank, &won);   // the first poster activates the round
             r = won ? 1 : 0;
             if (won) ++s->n_activated;
         }
@@ -603,6 +632,7 @@ int sched_delete(Sched *s) {
         std::lock_guard<std::mutex> lk(g_reg_mu);
         g_reg.erase(std::remove(g_reg.begin(), g_reg.end(), s), g_reg.end());
         g_reg_set.erase(s);
+        if (s->id >= 0 && s->id < kMaxSched) g_by_id[s->id].store(nullptr, std::memory_order_release);
     }
     // The progress thread may be inside a pass over a registry copy that still holds s:
     // wait until a pass that began after the erase has finished (two epochs).
@@ -637,10 +667,10 @@ Sched *sched_lookup(uint64_t handle) {
 // has just posted, sched_post); every other stage is left to the progress thread
 static bool step(Sched &s, bool join_only = false) {
     std::lock_guard<std::mutex> lk(s.mu);
-    if (s.error || !s.live.load()) { s.awaiting = false; return false; }
+    if (s.error || !s.live.load()) { s.awaiting = false; hot_busy(s); return false; }
     if (join_only && s.stage != ST_IDLE) return false;
     SchedShm *sh = s.sh;
-    auto enter = [&](Stage st) { s.stage = st; s.stage_t0 = now_s(); };
+    auto enter = [&](Stage st) { s.stage = st; s.stage_t0 = now_s(); hot_busy(s); };
     auto check = [&](int rc, const char *what) {
         if (rc < 0) {
             std::string m = std::string(what) + ": " + esgd_last_error();
@@ -652,14 +682,16 @@ static bool step(Sched &s, bool join_only = false) {
     switch (s.stage) {
     case ST_IDLE: {
         s.awaiting = false;
+        hot_busy(s);
         // hold mode: the caller has not yet taken (wait) and released the last round
         if (s.hold_mode && s.released < s.joined) return false;
         const uint32_t next = s.joined + 1;
         const bool sync = round_is_sync(s, next);
         const uint32_t posted = s.posted.load(std::memory_order_acquire);
-        const bool go = sync ? posted >= next : sh->activated.load(std::memory_order_acquire) >= next;
+        const bool go = sync ? posted >= next : s.activated->load(std::memory_order_acquire) >= next;
         if (!go) {
             s.awaiting = posted >= next;
+            hot_busy(s);
             return false;
         }
         const uint64_t j0 = mono_ns();
@@ -673,6 +705,7 @@ static bool step(Sched &s, bool join_only = false) {
         s.cur = next;
         s.cur_fresh = posted >= next;
         s.joined = next;
+        g_hot[s.id].joined.store(next, std::memory_order_release);
         s.fresh_set(next, s.cur_fresh);
         // FFCOLL_BUFFERS: a round joined on a peer's activation re-resolves the buffers
         // here (a fresh round did at its post)
@@ -733,6 +766,7 @@ static bool step(Sched &s, bool join_only = false) {
         s.completed = s.cur;
         s.completed_a.store(s.cur, std::memory_order_release);
         s.stage = ST_IDLE;
+        hot_busy(s);
         s.cv.notify_all();
         return true;
     }
@@ -743,25 +777,26 @@ static bool step(Sched &s, bool join_only = false) {
 // An idle schedule whose next round is neither posted here nor activated by a peer has
 // nothing to do: the pass skips it without taking its mutex (step() would return false).
 // With hundreds of schedules (one per gradient tensor) most are quiet in any pass.
-static bool quiet(const Sched &s) {
+static bool quiet(int id) {
     static const bool off = getenv("ESGD_PASS_SKIP") && *getenv("ESGD_PASS_SKIP") == '0';   // A/B
     if (off) return false;
-    if (s.stage.load(std::memory_order_acquire) != ST_IDLE || s.awaiting) return false;
-    const uint32_t next = s.joined.load(std::memory_order_acquire) + 1;
-    return s.posted.load(std::memory_order_acquire) < next && s.sh->activated.load(std::memory_order_acquire) < next;
+    const HotState &h = g_hot[id];
+    if (h.busy.load(std::memory_order_acquire)) return false;
+    const uint32_t next = h.joined.load(std::memory_order_acquire) + 1;
+    return h.posted.load(std::memory_order_acquire) < next && g_seg->activated[id].load(std::memory_order_acquire) < next;
 }
 
 // Launch rounds strictly in ring order (the same sequence on every rank).
-static bool pump_tickets(const std::vector<Sched *> &snap) {
+static bool pump_tickets() {
     if (!g_seg) return false;
     bool any = false;
     for (;;) {
         const uint64_t cur = g_cursor.load(std::memory_order_relaxed);
         TicketSlot &slot = g_seg->ring[cur % kRing];
         if (slot.tag.load(std::memory_order_acquire) != cur + 1) break;
-        Sched *target = nullptr;
-        for (Sched *s : snap)
-            if (uint32_t(s->id) == slot.sched) { target = s; break; }
+        // by id: a scan of the registry cost O(schedules) per round -- in a process holding
+        // ~1700 schedules (the bench's legs) most of the pass
+        Sched *target = slot.sched < uint32_t(kMaxSched) ? g_by_id[slot.sched].load(std::memory_order_acquire) : nullptr;
         if (!target) break;                      // schedule not registered here yet
         {
             std::lock_guard<std::mutex> lk(target->mu);
@@ -782,6 +817,7 @@ static bool pump_tickets(const std::vector<Sched *> &snap) {
                 } else {
                     target->stage = ST_INFLIGHT;
                     target->stage_t0 = now_s();
+                    hot_busy(*target);
                     target->launched_a.store(target->cur, std::memory_order_release);
                 }
             }
@@ -823,17 +859,18 @@ void engine_profile(uint64_t out[7]) {
 
 bool engine_progress_once() {
     const uint64_t p0 = mono_ns();
-    std::vector<Sched *> snap;
-    {
-        std::lock_guard<std::mutex> lk(g_reg_mu);
-        snap = g_reg;
-    }
-    bool any = pump_tickets(snap);
+    if (!g_seg) return false;
+    bool any = pump_tickets();
     const uint64_t p1 = mono_ns();
     if (any) g_prof_pump_ns.fetch_add(p1 - p0, std::memory_order_relaxed);
     int active = 0;
-    for (Sched *s : snap) {
-        if (quiet(*s)) continue;
+    // every registered schedule, by id (a schedule deleted meanwhile is freed only two
+    // epochs after its entry was cleared, so one read here stays valid for this pass)
+    const int end = g_id_end.load(std::memory_order_acquire);
+    for (int id = 0; id < end; ++id) {
+        if (quiet(id)) continue;
+        Sched *s = g_by_id[id].load(std::memory_order_acquire);
+        if (!s) continue;
         while (step(*s)) any = true;   // run a schedule until it has to wait
         // in flight, or posted and waiting for its activation (majority: the drawn
         // activator's post; solo: a sync round's last poster): the join is imminent and

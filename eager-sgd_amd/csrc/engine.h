@@ -118,6 +118,7 @@ struct Sched {
     size_t esize = 4;
     int rank = 0, world = 1;
     SchedShm *sh = nullptr;
+    std::atomic<uint32_t> *activated = nullptr;   // Segment::activated[id]
     uint32_t gen = 0;
     int connect_attempt = 0;   // creation: which connect attempt maps peers now (SchedShm::remap)
     int remaps = 0;            // creation retries this schedule needed (diagnostics)

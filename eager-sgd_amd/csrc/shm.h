@@ -18,7 +18,7 @@ namespace esgd {
 constexpr int kMaxRanks = 16;     // ranks per node
 constexpr int kRemapTries = 3;    // creation retries after a peer's mapping showed other memory
 constexpr int kMaxSched = 2048;   // persistent schedules per job (the ResNet-50 wrapper uses 161)
-constexpr uint64_t kShmMagic = 0x314d4853444753ull;  // "ESGDSHM1"
+constexpr uint64_t kShmMagic = 0x324d4853444753ull;  // "ESGDSHM2" (round 5: packed activation counters)
 
 // One registered device buffer: the allocation's IPC handle plus the offset of the
 // buffer inside it (torch's caching allocator hands out sub-allocations).
@@ -37,7 +37,9 @@ struct alignas(64) IpcSlot {
 };
 
 struct alignas(64) SchedShm {
-    std::atomic<uint32_t> activated;      // highest round activated (solo async / majority)
+    // (the highest round activated lives in Segment::activated[id], packed: every progress
+    // pass reads it for every schedule, and one cache line there covers 16 schedules where a
+    // field here cost a page -- SchedShm is several KiB -- apiece)
     std::atomic<int32_t> last_activator;  // diagnostics only (may lag `activated`)
     // per-round activation record, (round << 32) | (rank + 1), claimed by CAS BEFORE
     // `activated` is raised: whoever sees activated >= t also sees round t's activator
@@ -106,6 +108,9 @@ struct Segment {
     // HBM; dataplane.cpp)
     IpcSlot flagpage[2][kMaxRanks];
     TicketSlot ring[kRing];
+    // highest round activated of schedule id (solo async / majority): raised by the
+    // activator's CAS (engine.cpp activate), read by every rank's progress pass
+    alignas(64) std::atomic<uint32_t> activated[kMaxSched];
     SchedShm sched[kMaxSched];
 };
 

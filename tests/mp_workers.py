@@ -1952,7 +1952,7 @@ def cp_fresh_queue(rank, world, rounds=300):
     return {"fresh": fresh, "joined": joined}
 
 
-def cp_pipelined_steps(rank, world, steps=50, kind=2, n=161):
+def cp_pipelined_steps(rank, world, steps=50, kind=2, n=161, idle=0):
     """The per-tensor call pattern on the control plane alone (ESGD_BUF_NONE: join, ticket,
     issue ring and completion with a transport that moves nothing): `n` schedules, every
     step posts all of them, then waits for all.  Median step and, on the last step, the
@@ -1961,6 +1961,9 @@ def cp_pipelined_steps(rank, world, steps=50, kind=2, n=161):
 
     import numpy as np
     comm = _comm()
+    # `idle` more schedules, never posted (a process that keeps other jobs' schedules alive:
+    # every progress pass still walks them)
+    others = [comm.Schedule(kind, None, None, 0, seed=6545343, buf=comm.BUF_NONE) for _ in range(idle)]
     scheds = [comm.Schedule(kind, None, None, 0, seed=6545343, buf=comm.BUF_NONE) for _ in range(n)]
     ts = []
     for _ in range(steps):
@@ -1985,7 +1988,7 @@ def cp_pipelined_steps(rank, world, steps=50, kind=2, n=161):
     # per schedule, in creation order: post, join, launch, completion relative to the first post
     per = [[round(float(r[i] - t0) / 1e3, 1) for i in (0, 1, 3, 4, 5)] for r in tl]
     comm.barrier()
-    for s in scheds:
+    for s in scheds + others:
         s.delete()
     comm.finalize()
     return {"step_us_median": round(statistics.median(ts[2:]) * 1e6, 1), "last_step": rel, "per_sched": per}

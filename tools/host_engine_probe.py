@@ -24,7 +24,8 @@ if __name__ == "__main__":
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--kind", type=int, default=2)
     ap.add_argument("--n", type=int, default=161)
+    ap.add_argument("--idle", type=int, default=0, help="schedules kept alive and never posted")
     a = ap.parse_args()
     import mp_workers
-    outs = mp_workers.run("cp_pipelined_steps", a.world, steps=a.steps, kind=a.kind, n=a.n)
+    outs = mp_workers.run("cp_pipelined_steps", a.world, steps=a.steps, kind=a.kind, n=a.n, idle=a.idle)
     print(json.dumps(outs[0]))
