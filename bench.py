@@ -708,6 +708,7 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
         finally:
             comm.set_config(key, -1)
     variants = _op_like_variants(comm, dev, lengths, steps)
+    launch_shape = _launch_shape_ab(comm, bufs, lengths, steps)
     for s, b in zip(scheds, bufs):
         _defer(s, b)
     _defer(one, fused)
@@ -723,7 +724,41 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
             "rank0_pipelined_step_us_one_launch_per_round": breakdown_u,
             "rank0_progress_thread_per_step_one_launch_per_round": prof_u,
             "ab_host_path_switches": ab,
-            "op_like_pipelined_variants": variants}
+            "op_like_pipelined_variants": variants,
+            "launch_shape_ab": launch_shape}
+
+
+def _launch_shape_ab(comm, bufs, lengths, steps):
+    """The pipelined 161-bucket step over schedules created with every ResNet-50 bucket a
+    one-launch round (small_round_bytes 16 MiB: the 9 buckets above 4 MiB too, no five-launch
+    rounds) and shared launches of up to 256 workers (batch_workers_max) -- against the
+    defaults (4 MiB, 64) measured above.  On the 1-GPU rehearsal this took the optimizer's
+    step from 1.48 to 1.14-1.23 ms at P = 2 and left P = 4 unchanged
+    (profiles/r05/threshold_workers_ab/); a GPU per rank decides the defaults."""
+    comm.set_config("small_round_bytes", 16 << 20)
+    comm.set_config("batch_workers_max", 256)
+    try:
+        scheds = [comm.Schedule(comm.MAJORITY, None, b, b.count, seed=6545343, buf=comm.BUF_DEVICE) for b in bufs]
+
+        def pipelined():
+            for s in scheds:
+                s.post()
+            for s in scheds:
+                s.wait()
+
+        for _ in range(2):
+            pipelined()
+        t = _timed_steps(comm, pipelined, steps)
+        breakdown = _step_breakdown_us(scheds)
+        workers = comm.get_config("batch_workers")
+    finally:
+        comm.set_config("small_round_bytes", -1)
+        comm.set_config("batch_workers_max", -1)
+    for s in scheds:
+        _defer(s)
+    return {"small_round_bytes": 16 << 20, "batch_workers_max": 256,
+            "step_ms_161_buckets_pipelined": round(t * 1e3, 3), "rank0_step_us": breakdown,
+            "last_launch_workers": workers}
 
 
 def _op_like_variants(comm, dev, lengths, steps):

@@ -119,6 +119,9 @@ static std::atomic<int64_t> g_cfg_depth{-1}, g_cfg_snap{-1}, g_cfg_inline{-1};
 // launch; only an explicit flush (another launch on the round stream, schedule deletion,
 // finalize) does -- so a test can finalize with rounds held
 static std::atomic<int64_t> g_cfg_hold{0};
+// "batch_workers_max" (ESGD_BATCH_WORKERS, default 64): a shared launch's worker cap, and the
+// phase tiles per entry of schedules whose first batched round comes after the setting
+static std::atomic<int64_t> g_cfg_workers{-1};
 // "event_device_scope" (ESGD_EVENT_DEVICE_SCOPE, default 0): the producer / consumer events
 // of posts and releases record with a device-scope release (hipEventReleaseToDevice) instead
 // of HIP's system-scope fence -- they only order the caller's stream before the round stream
@@ -214,6 +217,10 @@ int config_set(const char *key, int64_t value) {
     } else if (!std::strcmp(key, "batch_hold")) {
         ESGD_ARG(value >= -1 && value <= 1, "batch_hold: 0 or 1 (-1: the default, 0)");
         g_cfg_hold.store(value < 0 ? 0 : value);
+    } else if (!std::strcmp(key, "batch_workers_max")) {
+        ESGD_ARG(value == -1 || (value >= 1 && value <= int64_t(kBatchWorkersMax)),
+                 "batch_workers_max: 1..%u (-1: the default)", kBatchWorkersMax);
+        g_cfg_workers.store(value);
     } else if (!std::strcmp(key, "event_device_scope")) {
         ESGD_ARG(value >= -1 && value <= 1, "event_device_scope: 0 or 1 (-1: the default)");
         g_cfg_evscope.store(value);
@@ -222,8 +229,8 @@ int config_set(const char *key, int64_t value) {
         g_cfg_psync.store(value);
     } else {
         set_error("esgd_set_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
-                  "batch_rounds, batch_depth, snapshot_in_batch, inline_join, batch_hold, event_device_scope, "
-                  "producer_host_sync)", key);
+                  "batch_rounds, batch_depth, snapshot_in_batch, inline_join, batch_hold, batch_workers_max, "
+                  "event_device_scope, producer_host_sync)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -244,12 +251,13 @@ int config_get(const char *key, int64_t *value) {
     else if (!std::strcmp(key, "snapshot_in_batch")) *value = snapshot_in_batch() ? 1 : 0;
     else if (!std::strcmp(key, "inline_join")) *value = config_inline_join() ? 1 : 0;
     else if (!std::strcmp(key, "batch_hold")) *value = g_cfg_hold.load();
+    else if (!std::strcmp(key, "batch_workers_max")) *value = int64_t(batch_workers_max());
     else if (!std::strcmp(key, "event_device_scope")) *value = event_device_scope() ? 1 : 0;
     else if (!std::strcmp(key, "producer_host_sync")) *value = producer_host_sync() ? 1 : 0;
     else {
         set_error("esgd_get_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
                   "batch_rounds, launches, batch_workers, batch_depth, snapshot_in_batch, inline_join, batch_hold, "
-                  "event_device_scope, producer_host_sync)", key);
+                  "batch_workers_max, event_device_scope, producer_host_sync)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -1283,12 +1291,13 @@ static uint32_t g_qnext = 0;
 // ESGD_BATCH_STATIC=1: static tile assignment in shared launches (an A/B of the dynamic
 // counter; needs every worker resident at once)
 uint32_t batch_workers_max() {
-    static const uint32_t v = [] {
+    static const uint32_t env = [] {
         const char *e = getenv("ESGD_BATCH_WORKERS");
         const long n = (e && *e) ? atol(e) : long(kBatchWorkers);
         return uint32_t(std::max<long>(1, std::min<long>(long(kBatchWorkersMax), n)));
     }();
-    return v;
+    const int64_t v = g_cfg_workers.load(std::memory_order_relaxed);
+    return v > 0 ? uint32_t(v) : env;
 }
 
 static bool batch_static() {
