@@ -259,7 +259,7 @@ class Schedule:
         """esgd_schedule_post_iov: the round's data in fp32 pieces (tensors / buffers whose
         sizes sum to the schedule's count): packed (/ divisor) into the bucket and the result
         unpacked into dsts by the round itself, if this rank joins it at or after this post."""
-        from .device import as_ptr
+        from .device import ptr_array_of
         n = len(srcs)
         counts = (C.c_uint64 * max(1, n))(*[int(x.numel()) if hasattr(x, "numel") else int(x.count)
                                             for x in srcs])
@@ -267,8 +267,9 @@ class Schedule:
         s = None if stream is None else (stream.handle if hasattr(stream, "handle") else int(stream))
         if s == 0:
             s = 1   # ESGD_STREAM_NULL
-        check(lib().esgd_schedule_post_iov(self.handle, n, _lib.ptr_array([as_ptr(x) for x in srcs]),
-                                           _lib.ptr_array([as_ptr(x) for x in dsts]), counts, float(divisor), s,
+        src = ptr_array_of(srcs)
+        dst = src if dsts is srcs else ptr_array_of(dsts)
+        check(lib().esgd_schedule_post_iov(self.handle, n, src, dst, counts, float(divisor), s,
                                            C.byref(role)), "esgd_schedule_post_iov")
         return role.value
 

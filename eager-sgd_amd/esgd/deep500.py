@@ -142,12 +142,12 @@ class AllreduceOp:
     def forward_cuda_packed(self, grads, outs, divisor: float = 1.0, stream: int | None = None):
         """Bucket fusion: the tensors `grads` (fp32, contiguous, sizes summing to this op's
         size) packed in order, divided, reduced in one round and unpacked into `outs`."""
-        from .device import as_ptr
+        from .device import ptr_array_of
         n = len(grads)
         counts = (C.c_uint64 * max(1, n))(*[int(g.numel()) if hasattr(g, "numel") else int(g.size)
                                              for g in grads])
-        src = _lib.ptr_array([as_ptr(g) for g in grads])
-        dst = _lib.ptr_array([as_ptr(o) for o in outs])
+        src = ptr_array_of(grads)
+        dst = src if outs is grads else ptr_array_of(outs)
         _lib.check(lib().allreducef_forward_cuda_packed(self.handle, n, src, counts, dst, float(divisor),
                                                         stream), "allreducef_forward_cuda_packed")
         return outs
@@ -156,12 +156,12 @@ class AllreduceOp:
         """First half of forward_cuda_packed (allreducef_forward_cuda_packed_post): the round
         of the fused bucket posted with the pieces as its own data; wait_packed() finishes it.
         The tensors must stay alive until then.  Raises EsgdError."""
-        from .device import as_ptr
+        from .device import ptr_array_of
         n = len(grads)
         counts = (C.c_uint64 * max(1, n))(*[int(g.numel()) for g in grads])
-        _lib.check(lib().allreducef_forward_cuda_packed_post(self.handle, n, _lib.ptr_array([as_ptr(g) for g in grads]),
-                                                             counts, _lib.ptr_array([as_ptr(o) for o in outs]),
-                                                             float(divisor), stream),
+        src = ptr_array_of(grads)
+        dst = src if outs is grads else ptr_array_of(outs)
+        _lib.check(lib().allreducef_forward_cuda_packed_post(self.handle, n, src, counts, dst, float(divisor), stream),
                    "allreducef_forward_cuda_packed_post")
 
     def wait_packed(self, stream: int | None = None):
@@ -188,10 +188,10 @@ class AllreduceOp:
         """post_cuda for many ops in one call (allreducef_forward_cuda_post_many): every
         copy-in in one launch per 48 ops, the posts with one producer event.  Raises
         EsgdError; the ops before a failed post stay posted (wait_many drains them)."""
-        from .device import as_ptr
+        from .device import ptr_array_of
         n = len(ops)
         hs = _lib.ptr_array([op.handle for op in ops])
-        gs = _lib.ptr_array([as_ptr(g) for g in grads])
+        gs = ptr_array_of(grads)
         _lib.check(lib().allreducef_forward_cuda_post_many(hs, n, gs, float(divisor), stream),
                    "allreducef_forward_cuda_post_many")
 
@@ -202,11 +202,11 @@ class AllreduceOp:
         grads[i]) -- no copy-in or copy-out launch on the caller's stream.  wait_many(ops,
         outs) then copies out only the rounds a peer carried this rank through before the
         post.  Unaligned tensors or a bf16 wire fall back to post_many.  Raises EsgdError."""
-        from .device import as_ptr
+        from .device import ptr_array_of
         n = len(ops)
         hs = _lib.ptr_array([op.handle for op in ops])
-        gs = _lib.ptr_array([as_ptr(g) for g in grads])
-        os_ = _lib.ptr_array([as_ptr(o) for o in outs])
+        gs = ptr_array_of(grads)
+        os_ = gs if outs is grads else ptr_array_of(outs)
         _lib.check(lib().allreducef_forward_cuda_post_many_io(hs, n, gs, os_, float(divisor), stream),
                    "allreducef_forward_cuda_post_many_io")
 
@@ -218,10 +218,10 @@ class AllreduceOp:
         on_stream=True (allreducef_forward_cuda_wait_many_on): the rounds are waited for on
         the GPU -- `stream` waits for each, and the call returns once all are queued there;
         a round that fails later fails its op's next post."""
-        from .device import as_ptr
+        from .device import ptr_array_of
         n = len(ops)
         hs = _lib.ptr_array([op.handle for op in ops])
-        os_ = _lib.ptr_array([as_ptr(o) for o in outs])
+        os_ = ptr_array_of(outs)
         if on_stream:
             _lib.check(lib().allreducef_forward_cuda_wait_many_on(hs, n, os_, stream),
                        "allreducef_forward_cuda_wait_many_on")

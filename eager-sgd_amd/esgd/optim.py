@@ -116,7 +116,9 @@ class EagerSGDOptimizer:
             self._attach()
         self._side = None
         self.wire = wire        # "bf16": bf16 copies between ranks
-        self._ops = {}          # parameter -> op instance (one bucket per tensor)
+        # id(parameter) -> op instance (one bucket per tensor); by id: a Parameter's own
+        # __hash__ is a Python call, 161 of them a step (the parameters live in param_groups)
+        self._ops = {}
         self._fused = None      # (layout, op, packed bucket, reduced bucket)
         self._configured = False
 
@@ -235,9 +237,9 @@ class EagerSGDOptimizer:
         if not self._configured:
             deep500.configure(self.mode, self.async_, self.seed, self.wire)
             self._configured = True
-        op = self._ops.get(p)
+        op = self._ops.get(id(p))
         if op is None:
-            op = self._ops[p] = deep500.AllreduceOp(tuple(g.shape))
+            op = self._ops[id(p)] = deep500.AllreduceOp(tuple(g.shape))
         self._ready.append((op, g, p))
         if len(self._ready) >= self.overlap_group:
             self._post_ready(torch.cuda.current_stream().cuda_stream)
@@ -246,8 +248,8 @@ class EagerSGDOptimizer:
         group, self._ready = self._ready, []
         if group:
             self._bwd.extend(group)   # waited for in apply_gradients even if the post failed part-way
-            deep500.AllreduceOp.post_many_io([o for o, _, _ in group], [g for _, g, _ in group],
-                                             [g for _, g, _ in group], self.comm_size, stream)
+            gs = [g for _, g, _ in group]
+            deep500.AllreduceOp.post_many_io([o for o, _, _ in group], gs, gs, self.comm_size, stream)
 
     def detach(self):
         """Remove the overlap hooks (posts go back to apply_gradients)."""
@@ -279,14 +281,14 @@ class EagerSGDOptimizer:
                 if err is not None:
                     raise err
             posted = []
+            ops_of, f32 = self._ops, torch.float32
             for grad, var in reversed(gvs):
                 if grad is None:      # the reference would still feed None (:35-42); skip
                     continue
-                op = self._ops.get(var)
+                op = ops_of.get(id(var))
                 if op is None:
-                    op = self._ops[var] = deep500.AllreduceOp(tuple(grad.shape))
-                g = grad if (grad.dtype == torch.float32 and grad.is_contiguous()) \
-                    else grad.float().contiguous()
+                    op = ops_of[id(var)] = deep500.AllreduceOp(tuple(grad.shape))
+                g = grad if (grad.dtype is f32 and grad.is_contiguous()) else grad.float().contiguous()
                 if self.pipeline:
                     posted.append((op, g, grad, var))
                 else:
