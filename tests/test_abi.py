@@ -60,6 +60,25 @@ def test_no_device_fails_loudly():
     assert "no HIP device" in _lib.last_error()
 
 
+def test_ptr_array_of():
+    # the group calls' pointer arrays: torch tensors by data_ptr(), anything as_ptr takes
+    # (ints, objects with .ptr) through the fallback, the same values in the same order
+    import torch
+
+    from esgd.device import as_ptr, ptr_array_of
+
+    class Buf:
+        ptr = 0x5000
+
+    ts = [torch.empty(4), torch.empty(8)]
+    assert list(ptr_array_of(ts)) == [t.data_ptr() for t in ts]
+    mixed = [ts[0], 0x1000, Buf()]
+    assert list(ptr_array_of(mixed)) == [as_ptr(x) for x in mixed]
+    assert list(ptr_array_of([])) == [None]   # a one-slot array for n = 0, never read
+    with pytest.raises(TypeError):
+        ptr_array_of([object()])
+
+
 def test_argument_validation_without_device():
     from esgd import _lib
     lib = _lib.lib()
