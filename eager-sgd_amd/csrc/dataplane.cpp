@@ -122,6 +122,11 @@ static std::atomic<int64_t> g_cfg_hold{0};
 // "batch_workers_max" (ESGD_BATCH_WORKERS, default 64): a shared launch's worker cap, and the
 // phase tiles per entry of schedules whose first batched round comes after the setting
 static std::atomic<int64_t> g_cfg_workers{-1};
+// "snapshot_workers_max" (ESGD_SNAPSHOT_WORKERS, default 0 = batch_workers_max): the worker
+// cap of a shared launch that holds phase-0 snapshot tiles (rounds posted with their own
+// data, separate send buckets).  A snapshot is a plain copy: it wants waves, where the gated
+// phases want few spinning workgroups; process-local, read at each flush
+static std::atomic<int64_t> g_cfg_snapw{-1};
 // "event_device_scope" (ESGD_EVENT_DEVICE_SCOPE, default 0): the producer / consumer events
 // of posts and releases record with a device-scope release (hipEventReleaseToDevice) instead
 // of HIP's system-scope fence -- they only order the caller's stream before the round stream
@@ -221,6 +226,10 @@ int config_set(const char *key, int64_t value) {
         ESGD_ARG(value == -1 || (value >= 1 && value <= int64_t(kBatchWorkersMax)),
                  "batch_workers_max: 1..%u (-1: the default)", kBatchWorkersMax);
         g_cfg_workers.store(value);
+    } else if (!std::strcmp(key, "snapshot_workers_max")) {
+        ESGD_ARG(value >= -1 && value <= int64_t(kBatchWorkersMax),
+                 "snapshot_workers_max: 0..%u (0: batch_workers_max; -1: the default)", kBatchWorkersMax);
+        g_cfg_snapw.store(value);
     } else if (!std::strcmp(key, "event_device_scope")) {
         ESGD_ARG(value >= -1 && value <= 1, "event_device_scope: 0 or 1 (-1: the default)");
         g_cfg_evscope.store(value);
@@ -230,13 +239,14 @@ int config_set(const char *key, int64_t value) {
     } else {
         set_error("esgd_set_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
                   "batch_rounds, batch_depth, snapshot_in_batch, inline_join, batch_hold, batch_workers_max, "
-                  "event_device_scope, producer_host_sync)", key);
+                  "snapshot_workers_max, event_device_scope, producer_host_sync)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
 }
 
 static int batch_depth();
+static uint32_t snapshot_workers_max();
 static bool snapshot_in_batch();
 
 int config_get(const char *key, int64_t *value) {
@@ -252,12 +262,13 @@ int config_get(const char *key, int64_t *value) {
     else if (!std::strcmp(key, "inline_join")) *value = config_inline_join() ? 1 : 0;
     else if (!std::strcmp(key, "batch_hold")) *value = g_cfg_hold.load();
     else if (!std::strcmp(key, "batch_workers_max")) *value = int64_t(batch_workers_max());
+    else if (!std::strcmp(key, "snapshot_workers_max")) *value = int64_t(snapshot_workers_max());
     else if (!std::strcmp(key, "event_device_scope")) *value = event_device_scope() ? 1 : 0;
     else if (!std::strcmp(key, "producer_host_sync")) *value = producer_host_sync() ? 1 : 0;
     else {
         set_error("esgd_get_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
                   "batch_rounds, launches, batch_workers, batch_depth, snapshot_in_batch, inline_join, batch_hold, "
-                  "batch_workers_max, event_device_scope, producer_host_sync)", key);
+                  "batch_workers_max, snapshot_workers_max, event_device_scope, producer_host_sync)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -1300,6 +1311,17 @@ uint32_t batch_workers_max() {
     return v > 0 ? uint32_t(v) : env;
 }
 
+static uint32_t snapshot_workers_max() {
+    static const uint32_t env = [] {
+        const char *e = getenv("ESGD_SNAPSHOT_WORKERS");
+        const long n = (e && *e) ? atol(e) : 0L;
+        return uint32_t(std::max<long>(0, std::min<long>(long(kBatchWorkersMax), n)));
+    }();
+    const int64_t v = g_cfg_snapw.load(std::memory_order_relaxed);
+    const uint32_t w = v >= 0 ? uint32_t(v) : env;
+    return w ? std::max(w, batch_workers_max()) : batch_workers_max();
+}
+
 static bool batch_static() {
     static const bool on = getenv("ESGD_BATCH_STATIC") && *getenv("ESGD_BATCH_STATIC") == '1';
     return on;
@@ -1438,7 +1460,8 @@ static int batch_flush_locked() {
     a.tile0[n] = t0;
     a.tile1[n] = t1;
     a.tile2[n] = t2;
-    unsigned workers = std::min<unsigned>(batch_workers_max(), std::max<unsigned>(1, std::max(t0, std::max(t1, t2))));
+    const unsigned wmax = t0 ? snapshot_workers_max() : batch_workers_max();
+    unsigned workers = std::min<unsigned>(wmax, std::max<unsigned>(1, std::max(t0, std::max(t1, t2))));
     // The launch's rounds complete with the agent and one worker resident (the tile
     // counter), but the stream's next launch starts only once every workgroup of this one
     // was dispatched and left -- so the grid is kept to what the GPU can hold beside the

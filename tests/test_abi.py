@@ -127,6 +127,26 @@ def test_host_path_switches():
         assert comm.get_config(key) == v
 
 
+def test_snapshot_workers_max():
+    # a launch holding snapshot tiles may take more workers than batch_workers_max, never fewer
+    from esgd import _lib, comm  # noqa: F401
+    lib = _lib.lib()
+    assert lib.esgd_set_config(b"snapshot_workers_max", 513) == _lib.INVALID_ARG
+    assert lib.esgd_set_config(b"snapshot_workers_max", -2) == _lib.INVALID_ARG
+    try:
+        comm.set_config("batch_workers_max", 128)
+        comm.set_config("snapshot_workers_max", 0)      # 0: the same cap as batch_workers_max
+        assert comm.get_config("snapshot_workers_max") == 128
+        comm.set_config("snapshot_workers_max", 32)     # below it: batch_workers_max still
+        assert comm.get_config("snapshot_workers_max") == 128
+        comm.set_config("snapshot_workers_max", 256)
+        assert comm.get_config("snapshot_workers_max") == 256
+    finally:
+        comm.set_config("snapshot_workers_max", -1)
+        comm.set_config("batch_workers_max", -1)
+    assert comm.get_config("snapshot_workers_max") == comm.get_config("batch_workers_max")
+
+
 def test_op_error_policy_argument_checks():
     from esgd import _lib, deep500
     lib = _lib.lib()
