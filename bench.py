@@ -937,10 +937,11 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
             # A/B of the same step with one launch per round (esgd_set_config, process-local).
             # (r05d-r05g also A/B'd a device-scope event release and a host-side producer
             # sync here: within noise every time, profiles/r05/README.md; dropped)
-            # snapshot_workers_max: shared launches that hold the rounds' snapshots of the
-            # gradients (phase 0, a plain copy) get up to 256 workers instead of 64
+            # snapshot_workers_max 0: shared launches that hold the rounds' snapshots of the
+            # gradients (phase 0, a plain copy) capped at batch_workers_max (64) like the
+            # others, instead of 256 (the default since r05ac)
             for key, vals, what in (("batch_rounds", {"batch_rounds": 0}, "_one_launch_per_round_ms"),
-                                    ("snap256", {"snapshot_workers_max": 256}, "_snapshot_workers256_ms")):
+                                    ("snap64", {"snapshot_workers_max": 0}, "_snapshot_workers64_ms")):
                 for k, v in vals.items():
                     comm.set_config(k, v)
                 try:

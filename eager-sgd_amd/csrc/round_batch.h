@@ -25,6 +25,7 @@ namespace esgd {
 constexpr int kBatchMax = 64;          // rounds per launch: one agent lane each
 constexpr uint32_t kBatchWorkers = 64; // worker workgroups at most, by default (k_round_small's grid)
 constexpr uint32_t kBatchWorkersMax = 512;   // ... and with ESGD_BATCH_WORKERS (batch_workers_max())
+constexpr uint32_t kSnapshotWorkers = 256;   // ... of a launch holding snapshot tiles, by default
 // ESGD_BATCH_WORKERS (1..512, default kBatchWorkers): the worker cap of shared launches and
 // of a phase's tiles per entry (dataplane.cpp; read once per process)
 uint32_t batch_workers_max();

@@ -144,7 +144,8 @@ def test_snapshot_workers_max():
     finally:
         comm.set_config("snapshot_workers_max", -1)
         comm.set_config("batch_workers_max", -1)
-    assert comm.get_config("snapshot_workers_max") == comm.get_config("batch_workers_max")
+    want = int(os.environ.get("ESGD_SNAPSHOT_WORKERS", 256)) or comm.get_config("batch_workers_max")
+    assert comm.get_config("snapshot_workers_max") == max(want, comm.get_config("batch_workers_max"))
 
 
 def test_op_error_policy_argument_checks():
