@@ -933,6 +933,16 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
             out[name + "_rank0_step_us"] = _step_breakdown_us([op.schedule() for op in opt._ops.values()])
         else:
             out["fused_breakdown_us"] = _fused_breakdown(comm, opt, params, steps)
+        if name == "per_tensor_blocking":
+            # idle_skip: a post / release whose caller's stream is idle records no event (the
+            # round stream has nothing to wait for) -- the reference's blocking chain, 161
+            # cross-stream waits a step otherwise
+            comm.set_config("idle_skip", 1)
+            try:
+                step()
+                out[name + "_idle_skip_ms"] = round(_timed_steps(comm, step, steps) * 1e3, 3)
+            finally:
+                comm.set_config("idle_skip", -1)
         if name == "per_tensor_pipelined":
             # A/B of the same step with one launch per round (esgd_set_config, process-local).
             # (r05d-r05g also A/B'd a device-scope event release and a host-side producer
@@ -941,7 +951,8 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
             # gradients (phase 0, a plain copy) capped at batch_workers_max (64) like the
             # others, instead of 256 (the default since r05ac)
             for key, vals, what in (("batch_rounds", {"batch_rounds": 0}, "_one_launch_per_round_ms"),
-                                    ("snap64", {"snapshot_workers_max": 0}, "_snapshot_workers64_ms")):
+                                    ("snap64", {"snapshot_workers_max": 0}, "_snapshot_workers64_ms"),
+                                    ("idle", {"idle_skip": 1}, "_idle_skip_ms")):
                 for k, v in vals.items():
                     comm.set_config(k, v)
                 try:

@@ -136,6 +136,10 @@ static std::atomic<int64_t> g_cfg_snapw{-1};
 // the host for its producer stream's work instead of the round stream waiting on the GPU (no
 // cross-stream dependency; the posting thread blocks until the gradient is written).
 static std::atomic<int64_t> g_cfg_evscope{-1}, g_cfg_psync{-1};
+// "idle_skip" (ESGD_IDLE_SKIP, default 0): a post (release) whose caller's stream has nothing
+// left to run (hipStreamQuery) records no producer (consumer) event -- the gradient is
+// written (the copy-out done) already, so the round stream has nothing to wait for
+static std::atomic<int64_t> g_cfg_idle{-1};
 
 static bool env_flag(const char *name) {
     const char *e = getenv(name);
@@ -145,6 +149,12 @@ static bool env_flag(const char *name) {
 static bool event_device_scope() {
     static const bool env = env_flag("ESGD_EVENT_DEVICE_SCOPE");
     const int64_t v = g_cfg_evscope.load(std::memory_order_relaxed);
+    return v >= 0 ? v != 0 : env;
+}
+
+static bool idle_skip() {
+    static const bool env = env_flag("ESGD_IDLE_SKIP");
+    const int64_t v = g_cfg_idle.load(std::memory_order_relaxed);
     return v >= 0 ? v != 0 : env;
 }
 
@@ -238,10 +248,13 @@ int config_set(const char *key, int64_t value) {
     } else if (!std::strcmp(key, "producer_host_sync")) {
         ESGD_ARG(value >= -1 && value <= 1, "producer_host_sync: 0 or 1 (-1: the default)");
         g_cfg_psync.store(value);
+    } else if (!std::strcmp(key, "idle_skip")) {
+        ESGD_ARG(value >= -1 && value <= 1, "idle_skip: 0 or 1 (-1: the default)");
+        g_cfg_idle.store(value);
     } else {
         set_error("esgd_set_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
                   "batch_rounds, batch_depth, snapshot_in_batch, inline_join, batch_hold, batch_workers_max, "
-                  "snapshot_workers_max, event_device_scope, producer_host_sync)", key);
+                  "snapshot_workers_max, event_device_scope, producer_host_sync, idle_skip)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -267,10 +280,11 @@ int config_get(const char *key, int64_t *value) {
     else if (!std::strcmp(key, "snapshot_workers_max")) *value = int64_t(snapshot_workers_max());
     else if (!std::strcmp(key, "event_device_scope")) *value = event_device_scope() ? 1 : 0;
     else if (!std::strcmp(key, "producer_host_sync")) *value = producer_host_sync() ? 1 : 0;
+    else if (!std::strcmp(key, "idle_skip")) *value = idle_skip() ? 1 : 0;
     else {
         set_error("esgd_get_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
                   "batch_rounds, launches, batch_workers, batch_depth, snapshot_in_batch, inline_join, batch_hold, "
-                  "batch_workers_max, snapshot_workers_max, event_device_scope, producer_host_sync)", key);
+                  "batch_workers_max, snapshot_workers_max, event_device_scope, producer_host_sync, idle_skip)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -862,6 +876,20 @@ void dataplane_group_end(int which) {
 static int note_event(int which, void *stream, std::shared_ptr<hipEvent_t> *out) {
     GroupEvent &g = g_group[which];
     const bool same = g.open && g.stream == stream;
+    if (idle_skip() && !(same && g.ev)) {
+        if (same && g.synced) {   // the group found the stream idle already
+            out->reset();
+            return ESGD_SUCCESS;
+        }
+        const hipError_t q = hipStreamQuery(user_stream(stream));
+        if (q == hipSuccess) {    // everything queued there has run: nothing to wait for
+            out->reset();
+            if (same) g.synced = true;
+            return ESGD_SUCCESS;
+        }
+        (void)hipGetLastError();  // hipErrorNotReady is not a failure; later checks must not see it
+        if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery", __FILE__, __LINE__);
+    }
     if (which == 0 && producer_host_sync()) {   // wait here; nothing for the GPU to wait on
         out->reset();
         if (same && g.synced) return ESGD_SUCCESS;
@@ -917,8 +945,12 @@ static int base_note_producer(BaseState &st, uint32_t round, void *stream) {
 }
 
 static int base_note_consumer(BaseState &st, void *stream) {
-    if (int rc = note_event(1, stream, &st.consumer)) return rc;
-    st.consumer_pending = true;
+    std::shared_ptr<hipEvent_t> ev;
+    if (int rc = note_event(1, stream, &ev)) return rc;
+    if (ev) {   // none: the caller's stream was idle (idle_skip), nothing more to wait for
+        st.consumer = std::move(ev);
+        st.consumer_pending = true;
+    }
     return ESGD_SUCCESS;
 }
 

@@ -113,11 +113,12 @@ def test_host_path_switches():
     # them inside one job), -1 restores the env default
     from esgd import _lib, comm  # noqa: F401
     lib = _lib.lib()
-    defaults = {"batch_depth": 1, "snapshot_in_batch": 1, "inline_join": 1}
-    for key, bad in (("batch_depth", -2), ("snapshot_in_batch", 2), ("inline_join", 2)):
+    defaults = {"batch_depth": 1, "snapshot_in_batch": 1, "inline_join": 1,
+                "idle_skip": int(os.environ.get("ESGD_IDLE_SKIP", "0") == "1")}
+    for key, bad in (("batch_depth", -2), ("snapshot_in_batch", 2), ("inline_join", 2), ("idle_skip", 2)):
         assert lib.esgd_set_config(key.encode(), bad) == _lib.INVALID_ARG
     try:
-        for key, v in (("batch_depth", 3), ("snapshot_in_batch", 0), ("inline_join", 0)):
+        for key, v in (("batch_depth", 3), ("snapshot_in_batch", 0), ("inline_join", 0), ("idle_skip", 1)):
             comm.set_config(key, v)
             assert comm.get_config(key) == v
     finally:
