@@ -680,6 +680,7 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
         pipelined()
         fused_step()
     t161 = _timed_steps(comm, chain, steps)
+    chain_stages = _round_stages_us(scheds)
     l0, p0 = comm.get_config("launches"), comm.profile()
     t161p = _timed_steps(comm, pipelined, steps)
     launches = (comm.get_config("launches") - l0) / steps
@@ -715,6 +716,7 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
     return {"buckets": len(lengths), "fp32_elements": total,
             "step_ms_161_buckets": round(t161 * 1e3, 3),
             "step_ms_161_buckets_pipelined": round(t161p * 1e3, 3),
+            "rank0_chain_round_stages_us": chain_stages,
             "step_ms_one_fused_bucket": round(t1 * 1e3, 3),
             "fused_speedup": round(t161 / t1, 2), "steps": steps,
             "rank0_launches_per_pipelined_step": launches,
@@ -866,6 +868,30 @@ def _step_breakdown_us(scheds):
             "gpu_us_per_bucket": round(float(tl[:, 4].max() - tl[:, 2].min()) / 1e3 / len(tl), 2)}
 
 
+def _round_stages_us(scheds):
+    """A chain of rounds, one at a time (the reference's blocking pattern): where a round's
+    time goes on this rank, the median over the schedules' last rounds of each stage of the
+    host timeline (esgd_schedule_timeline), in us -- post -> join -> launch start -> launch
+    queued -> completion seen -> wait returned; and the median time from one round's post
+    to the next one's (the chain's cycle: what the caller does between rounds included)."""
+    import numpy as np
+    rows = []
+    for s in scheds:
+        tl = (s.timeline() if hasattr(s, "timeline") else _timeline_of(s)).astype(np.int64)
+        tl = tl[(tl[:, 0] > 0) & (tl[:, 5] > 0) & (tl[:, 1] > 0) & (tl[:, 2] > 0)]
+        if len(tl):
+            rows.append(tl[-1])
+    if len(rows) < 2:
+        return None
+    tl = np.array(rows)
+    tl = tl[np.argsort(tl[:, 0])]
+    med = lambda a: round(float(np.median(a)) / 1e3, 2)   # noqa: E731
+    return {"post_to_join": med(tl[:, 1] - tl[:, 0]), "join_to_launch": med(tl[:, 2] - tl[:, 1]),
+            "launch_host": med(tl[:, 3] - tl[:, 2]), "launch_to_completion": med(tl[:, 4] - tl[:, 3]),
+            "completion_to_wait": med(tl[:, 5] - tl[:, 4]), "post_to_wait": med(tl[:, 5] - tl[:, 0]),
+            "cycle": med(np.diff(tl[:, 0])), "rounds": len(tl)}
+
+
 def optimizer_resnet50_161(comm, rank, world, steps=8):
     """The drop-in caller path at C4's shape: EagerSGDOptimizer (majority, the reference's
     seed) over 161 torch parameters with the ResNet-50 bucket lengths
@@ -934,6 +960,7 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
         else:
             out["fused_breakdown_us"] = _fused_breakdown(comm, opt, params, steps)
         if name == "per_tensor_blocking":
+            out[name + "_round_stages_us"] = _round_stages_us([op.schedule() for op in opt._ops.values()])
             # idle_skip: a post / release whose caller's stream is idle records no event (the
             # round stream has nothing to wait for) -- the reference's blocking chain, 161
             # cross-stream waits a step otherwise
