@@ -964,12 +964,17 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
             # idle_skip: a post / release whose caller's stream is idle records no event (the
             # round stream has nothing to wait for) -- the reference's blocking chain, 161
             # cross-stream waits a step otherwise
-            comm.set_config("idle_skip", 1)
-            try:
-                step()
-                out[name + "_idle_skip_ms"] = round(_timed_steps(comm, step, steps) * 1e3, 3)
-            finally:
-                comm.set_config("idle_skip", -1)
+            # snapshot_in_batch 0: the round's copy-in (grad / P into the bucket) as a kernel
+            # queued before the round's launch instead of its phase 0 (the ready is then
+            # published at the launch's start)
+            for key, val, what in (("idle_skip", 1, "_idle_skip"), ("snapshot_in_batch", 0, "_snapshot_before_launch")):
+                comm.set_config(key, val)
+                try:
+                    step()
+                    out[name + what + "_ms"] = round(_timed_steps(comm, step, steps) * 1e3, 3)
+                    out[name + what + "_round_stages_us"] = _round_stages_us([op.schedule() for op in opt._ops.values()])
+                finally:
+                    comm.set_config(key, -1)
         if name == "per_tensor_pipelined":
             # A/B of the same step with one launch per round (esgd_set_config, process-local).
             # (r05d-r05g also A/B'd a device-scope event release and a host-side producer
