@@ -964,10 +964,9 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
             # idle_skip: a post / release whose caller's stream is idle records no event (the
             # round stream has nothing to wait for) -- the reference's blocking chain, 161
             # cross-stream waits a step otherwise
-            # snapshot_in_batch 0: the round's copy-in (grad / P into the bucket) as a kernel
-            # queued before the round's launch instead of its phase 0 (the ready is then
-            # published at the launch's start)
-            for key, val, what in (("idle_skip", 1, "_idle_skip"), ("snapshot_in_batch", 0, "_snapshot_before_launch")):
+            # (r05ah also A/B'd the copy-in as a kernel before the launch, snapshot_in_batch 0:
+            # 10.52 vs 10.20 ms, dropped)
+            for key, val, what in (("idle_skip", 1, "_idle_skip"),):
                 comm.set_config(key, val)
                 try:
                     step()
