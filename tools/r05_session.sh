@@ -1,6 +1,8 @@
 export ESGD_TIMEOUT_S=60
-O=gpurun_out/r05aj
+O=gpurun_out/r05ak
 mkdir -p $O
+L="python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 examples/resnet50_eager_sgd.py --mode allreduce --steps 20 --batch 64 --image 224"
 bash tools/gpu_steps.sh $O \
-  "400 bash tools/bench_round.sh r05aj n2 n4c4" \
-  "650 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread"
+  "240 $L > $O/example_full_after.json" \
+  "240 $L --overlap > $O/example_full_overlap.json" \
+  "240 $L --fuse > $O/example_full_fused.json"
