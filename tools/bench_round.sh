@@ -24,7 +24,7 @@ for s in $STEPS; do
           --output-format csv -- python $R/bench.py --no-pmc --no-trace --no-cpu-baseline --steps 100 \
           > $R/$O/bench_prof.json 2>&1) ;;
   profopt) (cd /tmp && export TMPDIR=/tmp && ESGD_BENCH_LEGS=optimizer_resnet50_161 ESGD_BENCH_RCCL=0 \
-          timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/profopt -o run --output-format csv \
+          timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/profopt -o run_%pid% --output-format csv \
           -- python $R/bench.py --gpus 2 --steps 20 --warmup 5 > $R/$O/bench_profopt_n2.json 2>&1) ;;
   bisect) timeout -k 10 500 python -u tools/ipc_bisect.py > $O/ipc_bisect.txt 2>&1 ;;
   sweep) test -f tools/bin/libesgd_sweeps.so   # built here by `make sweeps` (build() does it)
