@@ -983,6 +983,7 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
             # others, instead of 256 (the default since r05ac)
             for key, vals, what in (("batch_rounds", {"batch_rounds": 0}, "_one_launch_per_round_ms"),
                                     ("snap64", {"snapshot_workers_max": 0}, "_snapshot_workers64_ms"),
+                                    ("snap512", {"snapshot_workers_max": 512}, "_snapshot_workers512_ms"),
                                     ("idle", {"idle_skip": 1}, "_idle_skip_ms")):
                 for k, v in vals.items():
                     comm.set_config(k, v)
