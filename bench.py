@@ -980,10 +980,9 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
             # sync here: within noise every time, profiles/r05/README.md; dropped)
             # snapshot_workers_max 0: shared launches that hold the rounds' snapshots of the
             # gradients (phase 0, a plain copy) capped at batch_workers_max (64) like the
-            # others, instead of 256 (the default since r05ac)
+            # others, instead of 256 (the default since r05ac; 512 in r05ao: no further gain)
             for key, vals, what in (("batch_rounds", {"batch_rounds": 0}, "_one_launch_per_round_ms"),
                                     ("snap64", {"snapshot_workers_max": 0}, "_snapshot_workers64_ms"),
-                                    ("snap512", {"snapshot_workers_max": 512}, "_snapshot_workers512_ms"),
                                     ("idle", {"idle_skip": 1}, "_idle_skip_ms")):
                 for k, v in vals.items():
                     comm.set_config(k, v)
