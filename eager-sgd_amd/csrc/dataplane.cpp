@@ -225,9 +225,6 @@ int config_set(const char *key, int64_t value) {
     } else if (!std::strcmp(key, "batch_depth")) {
         ESGD_ARG(value >= -1, "batch_depth: >= 0 shared launches queued before one is held (-1: the default)");
         g_cfg_depth.store(value);
-    } else if (!std::strcmp(key, "snapshot_in_batch")) {
-        ESGD_ARG(value >= -1 && value <= 1, "snapshot_in_batch: 0 or 1 (-1: the default)");
-        g_cfg_snap.store(value);
     } else if (!std::strcmp(key, "inline_join")) {
         ESGD_ARG(value >= -1 && value <= 1, "inline_join: 0 or 1 (-1: the default)");
         g_cfg_inline.store(value);
@@ -262,7 +259,6 @@ int config_set(const char *key, int64_t value) {
 
 static int batch_depth();
 static uint32_t snapshot_workers_max();
-static bool snapshot_in_batch();
 
 int config_get(const char *key, int64_t *value) {
     ESGD_ARG(key && value, "esgd_get_config: null argument");
@@ -273,7 +269,6 @@ int config_get(const char *key, int64_t *value) {
     else if (!std::strcmp(key, "launches")) *value = int64_t(g_launches.load());
     else if (!std::strcmp(key, "batch_workers")) *value = g_batch_workers.load();
     else if (!std::strcmp(key, "batch_depth")) *value = batch_depth();
-    else if (!std::strcmp(key, "snapshot_in_batch")) *value = snapshot_in_batch() ? 1 : 0;
     else if (!std::strcmp(key, "inline_join")) *value = config_inline_join() ? 1 : 0;
     else if (!std::strcmp(key, "batch_hold")) *value = g_cfg_hold.load();
     else if (!std::strcmp(key, "batch_workers_max")) *value = int64_t(batch_workers_max());
@@ -503,8 +498,11 @@ static void *host_view(void *host) {
     return d;
 }
 
-int round_sync(const PairFlags &f, int world, uint32_t value, long long timeout_ticks,
-               uint32_t *err, uint32_t errval, uint64_t *ts, uint32_t *gate, uint32_t *fin, hipStream_t s);
+// errs: every rank's error word (the node segment); after_fail: a pairing after the round's
+// first publishes nothing once this rank's error word holds the round (failure contract)
+int round_sync(const PairFlags &f, int world, int rank, uint32_t value, long long timeout_ticks,
+               uint32_t *errs, uint32_t errval, bool after_fail, uint64_t *ts, uint32_t *gate, uint32_t *fin,
+               hipStream_t s);
 
 // ---- device pairing flags (schedules with flag_mode 1 or 2, opt-in) ----
 // Each rank owns a page of HBM per mode -- uncached (hipDeviceMallocUncached: loads and
@@ -609,8 +607,8 @@ static int pair_ranks(Sched &s, std::atomic<uint32_t> *flags, int which, uint32_
         if (int rc = ctr_words(s.id, cs, &ctr)) return rc;
         gate = ctr + 4 + which;
     }
-    return round_sync(pair_flags(s, flags, which), s.world, value ? value : round, ticks,
-                      dev_flag(&s.sh->gpu_err[s.rank]), round, ts, gate, fin ? dev_flag(fin) : nullptr, cs);
+    return round_sync(pair_flags(s, flags, which), s.world, s.rank, value ? value : round, ticks,
+                      dev_flag(&s.sh->gpu_err[0]), round, which > 0, ts, gate, fin ? dev_flag(fin) : nullptr, cs);
 }
 
 // ns between the GPU stamps of the last round (ESGD_GPU_TRACE=1), for the timeline
@@ -746,12 +744,8 @@ struct IpcState : BaseState {
     PeerMap rbmap[kMaxRanks], pubmap[kMaxRanks];
     // batched one-launch rounds: this schedule's BatchDesc is in the device table
     bool desc_built = false;
-    // the round's snapshot, deferred into the shared launch's copy kernel (k_copy_many):
-    // rb_dev = snap_src (nullptr: zeros), snap_bytes bytes
-    bool snap = false;
-    const void *snap_src = nullptr;
-    size_t snap_bytes = 0;
-    // ... or done by the launch's own workers (ESGD_SNAPSHOT_IN_BATCH): 1 rb = sb, 2 rb = 0
+    // the round's snapshot, done by the shared launch's own workers (phase 0): 1 rb = sb,
+    // 2 rb = 0, 3 rb = src / divisor (0: queued before the launch, or none)
     uint8_t snap_kind = 0;
     uint32_t t1 = 0, t2 = 0;          // its phase-1 / phase-2 tiles
 };
@@ -1236,6 +1230,27 @@ static std::string base_diagnose(Sched &s) {
     return m + ")";
 }
 
+// The failure contract: a round that failed on ANY rank -- a GPU flag wait
+// that timed out, or that found a peer's error word holding the round -- fails here too.
+// The GPU side already keeps a failed rank from publishing reduced / fin for the round, so
+// a late peer cannot complete it from that rank's stale shard; this check also fails a
+// round this rank completed while a peer gave up on it.
+static int round_failed(Sched &s) {
+    if (s.world < 2) return 0;
+    for (int q = 0; q < s.world; ++q) {
+        if (s.sh->gpu_err[q].load(std::memory_order_acquire) != s.cur) continue;
+        if (q == s.rank)
+            set_error("this rank's GPU waited more than %.0f s for its peers in round %u %s", engine_timeout(), s.cur,
+                      base_diagnose(s).c_str());
+        else
+            set_error("rank %d failed round %u (its GPU flag wait timed out or saw a failure), so this rank fails "
+                      "it too %s",
+                      q, s.cur, base_diagnose(s).c_str());
+        return ESGD_ERROR;
+    }
+    return 0;
+}
+
 static int base_query(Sched &s, BaseState &st) {
     if (st.batch_rc) return st.batch_rc;   // error message set by the failed launch
     if (st.fin_mode) {   // the round's last kernel writes fin (finish_round, k_round_small, done pairing)
@@ -1245,11 +1260,7 @@ static int base_query(Sched &s, BaseState &st) {
         // fin seen here comes with the error of that round, if there was one (a timed-out
         // k_round_small leaves without fin: the error alone fails the round then)
         const bool finished = int32_t(s.sh->fin[s.rank].load(std::memory_order_acquire) - s.cur) >= 0;
-        if (s.world > 1 && s.sh->gpu_err[s.rank].load(std::memory_order_acquire) == s.cur) {
-            set_error("this rank's GPU waited more than %.0f s for its peers in round %u %s",
-                      engine_timeout(), s.cur, base_diagnose(s).c_str());
-            return ESGD_ERROR;
-        }
+        if (int rc = round_failed(s)) return rc;
         if (finished) {
             // the kernel may still be retiring (not ready is fine); a fault is reported
             // against this round, not a later one
@@ -1274,11 +1285,7 @@ static int base_query(Sched &s, BaseState &st) {
                   (unsigned long long)s.count, s.dtype);
         return ESGD_ERROR;
     }
-    if (s.world > 1 && s.sh->gpu_err[s.rank].load(std::memory_order_acquire) == s.cur) {
-        set_error("this rank's GPU waited more than %.0f s for its peers in round %u %s",
-                  engine_timeout(), s.cur, base_diagnose(s).c_str());
-        return ESGD_ERROR;
-    }
+    if (int rc = round_failed(s)) return rc;
     return 1;
 }
 
@@ -1310,14 +1317,6 @@ struct BatchEntry {
     RoundIO io;     // the round's own data (src nullptr: none; dst nullptr: results in rb)
 };
 
-// ESGD_SNAPSHOT_IN_BATCH (default 1): a batched round's snapshot is phase 0 of the shared
-// launch itself instead of a k_copy_many launch queued before it (one launch per flush)
-static bool snapshot_in_batch() {
-    static const bool env = !(getenv("ESGD_SNAPSHOT_IN_BATCH") && *getenv("ESGD_SNAPSHOT_IN_BATCH") == '0');
-    const int64_t v = g_cfg_snap.load(std::memory_order_relaxed);
-    return v >= 0 ? v != 0 : env;
-}
-
 // the whole-bucket snapshot (rb = src) fits the kernel's 32-bit buffer ranges and 16-B
 // vectors (src nullptr: rb alone)
 static bool snap_eligible(const Sched &s, const IpcState &st, const void *src) {
@@ -1327,14 +1326,12 @@ static bool snap_eligible(const Sched &s, const IpcState &st, const void *src) {
 }
 static std::vector<BatchEntry> g_pend;
 static uint64_t g_batch_seq = 0;   // shared launches sent so far (g_batch_mu)
-static CopySet g_copy;   // the pending launch's snapshots (nseg 0: none)
-// the shared launches' tile counter (BatchArgs::queue; a device word behind the descriptor
-// table) and its value when the next launch starts
-static uint32_t *g_queue = nullptr;
-static uint32_t g_qnext = 0;
+// the shared launches' tile bookkeeping (BatchArgs::slots: kLaunchSlots x kSlotWords device
+// words behind the descriptor table); launch n uses slot n % kLaunchSlots, and each launch
+// zeroes the others on the GPU, so no host count has to track the device's
+static uint32_t *g_slots = nullptr;
+static uint32_t g_slot_seq = 0;
 
-// ESGD_BATCH_STATIC=1: static tile assignment in shared launches (an A/B of the dynamic
-// counter; needs every worker resident at once)
 uint32_t batch_workers_max() {
     static const uint32_t env = [] {
         const char *e = getenv("ESGD_BATCH_WORKERS");
@@ -1356,10 +1353,6 @@ static uint32_t snapshot_workers_max() {
     return w ? std::max(w, batch_workers_max()) : batch_workers_max();
 }
 
-static bool batch_static() {
-    static const bool on = getenv("ESGD_BATCH_STATIC") && *getenv("ESGD_BATCH_STATIC") == '1';
-    return on;
-}
 // shared launches queued and not yet seen complete, oldest first (their events)
 static std::deque<std::shared_ptr<hipEvent_t>> g_outstanding;
 
@@ -1384,12 +1377,13 @@ static int batch_depth() {
 static int batch_desc(Sched &s, IpcState &st, hipStream_t cs) {
     if (st.desc_built) return ESGD_SUCCESS;
     if (!g_desc_dev) {
-        ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&g_desc_dev), sizeof(BatchDesc) * kMaxSched + 256));
+        const size_t slot_bytes = size_t(kLaunchSlots) * kSlotWords * sizeof(uint32_t);
+        ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&g_desc_dev), sizeof(BatchDesc) * kMaxSched + slot_bytes));
         ESGD_HIP(hipHostMalloc(reinterpret_cast<void **>(&g_desc_host), sizeof(BatchDesc) * kMaxSched,
                                hipHostMallocDefault));
-        g_queue = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(g_desc_dev) + sizeof(BatchDesc) * kMaxSched);
-        ESGD_HIP(hipMemsetAsync(g_queue, 0, 256, cs));   // ahead of every launch on this stream
-        g_qnext = 0;
+        g_slots = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(g_desc_dev) + sizeof(BatchDesc) * kMaxSched);
+        ESGD_HIP(hipMemsetAsync(g_slots, 0, slot_bytes, cs));   // ahead of every launch on this stream
+        g_slot_seq = 0;
     }
     if (!st.ctr)
         if (int rc = ctr_words(s.id, cs, &st.ctr)) return rc;
@@ -1513,23 +1507,18 @@ static int batch_flush_locked() {
         set_error("batched rounds: no residency figure for dtype %d at %d ranks", g_pend[0].s->dtype,
                   g_pend[0].s->world);
         rc = ESGD_ERROR;
-        g_copy.nseg = 0;
     }
-    if (!rc && g_copy.nseg) {   // every entry's snapshot, before the launch that publishes its ready
-        rc = copy_many(g_copy, cs);
-        g_copy.nseg = 0;
-        if (!rc) ++g_launches;
-    }
-    // the tile counter: every worker's last grab finds the list done, so one launch moves
-    // it by (tiles + workers); a launch starts once the previous one on the stream ended
-    a.dynamic = batch_static() ? 0u : 1u;
-    a.queue = g_queue;
-    a.qbase = g_qnext;
+    // the launch's slot: zeroed by the previous launch that ran on this stream (every
+    // launch zeroes all slots but its own), whatever the host believes of earlier launches
+    a.slots = g_slots;
+    a.slot = g_slot_seq++ % kLaunchSlots;
+    // ranks sharing this GPU: a worker spinning on a closed gate for 2 ms gives its wave
+    // slots back -- the peer launch that opens the gate may be waiting for them (DESIGN.md
+    // §5, "Forward progress"); with a GPU per rank nothing of the job competes for them
+    a.yield = sharing > 1 ? (long long)(2e-3 * double(g_ticks_per_s)) : 0;
+    (void)hipGetLastError();   // a stale status (e.g. an event query's not-ready) is not this launch's
     if (!rc) rc = round_batch(g_pend[0].s->dtype, g_pend[0].s->world, a, workers, cs);
-    if (!rc) {
-        g_batch_workers.store(int64_t(workers), std::memory_order_relaxed);
-        if (a.dynamic) g_qnext += t0 + t1 + t2 + workers;
-    }
+    if (!rc) g_batch_workers.store(int64_t(workers), std::memory_order_relaxed);
     std::shared_ptr<hipEvent_t> sp;
     if (!rc) {
         sp = pooled_event();
@@ -1571,6 +1560,7 @@ int dataplane_flush_soft() {
     if (const int depth = batch_depth()) {
         while (!g_outstanding.empty() && hipEventQuery(*g_outstanding.front()) != hipErrorNotReady)
             g_outstanding.pop_front();   // finished (a fault is reported by its rounds)
+        (void)hipGetLastError();   // the not-ready status is not an error of the next launch
         if (int(g_outstanding.size()) >= depth) return ESGD_SUCCESS;
     }
     const double t0 = now_s();
@@ -1623,19 +1613,18 @@ void dataplane_profile(uint64_t *launches, uint64_t *flush_ns) {
 }
 
 // The snapshot of a round that goes out in a shared launch: the caller's producer and
-// consumer events are waited for now, on the round stream; the copy itself (rb = sb, or
-// rb = 0 for a FRESH_ONLY round this rank had not posted) joins the launch's k_copy_many
-// when the buckets are 16-B aligned and the copy fits the 32-bit descriptor range (else
-// it is queued now, as base_copy_in would).
+// consumer events are waited for now, on the round stream; the copy itself (rb = sb, rb = 0
+// for a FRESH_ONLY round this rank had not posted, or rb = src / divisor) is phase 0 of the
+// launch when the buckets are 16-B aligned and the copy fits the 32-bit descriptor range
+// (else it is queued now, as base_copy_in would).
 static int batch_snapshot(Sched &s, IpcState &st, uint32_t round, bool fresh, hipStream_t cs) {
     if (int rc = consumer_wait(st, cs)) return rc;
     if (int rc = producer_wait(st, round, fresh, cs)) return rc;
-    st.snap = false;
     st.snap_kind = 0;
     const size_t bytes = s.count * s.esize;
     if (!bytes) return ESGD_SUCCESS;
     if (st.io_on) {   // the round's own data (post_io): rb = src / div
-        if (snapshot_in_batch() && snap_eligible(s, st, st.cur_io.src)) {   // phase 0 of the shared launch
+        if (snap_eligible(s, st, st.cur_io.src)) {   // phase 0 of the shared launch
             st.snap_kind = st.cur_io.div == 1.0f ? 1 : 3;
             return ESGD_SUCCESS;
         }
@@ -1649,19 +1638,12 @@ static int batch_snapshot(Sched &s, IpcState &st, uint32_t round, bool fresh, hi
     else if (s.zero_sb) return move_zero(st.rb_dev, s.sb, bytes, cs);
     else if (!s.in_place) src = s.sb;
     else return ESGD_SUCCESS;                              // in place: nothing to move
-    if (snapshot_in_batch() && snap_eligible(s, st, src)) {   // phase 0 of the shared launch
+    if (snap_eligible(s, st, src)) {   // phase 0 of the shared launch
         st.snap_kind = src ? 1 : 2;
         return ESGD_SUCCESS;
     }
-    const uintptr_t al = reinterpret_cast<uintptr_t>(st.rb_dev) | reinterpret_cast<uintptr_t>(src);
-    if ((al & 15) || bytes >= (size_t(1) << 31)) {   // (a launch holds as many copies as rounds: <= kBatchMax)
-        if (!src) ESGD_HIP(hipMemsetAsync(st.rb_dev, 0, bytes, cs));
-        else ESGD_HIP(hipMemcpyAsync(st.rb_dev, src, bytes, hipMemcpyDeviceToDevice, cs));
-        return ESGD_SUCCESS;
-    }
-    st.snap = true;
-    st.snap_src = src;
-    st.snap_bytes = bytes;
+    if (!src) ESGD_HIP(hipMemsetAsync(st.rb_dev, 0, bytes, cs));
+    else ESGD_HIP(hipMemcpyAsync(st.rb_dev, src, bytes, hipMemcpyDeviceToDevice, cs));
     return ESGD_SUCCESS;
 }
 
@@ -1673,18 +1655,6 @@ static int batch_append(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) 
                             int64_t(g_pend.size()) >= batch_rounds()))
         batch_flush_locked();   // a failure is recorded in the rounds of that launch
     if (int rc = batch_desc(s, st, cs)) return rc;
-    if (st.snap) {
-        CopySet &c = g_copy;
-        if (c.nseg == 0) c.tile0[0] = 0;
-        const int i = c.nseg++;
-        c.src[i] = st.snap_src;
-        c.dst[i] = st.rb_dev;
-        c.nvec[i] = uint32_t(st.snap_bytes / 16);
-        c.tail[i] = uint32_t(st.snap_bytes % 16);
-        const uint32_t tiles = (c.nvec[i] + 1023) / 1024 + (c.nvec[i] == 0 && c.tail[i] ? 1 : 0);
-        c.tile0[i + 1] = c.tile0[i] + tiles;
-        st.snap = false;
-    }
     st.pub_round = round;
     st.fin_mode = true;
     st.batch_rc = 0;
@@ -1729,7 +1699,7 @@ static void batch_shutdown() {
         w.ev.reset();
     }
     g_outstanding.clear();
-    if (g_desc_dev) { hip_ignore(hipFree(g_desc_dev)); g_desc_dev = nullptr; g_queue = nullptr; }
+    if (g_desc_dev) { hip_ignore(hipFree(g_desc_dev)); g_desc_dev = nullptr; g_slots = nullptr; }
     if (g_desc_host) { hip_ignore(hipHostFree(g_desc_host)); g_desc_host = nullptr; }
     std::lock_guard<std::mutex> ek(g_evfree_mu);
     for (auto &pool : g_evfree) {

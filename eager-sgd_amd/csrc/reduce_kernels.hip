@@ -713,17 +713,26 @@ int seal_read(const void *src, uint64_t w[4]) {
 // Every rank's flag at once: lane q polls flags[q] (relaxed, system scope) and the wave
 // leaves when all of them reached `value` -- one host-memory round trip per sweep instead
 // of one per rank (8 serial PCIe reads at P = 8).  Called by a whole wave; rounds compare
-// modulo 2^32.  False on timeout.
+// modulo 2^32.  False on timeout -- or, every 16th sweep, when some rank's error word
+// (errs[q], the node segment's per-rank words; nullptr: not checked) holds `errval`: a rank
+// that failed this round publishes nothing more for it (the failure contract),
+// so waiting for it could only end in the timeout.
 __device__ __forceinline__ bool wave_wait_all(const uint32_t *flags, int world, uint32_t value, long long t0,
-                                              long long timeout) {
+                                              long long timeout, const uint32_t *errs = nullptr,
+                                              uint32_t errval = 0) {
     const int lane = int(threadIdx.x & 63u);
+    unsigned sweep = 0;
     for (;;) {
-        bool mine = true;
-        if (lane < world)
+        bool mine = true, bad = false;
+        if (lane < world) {
             mine = int32_t(__hip_atomic_load(const_cast<uint32_t *>(&flags[lane]), __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_SYSTEM) - value) >= 0;
+            if (!mine && errs && (++sweep & 15u) == 0)
+                bad = __hip_atomic_load(const_cast<uint32_t *>(&errs[lane]), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_SYSTEM) == errval;
+        }
         if (__all(mine)) return true;
-        if (wall_clock64() - t0 > timeout) return false;
+        if (__any(bad) || wall_clock64() - t0 > timeout) return false;
         __builtin_amdgcn_s_sleep(1);
     }
 }
@@ -745,17 +754,22 @@ __device__ __forceinline__ void publish_flags_drained(const PairFlags &f, uint32
 }
 
 //
+//
 // Peer buckets are coarse-grained memory of other processes (other GPUs on a node).  When
 // the phase after this pairing reads peers (`gate` != nullptr), every XCD's L2 (and the
 // L1 of every CU used) must first drop whatever lines of them it may still hold from an
 // earlier round: the launch then has one workgroup per CU (dealt round-robin over the
 // XCDs); workgroup 0 runs the pairing and raises the device word `gate` to `value`, the
 // others wait for it and run a system-scope acquire (buffer_inv sc0 sc1).  The dispatch's
-// own acquire scope is not relied on for this.  A timed-out pairing still raises the gate
-// (the error flag fails the round), so no workgroup is left waiting.
-__global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world,
+// own acquire scope is not relied on for this.  A failed pairing still raises the gate
+// (the error word fails the round), so no workgroup is left waiting.
+// Failure contract: `errs` = every rank's error word (this rank's is errs[rank]); a pairing
+// after the round's first (`after_fail`: reduced, done) publishes nothing when this rank's
+// error word already holds the round -- its shard was folded from stale peer buckets, and a
+// late peer must not take it for the round's (What's weak 1).
+__global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world, int rank,
                                                    uint32_t value, long long timeout,
-                                                   uint32_t *err, uint32_t errval, uint64_t *ts,
+                                                   uint32_t *errs, uint32_t errval, int after_fail, uint64_t *ts,
                                                    uint32_t *gate, uint32_t *fin) {
     const bool lead = threadIdx.x == 0;
     if (blockIdx.x != 0) {   // cache maintenance only
@@ -769,12 +783,20 @@ __global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world,
         }
         return;
     }
+    uint32_t *err = errs + rank;
+    __shared__ int failed;
     if (lead) {
+        failed = after_fail && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == errval;
         if (ts) ts[0] = uint64_t(wall_clock64());
-        publish_flags(f, value);
+        if (!failed) publish_flags(f, value);
+    }
+    __syncthreads();
+    if (failed) {   // nothing published, nothing waited for; the waiting workgroups leave
+        if (lead && gate) __hip_atomic_store(gate, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
     }
     const long long t0 = wall_clock64();
-    const bool ok = wave_wait_all(f.mine, world, value, t0, timeout);
+    const bool ok = wave_wait_all(f.mine, world, value, t0, timeout, errs, errval);
     if (!lead) return;
     if (!ok) __hip_atomic_store(err, errval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -790,12 +812,14 @@ __global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world,
 // ts (optional): wall-clock stamps of entry and exit (tracing, ESGD_GPU_TRACE=1);
 // errval: what a timed-out wait records in *err (the round, also when `value` numbers
 // a chunk of it)
-int round_sync(const PairFlags &f, int world, uint32_t value, long long timeout_ticks,
-               uint32_t *err, uint32_t errval, uint64_t *ts, uint32_t *gate, uint32_t *fin, hipStream_t s) {
-    ESGD_ARG(f.mine && err && world >= 1 && world <= kPairMax && f.ndst >= 1 && f.ndst <= kPairMax,
+int round_sync(const PairFlags &f, int world, int rank, uint32_t value, long long timeout_ticks,
+               uint32_t *errs, uint32_t errval, bool after_fail, uint64_t *ts, uint32_t *gate, uint32_t *fin,
+               hipStream_t s) {
+    ESGD_ARG(f.mine && errs && world >= 1 && world <= kPairMax && rank >= 0 && rank < world && f.ndst >= 1 &&
+                 f.ndst <= kPairMax,
              "round_sync: bad arguments");
-    hipLaunchKernelGGL(k_round_sync, dim3(gate ? unsigned(cu_count()) : 1u), dim3(64), 0, s, f, world,
-                       value, timeout_ticks, err, errval, ts, gate, fin);
+    hipLaunchKernelGGL(k_round_sync, dim3(gate ? unsigned(cu_count()) : 1u), dim3(64), 0, s, f, world, rank,
+                       value, timeout_ticks, errs, errval, after_fail ? 1 : 0, ts, gate, fin);
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;
 }
@@ -861,7 +885,7 @@ __device__ __forceinline__ bool block_wait(const SmallRoundArgs &a, const uint32
     if (threadIdx.x < 64) {   // the first wave
         bool good = true;
         if (leader) {         // every rank's flag at once, one lane per rank
-            good = wave_wait_all(flags, a.world, a.value, t0, a.timeout);
+            good = wave_wait_all(flags, a.world, a.value, t0, a.timeout, a.err - a.rank, a.value);
             // relaxed: the gate carries no data of this workgroup's -- every waiter runs
             // its own system-scope acquire after seeing it (an agent release here was a
             // buffer_wbl2 sc1, ~1.7 us, on every pairing's critical path)

@@ -61,7 +61,8 @@ struct BatchDesc {
     uint32_t *fin, *err;               // SchedShm::fin[rank], gpu_err[rank] (device views)
     uint32_t *ctr;                     // device words: [0] phase-1 arrivals, [1] phase-2
                                        // arrivals, [2] ready gate, [3] reduced gate,
-                                       // [4] snapshot arrivals
+                                       // [4] snapshot arrivals, [5] the round that failed
+                                       // here (no reduced / fin is published for it)
     // the snapshot inside the launch (BatchArgs::snap): rb = sb, or rb = 0, whole bucket
     const void *ssrc;                  // sb (nullptr: in place)
     void *sdst;                        // rb
@@ -79,27 +80,44 @@ struct BatchDesc {
     uint64_t own_off;
 };
 
+// The launch's tile bookkeeping: kLaunchSlots slots of kSlotWords device words behind the
+// descriptor table, launch n using slot n % kLaunchSlots.  Block 0 of every launch zeroes
+// every OTHER slot before any tile is taken, so the next launch on the round stream (which
+// starts only once this one has ended) finds its slot at zero whatever happened before --
+// a launch the host counted as failed but that ran, a launch that ended on a timeout
+// (a device counter the host had to mirror could drift for good).
+constexpr uint32_t kLaunchSlots = 4;
+constexpr uint32_t kSlotWords = 1024;
+constexpr uint32_t kSlotQueue = 0;   // next tile of the list (fetch-add)
+constexpr uint32_t kSlotDone = 1;    // tiles finished (the agent block leaves at T)
+constexpr uint32_t kSlotTail = 3;    // tiles deferred (each by a worker that gave its slots back)
+constexpr uint32_t kSlotRing = 8;    // deferred tiles (tile + 1; 0: being written; ~0: taken)
+static_assert(kSlotRing + kBatchWorkersMax <= kSlotWords, "one deferral per worker at most");
+
 // Kernel arguments: the entries of one launch, in issue-ring order.
 struct BatchArgs {
     const BatchDesc *table;            // device table, indexed by schedule id
-    // Tile assignment.  dynamic: every worker takes the next tile of the launch's list from
-    // the process's tile counter (*queue - qbase), in ring order, until the list is done --
-    // a tile is only started after every earlier tile was, so the launch completes with
-    // ANY number of its workers resident (one suffices; a concurrent kernel may hold the
-    // rest of the GPU).  Static (dynamic 0, ESGD_BATCH_STATIC=1, an A/B): tile g on worker
-    // 1 + g % workers -- every worker must then be resident at once.
-    uint32_t *queue;
-    uint32_t qbase;
-    uint32_t dynamic;
+    // Tile assignment: every worker takes the next tile of the launch's list from the slot's
+    // counter, in ring order, until the list is done -- a tile is only started after every
+    // earlier tile was, so the launch completes with ANY number of its workers resident.
+    uint32_t *slots;                   // kLaunchSlots x kSlotWords device words
+    uint32_t slot;                     // this launch's
     uint32_t nent;
+    // yield (ticks, 0: never): a worker whose tile's gate stays closed this long defers the
+    // tile (slot ring) and leaves, giving its wave slots back to the GPU; the agent block
+    // takes deferred tiles (any whose gate is open) and, once any were deferred, open tiles
+    // of the list itself.
+    // Set when ranks share this GPU: a peer's launch that cannot be dispatched beside our
+    // spinning workers is what opens their gates ("Forward progress").
+    long long yield;
     uint32_t tile1[kBatchMax + 1];     // phase-1 tiles before entry e (prefix)
     uint32_t tile2[kBatchMax + 1];     // phase-2 tiles before entry e (prefix)
     uint16_t sid[kBatchMax];
     uint32_t value[kBatchMax];         // the round of entry e
     long long timeout;                 // wall-clock ticks any flag wait may take
-    // snapshots done by the launch's own workers before the phases (ESGD_SNAPSHOT_IN_BATCH):
-    // entry e's kind (0 none / queued before the launch, 1 rb = sb, 2 rb = 0) and its
-    // 1024-vector tiles (prefix); the agent publishes e's ready once they have all landed
+    // snapshots done by the launch's own workers before the phases: entry e's kind (0 none /
+    // queued before the launch, 1 rb = sb, 2 rb = 0) and its 1024-vector tiles (prefix); the
+    // agent publishes e's ready once they have all landed
     uint32_t tile0[kBatchMax + 1];
     uint8_t snap[kBatchMax];           // 3: rb = isrc / idiv (fp32), the op's copy-in fused
     // the round's own send data and output (esgd_schedule_post_io): phase 0 reads isrc
@@ -110,18 +128,6 @@ struct BatchArgs {
 };
 static_assert(sizeof(BatchArgs) <= 4096, "k_round_batch's arguments must fit the kernel-argument segment");
 
-// The snapshots of a shared launch's rounds (rb = sb, or rb = 0 for a FRESH_ONLY round
-// this rank had not posted), all in one launch queued right before k_round_batch: up to
-// kBatchMax segments, 16-B aligned, write-through stores.
-struct CopySet {
-    const void *src[kBatchMax];        // nullptr: zero-fill
-    void *dst[kBatchMax];
-    uint32_t nvec[kBatchMax];          // 16-B vectors
-    uint32_t tail[kBatchMax];          // bytes after the last full vector
-    uint32_t tile0[kBatchMax + 1];     // 1024-vector tiles before segment i (prefix)
-    int nseg;
-};
-int copy_many(const CopySet &c, hipStream_t s);
 
 // world: ranks (2..ESGD_MAX_FANIN); grid = workers + 1 (the agent)
 int round_batch(int dtype, int world, const BatchArgs &a, unsigned workers, hipStream_t s);

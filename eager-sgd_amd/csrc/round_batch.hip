@@ -1,17 +1,19 @@
 // round_batch.hip — k_round_batch: the one-launch rounds due in issue order, in one kernel.
 //
 // Grid: ONE agent workgroup (block 0, dispatched first) plus `workers` workgroups of 256
-// threads.  Residency contract: the agent and at least ONE worker must be resident; the
-// other workers may be kept out by concurrent kernels (a torch stream, an RCCL kernel,
-// other ranks sharing the GPU).  Workers take tiles from a per-process counter in list
-// order (BatchArgs::dynamic), so every tile a resident worker spins on depends only on
-// tiles already taken -- by workers that are running -- and on peers' flags of entries no
-// later in the ring.  (Static assignment, tile g on worker 1 + g % workers, needed every
-// worker resident at once: one not dispatched while the others spun on gates its own tiles
-// would open deadlocked the launch -- round 4, 8 ranks on one GPU.)  The host still sizes
-// the grid to what the ranks sharing this GPU leave free (round_batch_capacity), for speed.
+// threads.  Workers take tiles from the launch slot's counter in list order, so every tile a
+// resident worker waits on depends only on tiles already taken and on peers' flags of entries
+// no later in the ring: the launch's rounds complete with the agent alone resident.
+//   * Forward progress whatever the dispatch order (round 6): where ranks share this GPU a
+//     worker whose gate stays closed for BatchArgs::yield defers its tile to the slot's ring
+//     and leaves -- a peer's launch that could not be dispatched beside our spinning
+//     workers is what opens those gates -- and the agent block does deferred tiles (any
+//     whose gate is open, not the oldest: r06a) and, once any were deferred, further open
+//     tiles of the list itself.  The agent block leaves only when every tile is done.
+//   * Static assignment (tile g on worker 1 + g % workers, round 4) needed every worker
+//     resident at once and is gone.
 //
-// Agent (wave 0 of block 0; lane e owns entry e):
+// Agent (wave 0 of block 0; lane e owns entry e; waves 1-3 join it to fold tiles):
 //   * publishes `ready` of every entry at once -- everything the entries' snapshots
 //     wrote was queued on the stream before this launch -- behind one system-scope
 //     release (L2 write-back) and a drain; an entry whose snapshot the workers do in this
@@ -20,10 +22,9 @@
 //     all lanes' loads in flight together) and raises the entry's device gates.
 // Workers walk a global tile list in ring order -- every entry's snapshot tiles, then its
 // phase-1 tiles, then its phase-2 tiles -- taking the next tile from the counter:
-//   * phase 0 (snapshot, ESGD_SNAPSHOT_IN_BATCH): 1024 vectors of rb = sb, rb = 0 or, for a
-//     round posted with its own send data (esgd_schedule_post_io), rb = src / divisor --
-//     write-through, drained, counted -- no gate: every snapshot tile is taken before any
-//     gated tile;
+//   * phase 0 (snapshot): 1024 vectors of rb = sb, rb = 0 or, for a round posted with its own
+//     send data (esgd_schedule_post_io), rb = src / divisor -- write-through, drained,
+//     counted -- no gate: every snapshot tile is taken before any gated tile;
 //   * phase 1 (reduce-scatter): wait for the entry's ready gate; fold one tile (tv1 16-B
 //     vectors) of shard `rank` of every rank's rb in the reference's tree order
 //     (ffallreduce.c:138-171 via tree_fold) into the local rb (or the round's own output)
@@ -35,6 +36,14 @@
 // The agent never waits for one entry before serving another, and a worker's tiles come
 // in ring order, so a flag of entry i depends only on flags of entries <= i on every rank:
 // ranks that cut the issue ring into launches differently cannot deadlock.
+//
+// Failure contract (round 6; the reference's comp never runs before its recv,
+// ffallreduce.c:155-162): a flag wait that times out -- or that finds a peer's error word
+// holding the round -- records the round in this rank's error word and opens the entry's
+// gates so no worker is left waiting, but the entry then publishes NOTHING more: no
+// `reduced`, no `fin`.  Its `ready` (already out) is true -- its snapshot landed -- but a
+// late peer can never complete the round from this rank's shard, which was folded from
+// stale peer buckets: it times out, or sees the error word and fails at once.
 //
 // Hand-offs (relaxed, as in k_round_small; strict with BatchDesc::strict): payload stores
 // are system-scope write-through (sc0 sc1) and drained by every wave before its workgroup
@@ -72,10 +81,12 @@ __device__ __forceinline__ void put_flags(const PairFlags &f, uint32_t v) {
     for (int q = 0; q < f.ndst; ++q) store_sys(f.dst[q], v);
 }
 
-// A timed-out wait: the host fails the round (err) and no worker is left waiting (both
-// gates open).  err is released at system scope before the gates: a worker's fin can only
-// follow an open gate, and the host reads fin before err (dataplane.cpp base_query).
+// A failed flag wait (timeout, or a peer's error word holding the round): the round is
+// recorded in the entry's failure word (device, read before any publication) and in the
+// error word (host; the host reads fin before err, dataplane.cpp base_query), both released
+// before the gates open -- so no worker is left waiting, and no worker publishes for it.
 __device__ __forceinline__ void fail_entry(const BatchDesc *d, uint32_t v) {
+    __hip_atomic_store(d->ctr + 5, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     store_sys(d->err, v);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -83,57 +94,125 @@ __device__ __forceinline__ void fail_entry(const BatchDesc *d, uint32_t v) {
     store_gate(d->ctr + 3, v, false);
 }
 
+__device__ __forceinline__ bool entry_failed(const BatchDesc &d, uint32_t v) {
+    return __hip_atomic_load(d.ctr + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v;
+}
+
+// Where tile g of the list lies: its phase, its index within the phase and its entry (`e`
+// is a hint: the search restarts when g lies before it, e.g. a deferred tile).
+struct TileAt {
+    int ph;
+    uint32_t t, e;
+};
+
+__device__ __forceinline__ TileAt locate(const BatchArgs &a, uint32_t g, uint32_t T0, uint32_t T1, uint32_t e) {
+    TileAt at;
+    at.ph = g < T0 ? 0 : g < T1 ? 1 : 2;
+    at.t = at.ph == 0 ? g : at.ph == 1 ? g - T0 : g - T1;
+    const uint32_t *pre = at.ph == 0 ? a.tile0 : at.ph == 1 ? a.tile1 : a.tile2;
+    if (e >= a.nent || at.t < pre[e]) e = 0;
+    while (at.t >= pre[e + 1]) ++e;
+    at.e = e;
+    return at;
+}
+
+__device__ __forceinline__ uint32_t load_agent(const uint32_t *p) {
+    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// phase-0 tiles have no gate; phase 1 waits for the ready gate, phase 2 for the reduced gate
+__device__ __forceinline__ bool gate_open(const BatchArgs &a, const TileAt &at) {
+    if (at.ph == 0) return true;
+    const BatchDesc &d = a.table[a.sid[at.e]];
+    return reached(load_agent(d.ctr + (at.ph == 2 ? 3 : 2)), a.value[at.e]);
+}
+
+// the slot's deferred ring: one entry per worker that gave its wave slots back (tile + 1;
+// 0 while being written, kTaken once the agent block took it).  Only the agent block takes
+// deferred tiles, and it takes ANY open one: a phase-2 tile deferred ahead of the phase-1
+// tiles whose `reduced` opens its gate must not block them (a first version that took
+// only the oldest deadlocked 8 ranks sharing a GPU, r06a).
+constexpr uint32_t kNoTile = 0xffffffffu, kTaken = 0xffffffffu;
+__device__ __forceinline__ void defer_tile(uint32_t *S, uint32_t g) {
+    const uint32_t i = __hip_atomic_fetch_add(S + kSlotTail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(S + kSlotRing + i, g + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int K>
-__device__ void agent(const BatchArgs &a, long long t0) {
+struct AgentLane {   // wave 0 of block 0: lane e's entry
+    const BatchDesc *d;
+    uint32_t v, snaps;
+    int st;          // -1: snapshot tiles pending, 0: waiting for every ready, 1: every reduced, 2: done
+    unsigned sweeps;
+};
+
+template <int K>
+__device__ void agent_init(const BatchArgs &a, AgentLane<K> &L) {
     const int lane = int(threadIdx.x);
     const bool act = lane < int(a.nent);
-    const BatchDesc *d = act ? &a.table[a.sid[lane]] : nullptr;
-    const uint32_t v = act ? a.value[lane] : 0u;
+    L.d = act ? &a.table[a.sid[lane]] : nullptr;
+    L.v = act ? a.value[lane] : 0u;
     // entries whose snapshot the workers do first wait for it (-1) before their ready
-    const uint32_t snaps = act && a.snap[lane] ? a.tile0[lane + 1] - a.tile0[lane] : 0u;
+    L.snaps = act && a.snap[lane] ? a.tile0[lane + 1] - a.tile0[lane] : 0u;
+    L.sweeps = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: what the snapshots wrote
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (act && !snaps) put_flags(d->ready, v);
-    int st = act ? (snaps ? -1 : 0) : 2;   // 0: waiting for every ready, 1: for every reduced, 2: done
-    for (;;) {
-        bool pub = false;   // this entry's snapshot has just landed
-        if (st == -1) {
-            // the snapshot tiles stored write-through and drained before counting: once all
-            // are counted the bucket is in memory, and the ready below follows a release
-            const uint32_t n = __hip_atomic_load(d->ctr + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (n >= snaps) {
-                __hip_atomic_store(d->ctr + 4, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                st = 0;
-                pub = true;
-            } else if (wall_clock64() - t0 > a.timeout) {
-                fail_entry(d, v);
-                st = 2;
-            }
+    if (act && !L.snaps) put_flags(L.d->ready, L.v);
+    L.st = act ? (L.snaps ? -1 : 0) : 2;
+}
+
+// one non-blocking sweep of the agent wave; true once every entry's flags are settled
+template <int K>
+__device__ bool agent_sweep(const BatchArgs &a, AgentLane<K> &L, long long t0) {
+    const BatchDesc *d = L.d;
+    const uint32_t v = L.v;
+    bool pub = false;   // this entry's snapshot has just landed
+    if (L.st == -1) {
+        // the snapshot tiles stored write-through and drained before counting: once all
+        // are counted the bucket is in memory, and the ready below follows a release
+        const uint32_t n = __hip_atomic_load(d->ctr + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n >= L.snaps) {
+            __hip_atomic_store(d->ctr + 4, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            L.st = 0;
+            pub = true;
+        } else if (wall_clock64() - t0 > a.timeout) {
+            fail_entry(d, v);
+            L.st = 2;
         }
-        if (__any(pub)) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        if (pub) put_flags(d->ready, v);
-        if (st >= 0 && st < 2) {
-            const uint32_t *f = st == 0 ? d->ready.mine : d->reduced.mine;
-            uint32_t got[K];
-#pragma unroll
-            for (int q = 0; q < K; ++q) got[q] = load_sys(&f[q]);   // all in flight at once
-            bool all = true;
-#pragma unroll
-            for (int q = 0; q < K; ++q) all = all && reached(got[q], v);
-            if (all) {
-                store_gate(d->ctr + 2 + st, v, d->strict != 0);
-                ++st;
-            } else if (wall_clock64() - t0 > a.timeout) {
-                fail_entry(d, v);
-                st = 2;
-            }
-        }
-        if (__all(st == 2)) return;
-        __builtin_amdgcn_s_sleep(1);
     }
+    if (__any(pub)) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (pub) put_flags(d->ready, v);
+    if (L.st >= 0 && L.st < 2) {
+        const uint32_t *f = L.st == 0 ? d->ready.mine : d->reduced.mine;
+        uint32_t got[K];
+#pragma unroll
+        for (int q = 0; q < K; ++q) got[q] = load_sys(&f[q]);   // all in flight at once
+        bool all = true;
+#pragma unroll
+        for (int q = 0; q < K; ++q) all = all && reached(got[q], v);
+        if (all) {
+            store_gate(d->ctr + 2 + L.st, v, d->strict != 0);
+            ++L.st;
+        } else if (wall_clock64() - t0 > a.timeout) {
+            fail_entry(d, v);
+            L.st = 2;
+        } else if ((++L.sweeps & 15u) == 0) {
+            // a peer that failed this round publishes nothing more for it: fail now rather
+            // than at the timeout (its error word sits beside ours in the node segment)
+            const uint32_t *errs = d->err - d->rank;
+            bool bad = false;
+#pragma unroll
+            for (int q = 0; q < K; ++q) bad = bad || load_sys(&errs[q]) == v;
+            if (bad) {
+                fail_entry(d, v);
+                L.st = 2;
+            }
+        }
+    }
+    return __all(L.st == 2);
 }
 
 // phase 1, tile `local` of an entry: fold the shard's vectors [local * tv1, +tv1) into
@@ -284,79 +363,49 @@ __device__ __forceinline__ void tile_gather(const BatchDesc &d, uint32_t local, 
     }
 }
 
-}  // namespace
-
+// One tile, by the whole workgroup, once its gate is open (or the wait gave up): the
+// tile's work, the drain, the entry's arrival count -- whose last arriver publishes the
+// entry's ready (phase 0: the agent does), reduced (phase 1) or fin (phase 2) unless the
+// entry failed here -- and the launch's done count.
 template <class Tr, int K>
-__global__ __launch_bounds__(256) void k_round_batch(BatchArgs a) {
-    const long long t0 = wall_clock64();
-    if (blockIdx.x == 0) {   // dispatched first: the agent never waits for a free slot
-        if (threadIdx.x < 64) agent<K>(a, t0);
-        return;
-    }
-    // stale peer lines of earlier launches out of this CU's L1 and this XCD's L2 (a worker
-    // that starts late still does this before its first tile)
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    const uint32_t workers = gridDim.x - 1;
-    // the tile list: every entry's snapshot tiles (phase 0), its phase-1 tiles, its phase-2
-    // tiles, each in ring order; a worker meets no gate before its snapshot tiles are done
-    const uint32_t T0 = a.tile0[a.nent], T1 = T0 + a.tile1[a.nent], T = T0 + a.tile1[a.nent] + a.tile2[a.nent];
-    __shared__ uint32_t s_next;
-    uint32_t e = 0;
-    int phase = 0;
-    for (uint32_t g = blockIdx.x - 1;; g += workers) {
-        if (a.dynamic) {   // the next tile of the list, whichever worker is free (BatchArgs)
-            if (threadIdx.x == 0)
-                s_next = __hip_atomic_fetch_add(a.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.qbase;
-            __syncthreads();
-            g = s_next;   // read by every thread before the next write (a barrier follows in each path)
-        }
-        if (g >= T) break;
-        const int ph = g < T0 ? 0 : g < T1 ? 1 : 2;
-        if (ph != phase) { phase = ph; e = 0; }
-        const uint32_t t = ph == 0 ? g : ph == 1 ? g - T0 : g - T1;
-        const uint32_t *pre = ph == 0 ? a.tile0 : ph == 1 ? a.tile1 : a.tile2;
-        while (t >= pre[e + 1]) ++e;
-        const BatchDesc &d = a.table[a.sid[e]];
-        const uint32_t v = a.value[e];
-        if (ph == 0) {
-            tile_snapshot(d, t - pre[e], a.snap[e], a.isrc[e], a.idiv[e]);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are in memory
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                if (d.strict) __hip_atomic_fetch_add(d.ctr + 4, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-                else __hip_atomic_fetch_add(d.ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            continue;
-        }
-        const bool gather = ph == 2;
-        if (threadIdx.x == 0) {
-            const uint32_t *gate = d.ctr + (gather ? 3 : 2);
-            while (!reached(__hip_atomic_load(const_cast<uint32_t *>(gate), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                            v)) {
-                if (wall_clock64() - t0 > 2 * a.timeout) break;   // the agent's timeout comes first
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (d.strict) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        }
-        __syncthreads();
-        const uint32_t local = t - pre[e];
-        // a round with its own output (esgd_schedule_post_io) lands there, at rb's offsets
-        const ptrdiff_t shift = a.iout[e] ? static_cast<char *>(a.iout[e]) - static_cast<char *>(d.rbase) : 0;
-        // a sourced in-launch snapshot skipped the own shard: its operand comes from the source
-        const uint8_t kind = a.snap[e];
-        const void *ssrc = a.isrc[e] ? a.isrc[e] : d.ssrc;
-        const void *own = (kind == 1 || kind == 3) && ssrc ? static_cast<const char *>(ssrc) + d.own_off : nullptr;
-        if (!gather) tile_reduce<Tr, K>(d, local, static_cast<char *>(d.out) + shift, own, kind == 3 ? a.idiv[e] : 1.0f);
-        else tile_gather(d, local, shift);
+__device__ void run_tile(const BatchArgs &a, uint32_t *S, const TileAt &at) {
+    const uint32_t e = at.e;
+    const uint32_t *pre = at.ph == 0 ? a.tile0 : at.ph == 1 ? a.tile1 : a.tile2;
+    const BatchDesc &d = a.table[a.sid[e]];
+    const uint32_t v = a.value[e];
+    const uint32_t local = at.t - pre[e];
+    if (at.ph == 0) {
+        tile_snapshot(d, local, a.snap[e], a.isrc[e], a.idiv[e]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are in memory
         __syncthreads();
         if (threadIdx.x == 0) {
-            uint32_t *cnt = d.ctr + (gather ? 1 : 0);
-            const uint32_t need = pre[e + 1] - pre[e];
-            const uint32_t old = d.strict ? __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT)
-                                          : __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (old + 1 == need) {   // the entry's last tile of this phase
-                __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (d.strict) __hip_atomic_fetch_add(d.ctr + 4, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            else __hip_atomic_fetch_add(d.ctr + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(S + kSlotDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        return;
+    }
+    const bool gather = at.ph == 2;
+    // a round with its own output (esgd_schedule_post_io) lands there, at rb's offsets
+    const ptrdiff_t shift = a.iout[e] ? static_cast<char *>(a.iout[e]) - static_cast<char *>(d.rbase) : 0;
+    // a sourced in-launch snapshot skipped the own shard: its operand comes from the source
+    const uint8_t kind = a.snap[e];
+    const void *ssrc = a.isrc[e] ? a.isrc[e] : d.ssrc;
+    const void *own = (kind == 1 || kind == 3) && ssrc ? static_cast<const char *>(ssrc) + d.own_off : nullptr;
+    if (!gather) tile_reduce<Tr, K>(d, local, static_cast<char *>(d.out) + shift, own, kind == 3 ? a.idiv[e] : 1.0f);
+    else tile_gather(d, local, shift);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores are in memory
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t *cnt = d.ctr + (gather ? 1 : 0);
+        const uint32_t need = pre[e + 1] - pre[e];
+        const uint32_t old = d.strict ? __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT)
+                                      : __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1 == need) {   // the entry's last tile of this phase
+            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // an entry whose flag wait failed publishes nothing more (the failure contract)
+            if (!entry_failed(d, v)) {
                 if (!gather) {
                     // every tile of the entry was stored write-through and drained before
                     // its count: no L2 write-back before the flag (strict: one anyway)
@@ -369,7 +418,142 @@ __global__ __launch_bounds__(256) void k_round_batch(BatchArgs a) {
                 }
             }
         }
+        __hip_atomic_fetch_add(S + kSlotDone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+}
+
+// Block 0: the flag agent (wave 0), and -- with all four waves -- the folder of tiles the
+// workers deferred, and of further open tiles of the list once any were deferred (the
+// workers that gave their slots back may have been the last ones dispatched).  Leaves when
+// every tile of the launch is done (4 timeouts at most: a kernel never spins for good).
+template <class Tr, int K>
+__device__ void agent_block(const BatchArgs &a, uint32_t *S, uint32_t T0, uint32_t T1, uint32_t T, long long t0) {
+    __shared__ uint32_t s_tile;
+    __shared__ int s_cmd;
+    // the next launch's slot starts at zero (and every other one: see kLaunchSlots)
+    for (uint32_t i = threadIdx.x; i < (kLaunchSlots - 1) * kSlotWords; i += blockDim.x) {
+        const uint32_t sl = (a.slot + 1u + i / kSlotWords) % kLaunchSlots;
+        __hip_atomic_store(a.slots + sl * kSlotWords + i % kSlotWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __shared__ uint32_t s_tail, s_pick;
+    __shared__ int s_help;
+    AgentLane<K> L;
+    bool settled = false;
+    if (threadIdx.x < 64) agent_init<K>(a, L);
+    uint32_t hint = 0;
+    for (;;) {
+        if (threadIdx.x < 64 && !settled) settled = agent_sweep<K>(a, L, t0);
+        if (threadIdx.x == 0) {
+            const uint32_t tail = load_agent(S + kSlotTail);
+            s_tail = tail < kBatchWorkersMax ? tail : kBatchWorkersMax;
+            s_pick = kNoTile;
+            // 2 leave, 1 help: some worker gave its slots back, or (ranks sharing the GPU)
+            // the launch has run for a yield period -- its workers may never be dispatched
+            // beside the peers' launches; 0 idle
+            s_help = load_agent(S + kSlotDone) >= T ? 2
+                   : (tail > 0 || (a.yield && wall_clock64() - t0 > a.yield)) ? 1 : 0;
+        }
         __syncthreads();
+        const int help = s_help;
+        if (help == 2) return;
+        uint32_t g = kNoTile;
+        if (help == 1) {
+            // every deferred tile whose gate is open, in parallel; the lowest ring index wins
+            for (uint32_t i = threadIdx.x; i < s_tail; i += blockDim.x) {
+                const uint32_t x = load_agent(S + kSlotRing + i);
+                if (x && x != kTaken && gate_open(a, locate(a, x - 1u, T0, T1, 0))) {
+                    atomicMin(&s_pick, i);
+                    break;
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                if (s_pick != kNoTile) {   // only this block takes deferred tiles
+                    const uint32_t i = s_pick;
+                    s_pick = load_agent(S + kSlotRing + i) - 1u;
+                    __hip_atomic_store(S + kSlotRing + i, kTaken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {   // the list's next tile, if its gate is open
+                    uint32_t q = load_agent(S + kSlotQueue);
+                    if (q < T && gate_open(a, locate(a, q, T0, T1, 0)) &&
+                        __hip_atomic_compare_exchange_strong(S + kSlotQueue, &q, q + 1u, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                        s_pick = q;
+                }
+            }
+            __syncthreads();
+            g = s_pick;
+        }
+        if (g != kNoTile) {
+            const TileAt at = locate(a, g, T0, T1, hint);
+            hint = at.e;
+            if (threadIdx.x == 0 && at.ph != 0 && a.table[a.sid[at.e]].strict)
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            run_tile<Tr, K>(a, S, at);   // ends with a barrier: the shared words are rewritten after it
+        } else {
+            if (!help && wall_clock64() - t0 > 4 * a.timeout) return;   // never spin for good
+            if (threadIdx.x < 64) __builtin_amdgcn_s_sleep(1);
+            __syncthreads();
+        }
+    }
+}
+
+}  // namespace
+
+template <class Tr, int K>
+__global__ __launch_bounds__(256) void k_round_batch(BatchArgs a) {
+    const long long t0 = wall_clock64();
+    uint32_t *S = a.slots + a.slot * kSlotWords;
+    // the tile list: every entry's snapshot tiles (phase 0), its phase-1 tiles, its phase-2
+    // tiles, each in ring order; a worker meets no gate before its snapshot tiles are done
+    const uint32_t T0 = a.tile0[a.nent], T1 = T0 + a.tile1[a.nent], T = T1 + a.tile2[a.nent];
+    if (blockIdx.x == 0) {   // dispatched first: the agent never waits for a free slot
+        // stale peer lines of earlier launches out of this CU's L1 and this XCD's L2 (the
+        // agent block folds tiles too)
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        agent_block<Tr, K>(a, S, T0, T1, T, t0);
+        return;
+    }
+    // stale peer lines of earlier launches out of this CU's L1 and this XCD's L2 (a worker
+    // that starts late still does this before its first tile)
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    __shared__ uint32_t s_next;
+    __shared__ int s_gave;
+    uint32_t hint = 0;
+    for (;;) {
+        if (threadIdx.x == 0) {   // the next tile of the list
+            const uint32_t g = __hip_atomic_fetch_add(S + kSlotQueue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_next = g < T ? g : kNoTile;
+        }
+        __syncthreads();
+        const uint32_t g = s_next;   // read by every thread before the next write (barriers follow)
+        if (g == kNoTile) break;
+        const TileAt at = locate(a, g, T0, T1, hint);
+        hint = at.e;
+        if (at.ph != 0) {
+            if (threadIdx.x == 0) {
+                const BatchDesc &d = a.table[a.sid[at.e]];
+                const uint32_t *gate = d.ctr + (at.ph == 2 ? 3 : 2);
+                const uint32_t v = a.value[at.e];
+                const long long w0 = wall_clock64();
+                int gave = 0;
+                while (!reached(load_agent(gate), v)) {
+                    const long long now = wall_clock64();
+                    if (a.yield && now - w0 > a.yield) {   // give the wave slots back
+                        defer_tile(S, g);
+                        gave = 1;
+                        break;
+                    }
+                    if (now - t0 > 2 * a.timeout) break;   // the agent's timeout comes first
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (!gave && d.strict) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                s_gave = gave;
+            }
+            __syncthreads();
+            if (s_gave) return;
+        }
+        run_tile<Tr, K>(a, S, at);
     }
 }
 
@@ -419,47 +603,6 @@ int round_batch_capacity(int dtype, int world) {
         cache[slot][world].store(c, std::memory_order_relaxed);
     }
     return c;
-}
-
-// The shared launch's snapshots: tile g (1024 16-B vectors of one segment) on block
-// g mod grid; nt loads, write-through stores (peers read these buckets over xGMI once
-// the kernel boundary and the agent's ready have passed); ragged tails byte by byte.
-__global__ __launch_bounds__(256) void k_copy_many(CopySet c) {
-    const uint32_t total = c.tile0[c.nseg];
-    int i = 0;
-    for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
-        while (g >= c.tile0[i + 1]) ++i;
-        const uint32_t nv = c.nvec[i];
-        const uint32_t v0 = (g - c.tile0[i]) * 1024u;
-        const __amdgpu_buffer_rsrc_t wd = __builtin_amdgcn_make_buffer_rsrc(c.dst[i], (short)0, int(nv * 16u), 0x00020000);
-        raw16 r[4];
-        if (c.src[i]) {
-            const __amdgpu_buffer_rsrc_t rd =
-                __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(c.src[i]), (short)0, int(nv * 16u), 0x00020000);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) r[u] = __builtin_amdgcn_raw_buffer_load_b128(rd, (v0 + u * 256 + threadIdx.x) * 16, 0, 2);
-        } else {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) r[u] = raw16{0u, 0u, 0u, 0u};
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(r[u], wd, (v0 + u * 256 + threadIdx.x) * 16, 0, 17);
-        if (v0 == 0 && threadIdx.x < c.tail[i]) {
-            uint8_t *d = static_cast<uint8_t *>(c.dst[i]) + size_t(nv) * 16;
-            const uint8_t *src = static_cast<const uint8_t *>(c.src[i]);
-            d[threadIdx.x] = src ? src[size_t(nv) * 16 + threadIdx.x] : uint8_t(0);
-        }
-    }
-}
-
-int copy_many(const CopySet &c, hipStream_t s) {
-    ESGD_ARG(c.nseg >= 1 && c.nseg <= kBatchMax, "copy_many: %d segments", c.nseg);
-    const uint32_t total = c.tile0[c.nseg];
-    if (!total) return ESGD_SUCCESS;
-    const unsigned grid = std::min<unsigned>(total, unsigned(cu_count()) * 4u);
-    hipLaunchKernelGGL(k_copy_many, dim3(grid), dim3(256), 0, s, c);
-    ESGD_HIP(hipGetLastError());
-    return ESGD_SUCCESS;
 }
 
 template <class Tr>

@@ -1790,8 +1790,7 @@ def gpu_post_io_late(rank, world, count=4099, steps=8, async_=3, late=1, on_stre
     return out
 
 
-def gpu_residency(rank, world, hog_ms=6000, free_cus=2, rounds=4, counts=(1 << 20, 65536, 17, 300007, 1025),
-                  static=False):
+def gpu_residency(rank, world, hog_ms=6000, free_cus=2, rounds=4, counts=(1 << 20, 65536, 17, 300007, 1025)):
     """Batched rounds while a concurrent kernel holds almost the whole GPU (verdict r04 item
     3): rank 0 starts k_occupy (tools/bin/libesgd_sweeps.so) on a side stream -- 2 x CUs -
     2 x free_cus workgroups of 16 waves, resident for hog_ms -- then every rank posts one
@@ -1809,8 +1808,6 @@ def gpu_residency(rank, world, hog_ms=6000, free_cus=2, rounds=4, counts=(1 << 2
 
     from esgd import _lib
     from esgd import device as dev
-    if static:
-        os.environ["ESGD_BATCH_STATIC"] = "1"
     comm = _comm()
     sw = C.CDLL(os.path.join(ROOT, "tools", "bin", "libesgd_sweeps.so"))
     sw.esgd_sweep_occupy.restype, sw.esgd_sweep_occupy.argtypes = C.c_int, [C.c_int, C.c_uint64, C.c_void_p]
@@ -1870,6 +1867,75 @@ def gpu_residency(rank, world, hog_ms=6000, free_cus=2, rounds=4, counts=(1 << 2
     note("schedules deleted")
     comm.finalize()
     return {"first_round_s": times[2], "round_s": times, "hog_s": hog_s, "ok": ok, "workers": workers}
+
+
+def gpu_late_peer_after_timeout(rank, world, cases, delay_s=4.0):
+    """The failure contract: rank 1's GPU runs the round
+    `delay_s` late -- its post names a producer stream on which a 1-workgroup k_occupy
+    (tools/bin/libesgd_sweeps.so) holds it, as a backward pass still writing the gradient
+    would -- so rank 0's GPU flag wait times out (ESGD_TIMEOUT_S, set by the caller to 2 s)
+    first.  Rank 0 must fail.  Rank 1 must fail too, or return the oracle's sum of the data
+    that really arrived -- never success with a sum built from rank 0's shard, which rank 0
+    folded from rank 1's STALE bucket (the previous round's result).  Each case (kind, path)
+    runs one good round (data A), then the late round (data B).  int32 inputs, exact."""
+    import ctypes as C
+
+    import numpy as np
+    import torch.distributed as dist
+
+    from esgd import _lib
+    from esgd import device as dev
+    comm = _comm()
+    sw = C.CDLL(os.path.join(ROOT, "tools", "bin", "libesgd_sweeps.so"))
+    sw.esgd_sweep_occupy.restype, sw.esgd_sweep_occupy.argtypes = C.c_int, [C.c_int, C.c_uint64, C.c_void_p]
+    side = dev.Stream()   # rank 1's "backward": the producer of its late round
+    kinds = {"allreduce": comm.ALLREDUCE, "solo": comm.SOLO, "majority": comm.MAJORITY}
+    out = []
+    for kind, path in cases:
+        count = (3 << 20) if path == "five" else 300007   # 12 MiB: above the one-launch threshold
+        comm.set_config("batch_rounds", 0 if path == "one" else -1)
+        sb, rb = dev.DeviceBuffer(count, _lib.INT32), dev.DeviceBuffer(count, _lib.INT32)
+        # solo with async 1: round 2 is synchronous, joined at each rank's own post (an async
+        # round would carry rank 1 through on rank 0's activation, without its producer)
+        s_ = comm.Schedule(kinds[kind], sb, rb, count, dtype=_lib.INT32, buf=comm.BUF_DEVICE, async_=1, seed=7)
+        a = [(np.arange(count) * 3 + 11 * r).astype(np.int32) for r in range(world)]
+        b = [(np.arange(count) % 977 + 1000 * r + 5).astype(np.int32) for r in range(world)]
+        sb.upload(a[rank])
+        dist.barrier()   # gloo: esgd's own barrier times out with the 2 s limit
+        s_.post()
+        s_.wait()
+        good = bool(np.array_equal(rb.download(), sum(a).astype(np.int32)))
+        sb.upload(b[rank])
+        dist.barrier()   # gloo: esgd's own barrier times out with the 2 s limit
+        t0 = time.perf_counter()
+        if rank == 1:
+            assert sw.esgd_sweep_occupy(1, int(delay_s * 1e6), side.handle) == 0
+            s_.post(stream=side)
+            # the host's own wait limit counts from wait(): wait only shortly before the GPU
+            # runs the round, so the GPU's flag protocol decides rank 1's outcome
+            time.sleep(delay_s - 0.5)
+        else:
+            s_.post()
+        err, result = None, None
+        try:
+            s_.wait()
+            got = rb.download()
+            result = "oracle" if np.array_equal(got, sum(b).astype(np.int32)) else "WRONG"
+        except Exception as e:   # esgd.EsgdError
+            err = str(e).splitlines()[0][:300]
+        side.synchronize()
+        el = time.perf_counter() - t0
+        dist.barrier()   # gloo: esgd's own barrier times out with the 2 s limit
+        s_.delete()
+        comm.set_config("batch_rounds", -1)
+        out.append({"kind": kind, "path": path, "first_round_ok": good, "failed": err is not None,
+                    "result": result, "err": err, "elapsed_s": round(el, 2),
+                    # the round's failure words (this rank's GPU, or a peer's), not the host's
+                    # own wait limit ("wait timed out [rank ...")
+                    "gpu_failure": err is not None and ("failed round" in err or "GPU waited" in err)})
+        print(f"[late_peer r{rank}] {kind}/{path}: {out[-1]}", file=sys.stderr, flush=True)
+    comm.finalize()
+    return out
 
 
 def op_void_peer_lost(rank, world, count=5000):

@@ -774,27 +774,53 @@ SWEEPS_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file
 
 @pytest.mark.skipif(not os.path.exists(SWEEPS_LIB), reason="tools/bin/libesgd_sweeps.so not built (make sweeps)")
 def test_batched_rounds_progress_beside_a_kernel_holding_the_gpu():
-    # the residency contract of k_round_batch: a kernel on another stream
-    # holds all but two CUs' wave slots for 6 s; the shared launch of each rank must finish
-    # its 5 rounds on the workgroups that fit, bit for bit, well before the hog leaves
-    # (static tile assignment waited for it: test below); the later rounds, bit for bit
-    # too, start once the launch's last workgroups could be dispatched
-    outs = run("gpu_residency", 2, timeout=150)   # under gpurun's 180 s of silence: a hang reports
+    # forward progress of k_round_batch: a kernel on another stream holds all
+    # but two CUs' wave slots for 6 s, and the two ranks' shared launches compete for the
+    # rest; each rank's launch must finish its 5 rounds on the workgroups that fit, bit for
+    # bit, well before the hog leaves -- whichever rank's workgroups the GPU dispatches
+    # first (workers give their slots back after 2 ms at a closed gate and the agent block
+    # folds what they left).  The later rounds, bit for bit too, start once the launch's
+    # last workgroups could be dispatched.  ESGD_TIMEOUT_S = 10: every bounded wait of the
+    # test together stays under the harness limit, itself under gpurun's 180 s of silence.
+    old = os.environ.get("ESGD_TIMEOUT_S")
+    os.environ["ESGD_TIMEOUT_S"] = "10"
+    try:
+        outs = run("gpu_residency", 2, timeout=150)
+    finally:
+        if old is None:
+            os.environ.pop("ESGD_TIMEOUT_S", None)
+        else:
+            os.environ["ESGD_TIMEOUT_S"] = old
     for o in outs:
         assert all(o["ok"]) and len(o["ok"]) == 30, o
         assert o["first_round_s"] < 0.25 * o["hog_s"], o
 
 
-@pytest.mark.diagnostic
 @pytest.mark.skipif(not os.path.exists(SWEEPS_LIB), reason="tools/bin/libesgd_sweeps.so not built (make sweeps)")
-def test_static_tile_assignment_waits_for_the_kernel_holding_the_gpu():
-    # the contrast (ESGD_BATCH_STATIC=1): a tile owned by a worker that is not resident
-    # waits until the hog leaves -- the rounds take about as long as the hog (still
-    # bit-exact: nothing deadlocks here because the hog ends)
-    outs = run("gpu_residency", 2, static=True, timeout=180)
-    for o in outs:
-        assert all(o["ok"]), o
-        assert o["first_round_s"] > 0.5 * o["hog_s"], o
+def test_late_peer_after_a_timeout_never_succeeds_with_a_stale_sum():
+    # the failure contract: rank 1's GPU runs the round
+    # 4 s late, rank 0's GPU flag wait gives up at 2 s.  Rank 0 fails; rank 1 fails as well
+    # or returns the oracle's sum -- for one-launch, batched and five-launch rounds of every
+    # kind.  (Before round 6 rank 1 returned success with rank 0's shard folded from its
+    # stale bucket.)
+    cases = [(k, p) for p in ("batched", "one", "five") for k in ("allreduce", "solo", "majority")]
+    old = os.environ.get("ESGD_TIMEOUT_S")
+    os.environ["ESGD_TIMEOUT_S"] = "2"
+    try:
+        outs = run("gpu_late_peer_after_timeout", 2, cases=cases, timeout=140)
+    finally:
+        if old is None:
+            os.environ.pop("ESGD_TIMEOUT_S", None)
+        else:
+            os.environ["ESGD_TIMEOUT_S"] = old
+    r0, r1 = outs
+    for c0, c1 in zip(r0, r1):
+        assert c0["first_round_ok"] and c1["first_round_ok"], (c0, c1)
+        assert c0["failed"], c0                                  # the rank that timed out
+        assert c1["failed"] or c1["result"] == "oracle", c1      # never a stale sum
+        assert c1["result"] != "WRONG", c1
+        # rank 1's outcome came from the GPU's flag protocol, not from its host wait limit
+        assert c1["gpu_failure"] or c1["result"] == "oracle", c1
 
 
 @pytest.mark.parametrize("delete_first", [False, True])
