@@ -23,6 +23,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import statistics
 import subprocess
 import sys
 import time
@@ -124,27 +125,56 @@ def _cpu_model():
     return None
 
 
+def _baseline_cpus(n: int):
+    """n cores for the CPU baseline's threads, from this process's affinity set: the first
+    n in id order (on the boxes seen, ids 0..n-1 share a socket).  None when fewer exist."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
+    return cpus[:n] if len(cpus) >= n else None
+
+
+def _pinned_samples(P: int, count: int, reps: int, samples: int = 3):
+    """`samples` runs of the pinned C1-shaped harness (each a median step over `reps`):
+    (median, [each], cores, every result correct)."""
+    from oracle import ffref
+    cpus = _baseline_cpus(2 * P)
+    ts, good = [], True
+    for _ in range(samples):
+        t, ok = ffref.time_c1(P, count, reps, cpus)
+        ts.append(t)
+        good = good and ok
+    return statistics.median(ts), ts, cpus, good
+
+
 def cpu_baseline(k: int, count: int):
     """fflib2 restated (oracle/ffref.c) on this host for the same k x bucket workload, with
     the core budget SURVEY.md §8(d) gives the reference: 2 cores per rank -- each simulated
     rank a main thread (the wrapper's copy-in, post, spin-wait, copy-out, zeroing of the
     send bucket) and a progress thread (the move + recursive doubling with VSUM; ff.c:72's
-    pthread), 2k threads in all.  Also reported: the recursive doubling alone, one pthread
-    per rank (the round-4 figure)."""
+    pthread), 2k threads in all, each pinned to a core of its own (round 6: unpinned, the
+    same CPU model gave 6.35 and 10.59 GB/s on two boxes).  The value is the median of 3
+    samples; the spread is beside it.  Also reported: the recursive doubling alone, one
+    pthread per rank (the round-4 figure, unpinned)."""
     from oracle import ffref
-    t1, _ = ffref.time_c1(k, count, 2)                       # warm + size the sample
-    reps = max(3, min(250, int(10.0 / max(t1, 1e-3))))   # ~10 s of CPU work
-    t, ok = ffref.time_c1(k, count, reps)
+    t1, _ = ffref.time_c1(k, count, 2, _baseline_cpus(2 * k))   # warm + size the sample
+    reps = max(3, min(250, int(4.0 / max(t1, 1e-3))))           # ~4 s of CPU work per sample
+    t, ts, cpus, ok = _pinned_samples(k, count, reps)
     t_rd1 = ffref.time_allreduce(k, count, k, max(1, reps // 2))
+    gbs = [k * count * 4 / x / 1e9 for x in ts]
     return {"value": round(k * count * 4 / t / 1e9, 3), "unit": "GB/s", "cores": 2 * k, "kind": "port",
             "sample": f"full workload: {k} ranks x {count * 4 / MiB:.0f} MiB fp32, each a main thread (copy-in, "
                       f"post, wait, copy-out, zero) + a progress thread (move + recursive doubling, VSUM) = "
-                      f"{2 * k} threads (oracle/ffref.c ffref_time_c1), median step of {reps}: {t * 1e3:.1f} ms",
-            "correct": ok,
+                      f"{2 * k} threads pinned one per core (oracle/ffref.c ffref_time_c1_pinned), median of 3 "
+                      f"samples, each the median step of {reps}: {t * 1e3:.1f} ms",
+            "samples_GBs": [round(x, 3) for x in gbs],
+            "spread": round((max(gbs) - min(gbs)) / statistics.median(gbs), 3),
+            "core_list": cpus, "correct": ok,
             "recursive_doubling_only_1_thread_per_rank": {
                 "value": round(k * count * 4 / t_rd1 / 1e9, 3), "cores": k,
-                "sample": f"{k}-rank recursive doubling alone (1 pthread/rank), best of {max(1, reps // 2)}: "
-                          f"{t_rd1 * 1e3:.1f} ms"},
+                "sample": f"{k}-rank recursive doubling alone (1 pthread/rank, unpinned), best of "
+                          f"{max(1, reps // 2)}: {t_rd1 * 1e3:.1f} ms"},
             "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
 
 
@@ -152,15 +182,20 @@ def cpu_baseline_c1(P: int = 2, count: int = 262144):
     """BASELINE.json configs[0] (C1): P ranks reducing one 1 MiB fp32 bucket per step the
     way the wrapper drives fflib2 -- each rank a main thread (copy-in, post, spin-wait,
     copy-out, zero) and a progress thread (move + recursive doubling, ff.c:72), i.e. 2
-    cores per rank; value = P x bucket bytes per step / step time."""
+    cores per rank, each thread pinned to a core of its own; value = P x
+    bucket bytes per step / step time, the median of 3 samples."""
     from oracle import ffref
-    t1, _ = ffref.time_c1(P, count, 20)
-    reps = max(50, min(20000, int(10.0 / max(t1, 1e-5))))   # ~10 s of steps
-    t, ok = ffref.time_c1(P, count, reps)
+    t1, _ = ffref.time_c1(P, count, 20, _baseline_cpus(2 * P))
+    reps = max(50, min(20000, int(4.0 / max(t1, 1e-5))))   # ~4 s of steps per sample
+    t, ts, cpus, ok = _pinned_samples(P, count, reps)
+    gbs = [P * count * 4 / x / 1e9 for x in ts]
     return {"value": round(P * count * 4 / t / 1e9, 3), "unit": "GB/s", "cores": 2 * P, "kind": "port",
-            "sample": f"C1: {P} ranks x {count * 4 / MiB:g} MiB fp32, main + progress thread per rank "
-                      f"(oracle/ffref.c ffref_time_c1), median step of {reps}: {t * 1e6:.1f} us",
-            "correct": ok, "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
+            "sample": f"C1: {P} ranks x {count * 4 / MiB:g} MiB fp32, main + progress thread per rank, each "
+                      f"pinned to a core (oracle/ffref.c ffref_time_c1_pinned), median of 3 samples, each the "
+                      f"median step of {reps}: {t * 1e6:.1f} us",
+            "samples_GBs": [round(x, 3) for x in gbs],
+            "spread": round((max(gbs) - min(gbs)) / statistics.median(gbs), 3),
+            "core_list": cpus, "correct": ok, "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
 
 
 PMC_CALLS = 5   # reduction calls of the PMC child run
@@ -697,17 +732,6 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
     finally:
         comm.set_config("batch_rounds", -1)
     t1 = _timed_steps(comm, fused_step, steps)
-    # A/B of the host path's switches, each against the defaults above
-    ab = {}
-    for key, val, what, fn in (("batch_depth", 0, "pipelined_batch_depth0_ms", pipelined),
-                               ("inline_join", 0, "pipelined_progress_thread_joins_ms", pipelined),
-                               ("inline_join", 0, "chain_progress_thread_joins_ms", chain)):
-        comm.set_config(key, val)
-        try:
-            fn()
-            ab[what] = round(_timed_steps(comm, fn, steps) * 1e3, 3)
-        finally:
-            comm.set_config(key, -1)
     variants = _op_like_variants(comm, dev, lengths, steps)
     launch_shape = _launch_shape_ab(comm, bufs, lengths, steps)
     for s, b in zip(scheds, bufs):
@@ -725,7 +749,6 @@ def c4_resnet50_161(comm, dev, rank, world, steps=8):
             "step_ms_161_buckets_pipelined_one_launch_per_round": round(t161u * 1e3, 3),
             "rank0_pipelined_step_us_one_launch_per_round": breakdown_u,
             "rank0_progress_thread_per_step_one_launch_per_round": prof_u,
-            "ab_host_path_switches": ab,
             "op_like_pipelined_variants": variants,
             "launch_shape_ab": launch_shape}
 
@@ -807,14 +830,6 @@ def _op_like_variants(comm, dev, lengths, steps):
         t = _timed_steps(comm, step, steps)
         out[name] = {"step_ms": round(t * 1e3, 3), "rank0_step_us": _step_breakdown_us(scheds),
                      "rank0_progress_thread_per_step": _profile_per_step(p0, comm.profile(), steps)}
-        if stream is not None:   # the cross-stream waits on the legacy NULL stream, A/B'd
-            for key in ("event_device_scope", "producer_host_sync"):
-                comm.set_config(key, 1)
-                try:
-                    step()
-                    out[name][key + "_step_ms"] = round(_timed_steps(comm, step, steps) * 1e3, 3)
-                finally:
-                    comm.set_config(key, -1)
         for sc, rb, sb in zip(scheds, rbs, sbs):
             _defer(sc, *([rb] if sb is None else [rb, sb]))
     return out
@@ -916,37 +931,21 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
     gen.manual_seed(SEED + rank)
     out = {}
     opts = []
-    side = None   # created for its variant only: one more stream is one more hardware queue,
-    #               which on a GPU shared by the ranks changes the timings
+    # (round 6: the A/B variants whose alternative lost -- rounds waited for on the GPU, the
+    # ops on the data plane's round stream, copy kernels instead of the rounds' own I/O, the
+    # caller on a side stream, idle-stream skips, snapshot worker caps -- are gone with their
+    # switches; their numbers are in profiles/r05/)
     for name, kw in (("per_tensor_pipelined", dict(fuse=False)),
-                     # the rounds waited for on the GPU (allreducef_forward_cuda_wait_many_on:
-                     # the wrapped step queued behind them while they run) instead of the host
-                     ("per_tensor_pipelined_stream_wait", dict(fuse=False, stream_wait=True)),
-                     # the ops' work and the wrapped SGD step on the data plane's round stream
-                     # (esgd_round_stream): ordered behind the rounds by the stream itself
-                     ("per_tensor_pipelined_round_stream", dict(fuse=False, round_stream=True, stream_wait=True)),
-                     # the same with copy-in / copy-out kernels on the caller's stream instead of
-                     # the rounds' own I/O (esgd_schedule_post_io): the A/B of the fused path
-                     ("per_tensor_pipelined_copy_kernels", dict(fuse=False, fused_io=False)),
                      ("per_tensor_blocking", dict(pipeline=False)),
-                     ("fused", dict(fuse=True)),
-                     # the pipelined step with the caller's work on a torch side stream instead
-                     # of the legacy NULL stream (the blocking pair above differs 1.6x)
-                     ("per_tensor_pipelined_side_stream", dict(fuse=False))):
-        if name.endswith("_side_stream") and side is None:
-            side = torch.cuda.Stream()
+                     ("fused", dict(fuse=True))):
         params = [torch.zeros(n, device=dev_t, requires_grad=True) for n in lengths]
         for p in params:
             p.grad = torch.rand(p.numel(), device=dev_t, generator=gen) - 0.5
         opt = EagerSGDOptimizer(torch.optim.SGD(params, lr=1e-3), world, mode="majority", **kw)
         opts.append(opt)
 
-        def step(opt=opt, stream=side if name.endswith("_side_stream") else None):
-            if stream is None:
-                opt.step()
-            else:   # the caller's work on a non-default stream instead of the legacy NULL stream
-                with torch.cuda.stream(stream):
-                    opt.step()
+        def step(opt=opt):
+            opt.step()
             torch.cuda.synchronize()
 
         step()   # creates the ops' schedules (collective, first step)
@@ -955,35 +954,15 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
         out[name + "_ms"] = round(_timed_steps(comm, step, steps) * 1e3, 3)
         out[name + "_progress_thread_per_step"] = _profile_per_step(p0, comm.profile(), steps)
         if name != "fused":
-            out[name + "_breakdown_us"] = _optimizer_breakdown(opt, steps, side if name.endswith("_side_stream") else None)
+            out[name + "_breakdown_us"] = _optimizer_breakdown(opt, steps, None)
             out[name + "_rank0_step_us"] = _step_breakdown_us([op.schedule() for op in opt._ops.values()])
         else:
             out["fused_breakdown_us"] = _fused_breakdown(comm, opt, params, steps)
         if name == "per_tensor_blocking":
             out[name + "_round_stages_us"] = _round_stages_us([op.schedule() for op in opt._ops.values()])
-            # idle_skip: a post / release whose caller's stream is idle records no event (the
-            # round stream has nothing to wait for) -- the reference's blocking chain, 161
-            # cross-stream waits a step otherwise
-            # (r05ah also A/B'd the copy-in as a kernel before the launch, snapshot_in_batch 0:
-            # 10.52 vs 10.20 ms, dropped)
-            for key, val, what in (("idle_skip", 1, "_idle_skip"),):
-                comm.set_config(key, val)
-                try:
-                    step()
-                    out[name + what + "_ms"] = round(_timed_steps(comm, step, steps) * 1e3, 3)
-                    out[name + what + "_round_stages_us"] = _round_stages_us([op.schedule() for op in opt._ops.values()])
-                finally:
-                    comm.set_config(key, -1)
         if name == "per_tensor_pipelined":
-            # A/B of the same step with one launch per round (esgd_set_config, process-local).
-            # (r05d-r05g also A/B'd a device-scope event release and a host-side producer
-            # sync here: within noise every time, profiles/r05/README.md; dropped)
-            # snapshot_workers_max 0: shared launches that hold the rounds' snapshots of the
-            # gradients (phase 0, a plain copy) capped at batch_workers_max (64) like the
-            # others, instead of 256 (the default since r05ac; 512 in r05ao: no further gain)
-            for key, vals, what in (("batch_rounds", {"batch_rounds": 0}, "_one_launch_per_round_ms"),
-                                    ("snap64", {"snapshot_workers_max": 0}, "_snapshot_workers64_ms"),
-                                    ("idle", {"idle_skip": 1}, "_idle_skip_ms")):
+            # the same step with one launch per round (no shared launches; process-local)
+            for key, vals, what in (("batch_rounds", {"batch_rounds": 0}, "_one_launch_per_round_ms"),):
                 for k, v in vals.items():
                     comm.set_config(k, v)
                 try:
@@ -1459,13 +1438,19 @@ def straggler_c4(comm, dev, rank, world, rounds=16, delay_fracs=(0.2, 2.0)):
         dev.synchronize()
 
     def one(delay):
+        """-> (post-to-wait seconds, contributors, the straggler's achieved delay).  The
+        delay is a spin to a perf_counter deadline (time.sleep cannot do tens of us), and the
+        achieved one is measured from the barrier to the post."""
         if not (late and delay):
             fill()
         comm.barrier()
-        if late and delay:
-            time.sleep(delay)
+        tb = time.perf_counter()
+        if late and delay:   # the late gradient, then a spin to the deadline
             fill()
+            while time.perf_counter() - tb < delay:
+                pass
         t0 = time.perf_counter()
+        achieved = t0 - tb
         sch.post()
         sch.wait()
         dt_ = time.perf_counter() - t0
@@ -1474,23 +1459,25 @@ def straggler_c4(comm, dev, rank, world, rounds=16, delay_fracs=(0.2, 2.0)):
         dev.synchronize()
         c = float(cell[0])
         comm.barrier()
-        return dt_, c
+        return dt_, c, achieved
 
     base = [one(0.0)[0] for _ in range(12)]
     T = _max_over_ranks(statistics.median(base))
     out = {"bucket_fp32": count, "world": world, "T_no_straggler_ms": round(T * 1e3, 3)}
     for f in delay_fracs:
         first = sch.stats()["joined"] + 1
-        lat, contrib = [], []
+        lat, contrib, ach = [], [], []
         for _ in range(rounds):
-            d, c = one(f * T)
-            lat.append(d); contrib.append(c)
+            d, c, a = one(f * T)
+            lat.append(d); contrib.append(c); ach.append(a)
         log = [e for e in sch.log() if first <= e["round"] < first + rounds]
         by_straggler = sum(1 for e in log if e["activator"] == world - 1)
         want = [world if e["activator"] == world - 1 else world - 1 for e in log]
         on_time = _max_over_ranks(statistics.median(lat) if not late else 0.0)
         out[f"delay_{f:g}T"] = {
-            "straggler_delay_ms": round(f * T * 1e3, 3),
+            "straggler_delay_requested_ms": round(f * T * 1e3, 3),
+            # the straggler's own measurement (the median over its rounds), shared by all ranks
+            "straggler_delay_achieved_ms": round(_max_over_ranks(statistics.median(ach) if late else 0.0) * 1e3, 3),
             "contributors_histogram": {str(int(k)): v for k, v in sorted(collections.Counter(contrib).items())},
             "mean_contributors": round(float(np.mean(contrib)), 3),
             "rounds": rounds, "rounds_activated_by_straggler": by_straggler,
@@ -1622,9 +1609,14 @@ def run_allreduce(args, rank, world):
         "data": "synthetic (splitmix64 uniform [-1,1), generated on device)",
         "config": {"workload": f"C3: {args.schedule}-allreduce of one {args.bucket_mib:g} MiB "
                                f"{args.dtype} bucket per GPU, in place",
-                   "bucket_bytes": S, "parallelism": f"dp{world} (one rank per GPU)",
+                   "bucket_bytes": S,
+                   # what ran, from the ranks' devices: a 1-GPU rehearsal is labelled as one
+                   "parallelism": (f"dp{world} ({world} ranks on one GPU: rehearsal)" if len(set(devs)) == 1
+                                   else f"dp{world} ({world} ranks on {len(set(devs))} GPUs, shared)" if SHARED_GPU
+                                   else f"dp{world} (one rank per GPU)"),
                    "transport": ("rccl p2p send/recv + tree kernel on a side stream" if transport == "rccl"
-                                 else "ipc pull (reduce-scatter tree kernel + all-gather) over xGMI")},
+                                 else "ipc pull (reduce-scatter tree kernel + all-gather) " +
+                                 ("in one GPU's HBM" if SHARED_GPU else "over xGMI"))},
         "algbw_GBs": round(algbw, 2), "busbw_GBs": round(busbw, 2),
         "xgmi_frac": None if SHARED_GPU else round(t_min / t_step, 4),
         "roofline": None if SHARED_GPU else {

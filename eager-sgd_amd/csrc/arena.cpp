@@ -55,9 +55,8 @@ namespace {
 constexpr size_t kGranule = size_t(2) << 20;
 constexpr size_t kSlab = size_t(4) << 20;
 size_t alloc_bytes(size_t usable);
-bool seal_on();
-// what a small-class slab hands out: its last 4 KiB hold the seal
-size_t slab_usable() { return seal_on() ? kSlab - kSealBytes : kSlab; }
+// what a small-class slab hands out: its last 4 KiB hold the seal (every chunk has one)
+size_t slab_usable() { return kSlab - kSealBytes; }
 constexpr size_t kMinBlock = 4096;
 
 struct Chunk {
@@ -126,7 +125,6 @@ void release_chunk(Chunk *c) {
     drop_free(c);
     g_by_base.erase(reinterpret_cast<uintptr_t>(c->base));
     g_chunks.erase(std::remove(g_chunks.begin(), g_chunks.end(), c), g_chunks.end());
-    if (c->exported) ipc_trace("free", -1, c->base, c->bytes, c->handle);
     hip_ignore(hipFree(c->base));
     delete c;
 }
@@ -142,18 +140,12 @@ void release_idle(int dev) {
     for (Chunk *c : idle) release_chunk(c);
 }
 
-// ESGD_SEAL=0 (an A/B switch): chunks without the seal and its room
-bool seal_on() {
-    static const bool on = !(getenv("ESGD_SEAL") && *getenv("ESGD_SEAL") == '0');
-    return on;
-}
 
 // A chunk of `usable` bytes is one hipMalloc of whole 2 MiB granules with room for the
 // seal right behind the usable bytes (whole granules: measured the same as without the
 // seal, round 4 r04m).  A slab gives up its last 4 KiB (slab_usable); a large chunk gets a
 // granule more than its blocks.
 size_t alloc_bytes(size_t usable) {
-    if (!seal_on()) return usable;
     return (usable + kSealBytes + kGranule - 1) / kGranule * kGranule;
 }
 
@@ -183,12 +175,11 @@ int new_chunk(size_t bytes, int dev, bool release, Chunk **out) {
     return ESGD_SUCCESS;
 }
 
-// ESGD_ARENA_BYPASS=1 (diagnostics only, tools/ipc_bisect.py): every block is its own
-// hipMalloc and is freed, exported or not -- the pre-arena behaviour whose re-exports read
-// back wrong, so the trigger can be re-checked on a new driver.
+// ESGD_TEST arena_bypass=1 (diagnostics only): every block is its own hipMalloc and is
+// freed, exported or not -- the pre-arena behaviour whose re-exports read back wrong
+// (DESIGN.md §5), so the trigger can be re-checked on a new driver.
 bool bypass() {   // 1: bypass; 2: also close peer mappings at schedule deletion (dataplane.cpp)
-    static const bool b = getenv("ESGD_ARENA_BYPASS") &&
-                          (*getenv("ESGD_ARENA_BYPASS") == '1' || *getenv("ESGD_ARENA_BYPASS") == '2');
+    static const bool b = test_knob("arena_bypass", 0) == 1 || test_knob("arena_bypass", 0) == 2;
     return b;
 }
 
@@ -398,22 +389,18 @@ static int export_impl(const void *p, size_t bytes, void **base, uint64_t *off, 
     // failed attempt is reported on stderr with the chunk's address and this process's pid.
     hipIpcMemHandle_t h;
     hipError_t e = hipSuccess;
-    // ESGD_FAIL_EXPORTS=N (tests): the process's first N chunk exports fail as the
-    // runtime's did.  The simulation walks the real path up to the runtime call -- the
+    // ESGD_TEST fail_exports=N: the process's first N chunk exports fail as the runtime's did.  The simulation walks the real path up to the runtime call -- the
     // seal is written into the chunk (on the round stream, synchronously) -- and then the
     // call is refused instead of made, so everything after it (quarantine, the buffers
     // moved, peers mapping the new chunk and reading its seal) is what a real refusal runs.
-    static int simulated = [] {
-        const char *v = getenv("ESGD_FAIL_EXPORTS");
-        return (v && *v) ? std::max(0, atoi(v)) : 0;
-    }();
+    static int simulated = int(std::max<int64_t>(0, test_knob("fail_exports", 0)));
     const bool simulate = sim && simulated > 0;
     if (simulate) --simulated;
-    if (!c->nonce && seal_on())
+    if (!c->nonce)
         if (int rc = write_seal(c)) return rc;
     if (simulate) {
         e = hipErrorInvalidValue;
-        std::fprintf(stderr, "esgd: pid %d: export of %p (%zu B chunk, sealed) fails by ESGD_FAIL_EXPORTS\n",
+        std::fprintf(stderr, "esgd: pid %d: export of %p (%zu B chunk, sealed) fails by ESGD_TEST fail_exports\n",
                      int(getpid()), static_cast<void *>(c->base), c->bytes);
     }
     for (int attempt = 0; !simulate && attempt < 2; ++attempt) {
@@ -430,7 +417,6 @@ static int export_impl(const void *p, size_t bytes, void **base, uint64_t *off, 
         // owns (a fresh chunk) and shadows a caller's bucket that lives here
         c->unexportable = true;
         drop_free(c);
-        ipc_trace(simulate ? "export-refused-simulated" : "export-refused", -1, c->base, c->bytes, nullptr);
         if (!simulate) {   // what the runtime believes this allocation is
             hipPointerAttribute_t pa;
             if (hipPointerGetAttributes(&pa, c->base) == hipSuccess)
@@ -453,7 +439,6 @@ static int export_impl(const void *p, size_t bytes, void **base, uint64_t *off, 
     }
     std::memcpy(c->handle, &h, 64);
     c->exported = true;
-    ipc_trace("export", -1, c->base, c->bytes, c->handle);
     return give(c);
 }
 

@@ -199,16 +199,6 @@ int esgd_schedule_wait_ex(esgd_sched_h h, int *fresh) {
     return sched_wait_ex(s, fresh);
 }
 
-int esgd_round_stream(void **stream) {
-    ESGD_ARG(stream, "esgd_round_stream: null output");
-    return dataplane_round_stream(stream);
-}
-
-int esgd_schedule_wait_on(esgd_sched_h h, void *stream, int *fresh) {
-    Sched *s = handle_to_sched(h);
-    if (!s) return ESGD_INVALID_ARG;
-    return sched_wait_on(s, stream, fresh);
-}
 
 int esgd_schedule_release(esgd_sched_h h, void *stream) {
     Sched *s = handle_to_sched(h);

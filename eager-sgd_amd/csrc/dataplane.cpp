@@ -44,17 +44,7 @@ int reduce_remote(int dtype, int k, const void *const *inputs, void *out, uint64
 int gather_remote(int n, const void *const *src, void *const *dst, const uint64_t *bytes,
                   hipStream_t s, unsigned max_blocks = 0);
 int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s);
-int snapshot_copy(void *dst, const void *src, uint64_t bytes, hipStream_t s);
 
-// ESGD_SNAPSHOT_KERNEL: 1 = device-bucket snapshots (rb = sb, rb = 0) by k_snapshot's
-// write-through stores; 0 = hipMemcpyAsync / hipMemsetAsync
-static bool snapshot_kernel() {
-    static const bool on = [] {
-        const char *e = getenv("ESGD_SNAPSHOT_KERNEL");
-        return e && *e == '1';
-    }();
-    return on;
-}
 int narrow_bf16(float *src, uint16_t *dst, uint64_t n, bool zero_src, hipStream_t s);
 int reduce_wire(int k, const void *const *inputs, uint16_t *outb, float *outf, uint64_t count, hipStream_t s);
 int gather_widen(int n, const void *const *src, void *const *dst, const uint64_t *count, hipStream_t s);
@@ -71,12 +61,11 @@ constexpr int kMaxSegs = 16;                      // segments per gather launch 
 // Bytes per input / segment of one remote launch: 64 MiB, the local tree kernel's window
 // (reduce_kernels.hip kWindowBytes; in the shared-GPU rehearsal 64 MiB pieces took C5's
 // 256 MiB - 1 GiB rounds 2-7 % faster than 1 GiB ones), at most 1 GiB (the kernels
-// address a shard through 32-bit buffer offsets).  ESGD_PIECE_BYTES (a multiple of
-// 1 KiB) overrides it; the tests drive the piecewise path with small pieces.
+// address a shard through 32-bit buffer offsets).  The tests drive the piecewise path with
+// small pieces (ESGD_TEST piece_bytes, a multiple of 1 KiB).
 static uint64_t piece_bytes() {
     static const uint64_t v = [] {
-        const char *e = getenv("ESGD_PIECE_BYTES");
-        const uint64_t b = (e && *e) ? uint64_t(strtoull(e, nullptr, 10)) : (uint64_t(64) << 20);
+        const uint64_t b = uint64_t(std::max<int64_t>(0, test_knob("piece_bytes", int64_t(64) << 20)));
         return std::max<uint64_t>(1024, std::min<uint64_t>(b, uint64_t(1) << 30) / 1024 * 1024);
     }();
     return v;
@@ -111,10 +100,6 @@ static int device_flags_env() {
 // All ranks must set the same values before the same creations (the creation signature
 // checks it), so a benchmark can A/B them inside one job.
 static std::atomic<int64_t> g_cfg_small{-1}, g_cfg_flags{-1}, g_cfg_strict{-1}, g_cfg_batch{-1};
-// process-local switches of the host path (-1 = the env default), read where they act:
-// batch_depth (ESGD_BATCH_DEPTH), snapshot_in_batch (ESGD_SNAPSHOT_IN_BATCH), inline_join
-// (ESGD_INLINE_JOIN, engine.cpp)
-static std::atomic<int64_t> g_cfg_depth{-1}, g_cfg_snap{-1}, g_cfg_inline{-1};
 // "batch_hold" (diagnostics / tests): 1 = the end of a pump never sends the pending shared
 // launch; only an explicit flush (another launch on the round stream, schedule deletion,
 // finalize) does -- so a test can finalize with rounds held
@@ -129,58 +114,14 @@ static std::atomic<int64_t> g_cfg_workers{-1};
 // GPU: the optimizer's per-tensor step 1.44 -> 1.35 ms at P = 2, 2.20 -> 1.93 at P = 4, with
 // 256 against 64); process-local, read at each flush
 static std::atomic<int64_t> g_cfg_snapw{-1};
-// "event_device_scope" (ESGD_EVENT_DEVICE_SCOPE, default 0): the producer / consumer events
-// of posts and releases record with a device-scope release (hipEventReleaseToDevice) instead
-// of HIP's system-scope fence -- they only order the caller's stream before the round stream
-// of the same GPU.  "producer_host_sync" (ESGD_PRODUCER_HOST_SYNC, default 0): a post waits on
-// the host for its producer stream's work instead of the round stream waiting on the GPU (no
-// cross-stream dependency; the posting thread blocks until the gradient is written).
-static std::atomic<int64_t> g_cfg_evscope{-1}, g_cfg_psync{-1};
-// "idle_skip" (ESGD_IDLE_SKIP, default 0): a post (release) whose caller's stream has nothing
-// left to run (hipStreamQuery) records no producer (consumer) event -- the gradient is
-// written (the copy-out done) already, so the round stream has nothing to wait for
-static std::atomic<int64_t> g_cfg_idle{-1};
-
-static bool env_flag(const char *name) {
-    const char *e = getenv(name);
-    return e && *e == '1';
-}
-
-static bool event_device_scope() {
-    static const bool env = env_flag("ESGD_EVENT_DEVICE_SCOPE");
-    const int64_t v = g_cfg_evscope.load(std::memory_order_relaxed);
-    return v >= 0 ? v != 0 : env;
-}
-
-static bool idle_skip() {
-    static const bool env = env_flag("ESGD_IDLE_SKIP");
-    const int64_t v = g_cfg_idle.load(std::memory_order_relaxed);
-    return v >= 0 ? v != 0 : env;
-}
-
-static bool producer_host_sync() {
-    static const bool env = env_flag("ESGD_PRODUCER_HOST_SYNC");
-    const int64_t v = g_cfg_psync.load(std::memory_order_relaxed);
-    return v >= 0 ? v != 0 : env;
-}
-
-bool config_inline_join() {
-    static const bool env = !(getenv("ESGD_INLINE_JOIN") && *getenv("ESGD_INLINE_JOIN") == '0');
-    const int64_t v = g_cfg_inline.load(std::memory_order_relaxed);
-    return v >= 0 ? v != 0 : env;
-}
 
 // One-launch rounds due together in issue order share one launch of at most this many
-// rounds (k_round_batch, round_batch.hip); 0 or 1 = one k_round_small launch per round.
-// ESGD_BATCH_ROUNDS sets the default (kBatchMax).  A process-local setting, not part of
+// rounds (k_round_batch, round_batch.hip; default kBatchMax); 0 or 1 = one k_round_small
+// launch per round (esgd_set_config("batch_rounds")).  A process-local setting, not part of
 // the creation signature: ranks may cut the issue ring into launches differently anyway.
 static int64_t batch_rounds() {
-    static const int64_t env = [] {
-        const char *e = getenv("ESGD_BATCH_ROUNDS");
-        return (e && *e) ? int64_t(atoll(e)) : int64_t(kBatchMax);
-    }();
     const int64_t v = g_cfg_batch.load();
-    return std::min<int64_t>(kBatchMax, v >= 0 ? v : env);
+    return std::min<int64_t>(kBatchMax, v >= 0 ? v : int64_t(kBatchMax));
 }
 
 bool config_strict_handoffs() {
@@ -222,12 +163,6 @@ int config_set(const char *key, int64_t value) {
         ESGD_ARG(value >= -1 && value <= kBatchMax, "batch_rounds: 0..%d rounds per launch (-1: the default)",
                  kBatchMax);
         g_cfg_batch.store(value);
-    } else if (!std::strcmp(key, "batch_depth")) {
-        ESGD_ARG(value >= -1, "batch_depth: >= 0 shared launches queued before one is held (-1: the default)");
-        g_cfg_depth.store(value);
-    } else if (!std::strcmp(key, "inline_join")) {
-        ESGD_ARG(value >= -1 && value <= 1, "inline_join: 0 or 1 (-1: the default)");
-        g_cfg_inline.store(value);
     } else if (!std::strcmp(key, "batch_hold")) {
         ESGD_ARG(value >= -1 && value <= 1, "batch_hold: 0 or 1 (-1: the default, 0)");
         g_cfg_hold.store(value < 0 ? 0 : value);
@@ -239,25 +174,14 @@ int config_set(const char *key, int64_t value) {
         ESGD_ARG(value >= -1 && value <= int64_t(kBatchWorkersMax),
                  "snapshot_workers_max: 0..%u (0: batch_workers_max; -1: the default)", kBatchWorkersMax);
         g_cfg_snapw.store(value);
-    } else if (!std::strcmp(key, "event_device_scope")) {
-        ESGD_ARG(value >= -1 && value <= 1, "event_device_scope: 0 or 1 (-1: the default)");
-        g_cfg_evscope.store(value);
-    } else if (!std::strcmp(key, "producer_host_sync")) {
-        ESGD_ARG(value >= -1 && value <= 1, "producer_host_sync: 0 or 1 (-1: the default)");
-        g_cfg_psync.store(value);
-    } else if (!std::strcmp(key, "idle_skip")) {
-        ESGD_ARG(value >= -1 && value <= 1, "idle_skip: 0 or 1 (-1: the default)");
-        g_cfg_idle.store(value);
     } else {
         set_error("esgd_set_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
-                  "batch_rounds, batch_depth, snapshot_in_batch, inline_join, batch_hold, batch_workers_max, "
-                  "snapshot_workers_max, event_device_scope, producer_host_sync, idle_skip)", key);
+                  "batch_rounds, batch_hold, batch_workers_max, snapshot_workers_max)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
 }
 
-static int batch_depth();
 static uint32_t snapshot_workers_max();
 
 int config_get(const char *key, int64_t *value) {
@@ -268,18 +192,12 @@ int config_get(const char *key, int64_t *value) {
     else if (!std::strcmp(key, "batch_rounds")) *value = batch_rounds();
     else if (!std::strcmp(key, "launches")) *value = int64_t(g_launches.load());
     else if (!std::strcmp(key, "batch_workers")) *value = g_batch_workers.load();
-    else if (!std::strcmp(key, "batch_depth")) *value = batch_depth();
-    else if (!std::strcmp(key, "inline_join")) *value = config_inline_join() ? 1 : 0;
     else if (!std::strcmp(key, "batch_hold")) *value = g_cfg_hold.load();
     else if (!std::strcmp(key, "batch_workers_max")) *value = int64_t(batch_workers_max());
     else if (!std::strcmp(key, "snapshot_workers_max")) *value = int64_t(snapshot_workers_max());
-    else if (!std::strcmp(key, "event_device_scope")) *value = event_device_scope() ? 1 : 0;
-    else if (!std::strcmp(key, "producer_host_sync")) *value = producer_host_sync() ? 1 : 0;
-    else if (!std::strcmp(key, "idle_skip")) *value = idle_skip() ? 1 : 0;
     else {
         set_error("esgd_get_config: unknown key '%s' (small_round_bytes, device_flags, strict_handoffs, "
-                  "batch_rounds, launches, batch_workers, batch_depth, snapshot_in_batch, inline_join, batch_hold, "
-                  "batch_workers_max, snapshot_workers_max, event_device_scope, producer_host_sync, idle_skip)", key);
+                  "batch_rounds, launches, batch_workers, batch_hold, batch_workers_max, snapshot_workers_max)", key);
         return ESGD_INVALID_ARG;
     }
     return ESGD_SUCCESS;
@@ -305,13 +223,10 @@ static std::map<IpcKey, void *> g_ipc;
 // move: SchedShm::remap); per thread, read right after the call
 static thread_local bool t_seal_mismatch = false;
 
-// ESGD_FAIL_MAPS=N (tests): this process's first N sealed mappings are treated as showing
+// ESGD_TEST fail_maps=N: this process's first N sealed mappings are treated as showing
 // other memory, so the re-publish-and-remap retry of schedule creation runs anywhere
 static bool simulated_map_failure() {
-    static std::atomic<int> left{[] {
-        const char *v = getenv("ESGD_FAIL_MAPS");
-        return (v && *v) ? std::max(0, atoi(v)) : 0;
-    }()};
+    static std::atomic<int> left{int(std::max<int64_t>(0, test_knob("fail_maps", 0)))};
     int n = left.load();
     while (n > 0 && !left.compare_exchange_weak(n, n - 1)) {
     }
@@ -337,7 +252,6 @@ static int ipc_open(int peer, const uint8_t *h, void **base, const IpcSlot *slot
     std::memcpy(&hh, h, sizeof(hh));
     void *p = nullptr;
     ESGD_HIP(hipIpcOpenMemHandle(&p, hh, hipIpcMemLazyEnablePeerAccess));
-    ipc_trace("open", peer, p, 0, h);
     if (slot && slot->seal_nonce) {
         ChunkSeal got;
         uint64_t w[4];
@@ -346,11 +260,9 @@ static int ipc_open(int peer, const uint8_t *h, void **base, const IpcSlot *slot
         const bool simulated = simulated_map_failure();
         if (simulated)
             std::fprintf(stderr, "esgd: pid %d: mapping of rank %d's chunk %#llx treated as showing other memory "
-                         "(ESGD_FAIL_MAPS)\n", int(getpid()), peer, (unsigned long long)slot->chunk_base);
+                         "(ESGD_TEST fail_maps)\n", int(getpid()), peer, (unsigned long long)slot->chunk_base);
         if (simulated || got.magic != kSealMagic || got.nonce != slot->seal_nonce || got.base != slot->chunk_base) {
             t_seal_mismatch = true;
-            ipc_trace(simulated ? "import-seal-mismatch-simulated" : "import-seal-mismatch", peer, p,
-                      slot->chunk_bytes, h);
             if (!simulated)
                 std::fprintf(stderr, "esgd: pid %d: rank %d's chunk %#llx (%llu B) mapped at %p shows other memory: seal "
                          "magic %#llx base %#llx nonce %#llx pid %u, expected base %#llx nonce %#llx\n", int(getpid()),
@@ -376,18 +288,17 @@ static bool g_mappings_closed = false;
 static void ipc_close_all() {
     std::lock_guard<std::mutex> lk(g_ipc_mu);
     for (auto &kv : g_ipc) {
-        ipc_trace("close", kv.first.peer, kv.second, 0, kv.first.h);
         hip_ignore(hipIpcCloseMemHandle(kv.second));
     }
     if (!g_ipc.empty()) g_mappings_closed = true;
     g_ipc.clear();
 }
 
-// ESGD_ARENA_BYPASS=2 (diagnostics only, tools/ipc_bisect.py): besides the arena bypass
-// (arena.cpp), a schedule's teardown closes the peer mappings it opened -- round 2's
-// pre-arena lifetime, where deletion was local and every rank closed its peers' buckets.
+// ESGD_TEST arena_bypass=2 (diagnostics only): besides the arena bypass (arena.cpp), a
+// schedule's teardown closes the peer mappings it opened -- round 2's pre-arena lifetime,
+// where deletion was local and every rank closed its peers' buckets.
 static bool close_on_delete() {
-    static const bool b = getenv("ESGD_ARENA_BYPASS") && *getenv("ESGD_ARENA_BYPASS") == '2';
+    static const bool b = test_knob("arena_bypass", 0) == 2;
     return b;
 }
 
@@ -398,7 +309,6 @@ static void ipc_close_one(int peer, const uint8_t *h) {
     std::memcpy(k.h, h, 64);
     auto it = g_ipc.find(k);
     if (it == g_ipc.end()) return;
-    ipc_trace("close", peer, it->second, 0, h);
     hip_ignore(hipIpcCloseMemHandle(it->second));
     g_ipc.erase(it);
 }
@@ -433,14 +343,6 @@ static int round_stream(hipStream_t *out) {
 // earliest round in flight anywhere has been launched by every rank and completes.
 int seal_stream(hipStream_t *out) { return round_stream(out); }
 
-// esgd_round_stream: a caller may queue work on the round stream itself, to be ordered
-// after the rounds launched so far by stream order alone (EagerSGDOptimizer's round_stream)
-int dataplane_round_stream(void **out) {
-    hipStream_t st = nullptr;
-    if (int rc = round_stream(&st)) return rc;
-    *out = st;
-    return ESGD_SUCCESS;
-}
 
 // Copy streams of the chunked host-bucket rounds (one per direction, so a chunk's D2H
 // runs while the next chunk's H2D does: PCIe is full duplex).  Created on first use.
@@ -455,12 +357,11 @@ static int copy_streams(hipStream_t *h2d, hipStream_t *d2h) {
     return ESGD_SUCCESS;
 }
 
-// Host buckets of at least two chunks of this many bytes run chunked rounds
-// (ESGD_HOST_CHUNK_BYTES, a multiple of 1 KiB; 0 = never).
+// Host buckets of at least two chunks of this many bytes run chunked rounds (16 MiB; the
+// tests drive it with small chunks: ESGD_TEST host_chunk_bytes, 0 = never).
 static uint64_t host_chunk_bytes() {
     static const uint64_t v = [] {
-        const char *e = getenv("ESGD_HOST_CHUNK_BYTES");
-        const uint64_t b = (e && *e) ? uint64_t(strtoull(e, nullptr, 10)) : (uint64_t(16) << 20);
+        const uint64_t b = uint64_t(std::max<int64_t>(0, test_knob("host_chunk_bytes", int64_t(16) << 20)));
         return b ? std::max<uint64_t>(16384, b / 1024 * 1024) : 0;
     }();
     return v;
@@ -813,28 +714,26 @@ static int base_setup(Sched &s, BaseState &st) {
 }
 
 static std::mutex g_evfree_mu;
-static std::vector<hipEvent_t> g_evfree[2];   // pooled events no round refers to any more [device scope]
+static std::vector<hipEvent_t> g_evfree;   // pooled events no round refers to any more
 
 // ---- events: a process-wide pool, and recordings shared by a group of schedules ----
 // A producer (consumer) event marks where the caller's stream stands at a post (release).
 // esgd_schedule_post_group / _release_group record ONE event for all the schedules they
 // name (dataplane_group_begin/end: this thread's posts / releases on that stream use it),
 // and the round stream waits for a recording once however many rounds refer to it.
-static std::shared_ptr<hipEvent_t> pooled_event(bool device_scope = false) {
+static std::shared_ptr<hipEvent_t> pooled_event() {
     hipEvent_t e = nullptr;
-    const int k = device_scope ? 1 : 0;
     {
         std::lock_guard<std::mutex> lk(g_evfree_mu);
-        if (!g_evfree[k].empty()) { e = g_evfree[k].back(); g_evfree[k].pop_back(); }
+        if (!g_evfree.empty()) { e = g_evfree.back(); g_evfree.pop_back(); }
     }
-    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming | (device_scope ? hipEventReleaseToDevice : 0u)) !=
-                  hipSuccess) {
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
         (void)hip_fail(hipGetLastError(), "hipEventCreateWithFlags", __FILE__, __LINE__);
         return nullptr;
     }
-    return std::shared_ptr<hipEvent_t>(new hipEvent_t(e), [k](hipEvent_t *p) {
+    return std::shared_ptr<hipEvent_t>(new hipEvent_t(e), [](hipEvent_t *p) {
         std::lock_guard<std::mutex> lk(g_evfree_mu);
-        g_evfree[k].push_back(*p);
+        g_evfree.push_back(*p);
         delete p;
     });
 }
@@ -847,7 +746,6 @@ struct GroupEvent {   // this thread's open group: [0] posts, [1] releases
     bool open = false;
     void *stream = nullptr;
     std::shared_ptr<hipEvent_t> ev;
-    bool synced = false;   // producer_host_sync: the group's producer work was waited for
 };
 static thread_local GroupEvent g_group[2];
 
@@ -856,7 +754,6 @@ int dataplane_group_begin(int which, void *stream) {
     g.open = true;
     g.stream = stream;
     g.ev.reset();   // recorded by the group's first schedule that needs it
-    g.synced = false;
     return ESGD_SUCCESS;
 }
 
@@ -870,35 +767,11 @@ void dataplane_group_end(int which) {
 static int note_event(int which, void *stream, std::shared_ptr<hipEvent_t> *out) {
     GroupEvent &g = g_group[which];
     const bool same = g.open && g.stream == stream;
-    if (idle_skip() && !(same && g.ev)) {
-        if (same && g.synced) {   // the group found the stream idle already
-            out->reset();
-            return ESGD_SUCCESS;
-        }
-        const hipError_t q = hipStreamQuery(user_stream(stream));
-        if (q == hipSuccess) {    // everything queued there has run: nothing to wait for
-            out->reset();
-            if (same) g.synced = true;
-            return ESGD_SUCCESS;
-        }
-        (void)hipGetLastError();  // hipErrorNotReady is not a failure; later checks must not see it
-        if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery", __FILE__, __LINE__);
-    }
-    if (which == 0 && producer_host_sync()) {   // wait here; nothing for the GPU to wait on
-        out->reset();
-        if (same && g.synced) return ESGD_SUCCESS;
-        std::shared_ptr<hipEvent_t> ev = pooled_event(event_device_scope());
-        if (!ev) return ESGD_ERROR;
-        ESGD_HIP(hipEventRecord(*ev, user_stream(stream)));
-        ESGD_HIP(hipEventSynchronize(*ev));
-        if (same) g.synced = true;
-        return ESGD_SUCCESS;
-    }
     if (same && g.ev) {
         *out = g.ev;
         return ESGD_SUCCESS;
     }
-    std::shared_ptr<hipEvent_t> ev = pooled_event(event_device_scope());
+    std::shared_ptr<hipEvent_t> ev = pooled_event();
     if (!ev) return ESGD_ERROR;
     ESGD_HIP(hipEventRecord(*ev, user_stream(stream)));
     if (g.open && g.stream == stream) g.ev = ev;
@@ -934,17 +807,15 @@ static int stream_wait(hipStream_t cs, const std::shared_ptr<hipEvent_t> &ev) {
 static int base_note_producer(BaseState &st, uint32_t round, void *stream) {
     std::shared_ptr<hipEvent_t> ev;
     if (int rc = note_event(0, stream, &ev)) return rc;
-    if (ev) st.producer[round] = std::move(ev);   // none: waited for on the host already
+    st.producer[round] = std::move(ev);
     return ESGD_SUCCESS;
 }
 
 static int base_note_consumer(BaseState &st, void *stream) {
     std::shared_ptr<hipEvent_t> ev;
     if (int rc = note_event(1, stream, &ev)) return rc;
-    if (ev) {   // none: the caller's stream was idle (idle_skip), nothing more to wait for
-        st.consumer = std::move(ev);
-        st.consumer_pending = true;
-    }
+    st.consumer = std::move(ev);
+    st.consumer_pending = true;
     return ESGD_SUCCESS;
 }
 
@@ -1064,31 +935,14 @@ static bool debug_on() {
 // Host buckets up to this many bytes move between host memory and HBM by kernel: the
 // round's stream reads / writes the pinned bucket directly over PCIe (16-B system-scope
 // loads, all in flight at once) instead of a DMA copy, whose fixed cost dominates small
-// buckets (C1, 1 MiB: DESIGN.md §7).  ESGD_HOST_KERNEL_COPY_BYTES overrides (0 = never).
-static uint64_t host_kernel_copy_bytes() {
-    static const uint64_t v = [] {
-        const char *e = getenv("ESGD_HOST_KERNEL_COPY_BYTES");
-        return (e && *e) ? uint64_t(strtoull(e, nullptr, 10)) : (uint64_t(4) << 20);
-    }();
-    return v;
-}
-
-// Chunked host rounds move their chunks by kernel through the pinned bucket's device view
-// (16-B system-scope accesses over PCIe, at most ESGD_HOST_CHUNK_KERNEL workgroups per
-// copy, beside the round's kernels) instead of DMA copies; 0 = DMA.
-static unsigned host_chunk_kernel_blocks() {
-    static const unsigned v = [] {
-        const char *e = getenv("ESGD_HOST_CHUNK_KERNEL");
-        return (e && *e) ? unsigned(strtoul(e, nullptr, 10)) : 0u;
-    }();
-    return v;
-}
+// buckets (C1, 1 MiB: DESIGN.md §7).
+constexpr uint64_t kHostKernelCopyBytes = uint64_t(4) << 20;
 
 // dst <- src, one of them pinned host memory with device view `view` (or nullptr)
 static int host_move(void *dst, const void *src, const void *view, bool h2d, size_t bytes, hipStream_t cs) {
     const void *ks = h2d ? view : src;
     void *kd = h2d ? dst : const_cast<void *>(view);
-    if (view && bytes <= host_kernel_copy_bytes() &&
+    if (view && bytes <= kHostKernelCopyBytes &&
         ((reinterpret_cast<uintptr_t>(ks) | reinterpret_cast<uintptr_t>(kd)) & 15) == 0) {
         const uint64_t b = bytes;
         return gather_remote(1, &ks, &kd, &b, cs);
@@ -1144,8 +998,6 @@ static int base_copy_in(Sched &s, BaseState &st, uint32_t round, bool fresh, hip
     if (s.fresh_only && !fresh) {
         // carried through a round it had not posted: this rank contributes zeros, and its
         // send bucket -- which the caller may be writing right now -- is not read
-        if (snapshot_kernel() && (reinterpret_cast<uintptr_t>(st.rb_dev) & 15) == 0)
-            return snapshot_copy(st.rb_dev, nullptr, bytes, cs);
         ESGD_HIP(hipMemsetAsync(st.rb_dev, 0, bytes, cs));
         return ESGD_SUCCESS;
     }
@@ -1159,8 +1011,6 @@ static int base_copy_in(Sched &s, BaseState &st, uint32_t round, bool fresh, hip
         if (int rc = move_zero(st.rb_dev, s.sb, bytes, cs)) return rc;
     } else if (!s.in_place || st.shadow) {
         const void *src = s.in_place ? s.rb : s.sb;
-        if (snapshot_kernel() && ((reinterpret_cast<uintptr_t>(st.rb_dev) | reinterpret_cast<uintptr_t>(src)) & 15) == 0)
-            return snapshot_copy(st.rb_dev, src, bytes, cs);
         ESGD_HIP(hipMemcpyAsync(st.rb_dev, src, bytes, hipMemcpyDeviceToDevice, cs));
     }
     return ESGD_SUCCESS;
@@ -1356,20 +1206,12 @@ static uint32_t snapshot_workers_max() {
 // shared launches queued and not yet seen complete, oldest first (their events)
 static std::deque<std::shared_ptr<hipEvent_t>> g_outstanding;
 
-// ESGD_BATCH_DEPTH: at the end of a pump the pending launch goes out only while fewer
-// than this many shared launches are queued and unfinished; rounds that come due
-// meanwhile join the next launch instead of each pump making its own (0: every pump
-// flushes).  Default 1 (round 4, ranks sharing one GPU, interleaved A/B: the 161-bucket
-// pipelined step 0.75-0.83 -> 0.66-0.71 ms at P = 2, 1.26-1.52 -> 0.97-0.99 ms at P = 4;
-// the optimizer's per-tensor step unchanged within noise; depth 2 and 3 slowed it at P = 4).
-static int batch_depth() {
-    static const int env = [] {
-        const char *e = getenv("ESGD_BATCH_DEPTH");
-        return e ? std::max(0, atoi(e)) : 1;
-    }();
-    const int64_t v = g_cfg_depth.load(std::memory_order_relaxed);
-    return v >= 0 ? int(v) : env;
-}
+// At the end of a pump the pending launch goes out only while no shared launch is queued
+// and unfinished; rounds that come due meanwhile join the next launch instead of each pump
+// making its own (round 4, ranks sharing one GPU, interleaved A/B: the 161-bucket pipelined
+// step 0.75-0.83 -> 0.66-0.71 ms at P = 2, 1.26-1.52 -> 0.97-0.99 ms at P = 4 against a
+// flush at every pump; holding more launches back slowed P = 4).
+constexpr size_t kBatchDepth = 1;
 
 // this schedule's BatchDesc: built at its first batched round and uploaded on the round
 // stream (ahead of the launch that reads it); its buckets, peers' mappings and flags never
@@ -1549,7 +1391,7 @@ int dataplane_flush() {
     return rc;
 }
 
-// The end of a pump: the pending launch goes out unless ESGD_BATCH_DEPTH shared launches
+// The end of a pump: the pending launch goes out unless kBatchDepth shared launches
 // are still queued.  A held launch cannot deadlock the node: the launches it waits behind
 // hold only rounds earlier in the issue order, which every peer has launched already (it
 // launched a later one) or will launch before any it holds back, so they complete, and
@@ -1557,30 +1399,16 @@ int dataplane_flush() {
 int dataplane_flush_soft() {
     std::lock_guard<std::mutex> lk(g_batch_mu);
     if (g_pend.empty() || g_cfg_hold.load(std::memory_order_relaxed)) return ESGD_SUCCESS;
-    if (const int depth = batch_depth()) {
-        while (!g_outstanding.empty() && hipEventQuery(*g_outstanding.front()) != hipErrorNotReady)
-            g_outstanding.pop_front();   // finished (a fault is reported by its rounds)
-        (void)hipGetLastError();   // the not-ready status is not an error of the next launch
-        if (int(g_outstanding.size()) >= depth) return ESGD_SUCCESS;
-    }
+    while (!g_outstanding.empty() && hipEventQuery(*g_outstanding.front()) != hipErrorNotReady)
+        g_outstanding.pop_front();   // finished (a fault is reported by its rounds)
+    (void)hipGetLastError();   // the not-ready status is not an error of the next launch
+    if (g_outstanding.size() >= kBatchDepth) return ESGD_SUCCESS;
     const double t0 = now_s();
     const int rc = batch_flush_locked();
     g_flush_ns.fetch_add(uint64_t((now_s() - t0) * 1e9), std::memory_order_relaxed);
     return rc;
 }
 
-void dataplane_extra_queues(int n) {
-    static std::vector<hipStream_t> keep;
-    static uint32_t *word = nullptr;
-    if (n <= 0 || (!word && hipMalloc(reinterpret_cast<void **>(&word), 64) != hipSuccess)) return;
-    for (int i = 0; i < n; ++i) {
-        hipStream_t st = nullptr;
-        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) break;
-        hip_ignore(hipMemsetAsync(word, 0, 4, st));   // the first command creates the queue
-        hip_ignore(hipStreamSynchronize(st));
-        keep.push_back(st);
-    }
-}
 
 // diagnostics for a timed-out wait: the shared launch being filled (schedule:round of each
 // entry), shared launches queued and not yet seen finished, and a seal I/O in progress
@@ -1665,32 +1493,6 @@ static int batch_append(Sched &s, IpcState &st, uint32_t round, hipStream_t cs) 
     return ESGD_SUCCESS;
 }
 
-// sched_wait_on: `stream` waits for the event after the round's last queued work -- its
-// shared launch's (once sent) or its own (st.ev, recorded last by every device round).  All
-// of them are queued on the process's one round stream, so a shared launch at or before one
-// `stream` already waits for (`seen`) needs no second wait: the 161 waits of the optimizer's
-// step become one per shared launch (~13).  Host buckets finish on the host (base_complete),
-// a failed shared launch is reported by the host wait.  Caller holds s.mu (in_batch is
-// written under it; batch_ev / batch_seq under g_batch_mu, after `flushed`).
-static int base_order_after(Sched &s, BaseState &st, uint32_t round, void *stream, uint64_t *seen) {
-    if (s.host_mode || st.copyout_pending) return 2;
-    hipEvent_t ev;
-    if (st.in_batch) {
-        if (st.flushed.load(std::memory_order_acquire) != round) return 0;   // still pending
-        if (user_stream(stream) == st.stream) return 1;   // the round stream: in order already
-        std::lock_guard<std::mutex> lk(g_batch_mu);
-        if (st.batch_rc || !st.batch_ev) return 2;
-        if (seen && *seen >= st.batch_seq) return 1;
-        ev = *st.batch_ev;
-        if (seen) *seen = st.batch_seq;
-    } else {
-        if (user_stream(stream) == st.stream) return 1;
-        ev = st.ev;
-    }
-    ESGD_HIP(hipStreamWaitEvent(user_stream(stream), ev, 0));
-    return 1;
-}
-
 static void batch_shutdown() {
     std::lock_guard<std::mutex> lk(g_batch_mu);
     (void)batch_flush_locked();
@@ -1702,10 +1504,8 @@ static void batch_shutdown() {
     if (g_desc_dev) { hip_ignore(hipFree(g_desc_dev)); g_desc_dev = nullptr; g_slots = nullptr; }
     if (g_desc_host) { hip_ignore(hipHostFree(g_desc_host)); g_desc_host = nullptr; }
     std::lock_guard<std::mutex> ek(g_evfree_mu);
-    for (auto &pool : g_evfree) {
-        for (hipEvent_t e : pool) hip_ignore(hipEventDestroy(e));
-        pool.clear();
-    }
+    for (hipEvent_t e : g_evfree) hip_ignore(hipEventDestroy(e));
+    g_evfree.clear();
 }
 
 struct IpcTransport final : Transport {
@@ -1863,9 +1663,9 @@ struct IpcTransport final : Transport {
         if (s.flag_mode > 0)
             if (int rc = flags_publish(s.rank, s.flag_mode)) return rc;
         // publish this rank's rb (peers map it in connect())
-        // ESGD_SHADOW=1 shadows every device bucket (caller buckets that are freed and
+        // ESGD_TEST shadow=1 shadows every device bucket (caller buckets that are freed and
         // re-allocated between rounds; also how the tests reach the fallback)
-        static const bool force_shadow = getenv("ESGD_SHADOW") && *getenv("ESGD_SHADOW") == '1';
+        static const bool force_shadow = test_knob("shadow", 0) == 1;
         if (int rc = publish_pub(s, *st)) return rc;
         if (s.host_mode || s.wire_bf16) return publish(s, *st);
         int rc = force_shadow ? ESGD_INVALID_ARG : publish(s, *st);
@@ -2149,12 +1949,6 @@ struct IpcTransport final : Transport {
         const bool stg = staged(s, st);
         const char *src = stg ? st.pin : static_cast<const char *>(s.sb ? s.sb : s.rb);
         char *dst = stg ? st.pin : static_cast<char *>(s.rb);
-        // device views of the same host buffers (kernel copies), when asked and aligned
-        const char *vsrc = stg ? st.view_pin : (s.sb ? st.view_sb : st.view_rb);
-        char *vdst = stg ? st.view_pin : st.view_rb;
-        const unsigned kb = host_chunk_kernel_blocks();
-        const bool kcopy = kb && vsrc && vdst &&
-                           ((reinterpret_cast<uintptr_t>(vsrc) | reinterpret_cast<uintptr_t>(vdst)) & 15) == 0;
         const uint64_t salign = 1024 / es;
         for (uint32_t c = 0; c < C; ++c) {
             const uint64_t c0 = uint64_t(c) * Q, n = std::min(Q, count - c0);
@@ -2162,11 +1956,6 @@ struct IpcTransport final : Transport {
             if (st.chunked_before) ESGD_HIP(hipStreamWaitEvent(hs, ed, 0));   // last round's D2H
             if (s.fresh_only && !fresh) {   // not posted: zeros, the host bucket is not read
                 ESGD_HIP(hipMemsetAsync(st.rb_dev + c0 * es, 0, n * es, hs));
-            } else if (kcopy) {
-                const void *ks = vsrc + c0 * es;
-                void *kd = st.rb_dev + c0 * es;
-                const uint64_t b = n * es;
-                if (int rc = gather_remote(1, &ks, &kd, &b, hs, kb)) return rc;
             } else {
                 ESGD_HIP(hipMemcpyAsync(st.rb_dev + c0 * es, src + c0 * es, n * es, hipMemcpyHostToDevice, hs));
             }
@@ -2206,14 +1995,7 @@ struct IpcTransport final : Transport {
             }
             ESGD_HIP(hipEventRecord(er, cs));
             ESGD_HIP(hipStreamWaitEvent(ds, er, 0));
-            if (kcopy) {
-                const void *ks = st.rb_dev + c0 * es;
-                void *kd = vdst + c0 * es;
-                const uint64_t b = n * es;
-                if (int rc = gather_remote(1, &ks, &kd, &b, ds, kb)) return rc;
-            } else {
-                ESGD_HIP(hipMemcpyAsync(dst + c0 * es, st.rb_dev + c0 * es, n * es, hipMemcpyDeviceToHost, ds));
-            }
+            ESGD_HIP(hipMemcpyAsync(dst + c0 * es, st.rb_dev + c0 * es, n * es, hipMemcpyDeviceToHost, ds));
             ESGD_HIP(hipEventRecord(ed, ds));
         }
         ESGD_HIP(hipStreamWaitEvent(cs, st.cev[3 * (C - 1) + 2], 0));   // ds is in order
@@ -2250,9 +2032,6 @@ struct IpcTransport final : Transport {
     }
 
     int query(Sched &s) override { return base_query(s, S(s)); }
-    int order_after(Sched &s, uint32_t round, void *stream, uint64_t *seen) override {
-        return base_order_after(s, S(s), round, stream, seen);
-    }
 
     int complete(Sched &s) override { return base_complete(s, S(s)); }
 
@@ -2301,12 +2080,11 @@ struct NullTransport final : Transport {
     bool ordered_;   // the "rccl" flavour (same protocol; named for the issue-order tests)
     const char *name() const override { return ordered_ ? "none-ordered" : "none"; }
     int setup(Sched &) override { return ESGD_SUCCESS; }
-    // ESGD_TEST_FAIL_CONNECT=<rank>: that rank's connect fails (control-plane tests of the
+    // ESGD_TEST fail_connect=<rank>: that rank's connect fails (control-plane tests of the
     // creation protocol; this transport moves no data)
     int connect(Sched &s) override {
-        const char *e = getenv("ESGD_TEST_FAIL_CONNECT");
-        if (e && *e && atoi(e) == s.rank) {
-            set_error("connect failed on rank %d (ESGD_TEST_FAIL_CONNECT)", s.rank);
+        if (test_knob("fail_connect", -1) == s.rank) {
+            set_error("connect failed on rank %d (ESGD_TEST fail_connect)", s.rank);
             return ESGD_ERROR;
         }
         return ESGD_SUCCESS;
@@ -2609,9 +2387,6 @@ struct RcclTransport final : Transport {
     }
 
     int query(Sched &s) override { return base_query(s, S(s)); }
-    int order_after(Sched &s, uint32_t round, void *stream, uint64_t *seen) override {
-        return base_order_after(s, S(s), round, stream, seen);
-    }
     int complete(Sched &s) override { return base_complete(s, S(s)); }
 
     void teardown(Sched &s) override {

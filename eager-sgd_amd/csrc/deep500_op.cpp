@@ -426,32 +426,13 @@ int allreducef_forward_cuda_packed_wait(void *handle, void *stream) {
     return rc;
 }
 
-int allreducef_forward_cuda_post(void *handle, const float *input, float divisor, void *stream) {
-    auto *op = static_cast<AllreduceOp *>(handle);
-    ESGD_ARG(op, "allreducef_forward_cuda_post: null handle");
-    ESGD_ARG(divisor == divisor && divisor != 0.0f, "allreducef_forward_cuda_post: bad divisor");
-    ESGD_ARG(!op->pending, "allreducef_forward_cuda_post: the previous round was not waited");
-    if (int rc = op->ensure(true)) return rc;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    if (int rc = cuda_copy_in(op, input, divisor, s)) return rc;
-    if (int rc = op->post_round(s)) return rc;
-    op->pending = true;
-    return ESGD_SUCCESS;
-}
-
-int allreducef_forward_cuda_wait(void *handle, float *output, void *stream) {
-    auto *op = static_cast<AllreduceOp *>(handle);
-    ESGD_ARG(op, "allreducef_forward_cuda_wait: null handle");
-    ESGD_ARG(op->pending, "allreducef_forward_cuda_wait: no round posted");
-    op->pending = false;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    return op->finish_round(s, [&]() -> int { return cuda_copy_out(op, output, s); });
-}
-
-int allreducef_forward_cuda_post_many(void *const *handles, int n, const float *const *inputs, float divisor,
-                                      void *stream) {
-    ESGD_ARG(n >= 0 && (n == 0 || (handles && inputs)), "allreducef_forward_cuda_post_many: bad arguments");
-    ESGD_ARG(divisor == divisor && divisor != 0.0f, "allreducef_forward_cuda_post_many: bad divisor");
+// the copy-in way of post_many_io: every op's copy-in (inputs[i] / divisor into its send
+// bucket; one launch per 48 ops) on stream, then the n rounds posted in order with ONE
+// producer event (the fallback for a group the fused round I/O cannot take)
+static int post_many_copy_in(void *const *handles, int n, const float *const *inputs, float divisor,
+                             void *stream) {
+    ESGD_ARG(n >= 0 && (n == 0 || (handles && inputs)), "allreducef_forward_cuda_post_many_io: bad arguments");
+    ESGD_ARG(divisor == divisor && divisor != 0.0f, "allreducef_forward_cuda_post_many_io: bad divisor");
     if (n == 0) return ESGD_SUCCESS;
     std::vector<AllreduceOp *> ops(static_cast<size_t>(n));
     std::vector<float *> sbs(static_cast<size_t>(n));
@@ -459,8 +440,8 @@ int allreducef_forward_cuda_post_many(void *const *handles, int n, const float *
     std::vector<esgd_sched_h> hs(static_cast<size_t>(n));
     for (int i = 0; i < n; ++i) {
         AllreduceOp *op = ops[i] = static_cast<AllreduceOp *>(handles[i]);
-        ESGD_ARG(op, "allreducef_forward_cuda_post_many: op %d is null", i);
-        ESGD_ARG(!op->pending, "allreducef_forward_cuda_post_many: op %d's previous round was not waited", i);
+        ESGD_ARG(op, "allreducef_forward_cuda_post_many_io: op %d is null", i);
+        ESGD_ARG(!op->pending, "allreducef_forward_cuda_post_many_io: op %d's previous round was not waited", i);
         if (int rc = op->ensure(true)) return rc;   // collective, in the callers' common order
         sbs[i] = op->sb;
         counts[i] = op->len;
@@ -494,7 +475,7 @@ int allreducef_forward_cuda_post_many_io(void *const *handles, int n, const floa
     }
     // a tensor the fused path cannot take (unaligned, bf16 wire): the whole group goes the
     // copy-in way, and wait_many copies out
-    if (!fits) return allreducef_forward_cuda_post_many(handles, n, inputs, divisor, stream);
+    if (!fits) return post_many_copy_in(handles, n, inputs, divisor, stream);
     void *ps = caller_stream(static_cast<hipStream_t>(stream));
     std::vector<int> roles(static_cast<size_t>(n), -1);
     const int rc = esgd_schedule_post_group_io(hs.data(), n, reinterpret_cast<const void *const *>(inputs),
@@ -511,23 +492,9 @@ int allreducef_forward_cuda_post_many_io(void *const *handles, int n, const floa
 
 namespace {
 
-// esgd_schedule_wait_on, remembering across the group the latest shared launch the stream
-// already waits for (one stream wait per shared launch, not per round)
-int wait_on(uint64_t h, void *ps, int *fresh, uint64_t *seen) {
-    esgd::Sched *s = esgd::sched_lookup(h);
-    if (!s) {
-        esgd::set_error("allreducef_forward_cuda_wait_many_on: unknown schedule");
-        return ESGD_INVALID_ARG;
-    }
-    return esgd::sched_wait_on(s, ps, fresh, seen);
-}
-
-// on_stream: each round is waited for on the GPU (esgd_schedule_wait_on): stream waits for
-// it, and the call returns once every round is queued instead of finished
-int wait_many_impl(void *const *handles, int n, float *const *outputs, void *stream, bool on_stream) {
+int wait_many_impl(void *const *handles, int n, float *const *outputs, void *stream) {
     ESGD_ARG(n >= 0 && (n == 0 || (handles && outputs)), "allreducef_forward_cuda_wait_many: bad arguments");
     void *ps = caller_stream(static_cast<hipStream_t>(stream));
-    uint64_t seen = 0;
     std::vector<float *> outs, rbs;
     std::vector<uint64_t> counts;
     std::vector<esgd_sched_h> hs, hs_io;   // copied out from rb / results already in place
@@ -540,7 +507,7 @@ int wait_many_impl(void *const *handles, int n, float *const *outputs, void *str
         const bool io = op->io_posted;
         op->io_posted = false;
         int fresh = 0;
-        if (int rc = on_stream ? wait_on(op->sched, ps, &fresh, &seen) : esgd_schedule_wait_ex(op->sched, &fresh)) {
+        if (int rc = esgd_schedule_wait_ex(op->sched, &fresh)) {
             if (!first) first = rc;
             continue;
         }
@@ -582,11 +549,7 @@ int wait_many_impl(void *const *handles, int n, float *const *outputs, void *str
 extern "C" {
 
 int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const *outputs, void *stream) {
-    return wait_many_impl(handles, n, outputs, stream, false);
-}
-
-int allreducef_forward_cuda_wait_many_on(void *const *handles, int n, float *const *outputs, void *stream) {
-    return wait_many_impl(handles, n, outputs, stream, true);
+    return wait_many_impl(handles, n, outputs, stream);
 }
 
 bool is_cuda_supported(void *) { return true; }

@@ -167,11 +167,6 @@ int engine_init(const char *job, int rank, int world, bool start_progress) {
         g_thread = std::thread(progress_main);
     }
     if (world > 1 && g_device >= 0) arena_warm();   // before any bucket of the job is exported
-    // diagnostics (on a GPU shared by the ranks, the number of hardware
-    // queues each rank process holds changes round times 2-3x): ESGD_EXTRA_QUEUES=n makes
-    // this process hold n more, each created by a stream's first command
-    if (const char *e = getenv("ESGD_EXTRA_QUEUES"))
-        if (g_device >= 0) dataplane_extra_queues(atoi(e));
     return ESGD_SUCCESS;
 }
 
@@ -423,8 +418,6 @@ static int activator_of(SchedShm *sh, uint32_t round) {
 
 static bool step(Sched &s, bool join_only);
 
-static bool inline_join() { return config_inline_join(); }
-
 int sched_post(Sched *s, void *producer_stream, int *role, const RoundIO *io) {
     ESGD_ARG(s, "schedule post: null schedule");
     int r = 0;
@@ -473,12 +466,12 @@ int sched_post(Sched *s, void *producer_stream, int *role, const RoundIO *io) {
         }
     }
     // the round this post makes due is joined right here, on the caller's thread, instead
-    // of at the progress thread's next pass (ESGD_INLINE_JOIN=0: always there): the join is
+    // of at the progress thread's next pass: the join is
     // per-schedule work under its mutex plus the issue-ring append (atomics), and joining at
     // the post takes it off the progress thread, which then only launches.  Device buckets
     // without FFCOLL_BUFFERS only (a host bucket's join stages the bucket; a resolve
     // schedule's re-resolves it).
-    if (inline_join() && !s->resolve && !s->host_mode) (void)step(*s, true);
+    if (!s->resolve && !s->host_mode) (void)step(*s, true);
     seg_wake(g_seg);
     if (role) *role = r;
     return ESGD_SUCCESS;
@@ -496,10 +489,7 @@ int sched_wait_ex(Sched *s, int *fresh) {
     }
     // a round about to complete is seen ~5 us sooner by spinning than through the
     // condition variable's futex wake: spin briefly, then block
-    static const double spin_s = [] {
-        const char *e = getenv("ESGD_WAIT_SPIN_US");
-        return ((e && *e) ? atof(e) : 200.0) * 1e-6;
-    }();
+    constexpr double spin_s = 200e-6;
     const double t0 = now_s();
     if (roctx_on()) roctxRangePushA("esgd wait");
     while (int32_t(s->completed_a.load(std::memory_order_acquire) - target) < 0 && now_s() - t0 < spin_s)
@@ -519,66 +509,6 @@ int sched_wait_ex(Sched *s, int *fresh) {
     s->mark(target, 5);
     if (s->hold_mode) s->held = true;
     // the fresh bit of the round returned
-    const int f = s->fresh_take(target) ? 1 : 0;
-    if (fresh) *fresh = f;
-    return ESGD_SUCCESS;
-}
-
-// wait(), ordered on the GPU: returns once `stream` waits (hipStreamWaitEvent) for the
-// round's last queued work -- as soon as the progress thread has queued the round, not when
-// the host sees it finish -- or once the round has finished.  The caller's work on `stream`
-// (the wrapped optimizer reading the reduced gradient) is then queued behind the round
-// while the round still runs, as torch.distributed's Work.wait() orders the caller's
-// stream behind an RCCL collective.  The round's outcome is not known yet: a failure that
-// comes later is reported by the schedule's next post / wait (the error is sticky).
-// Transports or buckets without such an event (host buckets) wait on the host.
-int sched_wait_on(Sched *s, void *stream, int *fresh, uint64_t *seen) {
-    ESGD_ARG(s && stream, "schedule wait_on: null schedule or stream (ESGD_STREAM_NULL names the legacy stream)");
-    uint32_t target;
-    {
-        std::lock_guard<std::mutex> lk(s->mu);
-        ESGD_ARG(!s->held, "schedule %d: release() the round wait() returned before waiting for the next", s->id);
-        target = s->waited + 1;
-    }
-    const double t0 = now_s();
-    unsigned polls = 0;
-    if (roctx_on()) roctxRangePushA("esgd wait_on");
-    struct Pop {
-        ~Pop() { if (roctx_on()) roctxRangePop(); }
-    } pop;
-    // spin on the lock-free counters; the schedule's mutex is taken only once the round is
-    // launched (or finished) and every 1024 polls (errors, the timeout): a waiter that
-    // took it every poll slowed the progress thread's launches and flushes 1.5x (r05h)
-    bool host_wait = false;
-    for (;;) {
-        const bool due = int32_t(s->completed_a.load(std::memory_order_acquire) - target) >= 0 ||
-                         int32_t(s->launched_a.load(std::memory_order_acquire) - target) >= 0;
-        if (due || (polls & 1023) == 1023) {
-            std::lock_guard<std::mutex> lk(s->mu);
-            if (s->error) { set_error("%s", s->errmsg); return s->error; }
-            if (s->completed >= target) break;
-            if (s->stage == ST_INFLIGHT && s->cur == target) {
-                const int q = s->tp->order_after(*s, target, stream, seen);
-                if (q < 0) return q;
-                if (q == 1) break;
-                if (q == 2) { host_wait = true; break; }   // wait_ex below, with mu released
-            }
-            if (now_s() - t0 > g_timeout) {
-                const std::string m = "wait timed out " + sched_state(*s);
-                fail_locked(*s, ESGD_ERROR, m.c_str());
-                set_error("%s", s->errmsg);
-                return s->error;
-            }
-        }
-        backoff(polls);
-    }
-    // no GPU event for this round (host buckets): wait on the host -- outside the loop, whose
-    // guard of s->mu wait_ex would otherwise try to take a second time (r05k2: hung)
-    if (host_wait) return sched_wait_ex(s, fresh);
-    std::lock_guard<std::mutex> lk(s->mu);
-    s->waited = target;
-    s->mark(target, 5);
-    if (s->hold_mode) s->held = true;
     const int f = s->fresh_take(target) ? 1 : 0;
     if (fresh) *fresh = f;
     return ESGD_SUCCESS;
@@ -778,8 +708,6 @@ static bool step(Sched &s, bool join_only = false) {
 // nothing to do: the pass skips it without taking its mutex (step() would return false).
 // With hundreds of schedules (one per gradient tensor) most are quiet in any pass.
 static bool quiet(int id) {
-    static const bool off = getenv("ESGD_PASS_SKIP") && *getenv("ESGD_PASS_SKIP") == '0';   // A/B
-    if (off) return false;
     const HotState &h = g_hot[id];
     if (h.busy.load(std::memory_order_acquire)) return false;
     const uint32_t next = h.joined.load(std::memory_order_acquire) + 1;
@@ -818,7 +746,6 @@ static bool pump_tickets() {
                     target->stage = ST_INFLIGHT;
                     target->stage_t0 = now_s();
                     hot_busy(*target);
-                    target->launched_a.store(target->cur, std::memory_order_release);
                 }
             }
         }

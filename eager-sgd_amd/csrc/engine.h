@@ -90,13 +90,6 @@ struct Transport {
     virtual int prepare(Sched &s, uint32_t round, bool fresh) = 0;
     virtual int launch(Sched &s, uint32_t round, bool fresh) = 0;
     virtual int query(Sched &s) = 0;
-    // stream-ordered completion (sched_wait_on): make `stream` wait on the GPU for the
-    // launched round's last queued work.  1: done; 0: the round is not on the GPU yet (it
-    // sits in the pending shared launch); 2: no such event (host buckets: wait on the host).
-    // seen (may be null): the latest shared launch `stream` already waits for -- a round in
-    // that launch or an earlier one (one round stream: launches finish in order) needs no
-    // second wait; updated
-    virtual int order_after(Sched &, uint32_t, void *, uint64_t *) { return 2; }
     // host-side work once the copy-out has landed (before wait() returns)
     virtual int complete(Sched &) { return ESGD_SUCCESS; }
     // why a launched round has not finished (timeouts), "" if unknown
@@ -142,7 +135,6 @@ struct Sched {
     std::atomic<uint32_t> joined{0};
     uint32_t completed = 0, waited = 0;
     std::atomic<uint32_t> completed_a{0};   // = completed, for wait()'s lock-free spin
-    std::atomic<uint32_t> launched_a{0};    // last round launch() queued (wait_on's lock-free spin)
     std::atomic<Stage> stage{ST_IDLE};
     uint32_t cur = 0;
     bool cur_fresh = false;
@@ -236,8 +228,6 @@ int sched_post(Sched *s, void *producer_stream, int *role, const RoundIO *io = n
 int sched_wait(Sched *s);
 // wait, and say whether this rank had posted the round it returns before joining it
 int sched_wait_ex(Sched *s, int *fresh);
-// the same, ordered on the GPU: `stream` waits for the round (engine.cpp)
-int sched_wait_on(Sched *s, void *stream, int *fresh, uint64_t *seen = nullptr);
 // hold mode: the caller is done with the round wait() returned; work it queued on
 // `stream` (may be null) is waited for by the next round's snapshot
 int sched_release(Sched *s, void *stream);
@@ -266,10 +256,8 @@ void dataplane_shutdown();
 // launch the rounds appended to the pending shared launch (k_round_batch); the engine calls
 // it after every pump of the issue ring, transports before queuing anything else
 int dataplane_flush();
-int dataplane_round_stream(void **out);   // esgd_round_stream
+// the end of a pump: flush unless a shared launch is still queued (kBatchDepth)
 int dataplane_flush_soft();
-bool config_inline_join();   // esgd_set_config("inline_join") / ESGD_INLINE_JOIN
-void dataplane_extra_queues(int n);   // diagnostics: n more streams, each with a queue   // the end of a pump: flush unless ESGD_BATCH_DEPTH launches are queued
 // esgd_schedule_post_group / _release_group: until the end call, this thread's posts
 // (which 0) or releases (1) on `stream` share ONE event recording
 int dataplane_group_begin(int which, void *stream);

@@ -53,11 +53,18 @@ struct PairFlags {
     int ndst;
 };
 
-// ESGD_IPC_TRACE=1 (diagnostics): every IPC export / open / close on stderr with the
-// handle's bytes, so a repeated handle or a stale mapping can be seen;
-// ESGD_IPC_TRACE_FILE=<path>: the same lines appended to that file (every process of a
-// test session into one log), refused exports included.
-void ipc_trace(const char *what, int peer, const void *ptr, size_t bytes, const uint8_t handle[64]);
+// ESGD_TEST (tests and diagnostics only; one variable for every fault hook): comma-separated
+// key=value pairs, e.g. ESGD_TEST=fail_exports=2,piece_bytes=65536 (fail_connect is read
+// at every creation, the others once per process)
+//   fail_exports=N      the process's first N chunk exports are refused as the runtime does
+//   fail_maps=N         its first N sealed mappings read back as another chunk's
+//   fail_connect=R      rank R's connect fails (the creation vote fails on every rank)
+//   arena_bypass=1|2    every bucket its own allocation (2: freed once peers closed their
+//                       mappings) -- the ROCm IPC re-export probe
+//   piece_bytes=B       remote launches in B-byte pieces (default 64 MiB)
+//   shadow=1            every device bucket reduced through an arena shadow
+//   host_chunk_bytes=B  host buckets of at least 2 x B bytes run chunked (default 16 MiB)
+int64_t test_knob(const char *key, int64_t dflt);
 
 // release_idle_chunks: a new chunk may first give idle never-exported chunks back to the
 // driver (hipFree synchronises the device: callers' threads only, never the progress thread);

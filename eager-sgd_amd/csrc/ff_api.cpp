@@ -157,11 +157,10 @@ int ffbuffer_get_data(ffbuffer_h h, void **mem) {
 
 int ffinit(int *, char ***) {
     if (engine_ready()) return FFSUCCESS;   // already joined (esgd_comm_init / earlier ffinit)
-    const int rank = env_int({"ESGD_RANK", "RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID"}, 0);
-    const int world = env_int({"ESGD_WORLD_SIZE", "WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE",
-                               "SLURM_NTASKS"}, 1);
-    const int local = env_int({"ESGD_LOCAL_RANK", "LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK",
-                               "SLURM_LOCALID"}, rank);
+    // the launcher's own variables (torch.distributed.run, Open MPI, PMI, Slurm)
+    const int rank = env_int({"RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID"}, 0);
+    const int world = env_int({"WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS"}, 1);
+    const int local = env_int({"LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "SLURM_LOCALID"}, rank);
     std::string job;
     if (const char *j = getenv("ESGD_JOB_ID")) job = j;
     else if (const char *t = getenv("TORCHELASTIC_RUN_ID")) job = std::string(t) + "-" + (getenv("MASTER_PORT") ? getenv("MASTER_PORT") : "0");
@@ -173,8 +172,7 @@ int ffinit(int *, char ***) {
     }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0) {
-        const int dev = env_int({"ESGD_DEVICE"}, local % ndev);
-        ESGD_HIP(hipSetDevice(dev));
+        ESGD_HIP(hipSetDevice(local % ndev));
     }
     int rc = engine_init(job.c_str(), rank, world, true);
     if (!rc) g_ff_owns_comm = true;

@@ -10,7 +10,7 @@
 // buckets, 62 GB/s over the link, against 10.8 ms for H2D + tree + D2H in sequence and
 // 10.5 ms for the chunked DMA pipeline below (16-32 MiB chunks; 1-4 MiB chunks are slower
 // than the sequence: 17 / 13 / 11.5 ms, the per-copy cost).
-// Other buckets (pageable memory, or ESGD_HOST_REDUCE_MODE=dma) run in chunks through
+// Other buckets (pageable memory) run in chunks through
 // three process-wide streams so the PCIe link works in both directions at once:
 //   copy stream 1: H2D of chunk c of every input into staging set c % kStages
 //   compute stream: the tree kernel (esgd_reduce) of chunk c, staging -> staged output
@@ -48,24 +48,9 @@ struct HostReduce {
 
 HostReduce g_hr;
 
-// bytes per input per chunk: ESGD_HOST_REDUCE_CHUNK (multiple of 4 KiB), default 16 MiB
-size_t chunk_bytes() {
-    static const size_t v = [] {
-        const char *e = getenv("ESGD_HOST_REDUCE_CHUNK");
-        const size_t b = (e && *e) ? size_t(strtoull(e, nullptr, 10)) : (size_t(16) << 20);
-        return std::max<size_t>(4096, b / 4096 * 4096);
-    }();
-    return v;
-}
-
-// 0 auto (zero-copy when every bucket is pinned and mapped, else chunked DMA), 1 dma
-int host_mode() {
-    static const int m = [] {
-        const char *e = getenv("ESGD_HOST_REDUCE_MODE");
-        return (e && !strcmp(e, "dma")) ? 1 : 0;
-    }();
-    return m;
-}
+// bytes per input per chunk of the DMA pipeline: 16 MiB (16-32 MiB chunks measured best,
+// profiles/r02/host_reduce_sweep.jsonl)
+constexpr size_t kChunkBytes = size_t(16) << 20;
 
 // the device address of pinned, mapped host memory; nullptr otherwise
 void *mapped(void *host) {
@@ -94,7 +79,7 @@ int ensure(HostReduce &h) {
             if (!*e) ESGD_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     for (hipEvent_t *e : {&h.start, &h.done})
         if (!*e) ESGD_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    h.chunk = chunk_bytes();
+    h.chunk = kChunkBytes;
     ESGD_HIP(hipMalloc(reinterpret_cast<void **>(&h.stage), size_t(kStages) * (ESGD_MAX_FANIN + 1) * h.chunk));
     h.device = dev;
     return ESGD_SUCCESS;
@@ -117,8 +102,8 @@ extern "C" int esgd_reduce_host(int dtype, int k, const void *const *inputs, voi
     if (int rc = require_device()) return rc;
     hipStream_t cs = stream == ESGD_STREAM_NULL ? nullptr : as_stream(stream);
     // pinned and mapped buckets: the tree kernel reads and writes them in place over
-    // PCIe (zero-copy), unless ESGD_HOST_REDUCE_MODE=dma
-    if (host_mode() != 1) {
+    // PCIe (zero-copy)
+    {
         const void *view[ESGD_MAX_FANIN];
         void *oview = mapped(out);
         bool all = oview != nullptr;

@@ -431,54 +431,6 @@ int store_fin(uint32_t *fin, uint32_t value, hipStream_t s) {
     return ESGD_SUCCESS;
 }
 
-// Snapshot of a round into a bucket its peers will read (rb = sb, or rb = 0 for a rank
-// carried through a round it had not posted): 16-B nt loads, write-through (sc1) stores,
-// so that no dirty line of the bucket is left in any XCD's L2 to be written back over the
-// round's results later; ragged bytes by single system-scope stores.  src == nullptr:
-// zero-fill.
-template <bool COPY>
-__global__ __launch_bounds__(256) void k_snapshot(uint8_t *dst, const uint8_t *src, uint32_t nvec, uint32_t ntail) {
-    const int bytes = int(nvec * 16u);
-    __amdgpu_buffer_rsrc_t ws = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, bytes, 0x00020000);
-    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(COPY ? src : dst), (short)0,
-                                                                 bytes, 0x00020000);
-    const raw16 z = {0u, 0u, 0u, 0u};
-    const uint32_t step = gridDim.x * 1024u;
-    for (uint32_t i = blockIdx.x * 1024u + threadIdx.x; i < nvec; i += step) {
-        raw16 r[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            r[u] = COPY ? __builtin_amdgcn_raw_buffer_load_b128(rs, (i + u * 256) * 16, 0, 2) : z;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) __builtin_amdgcn_raw_buffer_store_b128(r[u], ws, (i + u * 256) * 16, 0, 16);
-    }
-    if (blockIdx.x == 0 && threadIdx.x < ntail) {
-        const uint8_t v = COPY ? src[size_t(nvec) * 16 + threadIdx.x] : uint8_t(0);
-        __hip_atomic_store(dst + size_t(nvec) * 16 + threadIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
-// dst = src (or 0 when src is nullptr), `bytes` at 16-B aligned addresses; larger than a
-// 32-bit descriptor range in windows
-int snapshot_copy(void *dst, const void *src, uint64_t bytes, hipStream_t s) {
-    constexpr uint64_t kWin = uint64_t(1) << 30;
-    ESGD_ARG(((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0,
-             "snapshot: buckets must be 16-B aligned");
-    for (uint64_t o = 0; o < bytes; o += kWin) {
-        const uint64_t n = std::min(kWin, bytes - o);
-        const uint32_t nvec = uint32_t(n / 16), ntail = uint32_t(n % 16);
-        const unsigned grid = grid_for(1024, nvec ? nvec : 1, 4);
-        uint8_t *d = static_cast<uint8_t *>(dst) + o;
-        if (src)
-            hipLaunchKernelGGL(k_snapshot<true>, dim3(grid), dim3(256), 0, s, d, static_cast<const uint8_t *>(src) + o,
-                               nvec, ntail);
-        else
-            hipLaunchKernelGGL(k_snapshot<false>, dim3(grid), dim3(256), 0, s, d, nullptr, nvec, ntail);
-        ESGD_HIP(hipGetLastError());
-    }
-    return ESGD_SUCCESS;
-}
-
 int move_zero(void *dst, void *src, uint64_t bytes, hipStream_t s) {
     if (!bytes) return ESGD_SUCCESS;
     if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0) {
@@ -1093,12 +1045,8 @@ int round_small(int dtype, const void *const *src, void *out, void *pub, uint64_
     a.counter = counter;
     a.rank = rank; a.world = world; a.value = value; a.timeout = timeout_ticks;
     a.strict = strict;
-    // ESGD_SMALL_GRID caps the workgroups (default kSmallBlocks); every one must be resident
-    static const uint64_t cap = [] {
-        const char *e = getenv("ESGD_SMALL_GRID");
-        const long v = (e && *e) ? strtol(e, nullptr, 10) : kSmallBlocks;
-        return uint64_t(std::max(1L, std::min(v, 256L)));
-    }();
+    // at most kSmallBlocks workgroups: every one must be resident
+    constexpr uint64_t cap = kSmallBlocks;
     const unsigned grid = unsigned(std::min<uint64_t>(cap, std::max<uint64_t>(1, (maxv + 1023) / 1024)));
     switch (dtype) {
     case ESGD_FLOAT: return launch_small_t<F32>(a, grid, s);

@@ -429,8 +429,6 @@ __device__ void run_tile(const BatchArgs &a, uint32_t *S, const TileAt &at) {
 // every tile of the launch is done (4 timeouts at most: a kernel never spins for good).
 template <class Tr, int K>
 __device__ void agent_block(const BatchArgs &a, uint32_t *S, uint32_t T0, uint32_t T1, uint32_t T, long long t0) {
-    __shared__ uint32_t s_tile;
-    __shared__ int s_cmd;
     // the next launch's slot starts at zero (and every other one: see kLaunchSlots)
     for (uint32_t i = threadIdx.x; i < (kLaunchSlots - 1) * kSlotWords; i += blockDim.x) {
         const uint32_t sl = (a.slot + 1u + i / kSlotWords) % kLaunchSlots;

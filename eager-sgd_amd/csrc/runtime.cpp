@@ -15,6 +15,7 @@
 #include <cstring>
 #include <atomic>
 #include <mutex>
+#include <string>
 
 #include "esgd_internal.h"
 
@@ -31,24 +32,22 @@ void set_error(const char *fmt, ...) {
 
 void clear_error() { g_err[0] = 0; }
 
-void ipc_trace(const char *what, int peer, const void *ptr, size_t bytes, const uint8_t handle[64]) {
-    static const bool on = getenv("ESGD_IPC_TRACE") && *getenv("ESGD_IPC_TRACE") == '1';
-    static const char *file = getenv("ESGD_IPC_TRACE_FILE");
-    if (!on && !(file && *file)) return;
-    char hex[129];
-    for (int i = 0; i < 64; ++i) std::snprintf(hex + 2 * i, 3, "%02x", handle ? handle[i] : 0);
-    char line[512];
-    const int n = std::snprintf(line, sizeof(line), "esgd-ipc pid %d %s peer %d ptr %p bytes %zu handle %s\n",
-                                int(getpid()), what, peer, ptr, bytes, hex);
-    if (on) std::fputs(line, stderr);
-    if (file && *file && n > 0) {   // one write per line, O_APPEND: lines of many processes interleave whole
-        const int fd = open(file, O_WRONLY | O_CREAT | O_APPEND, 0644);
-        if (fd >= 0) {
-            ssize_t w = write(fd, line, size_t(std::min<int>(n, int(sizeof(line)) - 1)));
-            (void)w;
-            close(fd);
-        }
+// ESGD_TEST: "key=value,key=value" (see esgd_internal.h); read at each call -- the hooks
+// that must stay fixed for the process keep their first value themselves
+int64_t test_knob(const char *key, int64_t dflt) {
+    const char *e = getenv("ESGD_TEST");
+    if (!e || !*e) return dflt;
+    const std::string spec(e);
+    const size_t klen = std::strlen(key);
+    size_t i = 0;
+    while (i < spec.size()) {
+        size_t j = spec.find(',', i);
+        if (j == std::string::npos) j = spec.size();
+        if (j - i > klen && spec.compare(i, klen, key) == 0 && spec[i + klen] == '=')
+            return int64_t(strtoll(spec.c_str() + i + klen + 1, nullptr, 10));
+        i = j + 1;
     }
+    return dflt;
 }
 
 int hip_fail(hipError_t e, const char *what, const char *file, int line) {

@@ -44,8 +44,6 @@ def _bind(h):
         "esgd_schedule_create": (i, [i, i, vp, vp, u64, i, i, C.c_uint, C.POINTER(u64)]),
         "esgd_schedule_create_ex": (i, [i, i, vp, vp, u64, i, i, C.c_uint, C.c_uint, C.POINTER(u64)]),
         "esgd_schedule_wait_ex": (i, [u64, C.POINTER(i)]),
-        "esgd_schedule_wait_on": (i, [u64, vp, C.POINTER(i)]),
-        "esgd_round_stream": (i, [C.POINTER(vp)]),
         "esgd_schedule_post_iov": (i, [u64, i, C.POINTER(vp), C.POINTER(vp), C.POINTER(u64), C.c_float, vp,
                                        C.POINTER(i)]),
         "esgd_schedule_release": (i, [u64, vp]),
@@ -175,15 +173,6 @@ def barrier():
     check(lib().esgd_barrier(), "esgd_barrier")
 
 
-def round_stream() -> int:
-    """esgd_round_stream: the handle of the process's round stream (every round is queued
-    on it in issue order); work queued there runs after the rounds launched so far.  Wrap it
-    with torch.cuda.ExternalStream to queue torch work on it."""
-    h = C.c_void_p()
-    check(lib().esgd_round_stream(C.byref(h)), "esgd_round_stream")
-    return int(h.value or 0)
-
-
 def _buf_arg(x, buf):
     if x is None:
         return None
@@ -278,18 +267,6 @@ class Schedule:
         peer's activation carried it through with what its send bucket held)."""
         f = C.c_int()
         check(lib().esgd_schedule_wait_ex(self.handle, C.byref(f)), "esgd_schedule_wait")
-        return bool(f.value)
-
-    def wait_on(self, stream) -> bool:
-        """esgd_schedule_wait_on: wait() ordered on the GPU -- `stream` (a torch stream, a
-        handle, or 0 = the legacy default stream) waits for the round; returns once the round
-        is queued on the GPU (or finished), with wait()'s fresh bit."""
-        f = C.c_int()
-        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else (
-            stream.handle if hasattr(stream, "handle") else int(stream))
-        if s == 0:
-            s = 1   # ESGD_STREAM_NULL
-        check(lib().esgd_schedule_wait_on(self.handle, s, C.byref(f)), "esgd_schedule_wait_on")
         return bool(f.value)
 
     def release(self, stream=None):

@@ -52,12 +52,6 @@ def _bind(h):
     h.allreducef_forward_cuda_packed.restype = C.c_int
     h.allreducef_forward_cuda_packed.argtypes = [vp, C.c_int, C.POINTER(vp), C.POINTER(C.c_uint64),
                                                  C.POINTER(vp), C.c_float, vp]
-    h.allreducef_forward_cuda_post.restype = C.c_int
-    h.allreducef_forward_cuda_post.argtypes = [vp, vp, C.c_float, vp]
-    h.allreducef_forward_cuda_wait.restype = C.c_int
-    h.allreducef_forward_cuda_wait.argtypes = [vp, vp, vp]
-    h.allreducef_forward_cuda_post_many.restype = C.c_int
-    h.allreducef_forward_cuda_post_many.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), C.c_float, vp]
     h.allreducef_forward_cuda_wait_many.restype = C.c_int
     h.allreducef_forward_cuda_wait_many.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), vp]
     h.allreducef_forward_cuda_packed_post.restype = C.c_int
@@ -65,8 +59,6 @@ def _bind(h):
                                                       C.POINTER(vp), C.c_float, vp]
     h.allreducef_forward_cuda_packed_wait.restype = C.c_int
     h.allreducef_forward_cuda_packed_wait.argtypes = [vp, vp]
-    h.allreducef_forward_cuda_wait_many_on.restype = C.c_int
-    h.allreducef_forward_cuda_wait_many_on.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), vp]
     h.allreducef_forward_cuda_post_many_io.restype = C.c_int
     h.allreducef_forward_cuda_post_many_io.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(vp), C.POINTER(vp),
                                                        C.c_float, vp]
@@ -168,40 +160,14 @@ class AllreduceOp:
         """Second half: wait for the fused bucket's round (results in the outputs)."""
         _lib.check(lib().allreducef_forward_cuda_packed_wait(self.handle, stream), "allreducef_forward_cuda_packed_wait")
 
-    def post_cuda(self, grad, divisor: float = 1.0, stream: int | None = None):
-        """First half of forward_cuda_div: queue the copy-in (divided) and post the round,
-        without waiting -- post every op's round, then wait_cuda() each, in the same order
-        on every rank.  Raises EsgdError."""
-        from .device import as_ptr
-        _lib.check(lib().allreducef_forward_cuda_post(self.handle, as_ptr(grad), float(divisor), stream),
-                   "allreducef_forward_cuda_post")
-
-    def wait_cuda(self, out, stream: int | None = None):
-        """Second half: wait for the posted round and queue the copy-out into `out`."""
-        from .device import as_ptr
-        _lib.check(lib().allreducef_forward_cuda_wait(self.handle, as_ptr(out), stream),
-                   "allreducef_forward_cuda_wait")
-        return out
-
-    @staticmethod
-    def post_many(ops, grads, divisor: float = 1.0, stream: int | None = None):
-        """post_cuda for many ops in one call (allreducef_forward_cuda_post_many): every
-        copy-in in one launch per 48 ops, the posts with one producer event.  Raises
-        EsgdError; the ops before a failed post stay posted (wait_many drains them)."""
-        from .device import ptr_array_of
-        n = len(ops)
-        hs = _lib.ptr_array([op.handle for op in ops])
-        gs = ptr_array_of(grads)
-        _lib.check(lib().allreducef_forward_cuda_post_many(hs, n, gs, float(divisor), stream),
-                   "allreducef_forward_cuda_post_many")
-
     @staticmethod
     def post_many_io(ops, grads, outs, divisor: float = 1.0, stream: int | None = None):
-        """post_many with the outputs named at the post (allreducef_forward_cuda_post_many_io):
-        each round reads grads[i] / divisor itself and writes its result into outs[i] (may be
-        grads[i]) -- no copy-in or copy-out launch on the caller's stream.  wait_many(ops,
-        outs) then copies out only the rounds a peer carried this rank through before the
-        post.  Unaligned tensors or a bf16 wire fall back to post_many.  Raises EsgdError."""
+        """The rounds of many ops posted in one call (allreducef_forward_cuda_post_many_io), in
+        this order, with one producer event: each round reads grads[i] / divisor itself and
+        writes its result into outs[i] (may be grads[i]) -- no copy-in or copy-out launch on the
+        caller's stream.  wait_many(ops, outs) then copies out only the rounds a peer carried
+        this rank through before the post.  Unaligned tensors or a bf16 wire make the group go
+        the copy-in way.  Raises EsgdError; the ops before a failed post stay posted."""
         from .device import ptr_array_of
         n = len(ops)
         hs = _lib.ptr_array([op.handle for op in ops])
@@ -211,23 +177,17 @@ class AllreduceOp:
                    "allreducef_forward_cuda_post_many_io")
 
     @staticmethod
-    def wait_many(ops, outs, stream: int | None = None, on_stream: bool = False):
-        """wait_cuda for many ops in one call: every posted op's round waited for in order,
-        every copy-out in one launch per 48 ops, one release event; ops not posted are
-        skipped.  Raises EsgdError (the first failure) after every round was waited for.
-        on_stream=True (allreducef_forward_cuda_wait_many_on): the rounds are waited for on
-        the GPU -- `stream` waits for each, and the call returns once all are queued there;
-        a round that fails later fails its op's next post."""
+    def wait_many(ops, outs, stream: int | None = None):
+        """The other half (allreducef_forward_cuda_wait_many): every posted op's round waited
+        for in order, the copy-outs a round did not do itself in one launch per 48 ops, one
+        release event; ops not posted are skipped.  Raises EsgdError (the first failure)
+        after every round was waited for."""
         from .device import ptr_array_of
         n = len(ops)
         hs = _lib.ptr_array([op.handle for op in ops])
         os_ = ptr_array_of(outs)
-        if on_stream:
-            _lib.check(lib().allreducef_forward_cuda_wait_many_on(hs, n, os_, stream),
-                       "allreducef_forward_cuda_wait_many_on")
-        else:
-            _lib.check(lib().allreducef_forward_cuda_wait_many(hs, n, os_, stream),
-                       "allreducef_forward_cuda_wait_many")
+        _lib.check(lib().allreducef_forward_cuda_wait_many(hs, n, os_, stream),
+                   "allreducef_forward_cuda_wait_many")
 
     def forward_void(self, grad: np.ndarray) -> np.ndarray:
         """The reference ABI's void allreducef_forward verbatim (host buffers): on a failed

@@ -23,16 +23,22 @@ the reference's blocking ops do (:304-307); the same rounds over the same operan
 same bits.  The posts and the waits each go through ONE call
 (allreducef_forward_cuda_post_many_io / _wait_many, one producer event), and the data plane
 runs the rounds that come due together in shared launches, each round reading grad /
-comm_size and writing the reduced gradient back into p.grad itself (fused_io; no copy-in or
-copy-out launch on the caller's stream, 2 HBM passes of the gradient fewer -- only a round a
-peer carried this rank through before its post is copied out of the op's bucket).
-stream_wait=True orders the waits on the GPU instead: the ops' stream waits for each
-shared launch's event, so the wrapped optimizer's step is queued while the rounds still
-run -- the way torch.distributed's Work.wait() orders a stream behind an RCCL collective --
-and a round that fails later fails the next step's post; round_stream=True queues the ops'
-work and the wrapped step on the data plane's round stream itself (esgd_round_stream).  Both
-are opt-in A/Bs (measured no faster on the 1-GPU rehearsal).
+comm_size and writing the reduced gradient back into p.grad itself (no copy-in or copy-out
+launch on the caller's stream, 2 HBM passes of the gradient fewer -- only a round a peer
+carried this rank through before its post is copied out of the op's bucket).
 pipeline=False keeps the blocking chain (each op fused the same way).
+When the caller works on the legacy default stream (torch's default), the ops' posts, waits
+and copies go through a stream of the optimizer's own, ordered after the caller's stream on
+entry and before it on exit (the ops on the legacy stream cost 1.3-1.6x per step on the
+1-GPU rehearsal: profiles/r05/README.md).
+
+Not here, by design (round 6): gradients as views into the ops' buckets.  A
+solo / majority round a peer activates while this rank is still in backward must read a
+send bucket backward is not writing -- the move sb -> rb that opens every round of the
+reference (F/src/colls/ffallreduce.c:126-130) is the algorithm, not overhead -- and with
+p.grad a persistent view, autograd accumulates into it (zero + read-add-write, 4 passes
+of the gradient and a kernel per tensor in backward) instead of stealing the fresh
+gradient: more HBM traffic than the snapshot it would save.
 
 fuse=True (SURVEY.md §8(f) "bucket fusion"): the reference runs one schedule per tensor,
 161 per ResNet-50 step (opt_esgd_solo_imagenet_imbalance.py:85-248), each a
@@ -54,11 +60,17 @@ def _nullcontext():
 
 
 class EagerSGDOptimizer:
+    # fuse=True with overlap=True: gradients go in buckets of about this many MiB (DDP's
+    # default bucket_cap_mb); a subclass or the class attribute changes it before construction
+    bucket_mb = 25.0
+    # overlap=True: the hooks post in groups of this many tensors (one call, one producer
+    # event each): a post per tensor from Python cost ~15 us of host time apiece, on the
+    # backward's host path (r05t)
+    overlap_group = 16
+
     def __init__(self, optimizer, comm_size: int, mode: str = "solo", async_: int = 32,
                  seed: int = 6545343, fuse: bool = False, wire: str = "fp32",
-                 pipeline: bool = True, fused_io: bool = True, side_stream: bool = True,
-                 stream_wait: bool = False, round_stream: bool = False, overlap: bool = False,
-                 overlap_group: int = 16, bucket_mb: float = 25.0):
+                 pipeline: bool = True, overlap: bool = False):
         if mode not in deep500.MODES:
             raise ValueError(f"mode must be one of {sorted(deep500.MODES)}")
         if wire not in deep500.WIRES:
@@ -70,46 +82,23 @@ class EagerSGDOptimizer:
         self.mode, self.async_, self.seed = mode, int(async_), int(seed)
         self.fuse = bool(fuse)
         self.pipeline = bool(pipeline)
-        # per tensor: the rounds read grad / comm_size and write the result back themselves
-        # (allreducef_forward_cuda_post_many_io); False: copy-in / copy-out kernels on the
-        # caller's stream around them (an A/B)
-        self.fused_io = bool(fused_io)
-        # when the caller works on the legacy default stream (torch's default), the ops'
-        # posts, waits and copies go through a stream of the optimizer's own, ordered after
-        # the caller's stream on entry and before it on exit (the ops on the legacy stream
-        # cost 1.3-1.6x per step on the 1-GPU rehearsal: profiles/r05/README.md)
-        self.side_stream = bool(side_stream)
-        # stream_wait=True: pipelined per-tensor rounds are waited for on the GPU
-        # (allreducef_forward_cuda_wait_many_on): the wrapped step is queued behind the rounds
-        # while they still run; a round that fails after that fails the next step's post.
-        # Off by default: on the 1-GPU rehearsal the side stream's pending waits slowed the
-        # rounds' completion 1.4x, and on the round stream it gained nothing (the last shared
-        # launch goes out when the one before it finishes), profiles/r05/README.md
-        self.stream_wait = bool(stream_wait)
-        # the ops' work AND the wrapped step queued on the data plane's round stream itself
-        # (esgd_round_stream): the step follows the rounds by stream order, no event wait
-        # between queues, one hardware queue fewer per process than the side stream
-        self.round_stream = bool(round_stream)
-        self._rs = None
         # overlap=True: every tensor's round is posted from a post-accumulate-grad hook, as
         # soon as backward has written that gradient -- the way TF's dataflow runs the
-        # reference's ops as their inputs become ready -- and apply_gradients waits for them
-        # (one backward per step).  With fuse=True the gradients go in buckets of about
-        # bucket_mb MiB (reversed parameter order, the order backward produces them), one
-        # fused round per bucket, posted once its last gradient exists
+        # reference's ops as their inputs become ready -- and apply_gradients waits for them.
+        # With fuse=True the gradients go in buckets of about bucket_mb MiB (reversed
+        # parameter order, the order backward produces them), one fused round per bucket,
+        # posted once its last gradient exists.  One backward per step: a gradient's round is
+        # posted once per step (a second backward before apply_gradients -- gradient
+        # accumulation -- is refused by a clear error)
         self.overlap = bool(overlap)
-        self.bucket_mb = float(bucket_mb)
         self._buckets = None    # fuse + overlap: [[param, ...], ...] in reversed order
         self._bucket_of = {}    # id(param) -> bucket index
         self._bucket_ops = []   # one AllreduceOp per bucket (created at its first post)
         self._bucket_left = []  # gradients each bucket still waits for in this backward
         self._bucket_posted = []
         self._conv = []         # (param, its gradient, the fp32 copy the bucket reduces)
-        # the hooks post in groups of this many tensors (one call, one producer event each):
-        # a post per tensor from Python cost ~15 us of host time apiece, on the backward's
-        # host path (r05t)
-        self.overlap_group = max(1, int(overlap_group))
         self._ready = []        # (op, grad, param) whose gradient exists, not yet posted
+        self._seen = set()      # id(param) whose gradient the hooks saw since the last step
         self._bwd = []          # (op, grad, param) posted by the hooks since the last step
         self._hooks = []
         if self.overlap:
@@ -133,11 +122,10 @@ class EagerSGDOptimizer:
         if not self._configured:
             deep500.configure(self.mode, self.async_, self.seed, self.wire)
             self._configured = True
+        self._seen = set()   # the next backward's hooks start afresh
         caller = torch.cuda.current_stream()
-        if self.round_stream and not self.fuse:
-            return self._apply_on_round_stream(grads_and_vars, caller, global_step)
         side = None
-        if self.side_stream and caller.cuda_stream == 0:
+        if caller.cuda_stream == 0:
             if self._side is None or self._side.device != caller.device:
                 self._side = torch.cuda.Stream(device=caller.device)
             side = self._side
@@ -149,24 +137,6 @@ class EagerSGDOptimizer:
             for t in made:                 # gradients converted on the side stream: the
                 t.record_stream(caller)    # caller's stream uses them too
         r = self.optimizer.step()
-        if global_step is not None and hasattr(global_step, "add_"):
-            global_step.add_(1)
-        return r
-
-    def _apply_on_round_stream(self, grads_and_vars, caller, global_step):
-        import torch
-
-        from . import comm
-        if self._rs is None or self._rs.device != caller.device:
-            self._rs = torch.cuda.ExternalStream(comm.round_stream(), device=caller.device)
-        rs = self._rs
-        rs.wait_stream(caller)            # the gradients were written on the caller's stream
-        with torch.cuda.stream(rs):
-            made = self._reduce(list(grads_and_vars), rs.cuda_stream)
-            r = self.optimizer.step()     # behind the rounds on the same stream
-        caller.wait_stream(rs)
-        for t in made:
-            t.record_stream(caller)
         if global_step is not None and hasattr(global_step, "add_"):
             global_step.add_(1)
         return r
@@ -224,6 +194,11 @@ class EagerSGDOptimizer:
         take (not fp32 contiguous and 16-B aligned) waits for apply_gradients.  fuse=True: the
         bucket's round once its last gradient is there."""
         import torch
+        if id(p) in self._seen:   # a second backward of this step (gradient accumulation)
+            raise RuntimeError("EagerSGDOptimizer(overlap=True) posts each gradient's round during the step's one "
+                               "backward; a second backward before apply_gradients (gradient accumulation) would "
+                               "change a gradient whose round is already posted -- use overlap=False for it")
+        self._seen.add(id(p))
         if self.fuse:
             b = self._bucket_of.get(id(p))
             if b is not None and not self._bucket_posted[b]:
@@ -273,8 +248,7 @@ class EagerSGDOptimizer:
                 done = {id(p) for _, _, p in early}
                 err = None
                 try:
-                    deep500.AllreduceOp.wait_many([o for o, _, _ in early], [g for _, g, _ in early], stream,
-                                                  on_stream=self.stream_wait)
+                    deep500.AllreduceOp.wait_many([o for o, _, _ in early], [g for _, g, _ in early], stream)
                 except Exception as e:   # noqa: BLE001 -- re-raised after the rest
                     err = e
                 gvs = [(g, v) for g, v in gvs if id(v) not in done]
@@ -300,14 +274,11 @@ class EagerSGDOptimizer:
                 ops, gs = [p[0] for p in posted], [p[1] for p in posted]
                 err = None
                 try:   # :40 and the copy-in / copy-out fused into the rounds themselves
-                    if self.fused_io:
-                        deep500.AllreduceOp.post_many_io(ops, gs, gs, self.comm_size, stream)
-                    else:
-                        deep500.AllreduceOp.post_many(ops, gs, self.comm_size, stream)
+                    deep500.AllreduceOp.post_many_io(ops, gs, gs, self.comm_size, stream)
                 except Exception as e:   # noqa: BLE001 -- re-raised below
                     err = e
                 try:   # every posted round is waited for, even after a failed post
-                    deep500.AllreduceOp.wait_many(ops, gs, stream, on_stream=self.stream_wait)
+                    deep500.AllreduceOp.wait_many(ops, gs, stream)
                 except Exception as e:   # noqa: BLE001
                     err = err or e
                 if err is not None:

@@ -247,21 +247,6 @@ int esgd_schedule_wait(esgd_sched_h h);
  * (0: a peer's activation carried this rank through the round with whatever its send
  * bucket held -- the caller's late gradient did not take part) */
 int esgd_schedule_wait_ex(esgd_sched_h h, int *fresh);
-/* wait_ex ordered on the GPU (device buckets; extension): returns once `stream`
- * (ESGD_STREAM_NULL: the legacy default stream; not NULL) waits for the round's last queued
- * work -- as soon as the round is queued on the GPU, not when the host sees it finish --
- * or once the round has finished.  Work queued on `stream` afterwards sees the result, as
- * after torch.distributed's Work.wait().  The round's outcome is not known at return: a
- * failure that comes later fails the schedule's next post / wait.  Host buckets wait on the
- * host (as wait_ex).  Until the round finishes, esgd_schedule_stats counts it as waited but
- * not completed. */
-int esgd_schedule_wait_on(esgd_sched_h h, void *stream, int *fresh);
-/* The process's round stream (a hipStream_t; created on first use on the current device):
- * every round of every schedule is queued on it in the node's issue order.  Work a caller
- * queues there runs after the rounds launched so far, by stream order alone -- e.g. the
- * optimizer step that reads the reduced gradients (wait_on with this stream needs no event
- * wait).  Never synchronise on it from inside a round's producer work. (extension) */
-int esgd_round_stream(void **stream);
 /* ESGD_SCHED_HOLD schedules: done with the round wait returned.  Work queued on
  * `stream` so far (copy-out of rb, zeroing sb; NULL = nothing queued) is waited for by
  * the next round's snapshot on the GPU. */

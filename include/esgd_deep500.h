@@ -70,42 +70,24 @@ int allreducef_forward_cuda_div(void *handle, const float *input, float *output,
 int allreducef_forward_cuda_packed(void *handle, int n, const float *const *grads,
                                    const uint64_t *counts, float *const *outs, float divisor,
                                    void *stream);
-/* Extension: allreducef_forward_cuda_div split in two, so a caller can post the rounds of
- * many ops (one per gradient tensor) before waiting for the first -- the reference's ops
- * block one after another (opt_esgd_solo_imagenet_imbalance.py:304-307); the rounds, their
- * operands and their sums are the same, the host round trips overlap.  _post queues the
- * copy-in (divided by divisor; 1.0f = plain copy) on stream and posts; _wait waits for the
- * round, queues the copy-out into output on stream and releases the round.  One round per
- * op in flight: a second _post before _wait, a _wait without a _post, or a blocking forward
- * between them is ESGD_INVALID_ARG.  Every rank must post its ops in the same order. */
-int allreducef_forward_cuda_post(void *handle, const float *input, float divisor, void *stream);
-int allreducef_forward_cuda_wait(void *handle, float *output, void *stream);
-/* Extension: the same for n ops in one call each way (EagerSGDOptimizer's per-tensor step):
- * _post_many queues every op's copy-in (inputs[i] / divisor into op i's send bucket; one
- * launch per 48 ops) on stream, then posts the n rounds in this order with ONE producer
- * event -- the same rounds, draws and activations as n _post calls.  It stops at the first
- * failure (its status); the ops before it stay posted.  _wait_many waits for the rounds of
- * the ops that are posted, in order, queues every copy-out (one launch per 48 ops) and
- * releases the rounds with ONE consumer event; ops that are not posted are skipped; the
- * first failure's status is returned after every round was waited for. */
-int allreducef_forward_cuda_post_many(void *const *handles, int n, const float *const *inputs, float divisor,
-                                      void *stream);
-int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const *outputs, void *stream);
-/* Extension: _post_many with the outputs known at the post (EagerSGDOptimizer writes the
- * reduced gradients back into the gradient tensors): each round reads inputs[i] / divisor
- * itself in its snapshot and writes its result into outputs[i] (esgd_schedule_post_io) --
- * no copy-in or copy-out launch on stream, no consumer event.  _wait_many (with the same
- * outputs) then only copies out the rounds a peer's activation carried this rank through
- * before the post (their results are in the op's bucket).  Tensors must be 16-B aligned
- * and the ops fp32 on the wire; otherwise the group is posted as by _post_many. */
+/* Extension: the per-tensor step of EagerSGDOptimizer in one call each way.  The
+ * reference's ops block one after another (opt_esgd_solo_imagenet_imbalance.py:304-307);
+ * here a caller posts the rounds of many ops (one per gradient tensor) before waiting for
+ * the first -- the same rounds, operands and sums, the host round trips overlapped.
+ * _post_many_io posts the n rounds in this order with ONE producer event; each round reads
+ * inputs[i] / divisor itself in its snapshot and writes its result into outputs[i] (may
+ * alias inputs[i]; esgd_schedule_post_io) -- no copy-in or copy-out launch on stream.
+ * Tensors that are not 16-B aligned, or ops with a bf16 wire, make the group go the copy-in
+ * way (inputs[i] / divisor into the op's bucket, one launch per 48 ops).  It stops at the
+ * first failure (its status); the ops before it stay posted.  _wait_many waits for the
+ * rounds of the ops that are posted, in order, copies out only what a round did not write
+ * itself (a peer's activation carried this rank through before the post, or the copy-in
+ * way; one launch per 48 ops) and releases the rounds with ONE consumer event; ops not
+ * posted are skipped; the first failure's status is returned after every round was waited
+ * for.  One round per op in flight; every rank posts its ops in the same order. */
 int allreducef_forward_cuda_post_many_io(void *const *handles, int n, const float *const *inputs,
                                          float *const *outputs, float divisor, void *stream);
-/* Extension: _wait_many ordered on the GPU (esgd_schedule_wait_on): stream waits for each
- * round on the GPU, and the call returns once every round is queued there, not finished --
- * the wrapped optimizer's step is queued behind the rounds while they run, as after
- * torch.distributed's Work.wait().  A round that fails after this returned fails its op's
- * next post. */
-int allreducef_forward_cuda_wait_many_on(void *const *handles, int n, float *const *outputs, void *stream);
+int allreducef_forward_cuda_wait_many(void *const *handles, int n, float *const *outputs, void *stream);
 /* Extension: allreducef_forward_cuda_packed split in two (posting a fused bucket while
  * backward still runs): _packed_post hands the n pieces to the round (esgd_schedule_post_iov:
  * packed / divisor into the op's bucket and unpacked into outs by the round; bf16 wire:

@@ -344,8 +344,21 @@ static void *ffref_c1_main(void *p) {
     return NULL;
 }
 
-double ffref_time_c1(int P, uint32_t count, int reps, int *ok) {
+/* Each simulated rank on cores of its own (2 cores per rank; the
+ * reference's ff.c:72 starts one progress pthread beside each MPI rank): rank r's progress
+ * thread on cpus[2r], its main thread on cpus[2r + 1] (cpus NULL or ncpus < 2P: unpinned,
+ * the scheduler's choice -- round 5's figures moved 1.7x between boxes that way). */
+static void ffref_pin(pthread_t t, const int *cpus, int ncpus, int i) {
+    if (!cpus || i >= ncpus) return;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(cpus[i], &set);
+    (void)pthread_setaffinity_np(t, sizeof(set), &set);
+}
+
+double ffref_time_c1_pinned(int P, uint32_t count, int reps, const int *cpus, int ncpus, int *ok) {
     if (P < 1 || P > 64 || reps < 1) return -1.0;
+    if (ncpus < 2 * P) cpus = NULL;
     const size_t bytes = (size_t)count * 4;
     float *bufs[5][64];
     for (int k = 0; k < 5; ++k)
@@ -361,6 +374,8 @@ double ffref_time_c1(int P, uint32_t count, int reps, int *ok) {
                                  posted, done, ready, taken, &bar, &stop};
         pthread_create(&th[2 * r], NULL, ffref_c1_progress, &args[r]);
         pthread_create(&th[2 * r + 1], NULL, ffref_c1_main, &args[r]);
+        ffref_pin(th[2 * r], cpus, ncpus, 2 * r);
+        ffref_pin(th[2 * r + 1], cpus, ncpus, 2 * r + 1);
     }
     for (int i = 0; i < 2 * P; ++i) pthread_join(th[i], NULL);
     pthread_barrier_destroy(&bar);
@@ -374,4 +389,8 @@ double ffref_time_c1(int P, uint32_t count, int reps, int *ok) {
     for (int k = 0; k < 5; ++k)
         for (int r = 0; r < P; ++r) free(bufs[k][r]);
     return ffref_c1_median;
+}
+
+double ffref_time_c1(int P, uint32_t count, int reps, int *ok) {
+    return ffref_time_c1_pinned(P, count, reps, NULL, 0, ok);
 }

@@ -99,6 +99,8 @@ double ffref_time_allreduce(int P, uint32_t count, int threads, int reps);
  * Returns the median per-step seconds over `reps` steps (after one warm-up step); *ok = 1
  * if every rank's last result equals the oracle tree of the P buckets. */
 double ffref_time_c1(int P, uint32_t count, int reps, int *ok);
+/* the same with rank r's progress / main thread pinned to cpus[2r] / cpus[2r + 1] */
+double ffref_time_c1_pinned(int P, uint32_t count, int reps, const int *cpus, int ncpus, int *ok);
 
 #ifdef __cplusplus
 }

@@ -55,6 +55,8 @@ def lib():
         h.ffref_time_allreduce.restype = C.c_double
         h.ffref_time_c1.argtypes = [i, u32, i, C.POINTER(i)]
         h.ffref_time_c1.restype = C.c_double
+        h.ffref_time_c1_pinned.argtypes = [i, u32, i, C.POINTER(i), i, C.POINTER(i)]
+        h.ffref_time_c1_pinned.restype = C.c_double
         _lib = h
     return _lib
 
@@ -144,11 +146,16 @@ def time_allreduce(P: int, count: int, threads: int, reps: int) -> float:
     return float(lib().ffref_time_allreduce(P, count, threads, reps))
 
 
-def time_c1(P: int, count: int, reps: int):
-    """(best seconds per step, every rank's result == tree) of the C1-shaped baseline:
-    P ranks x (main + progress thread) (ffref.h: ffref_time_c1)."""
+def time_c1(P: int, count: int, reps: int, cpus=None):
+    """(median seconds per step, every rank's result == tree) of the C1-shaped baseline:
+    P ranks x (main + progress thread) (ffref.h: ffref_time_c1); cpus: 2P core ids, rank r's
+    progress / main thread pinned to cpus[2r] / cpus[2r + 1] (ffref_time_c1_pinned)."""
     ok = C.c_int(0)
-    t = float(lib().ffref_time_c1(P, count, reps, C.byref(ok)))
+    if cpus:
+        arr = (C.c_int * len(cpus))(*cpus)
+        t = float(lib().ffref_time_c1_pinned(P, count, reps, arr, len(cpus), C.byref(ok)))
+    else:
+        t = float(lib().ffref_time_c1(P, count, reps, C.byref(ok)))
     return t, bool(ok.value)
 
 

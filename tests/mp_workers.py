@@ -110,6 +110,14 @@ def run(fn_name: str, world: int, timeout: float = 240.0, **kw):
 
 # --------------------------------------------------------------------------- workers
 
+def set_test_knobs(**knobs):
+    """The library's test hooks (ESGD_TEST, read once per process: set before the first
+    schedule): e.g. set_test_knobs(fail_exports=2, shadow=1); None values are left out."""
+    have = dict(kv.split("=", 1) for kv in os.environ.get("ESGD_TEST", "").split(",") if "=" in kv)
+    have.update({k: str(int(v)) for k, v in knobs.items() if v is not None})
+    os.environ["ESGD_TEST"] = ",".join(f"{k}={v}" for k, v in have.items())
+
+
 def local_device(rank=None):
     """rank % device_count (0 when there is no device)."""
     import esgd
@@ -145,7 +153,7 @@ def _comm():
 
 
 def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0.0,
-              first_poster_rotates=False, barrier_each=False, use_test=False, wait_on=False):
+              first_poster_rotates=False, barrier_each=False, use_test=False):
     """Control plane only (ESGD_BUF_NONE): drive `rounds` post/wait cycles and return
     this rank's per-round log, post roles and stats."""
     comm = _comm()
@@ -169,8 +177,6 @@ def cp_rounds(rank, world, kind, rounds, async_=0, seed=0, straggler=-1, delay=0
         if use_test:
             while not s.test():
                 time.sleep(0.0005)
-        elif wait_on:   # esgd_schedule_wait_on: no GPU event here, so the host wait runs
-            s.wait_on(0)
         else:
             s.wait()
     comm.barrier()
@@ -204,14 +210,13 @@ def mismatch(t, got, want, xs, sched=None):
             m["stats"] = sched.stats()
         except Exception as e:   # noqa: BLE001 -- diagnostics only
             m["stats"] = repr(e)
-    m["env"] = {k: v for k, v in os.environ.items()
-                if k in ("ESGD_FAIL_EXPORTS", "ESGD_SHADOW", "ESGD_BATCH_ROUNDS", "ESGD_SMALL_ROUND_BYTES")}
+    m["env"] = {k: v for k, v in os.environ.items() if k in ("ESGD_TEST", "ESGD_SMALL_ROUND_BYTES")}
     return m
 
 
 def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0, buf="device",
                   in_place=False, transport="ipc", shadow_ranks=(), small_bytes=None,
-                  piece_bytes=None, host_chunk=None, device_flags=None, wire=False, chunk_kernel=None,
+                  piece_bytes=None, host_chunk=None, device_flags=None, wire=False,
                   fail_exports=None, batch=None, fail_maps=None):
     """Data plane on the GPU: every rank reduces its splitmix bucket; returns the
     result bytes' digest per round plus a bit-exactness verdict against the oracle.
@@ -222,30 +227,23 @@ def gpu_allreduce(rank, world, dtype_name="fp32", count=100003, rounds=3, kind=0
     is the oracle's bf16 tree of the bf16-rounded inputs, widened to fp32."""
     import numpy as np
 
-    if rank in shadow_ranks:
-        os.environ["ESGD_SHADOW"] = "1"
-    if fail_exports is not None and fail_exports[rank]:   # this rank's first N chunk exports fail
-        os.environ["ESGD_FAIL_EXPORTS"] = str(fail_exports[rank])
-    if fail_maps is not None and fail_maps[rank]:   # this rank's first N mappings "show other memory"
-        os.environ["ESGD_FAIL_MAPS"] = str(fail_maps[rank])
-    if batch is not None:
-        os.environ["ESGD_BATCH_ROUNDS"] = str(batch)
+    set_test_knobs(shadow=1 if rank in shadow_ranks else None,
+                   # this rank's first N chunk exports fail / N mappings "show other memory"
+                   fail_exports=fail_exports[rank] if fail_exports is not None and fail_exports[rank] else None,
+                   fail_maps=fail_maps[rank] if fail_maps is not None and fail_maps[rank] else None,
+                   piece_bytes=piece_bytes, host_chunk_bytes=host_chunk)
     if small_bytes is not None:
         os.environ["ESGD_SMALL_ROUND_BYTES"] = str(small_bytes)
-    if piece_bytes is not None:
-        os.environ["ESGD_PIECE_BYTES"] = str(piece_bytes)
-    if host_chunk is not None:
-        os.environ["ESGD_HOST_CHUNK_BYTES"] = str(host_chunk)
     if device_flags is not None:
         os.environ["ESGD_DEVICE_FLAGS"] = str(device_flags)
-    if chunk_kernel is not None:
-        os.environ["ESGD_HOST_CHUNK_KERNEL"] = str(chunk_kernel)
 
     from esgd import _lib
     from esgd import device as dev
     from oracle import ffref
     comm = _comm()
     comm.set_transport(transport)
+    if batch is not None:
+        comm.set_config("batch_rounds", batch)
     seed = 0x5EEDE56D
     dt = {"fp32": _lib.FLOAT, "int32": _lib.INT32, "fp64": _lib.DOUBLE, "int64": _lib.INT64,
           "bf16": _lib.BF16}[dtype_name]
@@ -543,7 +541,7 @@ def op_device_pattern(rank, world, count=25559081, steps=9, mode="solo", packed=
     return out
 
 
-def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp32", pipeline=True, fused_io=True,
+def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp32", pipeline=True, bucket_mb=None,
                    **opt_kw):
     """EagerSGDOptimizer on PyTorch-ROCm: every rank's p.grad after apply_gradients must
     equal the oracle tree of (grad_r / P) over ranks, bit for bit (allreduce), or over
@@ -566,8 +564,11 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp3
     if opt_kw.get("overlap"):   # the local gradients, taken before the optimizer's hooks post them
         for prm in model.parameters():
             prm.register_post_accumulate_grad_hook(lambda q: captured.__setitem__(id(q), q.grad.detach().clone()))
-    opt = EagerSGDOptimizer(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9), world, mode=mode,
-                            fuse=fuse, wire=wire, pipeline=pipeline, fused_io=fused_io, **opt_kw)
+    cls = EagerSGDOptimizer
+    if bucket_mb is not None:   # the fused buckets' size is a class attribute
+        cls = type("SmallBuckets", (EagerSGDOptimizer,), {"bucket_mb": bucket_mb})
+    opt = cls(torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9), world, mode=mode,
+              fuse=fuse, wire=wire, pipeline=pipeline, **opt_kw)
     ok = []
     for t in range(steps):
         g = torch.Generator().manual_seed(100 * t + rank)
@@ -584,7 +585,7 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp3
         dist.all_gather_object(allg, local)
         comm.barrier()
         late = t > 0 and rank in late_ranks(mode, world, t)
-        names = ("forward_cuda_div", "forward_cuda_packed", "post_cuda", "post_many", "post_many_io")
+        names = ("forward_cuda_div", "forward_cuda_packed", "post_many_io")
         orig = {n: getattr(deep500.AllreduceOp, n) for n in names}
         if late:   # every op call (or post) of this step comes LATE_S after the peers'
             def delayed(fn):
@@ -616,11 +617,13 @@ def optimizer_step(rank, world, mode="allreduce", steps=2, fuse=False, wire="fp3
 
 
 def op_group(rank, world, steps=3, sizes=(1, 17, 1000, 4099, 262147, (2 << 20) + 5, 64, 300007)):
-    """allreducef_forward_cuda_post_many / _wait_many against the single-op path: one set
-    of ops driven by the group calls, a second set by forward_cuda_div one op at a time
-    (allreduce mode: every rank posts every round, so both must give the same bits, and
-    the oracle tree of grad_r / P); plus the misuse rules: a group post over an op still
-    posted fails with ESGD_INVALID_ARG and leaves it posted, wait_many skips ops not posted."""
+    """allreducef_forward_cuda_post_many_io / _wait_many against the single-op path: one set
+    of ops posted as a group over 16-B aligned tensors (the rounds read and write them
+    themselves), one over tensors 4 bytes off that alignment (the group goes the copy-in way
+    and wait_many copies out), a third driven by forward_cuda_div one op at a time
+    (allreduce mode: every rank posts every round, so all must give the same bits, the
+    oracle tree of grad_r / P); plus the misuse rules: a group post over an op still posted
+    fails with ESGD_INVALID_ARG and leaves it posted, wait_many skips ops not posted."""
     import numpy as np
     import torch
 
@@ -631,53 +634,46 @@ def op_group(rank, world, steps=3, sizes=(1, 17, 1000, 4099, 262147, (2 << 20) +
     dev = torch.device("cuda", local_device())
     torch.cuda.set_device(dev)
     deep500.configure("allreduce", 32, 6545343)
-    grp = [deep500.AllreduceOp((n,)) for n in sizes]
+    fio = [deep500.AllreduceOp((n,)) for n in sizes]   # aligned: the rounds do the copies
+    grp = [deep500.AllreduceOp((n,)) for n in sizes]   # unaligned: copy-in / copy-out
     one = [deep500.AllreduceOp((n,)) for n in sizes]
-    fio = [deep500.AllreduceOp((n,)) for n in sizes]   # post_many_io: the rounds do the copies
-    # the same two group paths waited for on the GPU (wait_many(on_stream=True)): clones
-    # queued right after the call read the results only if the stream waits for the rounds
-    fon = [deep500.AllreduceOp((n,)) for n in sizes]
-    gon = [deep500.AllreduceOp((n,)) for n in sizes]
     ok, errs = [], {}
+
+    def unaligned(x):   # a copy of x starting 4 bytes past a 16-B boundary
+        buf = torch.empty(x.numel() + 4, dtype=torch.float32, device=dev)
+        v = buf[1:1 + x.numel()]
+        v.copy_(x)
+        assert v.data_ptr() % 16 == 4
+        return v
+
     for t in range(steps):
         xs = [[ffref.fill_uniform(0xA11 + 13 * t + i, r, n) for r in range(world)] for i, n in enumerate(sizes)]
-        g = [torch.from_numpy(x[rank]).to(dev) for x in xs]
-        g0 = [gi.clone() for gi in g]
-        h = [gi.clone() for gi in g]
-        k = [gi.clone() for gi in g]
+        k = [torch.from_numpy(x[rank]).to(dev) for x in xs]
+        g = [unaligned(ki) for ki in k]
+        h = [ki.clone() for ki in k]
         comm.barrier()
-        deep500.AllreduceOp.post_many(grp, g, float(world))
+        deep500.AllreduceOp.post_many_io(fio, k, k, float(world))
+        deep500.AllreduceOp.wait_many(fio, k)
+        deep500.AllreduceOp.post_many_io(grp, g, g, float(world))
         deep500.AllreduceOp.wait_many(grp, g)
         for op, hi in zip(one, h):
             op.forward_cuda_div(hi, hi, float(world))
-        deep500.AllreduceOp.post_many_io(fio, k, k, float(world))
-        deep500.AllreduceOp.wait_many(fio, k)
-        m = [gi.clone() for gi in g0]
-        q = [gi.clone() for gi in g0]
-        deep500.AllreduceOp.post_many_io(fon, m, m, float(world))
-        deep500.AllreduceOp.wait_many(fon, m, on_stream=True)
-        mc = [mi.clone() for mi in m]
-        deep500.AllreduceOp.post_many(gon, q, float(world))
-        deep500.AllreduceOp.wait_many(gon, q, on_stream=True)
-        qc = [qi.clone() for qi in q]
         torch.cuda.synchronize()
         for i, x in enumerate(xs):
             want = ffref.tree_sum([np.float32(xr) / np.float32(world) for xr in x])
             a, b, c = g[i].cpu().numpy(), h[i].cpu().numpy(), k[i].cpu().numpy()
             ok.append(bool(np.array_equal(a.view(np.uint32), want.view(np.uint32)) and
                            np.array_equal(a.view(np.uint32), b.view(np.uint32)) and
-                           np.array_equal(a.view(np.uint32), c.view(np.uint32)) and
-                           all(np.array_equal(a.view(np.uint32), y[i].cpu().numpy().view(np.uint32))
-                               for y in (m, mc, q, qc))))
+                           np.array_equal(a.view(np.uint32), c.view(np.uint32))))
     # misuse: op 0 posted alone, then a group post naming it fails and leaves it posted
     x = [torch.ones(n, device=dev) for n in sizes]
-    grp[0].post_cuda(x[0], float(world))
+    deep500.AllreduceOp.post_many_io(fio[:1], x[:1], x[:1], float(world))
     try:
-        deep500.AllreduceOp.post_many(grp, x, float(world))
+        deep500.AllreduceOp.post_many_io(fio, x, x, float(world))
         errs["post_many_over_posted"] = None
     except EsgdError as e:
         errs["post_many_over_posted"] = e.rc
-    deep500.AllreduceOp.wait_many(grp, x)   # waits op 0 only (the others are not posted)
+    deep500.AllreduceOp.wait_many(fio, x)   # waits op 0 only (the others are not posted)
     torch.cuda.synchronize()
     want0 = ffref.tree_sum([np.ones(sizes[0], np.float32) / np.float32(world)] * world)
     errs["drained_op0"] = bool(np.array_equal(x[0].cpu().numpy(), want0))
@@ -842,7 +838,7 @@ def gpu_config(rank, world, kind, counts, dtype_name="fp32", rounds=2, async_=32
         else:
             s.delete()
             if close_before_free:
-                # every rank's deletion (closing its peer mappings under ESGD_ARENA_BYPASS=2)
+                # every rank's deletion (closing its peer mappings under ESGD_TEST arena_bypass=2)
                 # happens before any rank frees a bucket a peer had mapped
                 comm.barrier()
             if alloc_ahead and i + 1 < len(counts):
@@ -894,10 +890,13 @@ def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, dela
         if rank != late or d == 0:
             fill()
         comm.barrier()
-        if rank == late and d > 0:
-            time.sleep(d)
-            fill()
+        tb = time.perf_counter()
+        if rank == late and d > 0:   # the late gradient, then a spin to the deadline (time.sleep
+            fill()                   # cannot do tens of us)
+            while time.perf_counter() - tb < d:
+                pass
         t0 = time.perf_counter()
+        achieved.append(t0 - tb)   # barrier -> post, as this rank saw it
         s.post()
         s.wait()
         el = time.perf_counter() - t0
@@ -912,6 +911,7 @@ def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, dela
         return el, float(head[0]), uniform
 
     slices = []                            # per round: (min, max, crc32) of head + tail
+    achieved = []                          # per round: barrier -> post on this rank (s)
     warm = [one(0)[0] for _ in range(3)]   # rounds 1..3: everyone on time
     tt = torch.tensor([statistics.median(warm)], dtype=torch.float64)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -921,7 +921,8 @@ def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, dela
     for t in range(4, 4 + rounds):
         _, c, u = one(d)
         res.append((t, c, u))
-    out = {"rounds": res, "log": s.log(), "T_s": T, "delay_s": d, "slices": slices[3:]}
+    out = {"rounds": res, "log": s.log(), "T_s": T, "delay_requested_s": d,
+           "delay_achieved_s": statistics.median(achieved[3:]), "slices": slices[3:]}
     comm.barrier()
     s.delete()
     comm.finalize()
@@ -1220,7 +1221,7 @@ def gpu_stress_pipelined(rank, world, kind, counts=(4096, 65536, 17, (1 << 20) +
     carry ranks through rounds they have not posted.  A rank's share of every round must
     be its tag iff it had posted the round before joining it, never torn.  batch: rounds
     per shared launch for this rank (a list: one value per rank).  fail_exports: per rank,
-    how many of its first chunk exports fail (ESGD_FAIL_EXPORTS, the runtime's refusals)."""
+    how many of its first chunk exports fail (ESGD_TEST fail_exports, the runtime's refusals)."""
     import random
 
     import numpy as np
@@ -1228,7 +1229,7 @@ def gpu_stress_pipelined(rank, world, kind, counts=(4096, 65536, 17, (1 << 20) +
     from esgd import _lib
     from esgd import device as dev
     if fail_exports is not None and fail_exports[rank]:
-        os.environ["ESGD_FAIL_EXPORTS"] = str(fail_exports[rank])
+        set_test_knobs(fail_exports=fail_exports[rank])
     os.environ.update(env or {})   # data-plane switches, read at their first use
     comm = _comm()
     if batch is not None:
@@ -1692,12 +1693,12 @@ def gpu_post_io(rank, world, count=4099, rounds=3, small_bytes=None, batch=None,
     from esgd import device as dev
     from oracle import ffref
     if rank in shadow_ranks:
-        os.environ["ESGD_SHADOW"] = "1"
-    if batch is not None:
-        os.environ["ESGD_BATCH_ROUNDS"] = str(batch)
+        set_test_knobs(shadow=1)
     if small_bytes is not None:
         os.environ["ESGD_SMALL_ROUND_BYTES"] = str(small_bytes)
     comm = _comm()
+    if batch is not None:
+        comm.set_config("batch_rounds", batch)
     dt = {"fp32": _lib.FLOAT, "int32": _lib.INT32}[dtype_name]
     div = float(world if divisor is None else divisor) if dt == _lib.FLOAT else 1.0
     sb, rb = dev.DeviceBuffer(count, dt), dev.DeviceBuffer(count, dt)
@@ -1732,16 +1733,14 @@ def gpu_post_io(rank, world, count=4099, rounds=3, small_bytes=None, batch=None,
     return {"verdicts": verdicts, "fresh": fresh}
 
 
-def gpu_post_io_late(rank, world, count=4099, steps=8, async_=3, late=1, on_stream=False):
+def gpu_post_io_late(rank, world, count=4099, steps=8, async_=3, late=1):
     """post_io under solo's asynchronous rounds: HOLD | FRESH_ONLY (how the deep500 op runs
     them), rank `late` posts LATE_S after its peers every step.  A round the early rank's
     activation carries the late rank through before its post does not take its data: wait
     says fresh = 0, its dst keeps what it held, and the round's result (its share zero) is
     in rb; a round it posted in time takes src and writes dst.  Every rank's result must be
     the oracle tree of (x_r / P if rank r's round was fresh else 0), the same bits on every
-    rank.  on_stream: waited for with wait_on(stream) (esgd_schedule_wait_on), the result
-    copied by a kernel queued on that stream right after it returns -- before the round has
-    necessarily finished -- so the copy holds the result only if the stream waits for it."""
+    rank."""
     import numpy as np
     import torch.distributed as dist
 
@@ -1750,11 +1749,6 @@ def gpu_post_io_late(rank, world, count=4099, steps=8, async_=3, late=1, on_stre
     comm = _comm()
     rb = dev.DeviceBuffer(count)
     src, dst = dev.DeviceBuffer(count), dev.DeviceBuffer(count)
-    if on_stream:
-        import torch
-        torch.cuda.set_device(local_device())
-        stream = torch.cuda.Stream()
-        copy = torch.empty(count, dtype=torch.float32, device="cuda")
     s = comm.Schedule(comm.SOLO, None, rb, count, async_=async_, seed=6545343, buf=comm.BUF_DEVICE,
                       flags=comm.HOLD | comm.FRESH_ONLY)
     out = []
@@ -1766,18 +1760,10 @@ def gpu_post_io_late(rank, world, count=4099, steps=8, async_=3, late=1, on_stre
         if rank == late and t > 0:
             time.sleep(LATE_S)
         s.post_io(src, dst, float(world))
-        if on_stream:
-            f = s.wait_on(stream)
-            dev.pack_div([dst if f else rb], [count], copy, 1.0, stream.cuda_stream)
-            s.release(None if f else stream.cuda_stream)
-            stream.synchronize()
-            res = copy.cpu().numpy()
-        else:
-            f = s.wait()
-            res = (dst if f else rb).download()
+        f = s.wait()
+        res = (dst if f else rb).download()
         untouched = f or bool(np.all(dst.download() == np.float32(3.0)))
-        if not on_stream:
-            s.release()
+        s.release()
         fr = [None] * world
         dist.all_gather_object(fr, bool(f))
         want = ffref.tree_sum([x / np.float32(world) if fr[r] else np.zeros_like(x) for r, x in enumerate(xs)])
@@ -1965,7 +1951,7 @@ def cp_connect_failure(rank, world, bad_rank=1):
     second creation barrier), none waits for the timeout, and the communicator stays
     usable for the next schedule."""
     if rank == bad_rank:
-        os.environ["ESGD_TEST_FAIL_CONNECT"] = str(rank)
+        set_test_knobs(fail_connect=rank)
     from esgd import comm
     from esgd._lib import EsgdError
     comm.init()
@@ -1978,7 +1964,7 @@ def cp_connect_failure(rank, world, bad_rank=1):
     t_fail = time.time() - t0
     if s is not None:
         s.delete()
-    os.environ.pop("ESGD_TEST_FAIL_CONNECT", None)
+    os.environ.pop("ESGD_TEST", None)
     comm.barrier()
     s2 = comm.Schedule(comm.ALLREDUCE, None, None, 0, buf=comm.BUF_NONE)
     for _ in range(2):
@@ -2117,121 +2103,6 @@ def cp_create_many(rank, world, n=161, rounds=1):
         s.delete()
     comm.finalize()
     return {"create_ms_per_schedule": t_create * 1e3 / n}
-
-
-def op_split_misuse(rank, world, count=4096):
-    """allreducef_forward_cuda_post / _wait: one round per op in flight; misuse is
-    ESGD_INVALID_ARG and leaves the op usable; a posted round gives forward_cuda_div's bits."""
-    import torch
-
-    from esgd import deep500
-    from esgd._lib import EsgdError
-    comm = _comm()
-    dev = torch.device("cuda", local_device())
-    torch.cuda.set_device(dev)
-    op = deep500.AllreduceOp((count,))
-    ref = deep500.AllreduceOp((count,))
-    x = torch.arange(count, dtype=torch.float32, device=dev) * (rank + 1)
-    errs = {}
-
-    def expect_err(name, fn):
-        try:
-            fn()
-            errs[name] = None
-        except EsgdError as e:
-            errs[name] = e.rc
-
-    expect_err("wait_without_post", lambda: op.wait_cuda(x.clone()))
-    g = x.clone()
-    op.post_cuda(g, float(world))
-    expect_err("second_post", lambda: op.post_cuda(g, float(world)))
-    expect_err("blocking_between", lambda: op.forward_cuda_div(g, g, float(world)))
-    op.wait_cuda(g)
-    h = x.clone()
-    ref.forward_cuda_div(h, h, float(world))
-    torch.cuda.synchronize()
-    same = bool(torch.equal(g, h))
-    comm.barrier()
-    comm.finalize()
-    return {"errs": errs, "same": same}
-
-
-def op_queue_probe(rank, world, side=False, steps=3, sizes=(4099, 100003, 1 << 20)):
-    """Diagnostics (tools/queue_probe.py): deep500 ops driven the blocking way on torch's
-    current stream (the legacy NULL stream), optionally after creating one more torch
-    stream, under AMD_LOG_LEVEL so the runtime names the hardware queue of every dispatch.
-    Returns the time per blocking round."""
-    import torch
-
-    from esgd import deep500
-    _comm()
-    dev = torch.device("cuda", local_device())
-    torch.cuda.set_device(dev)
-    extra = torch.cuda.Stream() if side else None   # noqa: F841 -- kept alive: one more queue
-    deep500.configure("allreduce")
-    ops = [deep500.AllreduceOp((n,)) for n in sizes]
-    gs = [torch.rand(n, device=dev) for n in sizes]
-    stream = torch.cuda.current_stream().cuda_stream
-    for op, g in zip(ops, gs):   # creation (collective), untimed
-        op.forward_cuda_div(g, g, world, stream)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        for op, g in zip(ops, gs):
-            op.forward_cuda_div(g, g, world, stream)
-    torch.cuda.synchronize()
-    us = (time.perf_counter() - t0) / (steps * len(ops)) * 1e6
-    for op in ops:
-        op.close()
-    return {"us_per_round": round(us, 1), "side": side}
-
-
-def gpu_wait_on_paths(rank, world, rounds=3):
-    """esgd_schedule_wait_on on the round paths the optimizer test does not reach: a
-    five-launch round (4 MiB + 12 B: its own event, no shared launch), a one-launch round
-    (a shared launch of its own), and host buckets (no GPU event: the host wait instead).
-    Each result is read by a copy queued on the waited stream right after wait_on returned
-    (device buckets) or straight from host memory; the oracle tree of the ranks' inputs."""
-    import numpy as np
-
-    from esgd import device as dev
-    from oracle import ffref
-    comm = _comm()
-    stream = dev.Stream()
-    out = {}
-    big = (1 << 20) + 3
-    cases = {"five_launch": (big, False), "one_launch": (4099, False), "host": (4099, True)}
-    for name, (count, host) in cases.items():
-        if host:
-            sb, rb = np.zeros(count, np.float32), np.zeros(count, np.float32)
-            s = comm.Schedule(comm.ALLREDUCE, sb, rb, count, buf=comm.BUF_HOST)
-        else:
-            sb, rb = dev.DeviceBuffer(count), dev.DeviceBuffer(count)
-            s = comm.Schedule(comm.ALLREDUCE, sb, rb, count, buf=comm.BUF_DEVICE)
-            copy = dev.DeviceBuffer(count)
-        ok = []
-        for t in range(rounds):
-            xs = [ffref.fill_uniform(0x3A1 + 7 * t, r, count) for r in range(world)]
-            if host:
-                sb[:] = xs[rank]
-            else:
-                sb.upload(xs[rank])
-            comm.barrier()
-            s.post()
-            fresh = s.wait_on(stream)
-            if host:
-                got = rb.copy()
-            else:
-                dev.pack_div([rb], [count], copy, 1.0, stream.handle)
-                stream.synchronize()
-                got = copy.download()
-            want = ffref.tree_sum(xs)
-            ok.append(bool(fresh) and bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
-            comm.barrier()
-        s.delete()
-        out[name] = ok
-    comm.finalize()
-    return out
 
 
 def gpu_post_iov(rank, world, count=4099, rounds=3, in_place=False):

@@ -25,3 +25,17 @@ def test_optimizer_validation():
 def test_configure_rejects_bad_mode():
     with pytest.raises(KeyError):
         deep500.configure("ring")
+
+
+def test_overlap_refuses_a_second_backward_before_the_step():
+    # with overlap=True the hooks post each gradient's round during backward; a
+    # second backward before apply_gradients (gradient accumulation) would change gradients
+    # whose rounds are already posted -- a clear error instead of autograd's deep one
+    import torch
+    model = torch.nn.Linear(4, 3)
+    opt = EagerSGDOptimizer(torch.optim.SGD(model.parameters(), lr=0.1), 2, mode="allreduce", overlap=True)
+    x = torch.randn(5, 4)
+    model(x).sum().backward()   # two tensors: below the hooks' posting group, nothing posted
+    with pytest.raises(RuntimeError, match="gradient accumulation"):
+        model(x).sum().backward()
+    opt.detach()

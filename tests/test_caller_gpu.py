@@ -41,15 +41,7 @@ def test_deep500_op_device_late_gradient_dropped(on_time, count):
         assert o["sync_rounds"] == [r % 4 == 0 for r in range(2, 10)]
 
 
-VARIANTS = {"blocking": dict(pipeline=False), "pipelined": dict(pipeline=True), "fused": dict(fuse=True),
-            # the per-tensor rounds with copy-in / copy-out kernels on the caller's stream
-            # instead of the fused round I/O (an A/B): the same bits
-            "pipelined_copy_kernels": dict(pipeline=True, fused_io=False),
-            # the rounds waited for on the GPU instead of the host (wait_many_on); the ops and
-            # the wrapped step on the data plane's round stream (esgd_round_stream), either wait
-            "pipelined_stream_wait": dict(pipeline=True, stream_wait=True),
-            "pipelined_round_stream": dict(pipeline=True, round_stream=True, stream_wait=True),
-            "pipelined_round_stream_host_wait": dict(pipeline=True, round_stream=True)}
+VARIANTS = {"blocking": dict(pipeline=False), "pipelined": dict(pipeline=True), "fused": dict(fuse=True)}
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
@@ -66,15 +58,14 @@ def test_eager_sgd_optimizer(mode, variant):
         assert outs[0]["params_digest"] == outs[1]["params_digest"]
 
 
-@pytest.mark.parametrize("variant", ["host_wait", "stream_wait", "fused_buckets"])
+@pytest.mark.parametrize("variant", ["per_tensor", "fused_buckets"])
 def test_eager_sgd_optimizer_rounds_posted_during_backward(variant):
     # overlap=True: each tensor's round posted from its post-accumulate-grad hook while
     # backward still runs (TF's dataflow order for the reference's ops), waited for in
     # apply_gradients -- the same rounds, so the oracle's bits and identical replicas;
     # fused_buckets: fuse=True in buckets of ~4 KiB (this model: several), each bucket's
     # fused round posted once its last gradient exists
-    kw = dict(fuse=True, bucket_mb=4096 / (1 << 20)) if variant == "fused_buckets" else \
-        dict(stream_wait=variant == "stream_wait")
+    kw = dict(fuse=True, bucket_mb=4096 / (1 << 20)) if variant == "fused_buckets" else {}
     outs = run("optimizer_step", 2, mode="allreduce", steps=3, overlap=True, **kw)
     for o in outs:
         assert all(o["ok"]) and o["ok"], o["ok"]
@@ -125,8 +116,9 @@ def test_op_result_ordered_on_the_callers_default_stream(packed, host):
 @pytest.mark.parametrize("world", [2, 3])
 def test_group_post_wait_same_bits_as_single_ops(world):
     # the optimizer's per-tensor step through ONE post and ONE wait call
-    # (allreducef_forward_cuda_post_many / _wait_many) against one forward_cuda_div per op:
-    # the oracle's bits, ragged and tiny tensors and a five-launch size among them
+    # (allreducef_forward_cuda_post_many_io / _wait_many; aligned tensors, and unaligned ones
+    # that go the copy-in way) against one forward_cuda_div per op: the oracle's bits,
+    # ragged and tiny tensors and a five-launch size among them
     outs = run("op_group", world)
     for o in outs:
         assert all(o["ok"]) and o["ok"], o["ok"]

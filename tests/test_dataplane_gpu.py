@@ -243,7 +243,7 @@ def test_shadowed_rank_beside_batched_ranks(count):
 @pytest.mark.parametrize("count", [1, 17, 4099])
 def test_refused_export_on_one_rank(count, batch):
     # the runtime refused a fresh process's first chunk export on ONE rank (round 4, r04d:
-    # count 1 at P = 2 then came out wrong on both ranks); ESGD_FAIL_EXPORTS on that rank
+    # count 1 at P = 2 then came out wrong on both ranks); ESGD_TEST fail_exports on that rank
     # only: its published shard moves to a fresh chunk and its bucket is shadowed, while
     # the peer's rounds stay batched
     for fails in ((1, 0), (2, 0), (0, 2)):
@@ -255,7 +255,7 @@ def test_refused_export_on_one_rank(count, batch):
 @pytest.mark.parametrize("fails", [(1, 0), (0, 2), (3, 0)])
 def test_wrong_mapping_is_remapped(fails, count, small):
     # round 5 (r05b): a fresh mapping of a peer's chunk showed the importer's OWN exported
-    # chunk (the seal caught it).  ESGD_FAIL_MAPS makes a rank's first N sealed mappings
+    # chunk (the seal caught it).  ESGD_TEST fail_maps makes a rank's first N sealed mappings
     # count as such: the exporter moves the publication to a new chunk (its own bucket is
     # shadowed), every rank maps again, up to kRemapTries (3) times -- then bit-exact rounds
     verdicts = run("gpu_allreduce", 2, count=count, rounds=2, fail_maps=fails, small_bytes=small)
@@ -313,7 +313,9 @@ def test_c5_majority_8_ranks_sweep(dtype):
 def _check_straggler(outs, world, kind, async_=3, seed=6545343):
     acts = ffref.activators(seed, world, 64)
     for r, o in enumerate(outs):
-        assert o["delay_s"] >= 2 * o["T_s"], o
+        assert o["delay_requested_s"] >= 2 * o["T_s"], o
+        if r == world - 1:
+            assert o["delay_achieved_s"] >= o["delay_requested_s"], o
         for t, c, uniform in o["rounds"]:
             assert uniform, (r, t)
             if kind == MAJORITY:
@@ -343,7 +345,14 @@ def test_majority_straggler_c4_20pct():
     outs = run("gpu_straggler", world, kind=MAJORITY, count=25559081, rounds=8, delay_frac=0.2, timeout=420)
     acts = ffref.activators(6545343, world, 64)
     for r, o in enumerate(outs):
-        assert abs(o["delay_s"] - 0.2 * o["T_s"]) < 1e-9, o
+        # the straggler's ACHIEVED delay (its gradient written, then a spin to the deadline;
+        # measured barrier -> post) is the 0.2 T asked for, within 10 % or 100 us; the on-time
+        # ranks post at once
+        want = 0.2 * o["T_s"]
+        if r == world - 1:
+            assert want <= o["delay_achieved_s"] <= want + max(0.1 * want, 100e-6), o
+        else:
+            assert o["delay_achieved_s"] < want, o
         for (t, c, uniform), (lo, hi, crc) in zip(o["rounds"], o["slices"]):
             if acts[t - 1] == world - 1:
                 assert uniform and c == world, (r, t, c)
@@ -431,18 +440,6 @@ def test_wire_bf16_c3_size():
     # slices checked by gpu_config's digest path is not needed: the whole bucket is compared)
     verdicts = run("gpu_allreduce", 2, rounds=1, wire=True, count=(256 << 20) // 4, timeout=400)
     assert all(all(v) for v in verdicts), verdicts
-
-
-@pytest.mark.parametrize("in_place", [False, True])
-@pytest.mark.parametrize("world", [1, 2, 3])
-def test_allreduce_host_chunked_kernel_copies(world, in_place):
-    # ESGD_HOST_CHUNK_KERNEL: the chunks of a host bucket move host <-> HBM by kernel
-    # through the pinned bucket's device view (16 workgroups per copy) instead of DMA;
-    # 64 KiB chunks, ragged last chunk, 3 rounds back to back; fp32 and bf16
-    for dt in ("fp32", "bf16"):
-        verdicts = run("gpu_allreduce", world, dtype_name=dt, count=100003, rounds=3, buf="host",
-                       in_place=in_place, host_chunk=65536, chunk_kernel=16)
-        assert all(all(v) for v in verdicts), (dt, verdicts)
 
 
 STRESS = {"p3-one-launch": (3, 65536, "device"), "p3-five-launch": (3, (1 << 20) + 3, "device"),
@@ -554,24 +551,12 @@ def _check_pipelined(outs, world):
 @pytest.mark.parametrize("kind", [SOLO, MAJORITY])
 def test_pipelined_stress_refused_exports_p8(kind):
     # round 4's r04zp configuration: 8 ranks, the batched per-tensor stress, the first
-    # chunk export of ranks 4-7 refused -- through the real path now (ESGD_FAIL_EXPORTS
+    # chunk export of ranks 4-7 refused -- through the real path now (ESGD_TEST fail_exports
     # writes the seal, then refuses the runtime call): the refused chunks are quarantined,
     # the published shards move, the peers map the moved chunks and read their seals
     world = 8
     outs = run("gpu_stress_pipelined", world, kind=kind, rounds=60, fail_exports=[0, 0, 0, 0, 1, 1, 1, 1],
                timeout=400)
-    _check_pipelined(outs, world)
-
-
-@pytest.mark.parametrize("env", [{"ESGD_BATCH_DEPTH": "0"}, {"ESGD_BATCH_DEPTH": "3"},
-                                 {"ESGD_SNAPSHOT_IN_BATCH": "0"}, {"ESGD_INLINE_JOIN": "0"}],
-                         ids=["depth0", "depth3", "copy_kernel_snapshots", "progress_thread_joins"])
-def test_pipelined_stress_switches(env):
-    # the batched stress under each data-plane switch's other setting (the defaults run in
-    # test_pipelined_stress_batched): launches never held / held behind three, snapshots by
-    # a k_copy_many launch, every join on the progress thread
-    world = 4
-    outs = run("gpu_stress_pipelined", world, kind=SOLO, rounds=60, batch=[64, 0, 5, 2], env=env, timeout=300)
     _check_pipelined(outs, world)
 
 
@@ -689,21 +674,21 @@ def test_writer_then_post_visibility_across_gpus(path, flags, strict):
 @pytest.mark.parametrize("fails", [1, 2])
 def test_schedules_survive_refused_exports(fails):
     # The runtime sometimes refuses to export a fresh process's first chunk
-    # (hipErrorInvalidValue, round 3).  ESGD_FAIL_EXPORTS=N fails each rank's first N chunk
+    # (hipErrorInvalidValue, round 3).  ESGD_TEST fail_exports=N fails each rank's first N chunk
     # exports the same way: buffers the schedule owns (published shard, host-bucket
     # staging) move to fresh chunks, a caller's device bucket in a refused chunk is
     # shadowed, and every round is still bit-exact
-    old = os.environ.get("ESGD_FAIL_EXPORTS")
-    os.environ["ESGD_FAIL_EXPORTS"] = str(fails)
+    old = os.environ.get("ESGD_TEST")
+    os.environ["ESGD_TEST"] = f"fail_exports={fails}"
     try:
         for kw in (dict(count=4099), dict(count=300007, small_bytes=0), dict(count=70001, buf="host")):
             verdicts = run("gpu_allreduce", 2, rounds=2, **kw)
             assert all(all(v) for v in verdicts), (kw, verdicts)
     finally:
         if old is None:
-            os.environ.pop("ESGD_FAIL_EXPORTS", None)
+            os.environ.pop("ESGD_TEST", None)
         else:
-            os.environ["ESGD_FAIL_EXPORTS"] = old
+            os.environ["ESGD_TEST"] = old
 
 
 POST_IO_CASES = {
@@ -731,13 +716,11 @@ def test_post_io_rounds_read_src_and_write_dst(case, world):
         assert all(o["fresh"]), o["fresh"]
 
 
-@pytest.mark.parametrize("on_stream", [False, True], ids=["host_wait", "wait_on"])
-def test_post_io_round_carried_through_before_the_post(on_stream):
+def test_post_io_round_carried_through_before_the_post():
     # solo, rank 1 posts late: rounds rank 0's activation carries it through do not take
     # rank 1's data (fresh 0, dst untouched, result in rb, its share zero); synchronous
-    # rounds do; every rank the oracle's bits of that contributor set.  wait_on: the
-    # result is copied by a kernel queued right after esgd_schedule_wait_on returned
-    outs = run("gpu_post_io_late", 2, steps=9, on_stream=on_stream)
+    # rounds do; every rank the oracle's bits of that contributor set
+    outs = run("gpu_post_io_late", 2, steps=9)
     for o in outs:
         for step in o:
             assert step["ok"] and step["untouched"], step
@@ -756,16 +739,6 @@ def test_post_iov_pieces_packed_and_unpacked_by_the_round(world, count, in_place
     for o in outs:
         assert all(o["ok"]), o["ok"]
         assert all(o["fresh"]), o["fresh"]
-
-
-def test_wait_on_five_launch_one_launch_and_host_buckets():
-    # esgd_schedule_wait_on beyond the shared launches: a five-launch round (its own
-    # event), a one-launch round, and host buckets (the host wait fallback); the oracle's
-    # bits read right behind the wait on the waited stream
-    outs = run("gpu_wait_on_paths", 2)
-    for o in outs:
-        for name, ok in o.items():
-            assert all(ok), (name, ok)
 
 
 SWEEPS_LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "bin",
@@ -852,14 +825,14 @@ def test_ipc_reexport_sequence_bitexact(bypass):
     # the sequence behind round 2's wrong sums ("IPC arena"): 8 ranks, a
     # 16 MiB bucket exported, mapped by every peer, its schedule deleted and the bucket
     # freed, then a 256 MiB bucket exported and mapped.  Production (the arena: exported
-    # memory never freed) must be bit-exact.  ESGD_ARENA_BYPASS=2 (every bucket its own
+    # memory never freed) must be bit-exact.  ESGD_TEST arena_bypass=2 (every bucket its own
     # hipMalloc, freed after every rank closed its peer mappings) is the driver-level
     # diagnostic: it failed in 5 of 7 runs this round, always the same way -- all 64 bytes
     # of every handle distinct (exporter VA + pid), yet every importer of ONE rank's new
     # bucket reads a different rank's bucket (decoded per element: the tree sum with that
     # rank's input replaced by the other's).  So it is expected to fail, not required to.
     counts = [(16 << 20) // 4, (256 << 20) // 4]
-    env = {} if bypass is None else {"ESGD_ARENA_BYPASS": bypass}
+    env = {} if bypass is None else {"ESGD_TEST": f"arena_bypass={bypass}"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
