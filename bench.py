@@ -1439,16 +1439,16 @@ def straggler_c4(comm, dev, rank, world, rounds=16, delay_fracs=(0.2, 2.0)):
 
     def one(delay):
         """-> (post-to-wait seconds, contributors, the straggler's achieved delay).  The
-        delay is a spin to a perf_counter deadline (time.sleep cannot do tens of us), and the
-        achieved one is measured from the barrier to the post."""
+        delay is a spin to a perf_counter deadline (time.sleep cannot do tens of us) and then
+        the late gradient's write; the achieved one is measured from the barrier to the post."""
         if not (late and delay):
             fill()
         comm.barrier()
         tb = time.perf_counter()
-        if late and delay:   # the late gradient, then a spin to the deadline
-            fill()
+        if late and delay:   # a spin to the deadline, then the late gradient is written
             while time.perf_counter() - tb < delay:
                 pass
+            fill()
         t0 = time.perf_counter()
         achieved = t0 - tb
         sch.post()

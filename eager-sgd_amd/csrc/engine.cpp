@@ -436,10 +436,13 @@ int sched_post(Sched *s, void *producer_stream, int *role, const RoundIO *io) {
             }
             if (int rc = s->resolve(*s)) return rc;
         }
-        if (io)   // before the post counts: a join that sees it fresh finds its data
-            if (int rc = s->tp->note_io(*s, t, *io)) return rc;
+        // the producer first, the round's own data last (both before the post counts: a join
+        // that sees it fresh finds them): a failed note_producer leaves no RoundIO behind
+        // for a later post of round t to launch with stale pointers
         if (producer_stream)
             if (int rc = s->tp->note_producer(*s, t, producer_stream)) return rc;
+        if (io)
+            if (int rc = s->tp->note_io(*s, t, *io)) return rc;
         s->posted.store(t, std::memory_order_release);
         g_hot[s->id].posted.store(t, std::memory_order_release);
         s->mark(t, 0);

@@ -230,6 +230,10 @@ struct FFComp {
     void *a = nullptr, *b = nullptr, *c = nullptr;   // addresses (ffcomp)
     FFBuf *ba = nullptr, *bb = nullptr, *bc = nullptr;   // descriptors (ffcomp_b)
     int count = 0, dtype = 0, op = FFSUM;
+    // a user operator's function, captured when the comp is made: the reference copies the
+    // operator descriptor into the op (ffop_gcomp.c:9, ffop_gcomp_operator_get), so deleting
+    // or re-creating the handle afterwards changes nothing for this comp
+    ffoperator_fun_t fun = nullptr;
     bool device = false;
     hipEvent_t ev = nullptr;
     bool posted = false;
@@ -249,7 +253,8 @@ ffoperator_fun_t custom_fun(int op) {
 }
 
 int comp_make(FFComp *o, ffop_h *out) {
-    const bool custom = custom_fun(o->op) != nullptr;
+    o->fun = custom_fun(o->op);
+    const bool custom = o->fun != nullptr;
     ESGD_ARG(o->op == FFSUM || o->op == FFIDENTITY || custom,
              "ffcomp: operator %d -- FFSUM, FFIDENTITY or a handle from ffcomp_operator_create", o->op);
     ESGD_ARG(!custom || !o->device,
@@ -317,7 +322,7 @@ int ffop_post(ffop_h h) {
     int64_t n = o->ba ? int64_t(o->ba->count) : int64_t(o->count);
     if (o->bb) n = std::min<int64_t>(n, o->bb->count);
     if (o->bc) n = std::min<int64_t>(n, o->bc->count);
-    if (const ffoperator_fun_t fun = custom_fun(o->op)) {
+    if (const ffoperator_fun_t fun = o->fun) {
         // the user's host function over the host buffers, now (ffop_gcomp.c:52-55): the op
         // is complete when the post returns, and the function's status is the post's
         const int rc = fun(a, b, c, uint32_t(std::max<int64_t>(n, 0)), o->dtype);
@@ -327,6 +332,8 @@ int ffop_post(ffop_h h) {
         return FFSUCCESS;
     }
     o->host_done = false;
+    // never a user operator's handle through the sum (comp_make admitted only these two)
+    ESGD_ARG(o->op == FFSUM || o->op == FFIDENTITY, "ffop_post: operator %d is not FFSUM / FFIDENTITY", o->op);
     if (!o->ev) ESGD_HIP(hipEventCreateWithFlags(&o->ev, hipEventDisableTiming));
     hipStream_t s = default_stream();
     if (n > 0) {

@@ -891,12 +891,15 @@ def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, dela
             fill()
         comm.barrier()
         tb = time.perf_counter()
-        if rank == late and d > 0:   # the late gradient, then a spin to the deadline (time.sleep
-            fill()                   # cannot do tens of us)
-            while time.perf_counter() - tb < d:
+        tf = tb
+        if rank == late and d > 0:   # a spin to the deadline (time.sleep cannot do tens of us),
+            while time.perf_counter() - tb < d:   # then the late gradient is written
                 pass
+            tf = time.perf_counter()
+            fill()
         t0 = time.perf_counter()
-        achieved.append(t0 - tb)   # barrier -> post, as this rank saw it
+        achieved.append(t0 - tb)   # barrier -> post, as this rank saw it (the write included)
+        fills.append(t0 - tf)
         s.post()
         s.wait()
         el = time.perf_counter() - t0
@@ -912,6 +915,7 @@ def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, dela
 
     slices = []                            # per round: (min, max, crc32) of head + tail
     achieved = []                          # per round: barrier -> post on this rank (s)
+    fills = []                             # ... of which the late gradient's write
     warm = [one(0)[0] for _ in range(3)]   # rounds 1..3: everyone on time
     tt = torch.tensor([statistics.median(warm)], dtype=torch.float64)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -922,7 +926,8 @@ def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, dela
         _, c, u = one(d)
         res.append((t, c, u))
     out = {"rounds": res, "log": s.log(), "T_s": T, "delay_requested_s": d,
-           "delay_achieved_s": statistics.median(achieved[3:]), "slices": slices[3:]}
+           "delay_achieved_s": statistics.median(achieved[3:]), "fill_s": statistics.median(fills[3:]),
+           "slices": slices[3:]}
     comm.barrier()
     s.delete()
     comm.finalize()

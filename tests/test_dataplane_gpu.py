@@ -345,12 +345,12 @@ def test_majority_straggler_c4_20pct():
     outs = run("gpu_straggler", world, kind=MAJORITY, count=25559081, rounds=8, delay_frac=0.2, timeout=420)
     acts = ffref.activators(6545343, world, 64)
     for r, o in enumerate(outs):
-        # the straggler's ACHIEVED delay (its gradient written, then a spin to the deadline;
-        # measured barrier -> post) is the 0.2 T asked for, within 10 % or 100 us; the on-time
-        # ranks post at once
+        # the straggler's ACHIEVED delay (a spin to the deadline, then its late gradient
+        # written; measured barrier -> post) is the 0.2 T asked for plus that write, within
+        # 10 % or 100 us; the on-time ranks post at once
         want = 0.2 * o["T_s"]
         if r == world - 1:
-            assert want <= o["delay_achieved_s"] <= want + max(0.1 * want, 100e-6), o
+            assert want <= o["delay_achieved_s"] <= want + o["fill_s"] + max(0.1 * want, 100e-6), o
         else:
             assert o["delay_achieved_s"] < want, o
         for (t, c, uniform), (lo, hi, crc) in zip(o["rounds"], o["slices"]):

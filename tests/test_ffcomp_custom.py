@@ -102,3 +102,35 @@ def test_user_operator_handles_status_and_refusals():
     assert lib.ffcomp_operator_create(refuses, 0, C.byref(h3)) == FFSUCCESS and h3.value == h2.value
     lib.ffcomp_operator_delete(h3.value)
     lib.ffcomp_operator_delete(h1.value)
+
+
+@OPFUN
+def times_two(a, b, c, count, dtype):
+    ic = np.ctypeslib.as_array(C.cast(c, C.POINTER(C.c_int32)), (count,)) if count else np.zeros(0, np.int32)
+    ia = np.ctypeslib.as_array(C.cast(a, C.POINTER(C.c_int32)), (count,)) if count else np.zeros(0, np.int32)
+    ic[:] = ia * 2
+    return FFSUCCESS
+
+
+def test_comp_keeps_its_operator_after_the_handle_is_deleted_and_reused():
+    # the reference copies the operator into the op when the comp is made
+    # (ffop_gcomp.c:9, ffop_gcomp_operator_get).  Deleting the handle afterwards -- and a new
+    # ffcomp_operator_create taking the same slot -- must not change what the comp runs, nor
+    # send it down the FFSUM path.
+    lib = _lib()
+    h = C.c_int(-1)
+    assert lib.ffcomp_operator_create(plus_one, 1, C.byref(h)) == FFSUCCESS
+    n = 64
+    a = np.arange(n, dtype=np.int32)
+    b = np.full(n, 10, np.int32)
+    c = np.zeros(n, np.int32)
+    op = C.c_void_p()
+    assert lib.ffcomp(a.ctypes.data, b.ctypes.data, n, FFINT32, h.value, 0, c.ctypes.data, C.byref(op)) == FFSUCCESS
+    assert lib.ffcomp_operator_delete(h.value) == FFSUCCESS
+    h2 = C.c_int(-1)
+    assert lib.ffcomp_operator_create(times_two, 1, C.byref(h2)) == FFSUCCESS
+    assert h2.value == h.value                       # the slot was reused
+    assert lib.ffop_post(op) == FFSUCCESS and lib.ffop_wait(op) == FFSUCCESS
+    assert np.array_equal(c, ffref.comp_custom_plus_one(a, b, n))   # still a + b + 1
+    lib.ffop_free(op)
+    lib.ffcomp_operator_delete(h2.value)
