@@ -128,8 +128,9 @@ def main():
     model = resnet50().to(dev)
     params = [p for p in model.parameters() if p.requires_grad]
     sgd = torch.optim.SGD(params, lr=0.1, momentum=0.9)
-    opt = sgd if a.mode == "ddp" else EagerSGDOptimizer(sgd, world, mode=a.mode, fuse=a.fuse, wire=a.wire,
-                                                        overlap=a.overlap, bucket_mb=a.bucket_mb)
+    # the fused buckets' size (fuse + overlap) is a class attribute of the optimizer
+    cls = type("Opt", (EagerSGDOptimizer,), {"bucket_mb": a.bucket_mb})
+    opt = sgd if a.mode == "ddp" else cls(sgd, world, mode=a.mode, fuse=a.fuse, wire=a.wire, overlap=a.overlap)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     x = torch.randn(a.batch, 3, a.image, a.image, device=dev, generator=g)
     y = torch.randint(0, 1001, (a.batch,), device=dev, generator=g)
