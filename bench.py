@@ -1053,7 +1053,7 @@ def C_u64(v):
 
 def _optimizer_breakdown(opt, steps, stream=None):
     """Median host time per step inside apply_gradients (rank 0's view, untimed steps):
-    the wrapper's Python loop over the tensors, post_many, wait_many (or the blocking
+    the wrapper's Python loop over the tensors, post_many_io, wait_many (or the blocking
     per-tensor forward calls), the wrapped SGD step and the closing synchronize."""
     import contextlib
     import statistics
@@ -1073,12 +1073,11 @@ def _optimizer_breakdown(opt, steps, stream=None):
                 acc[key] = acc.get(key, 0.0) + time.perf_counter() - t0
         return g
 
-    saved = (Op.post_many, Op.wait_many, Op.forward_cuda_div, opt.optimizer.step, Op.post_many_io)
-    Op.post_many = staticmethod(timed("post_many", saved[0]))
-    Op.wait_many = staticmethod(timed("wait_many", saved[1]))
-    Op.forward_cuda_div = timed("forward_cuda_div", saved[2])
-    opt.optimizer.step = timed("sgd_step", saved[3])
-    Op.post_many_io = staticmethod(timed("post_many_io", saved[4]))
+    saved = (Op.wait_many, Op.forward_cuda_div, opt.optimizer.step, Op.post_many_io)
+    Op.wait_many = staticmethod(timed("wait_many", saved[0]))
+    Op.forward_cuda_div = timed("forward_cuda_div", saved[1])
+    opt.optimizer.step = timed("sgd_step", saved[2])
+    Op.post_many_io = staticmethod(timed("post_many_io", saved[3]))
     rows = []
     try:
         for _ in range(steps):
@@ -1095,11 +1094,12 @@ def _optimizer_breakdown(opt, steps, stream=None):
             row["synchronize"] = t2 - t1
             rows.append(row)
     finally:
-        Op.post_many, Op.wait_many = staticmethod(saved[0]), staticmethod(saved[1])
-        Op.forward_cuda_div = saved[2]
-        Op.post_many_io = staticmethod(saved[4])
+        Op.wait_many = staticmethod(saved[0])
+        Op.forward_cuda_div = saved[1]
+        Op.post_many_io = staticmethod(saved[3])
         del opt.optimizer.step   # the instance attribute; the class method shows again
-    return {k: round(statistics.median(r[k] for r in rows) * 1e6, 1) for k in rows[0]}
+    keys = sorted({k for r in rows for k in r})
+    return {k: round(statistics.median(r.get(k, 0.0) for r in rows) * 1e6, 1) for k in keys}
 
 
 def c3_over_rccl(comm, dev, rank, world, count, steps=20):

@@ -715,14 +715,16 @@ __device__ __forceinline__ void publish_flags_drained(const PairFlags &f, uint32
 // others wait for it and run a system-scope acquire (buffer_inv sc0 sc1).  The dispatch's
 // own acquire scope is not relied on for this.  A failed pairing still raises the gate
 // (the error word fails the round), so no workgroup is left waiting.
-// Failure contract: `errs` = every rank's error word (this rank's is errs[rank]); a pairing
-// after the round's first (`after_fail`: reduced, done) publishes nothing when this rank's
-// error word already holds the round -- its shard was folded from stale peer buckets, and a
-// late peer must not take it for the round's (What's weak 1).
+// Failure contract: `errs` = every rank's error word (this rank's is errs[rank]); a failed
+// pairing also records the round in `failw`, a device word of the schedule, and a pairing
+// after the round's first (`after_fail`: reduced, done) publishes nothing when failw holds
+// the round -- this rank's shard was folded from stale peer buckets, and a late peer must
+// not take it for the round's (What's weak 1).  (failw, not the host error
+// word: one HBM load instead of a PCIe round trip on every later pairing.)
 __global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world, int rank,
                                                    uint32_t value, long long timeout,
-                                                   uint32_t *errs, uint32_t errval, int after_fail, uint64_t *ts,
-                                                   uint32_t *gate, uint32_t *fin) {
+                                                   uint32_t *errs, uint32_t errval, uint32_t *failw, int after_fail,
+                                                   uint64_t *ts, uint32_t *gate, uint32_t *fin) {
     const bool lead = threadIdx.x == 0;
     if (blockIdx.x != 0) {   // cache maintenance only
         if (lead) {
@@ -738,7 +740,7 @@ __global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world, int r
     uint32_t *err = errs + rank;
     __shared__ int failed;
     if (lead) {
-        failed = after_fail && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == errval;
+        failed = after_fail && __hip_atomic_load(failw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == errval;
         if (ts) ts[0] = uint64_t(wall_clock64());
         if (!failed) publish_flags(f, value);
     }
@@ -750,7 +752,10 @@ __global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world, int r
     const long long t0 = wall_clock64();
     const bool ok = wave_wait_all(f.mine, world, value, t0, timeout, errs, errval);
     if (!lead) return;
-    if (!ok) __hip_atomic_store(err, errval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!ok) {
+        __hip_atomic_store(failw, errval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(err, errval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     if (gate) __hip_atomic_store(gate, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ok && ts) __hip_atomic_store(&ts[1], uint64_t(wall_clock64()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -765,13 +770,13 @@ __global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world, int r
 // errval: what a timed-out wait records in *err (the round, also when `value` numbers
 // a chunk of it)
 int round_sync(const PairFlags &f, int world, int rank, uint32_t value, long long timeout_ticks,
-               uint32_t *errs, uint32_t errval, bool after_fail, uint64_t *ts, uint32_t *gate, uint32_t *fin,
-               hipStream_t s) {
-    ESGD_ARG(f.mine && errs && world >= 1 && world <= kPairMax && rank >= 0 && rank < world && f.ndst >= 1 &&
-                 f.ndst <= kPairMax,
+               uint32_t *errs, uint32_t errval, uint32_t *failw, bool after_fail, uint64_t *ts, uint32_t *gate,
+               uint32_t *fin, hipStream_t s) {
+    ESGD_ARG(f.mine && errs && failw && world >= 1 && world <= kPairMax && rank >= 0 && rank < world &&
+                 f.ndst >= 1 && f.ndst <= kPairMax,
              "round_sync: bad arguments");
     hipLaunchKernelGGL(k_round_sync, dim3(gate ? unsigned(cu_count()) : 1u), dim3(64), 0, s, f, world, rank,
-                       value, timeout_ticks, errs, errval, after_fail ? 1 : 0, ts, gate, fin);
+                       value, timeout_ticks, errs, errval, failw, after_fail ? 1 : 0, ts, gate, fin);
     ESGD_HIP(hipGetLastError());
     return ESGD_SUCCESS;
 }

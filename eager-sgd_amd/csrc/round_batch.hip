@@ -9,7 +9,8 @@
 //     and leaves -- a peer's launch that could not be dispatched beside our spinning
 //     workers is what opens those gates -- and the agent block does deferred tiles (any
 //     whose gate is open, not the oldest: r06a) and, once any were deferred, further open
-//     tiles of the list itself.  The agent block leaves only when every tile is done.
+//     tiles of the list itself.  Once every gate is open the agent block leaves at once
+//     unless a tile was deferred; then it leaves when every tile is done.
 //   * Static assignment (tile g on worker 1 + g % workers, round 4) needed every worker
 //     resident at once and is gone.
 //
@@ -132,10 +133,21 @@ __device__ __forceinline__ bool gate_open(const BatchArgs &a, const TileAt &at) 
 // deferred tiles, and it takes ANY open one: a phase-2 tile deferred ahead of the phase-1
 // tiles whose `reduced` opens its gate must not block them (a first version that took
 // only the oldest deadlocked 8 ranks sharing a GPU, r06a).
-constexpr uint32_t kNoTile = 0xffffffffu, kTaken = 0xffffffffu;
-__device__ __forceinline__ void defer_tile(uint32_t *S, uint32_t g) {
-    const uint32_t i = __hip_atomic_fetch_add(S + kSlotTail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(S + kSlotRing + i, g + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// The tail word also records the agent block's leaving (kAgentGone): once every gate of the
+// launch is open and nothing was deferred, the agent leaves at once (the stream's next launch
+// waits for every workgroup) -- by a CAS of the tail from 0, so a worker either deferred
+// before (the agent stays) or sees the bit and does not defer (every gate is open by then).
+constexpr uint32_t kNoTile = 0xffffffffu, kTaken = 0xffffffffu, kAgentGone = 0x80000000u;
+__device__ __forceinline__ bool defer_tile(uint32_t *S, uint32_t g) {
+    uint32_t t = load_agent(S + kSlotTail);
+    for (;;) {
+        if (t & kAgentGone) return false;
+        if (__hip_atomic_compare_exchange_strong(S + kSlotTail, &t, t + 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            break;
+    }
+    __hip_atomic_store(S + kSlotRing + t, g + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
 }
 
 template <int K>
@@ -199,7 +211,7 @@ __device__ bool agent_sweep(const BatchArgs &a, AgentLane<K> &L, long long t0) {
         } else if (wall_clock64() - t0 > a.timeout) {
             fail_entry(d, v);
             L.st = 2;
-        } else if ((++L.sweeps & 15u) == 0) {
+        } else if ((++L.sweeps & 31u) == 0) {
             // a peer that failed this round publishes nothing more for it: fail now rather
             // than at the timeout (its error word sits beside ours in the node segment)
             const uint32_t *errs = d->err - d->rank;
@@ -440,17 +452,29 @@ __device__ void agent_block(const BatchArgs &a, uint32_t *S, uint32_t T0, uint32
     bool settled = false;
     if (threadIdx.x < 64) agent_init<K>(a, L);
     uint32_t hint = 0;
-    for (;;) {
+    for (unsigned it = 0;; ++it) {
         if (threadIdx.x < 64 && !settled) settled = agent_sweep<K>(a, L, t0);
         if (threadIdx.x == 0) {
-            const uint32_t tail = load_agent(S + kSlotTail);
-            s_tail = tail < kBatchWorkersMax ? tail : kBatchWorkersMax;
-            s_pick = kNoTile;
             // 2 leave, 1 help: some worker gave its slots back, or (ranks sharing the GPU)
             // the launch has run for a yield period -- its workers may never be dispatched
-            // beside the peers' launches; 0 idle
-            s_help = load_agent(S + kSlotDone) >= T ? 2
-                   : (tail > 0 || (a.yield && wall_clock64() - t0 > a.yield)) ? 1 : 0;
+            // beside the peers' launches; 0 idle.  Every gate is open once settled: the
+            // agent then leaves, unless a deferred tile may still need it.
+            int help = 0;
+            uint32_t tail = 0;
+            if (a.yield && (it & 7u) == 0) tail = load_agent(S + kSlotTail);
+            if (settled) {
+                uint32_t zero = 0;
+                if (load_agent(S + kSlotDone) >= T ||
+                    __hip_atomic_compare_exchange_strong(S + kSlotTail, &zero, kAgentGone, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    help = 2;
+                else
+                    tail = zero;   // the tail the CAS found (> 0: deferred tiles)
+            }
+            if (!help && (tail > 0 || (a.yield && wall_clock64() - t0 > a.yield))) help = 1;
+            s_tail = tail < kBatchWorkersMax ? tail : kBatchWorkersMax;
+            s_pick = kNoTile;
+            s_help = help;
         }
         __syncthreads();
         const int help = s_help;
@@ -537,8 +561,7 @@ __global__ __launch_bounds__(256) void k_round_batch(BatchArgs a) {
                 int gave = 0;
                 while (!reached(load_agent(gate), v)) {
                     const long long now = wall_clock64();
-                    if (a.yield && now - w0 > a.yield) {   // give the wave slots back
-                        defer_tile(S, g);
+                    if (a.yield && now - w0 > a.yield && defer_tile(S, g)) {   // give the wave slots back
                         gave = 1;
                         break;
                     }

@@ -1,13 +1,12 @@
 # One GPU session of bench work (round 3): the N = 1 line (PMC + kernel-trace passes), the
 # N = 2 line started the way a bare `bench.py --gpus 2` starts it (self-launched ranks,
-# sharing the box's one GPU: a rehearsal), rocprofv3 kernel statistics of the N = 1 bench,
-# and the IPC re-export bisection.  Each GPU step has its own time limit; the first
+# sharing the box's one GPU: a rehearsal) and rocprofv3 kernel statistics of the N = 1 bench.  Each GPU step has its own time limit; the first
 # failure ends the session.
-#   bash tools/bench_round.sh <tag> [steps...]   steps: smoke n1 n2 n4 n2c4 n4c4 prof profopt bisect sweep (default: n1 n2 prof bisect)
+#   bash tools/bench_round.sh <tag> [steps...]   steps: smoke n1 n2 n4 n2c4 n4c4 prof profopt sweep (default: n1 n2 prof)
 set -e
 export ESGD_TIMEOUT_S=60
 O=gpurun_out/${1:-bench_round}; shift || true
-STEPS=${*:-n1 n2 prof bisect}
+STEPS=${*:-n1 n2 prof}
 mkdir -p $O
 R=$PWD
 for s in $STEPS; do
@@ -26,7 +25,6 @@ for s in $STEPS; do
   profopt) (cd /tmp && export TMPDIR=/tmp && ESGD_BENCH_LEGS=optimizer_resnet50_161 ESGD_BENCH_RCCL=0 \
           timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/profopt -o run_%pid% --output-format csv \
           -- python $R/bench.py --gpus 2 --steps 20 --warmup 5 > $R/$O/bench_profopt_n2.json 2>&1) ;;
-  bisect) timeout -k 10 500 python -u tools/ipc_bisect.py > $O/ipc_bisect.txt 2>&1 ;;
   sweep) test -f tools/bin/libesgd_sweeps.so   # built here by `make sweeps` (build() does it)
       for m in 64 256 1024; do
         timeout -k 10 240 python tools/sweep_reduce.py --mib $m --grids 0 --unrolls 4 --nts 1 \
