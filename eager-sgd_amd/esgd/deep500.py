@@ -219,3 +219,86 @@ class AllreduceOp:
 
 def custom_op(shape: Sequence[int]) -> AllreduceOp:
     return AllreduceOp(shape)
+
+
+# ---- the op as a registered PyTorch operator -------------------------------------------
+# The reference's PyTorch bridge compiles forward_op / backward_op around the op's handle
+# and wraps them in a torch.autograd.Function inside an nn.Module
+# (D/frameworks/pytorch/custom_operators/pytorch.tmpl.cpp:30-56, pytorch.py:71-114,
+# CustomPytorchCPPModule).  Here the same op is a torch.library operator, esgd::allreducef,
+# so it can sit inside a traced (torch.fx) or exported graph: a fake (meta) implementation
+# gives its output's shape without running a round, and its backward is the reference op's
+# -- allreducef::backward writes nothing (opt_esgd_solo_imagenet_imbalance.py:321-326), so
+# the inputs' gradients are the zeros the bridge's buffers start as.
+
+_LIVE = {}   # handle -> AllreduceOp: the registered operator names ops by handle
+
+
+def _register_torch_op():
+    import torch
+
+    # the schema spelled out: this module's annotations are strings (postponed evaluation)
+    @torch.library.custom_op("esgd::allreducef", mutates_args=(),
+                             schema="(Tensor grad, Tensor last, int handle, float divisor) -> Tensor")
+    def allreducef(grad, last, handle, divisor):
+        op = _LIVE.get(handle)
+        if op is None:
+            raise RuntimeError(f"esgd::allreducef: no live op with handle {handle:#x} (AllreduceModule holds one)")
+        g = grad.detach().to(torch.float32).contiguous()
+        if g.is_cuda:   # the device path, ordered on the caller's current stream
+            out = torch.empty_like(g)
+            op.forward_cuda_div(g, out, divisor, torch.cuda.current_stream(g.device).cuda_stream or None)
+            return out
+        x = g.numpy() if divisor == 1.0 else (g / divisor).numpy()
+        return torch.from_numpy(op.forward(x)).view_as(g)   # the reference's host contract
+
+    @allreducef.register_fake
+    def _(grad, last, handle, divisor):
+        return torch.empty_like(grad, dtype=torch.float32)
+
+    def setup_context(ctx, inputs, output):
+        ctx.shapes = (inputs[0], inputs[1])
+
+    def backward(ctx, g_out):
+        grad, last = ctx.shapes
+        return torch.zeros_like(grad), torch.zeros_like(last), None, None
+
+    allreducef.register_autograd(backward, setup_context=setup_context)
+    return allreducef
+
+
+_TORCH_OP = None
+
+
+def torch_op():
+    """torch.ops.esgd.allreducef(grad, last, handle, divisor) (registered on first use)."""
+    global _TORCH_OP
+    if _TORCH_OP is None:
+        _TORCH_OP = _register_torch_op()
+    return _TORCH_OP
+
+
+def _module_base():
+    import torch
+    return torch.nn.Module
+
+
+class AllreduceModule(_module_base()):
+    """CustomPytorchCPPModule for the eager-SGD op: forward(grad, last) returns grad's
+    partial allreduce (divided by `divisor` first: the wrapper's grad / comm_size, :40) through
+    the registered operator esgd::allreducef -- the same round as AllreduceOp.forward_cuda_div
+    (device tensors) or AllreduceOp.forward (host tensors)."""
+
+    def __init__(self, shape: Sequence[int], divisor: float = 1.0):
+        super().__init__()
+        self.op = AllreduceOp(shape)
+        self.divisor = float(divisor)
+        _LIVE[self.op.handle] = self.op
+        torch_op()
+
+    def is_cuda_supported(self) -> bool:
+        return self.op.supports_cuda()
+
+    def forward(self, grad, last=None):
+        import torch
+        return torch.ops.esgd.allreducef(grad, grad if last is None else last, self.op.handle, self.divisor)

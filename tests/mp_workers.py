@@ -682,6 +682,52 @@ def op_group(rank, world, steps=3, sizes=(1, 17, 1000, 4099, 262147, (2 << 20) +
     return {"ok": ok, "errs": errs}
 
 
+def op_torch_registered(rank, world, shapes=((1000,), (64, 33), (4099,))):
+    """esgd::allreducef (the registered PyTorch operator) inside a torch.fx-traced module on
+    the GPU, allreduce mode: every output is the oracle tree of x_r / P over ranks, bit for
+    bit; the traced graph holds one op node per tensor; backward gives the reference op's zero
+    input gradients (allreducef::backward writes nothing)."""
+    import numpy as np
+    import torch
+    import torch.fx
+
+    from esgd import deep500
+    from oracle import ffref
+    comm = _comm()
+    dev = torch.device("cuda", local_device())
+    torch.cuda.set_device(dev)
+    deep500.configure("allreduce", 32, 6545343)
+    mods = [deep500.AllreduceModule(sh, divisor=float(world)) for sh in shapes]
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.ars = torch.nn.ModuleList(mods)
+
+        def forward(self, a, b, c):   # fixed arity: torch.fx traces no *args
+            return self.ars[0](a), self.ars[1](b), self.ars[2](c)
+
+    gm = torch.fx.symbolic_trace(Net())
+    nodes = sum(1 for n in gm.graph.nodes if n.op == "call_function" and n.target is torch.ops.esgd.allreducef)
+    ok = []
+    for t in range(2):
+        xs = [[ffref.fill_uniform(0x70C + 7 * t + i, r, int(np.prod(sh))).reshape(sh) for r in range(world)]
+              for i, sh in enumerate(shapes)]
+        ins = [torch.from_numpy(x[rank]).to(dev).requires_grad_(True) for x in xs]
+        comm.barrier()
+        outs = gm(*ins)
+        sum(o.sum() for o in outs).backward()
+        torch.cuda.synchronize()
+        for x, o, i in zip(xs, outs, ins):
+            want = ffref.tree_sum([np.float32(xr.ravel()) / np.float32(world) for xr in x])
+            got = o.detach().cpu().numpy().ravel()
+            ok.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
+            ok.append(bool(torch.count_nonzero(i.grad).item() == 0))
+    comm.barrier()
+    comm.finalize()
+    return {"ok": ok, "nodes": nodes}
+
+
 def cp_ordered(rank, world, nsched=3, rounds=6, seed=7):
     """Ordered (rccl-style) issue: several schedules posted with per-rank random jitter;
     every rank must issue the rounds in the same global order (ticket ring)."""

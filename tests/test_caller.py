@@ -39,3 +39,33 @@ def test_overlap_refuses_a_second_backward_before_the_step():
     with pytest.raises(RuntimeError, match="gradient accumulation"):
         model(x).sum().backward()
     opt.detach()
+
+
+def test_registered_torch_op_sits_in_traced_graphs():
+    # the reference's PyTorch bridge wraps the op in an autograd Function / nn.Module
+    # (pytorch.tmpl.cpp:30-56, pytorch.py:71-114); here it is the torch.library operator
+    # esgd::allreducef: torch.fx and torch.export keep it as one node, and its fake
+    # implementation gives the output's shape without running a round (no device needed)
+    import torch
+    import torch.fx
+    from torch._subclasses.fake_tensor import FakeTensorMode
+
+    ar = deep500.AllreduceModule((4, 3), divisor=2.0)
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.ar = ar
+
+        def forward(self, x):
+            return self.ar(x * 2.0) + 1.0
+
+    gm = torch.fx.symbolic_trace(Net())
+    targets = [n.target for n in gm.graph.nodes if n.op == "call_function"]
+    assert torch.ops.esgd.allreducef in targets
+    ep = torch.export.export(Net(), (torch.randn(4, 3),))
+    assert any(getattr(n.target, "name", lambda: "")() == "esgd::allreducef" for n in ep.graph.nodes
+               if n.op == "call_function")
+    with FakeTensorMode():
+        y = torch.ops.esgd.allreducef(torch.empty(4, 3), torch.empty(4, 3), ar.op.handle, 2.0)
+    assert tuple(y.shape) == (4, 3) and y.dtype == torch.float32

@@ -124,3 +124,13 @@ def test_group_post_wait_same_bits_as_single_ops(world):
         assert all(o["ok"]) and o["ok"], o["ok"]
         assert o["errs"]["post_many_over_posted"] == -2, o["errs"]   # ESGD_INVALID_ARG
         assert o["errs"]["drained_op0"], o["errs"]
+
+
+def test_registered_torch_op_in_a_traced_module():
+    # esgd::allreducef (torch.library) inside a torch.fx GraphModule, 2 ranks on the GPU:
+    # the oracle's bits of grad_r / P, one graph node per tensor, zero input gradients
+    # (the reference op's empty backward, opt_esgd_solo_imagenet_imbalance.py:321-326)
+    outs = run("op_torch_registered", 2)
+    for o in outs:
+        assert o["nodes"] == 3, o
+        assert all(o["ok"]) and len(o["ok"]) == 12, o
