@@ -125,21 +125,55 @@ def _cpu_model():
     return None
 
 
-def _baseline_cpus(n: int):
-    """n cores for the CPU baseline's threads, from this process's affinity set: the first
-    n in id order (on the boxes seen, ids 0..n-1 share a socket).  None when fewer exist."""
+def _baseline_cpus(P: int):
+    """2P cores for the CPU baseline's P simulated ranks: rank r's two threads on two
+    physical cores of L3 domain r mod G (each rank a CCD of its own where the host has them,
+    as `mpirun --map-by l3cache` places ranks), from this process's affinity set and the
+    kernel's cache / thread-sibling topology; the first 2P allowed ids when that is not
+    readable.  None when fewer than 2P are allowed."""
     try:
-        cpus = sorted(os.sched_getaffinity(0))
+        allowed = sorted(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         return None
-    return cpus[:n] if len(cpus) >= n else None
+    if len(allowed) < 2 * P:
+        return None
+
+    def read(path):
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except OSError:
+            return None
+
+    groups, seen_core = {}, set()
+    for c in allowed:
+        l3 = read(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list")
+        sib = read(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list")
+        if l3 is None:
+            return allowed[:2 * P]
+        if sib is not None and sib in seen_core:   # an SMT sibling of a core already listed
+            continue
+        seen_core.add(sib)
+        groups.setdefault(l3, []).append(c)
+    doms = [g for g in sorted(groups.values(), key=lambda g: g[0]) if len(g) >= 2]
+    if not doms:
+        return allowed[:2 * P]
+    out, used = [], {id(g): 0 for g in doms}
+    for r in range(P):
+        g = doms[r % len(doms)]
+        k = used[id(g)]
+        if k + 2 > len(g):
+            return allowed[:2 * P]
+        out += g[k:k + 2]
+        used[id(g)] = k + 2
+    return out
 
 
 def _pinned_samples(P: int, count: int, reps: int, samples: int = 3):
     """`samples` runs of the pinned C1-shaped harness (each a median step over `reps`):
     (median, [each], cores, every result correct)."""
     from oracle import ffref
-    cpus = _baseline_cpus(2 * P)
+    cpus = _baseline_cpus(P)
     ts, good = [], True
     for _ in range(samples):
         t, ok = ffref.time_c1(P, count, reps, cpus)
@@ -153,12 +187,13 @@ def cpu_baseline(k: int, count: int):
     the core budget SURVEY.md §8(d) gives the reference: 2 cores per rank -- each simulated
     rank a main thread (the wrapper's copy-in, post, spin-wait, copy-out, zeroing of the
     send bucket) and a progress thread (the move + recursive doubling with VSUM; ff.c:72's
-    pthread), 2k threads in all, each pinned to a core of its own (round 6: unpinned, the
-    same CPU model gave 6.35 and 10.59 GB/s on two boxes).  The value is the median of 3
+    pthread), 2k threads in all, each pinned to a physical core of its own, rank r's two on
+    L3 domain r (round 6: unpinned, the same CPU model gave 6.35 and 10.59 GB/s on two boxes;
+    pinned to cores 0-15 -- two CCDs -- 6.11 and 9.03).  The value is the median of 3
     samples; the spread is beside it.  Also reported: the recursive doubling alone, one
     pthread per rank (the round-4 figure, unpinned)."""
     from oracle import ffref
-    t1, _ = ffref.time_c1(k, count, 2, _baseline_cpus(2 * k))   # warm + size the sample
+    t1, _ = ffref.time_c1(k, count, 2, _baseline_cpus(k))   # warm + size the sample
     reps = max(3, min(250, int(4.0 / max(t1, 1e-3))))           # ~4 s of CPU work per sample
     t, ts, cpus, ok = _pinned_samples(k, count, reps)
     t_rd1 = ffref.time_allreduce(k, count, k, max(1, reps // 2))
@@ -166,7 +201,8 @@ def cpu_baseline(k: int, count: int):
     return {"value": round(k * count * 4 / t / 1e9, 3), "unit": "GB/s", "cores": 2 * k, "kind": "port",
             "sample": f"full workload: {k} ranks x {count * 4 / MiB:.0f} MiB fp32, each a main thread (copy-in, "
                       f"post, wait, copy-out, zero) + a progress thread (move + recursive doubling, VSUM) = "
-                      f"{2 * k} threads pinned one per core (oracle/ffref.c ffref_time_c1_pinned), median of 3 "
+                      f"{2 * k} threads pinned one per physical core, rank r's on L3 domain r (oracle/ffref.c "
+                      f"ffref_time_c1_pinned), median of 3 "
                       f"samples, each the median step of {reps}: {t * 1e3:.1f} ms",
             "samples_GBs": [round(x, 3) for x in gbs],
             "spread": round((max(gbs) - min(gbs)) / statistics.median(gbs), 3),
@@ -182,10 +218,11 @@ def cpu_baseline_c1(P: int = 2, count: int = 262144):
     """BASELINE.json configs[0] (C1): P ranks reducing one 1 MiB fp32 bucket per step the
     way the wrapper drives fflib2 -- each rank a main thread (copy-in, post, spin-wait,
     copy-out, zero) and a progress thread (move + recursive doubling, ff.c:72), i.e. 2
-    cores per rank, each thread pinned to a core of its own; value = P x
+    cores per rank, each thread pinned to a physical core of its own, rank
+    r's two on L3 domain r; value = P x
     bucket bytes per step / step time, the median of 3 samples."""
     from oracle import ffref
-    t1, _ = ffref.time_c1(P, count, 20, _baseline_cpus(2 * P))
+    t1, _ = ffref.time_c1(P, count, 20, _baseline_cpus(P))
     reps = max(50, min(20000, int(4.0 / max(t1, 1e-5))))   # ~4 s of steps per sample
     t, ts, cpus, ok = _pinned_samples(P, count, reps)
     gbs = [P * count * 4 / x / 1e9 for x in ts]
@@ -1445,9 +1482,13 @@ def straggler_c4(comm, dev, rank, world, rounds=16, delay_fracs=(0.2, 2.0)):
             fill()
         comm.barrier()
         tb = time.perf_counter()
-        if late and delay:   # a spin to the deadline, then the late gradient is written
-            while time.perf_counter() - tb < delay:
-                pass
+        if late and delay:   # wait to the deadline (asleep but for the last 2 ms, then a spin:
+            while True:      # a spinning thread would starve this rank's progress thread),
+                left = tb + delay - time.perf_counter()   # then the late gradient is written
+                if left <= 0:
+                    break
+                if left > 2e-3:
+                    time.sleep(left - 2e-3)
             fill()
         t0 = time.perf_counter()
         achieved = t0 - tb

@@ -110,6 +110,18 @@ def run(fn_name: str, world: int, timeout: float = 240.0, **kw):
 
 # --------------------------------------------------------------------------- workers
 
+def wait_until(deadline: float):
+    """Until time.perf_counter() reaches `deadline`: asleep while more than 2 ms remain (a
+    spinning thread starves the rank's own progress thread on a box's few cores: r06k), then
+    a spin (time.sleep cannot do tens of microseconds)."""
+    while True:
+        left = deadline - time.perf_counter()
+        if left <= 0:
+            return
+        if left > 2e-3:
+            time.sleep(left - 2e-3)
+
+
 def set_test_knobs(**knobs):
     """The library's test hooks (ESGD_TEST, read once per process: set before the first
     schedule): e.g. set_test_knobs(fail_exports=2, shadow=1); None values are left out."""
@@ -938,9 +950,8 @@ def gpu_straggler(rank, world, kind, count, rounds, async_=3, seed=6545343, dela
         comm.barrier()
         tb = time.perf_counter()
         tf = tb
-        if rank == late and d > 0:   # a spin to the deadline (time.sleep cannot do tens of us),
-            while time.perf_counter() - tb < d:   # then the late gradient is written
-                pass
+        if rank == late and d > 0:   # wait to the deadline, then the late gradient is written
+            wait_until(tb + d)
             tf = time.perf_counter()
             fill()
         t0 = time.perf_counter()
