@@ -126,47 +126,28 @@ def _cpu_model():
 
 
 def _baseline_cpus(P: int):
-    """2P cores for the CPU baseline's P simulated ranks: rank r's two threads on two
-    physical cores of L3 domain r mod G (each rank a CCD of its own where the host has them,
-    as `mpirun --map-by l3cache` places ranks), from this process's affinity set and the
-    kernel's cache / thread-sibling topology; the first 2P allowed ids when that is not
-    readable.  None when fewer than 2P are allowed."""
+    """2P cores for the CPU baseline's P simulated ranks: the first 2P physical cores of this
+    process's affinity set in id order (one thread of each SMT pair; rank r on the (2r,
+    2r + 1)-th), so neighbouring ranks share an L3 as an MPI job's packed placement does.
+    (Spreading the ranks one L3 domain each -- `--map-by l3cache` -- was slower for both
+    baselines on the 9575F boxes: 4.2 against 6.1-9.0 GB/s, and C1 2.7 against 6.0-6.8, the
+    ranks' exchanges then crossing CCDs; r06l.)  None when fewer than 2P exist."""
     try:
         allowed = sorted(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         return None
-    if len(allowed) < 2 * P:
-        return None
-
-    def read(path):
-        try:
-            with open(path) as f:
-                return f.read().strip()
-        except OSError:
-            return None
-
-    groups, seen_core = {}, set()
+    cores, seen = [], set()
     for c in allowed:
-        l3 = read(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list")
-        sib = read(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list")
-        if l3 is None:
-            return allowed[:2 * P]
-        if sib is not None and sib in seen_core:   # an SMT sibling of a core already listed
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                sib = f.read().strip()
+        except OSError:
+            sib = str(c)
+        if sib in seen:   # an SMT sibling of a core already taken
             continue
-        seen_core.add(sib)
-        groups.setdefault(l3, []).append(c)
-    doms = [g for g in sorted(groups.values(), key=lambda g: g[0]) if len(g) >= 2]
-    if not doms:
-        return allowed[:2 * P]
-    out, used = [], {id(g): 0 for g in doms}
-    for r in range(P):
-        g = doms[r % len(doms)]
-        k = used[id(g)]
-        if k + 2 > len(g):
-            return allowed[:2 * P]
-        out += g[k:k + 2]
-        used[id(g)] = k + 2
-    return out
+        seen.add(sib)
+        cores.append(c)
+    return cores[:2 * P] if len(cores) >= 2 * P else None
 
 
 def _pinned_samples(P: int, count: int, reps: int, samples: int = 3):
@@ -187,9 +168,9 @@ def cpu_baseline(k: int, count: int):
     the core budget SURVEY.md §8(d) gives the reference: 2 cores per rank -- each simulated
     rank a main thread (the wrapper's copy-in, post, spin-wait, copy-out, zeroing of the
     send bucket) and a progress thread (the move + recursive doubling with VSUM; ff.c:72's
-    pthread), 2k threads in all, each pinned to a physical core of its own, rank r's two on
-    L3 domain r (round 6: unpinned, the same CPU model gave 6.35 and 10.59 GB/s on two boxes;
-    pinned to cores 0-15 -- two CCDs -- 6.11 and 9.03).  The value is the median of 3
+    pthread), 2k threads in all, each pinned to a physical core of its own (_baseline_cpus).
+    DRAM-bound on a shared host: within a box the 3 samples agree to 1-5 %, across boxes the
+    same placement gave 6.11 and 9.03 GB/s (r06d, r06k; unpinned in round 5: 6.35 and 10.59).  The value is the median of 3
     samples; the spread is beside it.  Also reported: the recursive doubling alone, one
     pthread per rank (the round-4 figure, unpinned)."""
     from oracle import ffref
@@ -201,8 +182,8 @@ def cpu_baseline(k: int, count: int):
     return {"value": round(k * count * 4 / t / 1e9, 3), "unit": "GB/s", "cores": 2 * k, "kind": "port",
             "sample": f"full workload: {k} ranks x {count * 4 / MiB:.0f} MiB fp32, each a main thread (copy-in, "
                       f"post, wait, copy-out, zero) + a progress thread (move + recursive doubling, VSUM) = "
-                      f"{2 * k} threads pinned one per physical core, rank r's on L3 domain r (oracle/ffref.c "
-                      f"ffref_time_c1_pinned), median of 3 "
+                      f"{2 * k} threads pinned one per physical core (oracle/ffref.c ffref_time_c1_pinned), "
+                      f"median of 3 "
                       f"samples, each the median step of {reps}: {t * 1e3:.1f} ms",
             "samples_GBs": [round(x, 3) for x in gbs],
             "spread": round((max(gbs) - min(gbs)) / statistics.median(gbs), 3),
@@ -218,8 +199,8 @@ def cpu_baseline_c1(P: int = 2, count: int = 262144):
     """BASELINE.json configs[0] (C1): P ranks reducing one 1 MiB fp32 bucket per step the
     way the wrapper drives fflib2 -- each rank a main thread (copy-in, post, spin-wait,
     copy-out, zero) and a progress thread (move + recursive doubling, ff.c:72), i.e. 2
-    cores per rank, each thread pinned to a physical core of its own, rank
-    r's two on L3 domain r; value = P x
+    cores per rank, each thread pinned to a physical core of its own
+    (_baseline_cpus; 6.03 and 6.80 GB/s on two boxes, r06d / r06k); value = P x
     bucket bytes per step / step time, the median of 3 samples."""
     from oracle import ffref
     t1, _ = ffref.time_c1(P, count, 20, _baseline_cpus(P))
