@@ -772,15 +772,15 @@ def test_batched_rounds_progress_beside_a_kernel_holding_the_gpu():
 @pytest.mark.skipif(not os.path.exists(SWEEPS_LIB), reason="tools/bin/libesgd_sweeps.so not built (make sweeps)")
 def test_late_peer_after_a_timeout_never_succeeds_with_a_stale_sum():
     # the failure contract: rank 1's GPU runs the round
-    # 4 s late, rank 0's GPU flag wait gives up at 2 s.  Rank 0 fails; rank 1 fails as well
+    # 3 s late, rank 0's GPU flag wait gives up at 1.5 s.  Rank 0 fails; rank 1 fails as well
     # or returns the oracle's sum -- for one-launch, batched and five-launch rounds of every
     # kind.  (Before round 6 rank 1 returned success with rank 0's shard folded from its
     # stale bucket.)
     cases = [(k, p) for p in ("batched", "one", "five") for k in ("allreduce", "solo", "majority")]
     old = os.environ.get("ESGD_TIMEOUT_S")
-    os.environ["ESGD_TIMEOUT_S"] = "2"
+    os.environ["ESGD_TIMEOUT_S"] = "1.5"
     try:
-        outs = run("gpu_late_peer_after_timeout", 2, cases=cases, timeout=140)
+        outs = run("gpu_late_peer_after_timeout", 2, cases=cases, delay_s=3.0, timeout=140)
     finally:
         if old is None:
             os.environ.pop("ESGD_TIMEOUT_S", None)
