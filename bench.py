@@ -990,12 +990,47 @@ def optimizer_resnet50_161(comm, rank, world, steps=8):
                     for k in vals:
                         comm.set_config(k, -1)
     _OPTS.extend(opts)   # their schedules stay alive until the end, like every leg's
+    out["grad_view_backward_us"] = _grad_view_backward_us(params, steps)
     out["tensors"] = len(lengths)
     out["steps"] = steps
     return out
 
 
 _OPTS = []
+
+
+def _grad_view_backward_us(params, steps):
+    """What gradients as views into the buckets (DDP's gradient_as_bucket_view; VERDICT r05
+    item 4) would add to backward, per step on this rank's GPU: with
+    p.grad a persistent view, zero_grad zeroes it (one foreach launch, S written) and
+    AccumulateGrad adds the fresh gradient into it (one launch per tensor, 2S read, S
+    written) -- where today's path takes the fresh gradient as p.grad and the round's I/O
+    moves it.  Median GPU time over `steps` (torch events on the current stream); set this
+    against caller_vs_data_plane's op-like minus in-place rounds, the most views could
+    remove from the step."""
+    import statistics
+
+    import torch
+    views = [p.grad for p in params]
+    fresh = [torch.empty_like(v).copy_(v) for v in views]
+    zero_us, acc_us = [], []
+    for _ in range(steps + 1):
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        torch._foreach_zero_(views)
+        e1.record()
+        for v, g in zip(views, fresh):
+            v.add_(g)
+        e2.record()
+        e2.synchronize()
+        zero_us.append(e0.elapsed_time(e1) * 1e3)
+        acc_us.append(e1.elapsed_time(e2) * 1e3)
+    zero_us, acc_us = zero_us[1:], acc_us[1:]     # the first pass warms the kernels
+    total_bytes = sum(v.numel() for v in views) * 4
+    return {"zero_grad": round(statistics.median(zero_us), 1),
+            "accumulate_161": round(statistics.median(acc_us), 1),
+            "total": round(statistics.median(z + a for z, a in zip(zero_us, acc_us)), 1),
+            "hbm_bytes": 4 * total_bytes}
 
 
 def _fused_breakdown(comm, opt, params, steps):
