@@ -15,7 +15,9 @@ OUTLIB    := $(PKG)/esgd/libesgd.so
 BUILD     := build/obj
 
 HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off \
-             -Iinclude -I$(CSRC) -Wall -Wno-unused-result -D__HIP_PLATFORM_AMD__
+             -Iinclude -I$(CSRC) -Wall -Wno-unused-result
+# host-only sources (-x c++) include hip_runtime.h, which asks the platform of a non-HIP
+# translation unit (hipcc sets it for .hip files itself)
 CXXFLAGS  := -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -I$(CSRC) \
              -I$(ROCM)/include -D__HIP_PLATFORM_AMD__ -Wall
 LDFLAGS   := -shared -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -lpthread -lrt \

@@ -1367,6 +1367,13 @@ static int batch_flush_locked() {
         if (!sp) rc = ESGD_ERROR;
         else if (hipEventRecord(*sp, cs) != hipSuccess) rc = hip_fail(hipGetLastError(), "hipEventRecord", __FILE__, __LINE__);
     }
+    if (rc) {
+        // a launch counted as failed may still have run, or may not have: either way the
+        // next one finds every slot at zero (behind it on the stream), however many fail in
+        // a row -- the zeroing by a launch that runs covers only the launches after it
+        const size_t slot_bytes = size_t(kLaunchSlots) * kSlotWords * sizeof(uint32_t);
+        if (hipMemsetAsync(g_slots, 0, slot_bytes, cs) != hipSuccess) (void)hipGetLastError();
+    }
     ++g_batch_seq;
     for (BatchEntry &b : g_pend) {
         b.st->batch_ev = sp;

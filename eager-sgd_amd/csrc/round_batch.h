@@ -84,8 +84,10 @@ struct BatchDesc {
 // descriptor table, launch n using slot n % kLaunchSlots.  Block 0 of every launch zeroes
 // every OTHER slot before any tile is taken, so the next launch on the round stream (which
 // starts only once this one has ended) finds its slot at zero whatever happened before --
-// a launch the host counted as failed but that ran, a launch that ended on a timeout
-// (a device counter the host had to mirror could drift for good).
+// a launch that ended on a timeout, a launch the host counted as failed but that ran
+// (after such a launch the host also zeroes every slot on the stream, so launches that never
+// ran cannot leave a stale slot either; ADVICE r05: a device counter the host had to mirror
+// could drift for good).
 constexpr uint32_t kLaunchSlots = 4;
 constexpr uint32_t kSlotWords = 1024;
 constexpr uint32_t kSlotQueue = 0;   // next tile of the list (fetch-add)
