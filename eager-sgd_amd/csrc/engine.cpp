@@ -733,7 +733,9 @@ static bool pump_tickets() {
             std::lock_guard<std::mutex> lk(target->mu);
             if (target->error) {
                 // a failed schedule still consumes its tickets (its peers fail the same
-                // round by timeout); later rounds of other schedules must not stall
+                // round: by their own timeout, or at once through this rank's error word --
+                // DESIGN.md §5, "Failure contract"); later rounds of other schedules must
+                // not stall
             } else if (target->stage != ST_WAIT_TICKET || target->cur != slot.round) {
                 break;
             } else {
