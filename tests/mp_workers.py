@@ -1918,13 +1918,13 @@ def gpu_residency(rank, world, hog_ms=6000, free_cus=2, rounds=4, counts=(1 << 2
 
 
 def gpu_late_peer_after_timeout(rank, world, cases, delay_s=4.0):
-    """The failure contract: rank 1's GPU runs the round
-    `delay_s` late -- its post names a producer stream on which a 1-workgroup k_occupy
+    """The failure contract: the last rank's GPU runs the
+    round `delay_s` late -- its post names a producer stream on which a 1-workgroup k_occupy
     (tools/bin/libesgd_sweeps.so) holds it, as a backward pass still writing the gradient
-    would -- so rank 0's GPU flag wait times out (ESGD_TIMEOUT_S, set by the caller to 2 s)
-    first.  Rank 0 must fail.  Rank 1 must fail too, or return the oracle's sum of the data
-    that really arrived -- never success with a sum built from rank 0's shard, which rank 0
-    folded from rank 1's STALE bucket (the previous round's result).  Each case (kind, path)
+    would -- so the other ranks' GPU flag waits time out (ESGD_TIMEOUT_S, set by the caller)
+    first.  They must fail.  The late rank must fail too, or return the oracle's sum of the
+    data that really arrived -- never success with a sum built from its peers' shards, which
+    they folded from its STALE bucket (the previous round's result).  Each case (kind, path)
     runs one good round (data A), then the late round (data B).  int32 inputs, exact."""
     import ctypes as C
 
@@ -1936,7 +1936,8 @@ def gpu_late_peer_after_timeout(rank, world, cases, delay_s=4.0):
     comm = _comm()
     sw = C.CDLL(os.path.join(ROOT, "tools", "bin", "libesgd_sweeps.so"))
     sw.esgd_sweep_occupy.restype, sw.esgd_sweep_occupy.argtypes = C.c_int, [C.c_int, C.c_uint64, C.c_void_p]
-    side = dev.Stream()   # rank 1's "backward": the producer of its late round
+    late = world - 1
+    side = dev.Stream()   # the late rank's "backward": the producer of its late round
     kinds = {"allreduce": comm.ALLREDUCE, "solo": comm.SOLO, "majority": comm.MAJORITY}
     out = []
     for kind, path in cases:
@@ -1944,7 +1945,7 @@ def gpu_late_peer_after_timeout(rank, world, cases, delay_s=4.0):
         comm.set_config("batch_rounds", 0 if path == "one" else -1)
         sb, rb = dev.DeviceBuffer(count, _lib.INT32), dev.DeviceBuffer(count, _lib.INT32)
         # solo with async 1: round 2 is synchronous, joined at each rank's own post (an async
-        # round would carry rank 1 through on rank 0's activation, without its producer)
+        # round would carry the late rank through on a peer's activation, without its producer)
         s_ = comm.Schedule(kinds[kind], sb, rb, count, dtype=_lib.INT32, buf=comm.BUF_DEVICE, async_=1, seed=7)
         a = [(np.arange(count) * 3 + 11 * r).astype(np.int32) for r in range(world)]
         b = [(np.arange(count) % 977 + 1000 * r + 5).astype(np.int32) for r in range(world)]
@@ -1956,7 +1957,7 @@ def gpu_late_peer_after_timeout(rank, world, cases, delay_s=4.0):
         sb.upload(b[rank])
         dist.barrier()   # gloo: esgd's own barrier times out with the 2 s limit
         t0 = time.perf_counter()
-        if rank == 1:
+        if rank == late:
             assert sw.esgd_sweep_occupy(1, int(delay_s * 1e6), side.handle) == 0
             s_.post(stream=side)
             # the host's own wait limit counts from wait(): wait only shortly before the GPU

@@ -786,14 +786,38 @@ def test_late_peer_after_a_timeout_never_succeeds_with_a_stale_sum():
             os.environ.pop("ESGD_TIMEOUT_S", None)
         else:
             os.environ["ESGD_TIMEOUT_S"] = old
-    r0, r1 = outs
-    for c0, c1 in zip(r0, r1):
-        assert c0["first_round_ok"] and c1["first_round_ok"], (c0, c1)
-        assert c0["failed"], c0                                  # the rank that timed out
+    _check_late_peer(outs)
+
+
+def _check_late_peer(outs):
+    *on_time, late = outs
+    for i, c1 in enumerate(late):
+        cs = [r[i] for r in on_time]
+        assert all(c["first_round_ok"] for c in cs) and c1["first_round_ok"], (cs, c1)
+        assert all(c["failed"] for c in cs), cs                  # the ranks that timed out
         assert c1["failed"] or c1["result"] == "oracle", c1      # never a stale sum
         assert c1["result"] != "WRONG", c1
-        # rank 1's outcome came from the GPU's flag protocol, not from its host wait limit
+        # the late rank's outcome came from the GPU's flag protocol, not its host wait limit
         assert c1["gpu_failure"] or c1["result"] == "oracle", c1
+
+
+@pytest.mark.skipif(not os.path.exists(SWEEPS_LIB), reason="tools/bin/libesgd_sweeps.so not built (make sweeps)")
+def test_late_peer_among_four_ranks():
+    # the same contract at P = 4, the last rank late: three ranks time out (or see a peer's
+    # error word) and fail; the late rank fails through their error words.  Allreduce only:
+    # every rank joins each of its rounds (a solo / majority round may complete without the
+    # late rank, which is its semantics, not a failure)
+    old = os.environ.get("ESGD_TIMEOUT_S")
+    os.environ["ESGD_TIMEOUT_S"] = "1.5"
+    try:
+        outs = run("gpu_late_peer_after_timeout", 4, cases=[("allreduce", "batched"), ("allreduce", "five")],
+                   delay_s=3.0, timeout=140)
+    finally:
+        if old is None:
+            os.environ.pop("ESGD_TIMEOUT_S", None)
+        else:
+            os.environ["ESGD_TIMEOUT_S"] = old
+    _check_late_peer(outs)
 
 
 @pytest.mark.parametrize("delete_first", [False, True])
