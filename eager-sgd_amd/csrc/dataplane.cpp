@@ -402,7 +402,7 @@ static void *host_view(void *host) {
 // errs: every rank's error word (the node segment); after_fail: a pairing after the round's
 // first publishes nothing once this rank's error word holds the round (failure contract)
 int round_sync(const PairFlags &f, int world, int rank, uint32_t value, long long timeout_ticks,
-               uint32_t *errs, uint32_t errval, uint32_t *failw, bool after_fail, uint64_t *ts, uint32_t *gate,
+               uint32_t *errs, uint32_t errval, uint32_t *failw, bool after_fail, uint64_t *ts, bool drop_peer_lines,
                uint32_t *fin, hipStream_t s);
 
 // ---- device pairing flags (schedules with flag_mode 1 or 2, opt-in) ----
@@ -499,15 +499,13 @@ static int pair_ranks(Sched &s, std::atomic<uint32_t> *flags, int which, uint32_
     const long long ticks = (long long)(engine_timeout() * double(g_ticks_per_s));
     uint64_t *ts = gpu_trace_on() ? reinterpret_cast<uint64_t *>(dev_flag(&s.sh->gpu_ts[s.rank][2 * which]))
                                   : nullptr;
-    // the ready and reduced pairings are followed by a phase that reads peer buckets:
-    // their launch also drops stale peer lines from every XCD's caches (gate words 4, 5
-    // of the schedule's device counters)
+    // the ready and reduced pairings are followed by a phase that reads peer buckets: a
+    // kernel behind each drops stale peer lines from every XCD's caches
     uint32_t *ctr = nullptr;
     if (int rc = ctr_words(s.id, cs, &ctr)) return rc;
-    uint32_t *gate = which < 2 ? ctr + 4 + which : nullptr;
     // word 12: the round whose pairing failed here (the later pairings then publish nothing)
     return round_sync(pair_flags(s, flags, which), s.world, s.rank, value ? value : round, ticks,
-                      dev_flag(&s.sh->gpu_err[0]), round, ctr + 12, which > 0, ts, gate,
+                      dev_flag(&s.sh->gpu_err[0]), round, ctr + 12, which > 0, ts, which < 2,
                       fin ? dev_flag(fin) : nullptr, cs);
 }
 
@@ -529,7 +527,8 @@ void gpu_trace_read(Sched &s, uint64_t out[6]) {
 void rccl_shutdown();
 
 // Per-schedule device words -- k_round_small's two arrival counters and two gates
-// ([0..3]), the five-launch round's cache-maintenance gates ([4], [5]), the batched
+// ([0..3]), two unused ([4], [5]: the five-launch round's cache-maintenance gates until round
+// 6), the batched
 // rounds' words ([6..11], BatchDesc::ctr) and the five-launch round's failed round ([12]) -- one
 // allocation for the process: a hipMalloc per schedule, on the round path, is avoided
 // (host-side memory operations were seen to slow later peer-reading kernels).

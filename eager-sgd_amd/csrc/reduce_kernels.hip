@@ -705,16 +705,23 @@ __device__ __forceinline__ void publish_flags_drained(const PairFlags &f, uint32
     for (int q = 0; q < f.ndst; ++q) __hip_atomic_store(f.dst[q], value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-//
-//
 // Peer buckets are coarse-grained memory of other processes (other GPUs on a node).  When
-// the phase after this pairing reads peers (`gate` != nullptr), every XCD's L2 (and the
-// L1 of every CU used) must first drop whatever lines of them it may still hold from an
-// earlier round: the launch then has one workgroup per CU (dealt round-robin over the
-// XCDs); workgroup 0 runs the pairing and raises the device word `gate` to `value`, the
-// others wait for it and run a system-scope acquire (buffer_inv sc0 sc1).  The dispatch's
-// own acquire scope is not relied on for this.  A failed pairing still raises the gate
-// (the error word fails the round), so no workgroup is left waiting.
+// the phase after a pairing reads peers, every XCD's L2 (and the L1 of every CU used) must
+// first drop whatever lines of them it may still hold from an earlier round -- AFTER the
+// pairing saw the peers' flags (on a shared GPU another rank's kernel may re-cache a peer's
+// old lines until then).  k_drop_peer_lines, queued right behind the pairing on its stream,
+// does it: one workgroup per CU (dealt round-robin over the XCDs), each a system-scope
+// acquire (buffer_inv sc0 sc1), none waiting for anything.  The dispatch's own acquire scope
+// is not relied on for this.  (Until round 6 these were workgroups of the pairing launch
+// itself, spinning on a device gate while the pairing waited for its peers: 256 wave slots
+// held per rank for as long as the slowest peer took -- on a GPU shared by 8 ranks, slots
+// the peers' own kernels needed to reach the flags they were waiting for (DESIGN.md §5,
+// r04zp, r06p).)
+__global__ void __launch_bounds__(64) k_drop_peer_lines() {
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+// One lane pairs the ranks: publish this rank's flag, wait for every rank's.
 // Failure contract: `errs` = every rank's error word (this rank's is errs[rank]); a failed
 // pairing also records the round in `failw`, a device word of the schedule, and a pairing
 // after the round's first (`after_fail`: reduced, done) publishes nothing when failw holds
@@ -724,19 +731,8 @@ __device__ __forceinline__ void publish_flags_drained(const PairFlags &f, uint32
 __global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world, int rank,
                                                    uint32_t value, long long timeout,
                                                    uint32_t *errs, uint32_t errval, uint32_t *failw, int after_fail,
-                                                   uint64_t *ts, uint32_t *gate, uint32_t *fin) {
+                                                   uint64_t *ts, uint32_t *fin) {
     const bool lead = threadIdx.x == 0;
-    if (blockIdx.x != 0) {   // cache maintenance only
-        if (lead) {
-            const long long t0 = wall_clock64();
-            while (int32_t(__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - value) < 0) {
-                if (wall_clock64() - t0 > timeout) break;
-                __builtin_amdgcn_s_sleep(2);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        }
-        return;
-    }
     uint32_t *err = errs + rank;
     __shared__ int failed;
     if (lead) {
@@ -745,10 +741,7 @@ __global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world, int r
         if (!failed) publish_flags(f, value);
     }
     __syncthreads();
-    if (failed) {   // nothing published, nothing waited for; the waiting workgroups leave
-        if (lead && gate) __hip_atomic_store(gate, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
+    if (failed) return;   // nothing published, nothing waited for
     const long long t0 = wall_clock64();
     const bool ok = wave_wait_all(f.mine, world, value, t0, timeout, errs, errval);
     if (!lead) return;
@@ -757,7 +750,6 @@ __global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world, int r
         __hip_atomic_store(err, errval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    if (gate) __hip_atomic_store(gate, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ok && ts) __hip_atomic_store(&ts[1], uint64_t(wall_clock64()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // the round's last kernel reports completion itself (the host polls fin, not an event)
     if (ok && fin) {
@@ -768,16 +760,20 @@ __global__ void __launch_bounds__(64) k_round_sync(PairFlags f, int world, int r
 
 // ts (optional): wall-clock stamps of entry and exit (tracing, ESGD_GPU_TRACE=1);
 // errval: what a timed-out wait records in *err (the round, also when `value` numbers
-// a chunk of it)
+// a chunk of it); drop_peer_lines: the next phase reads peer memory (k_drop_peer_lines after)
 int round_sync(const PairFlags &f, int world, int rank, uint32_t value, long long timeout_ticks,
-               uint32_t *errs, uint32_t errval, uint32_t *failw, bool after_fail, uint64_t *ts, uint32_t *gate,
+               uint32_t *errs, uint32_t errval, uint32_t *failw, bool after_fail, uint64_t *ts, bool drop_peer_lines,
                uint32_t *fin, hipStream_t s) {
     ESGD_ARG(f.mine && errs && failw && world >= 1 && world <= kPairMax && rank >= 0 && rank < world &&
                  f.ndst >= 1 && f.ndst <= kPairMax,
              "round_sync: bad arguments");
-    hipLaunchKernelGGL(k_round_sync, dim3(gate ? unsigned(cu_count()) : 1u), dim3(64), 0, s, f, world, rank,
-                       value, timeout_ticks, errs, errval, failw, after_fail ? 1 : 0, ts, gate, fin);
+    hipLaunchKernelGGL(k_round_sync, dim3(1), dim3(64), 0, s, f, world, rank, value, timeout_ticks, errs, errval,
+                       failw, after_fail ? 1 : 0, ts, fin);
     ESGD_HIP(hipGetLastError());
+    if (drop_peer_lines) {
+        hipLaunchKernelGGL(k_drop_peer_lines, dim3(unsigned(cu_count())), dim3(64), 0, s);
+        ESGD_HIP(hipGetLastError());
+    }
     return ESGD_SUCCESS;
 }
 

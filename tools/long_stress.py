@@ -28,8 +28,16 @@ def main():
     ap.add_argument("--fail-exports", default=None,
                     help="per rank, comma-separated: that many of its first chunk exports fail (the runtime's refusals)")
     ap.add_argument("--kinds", default="solo,majority")
+    ap.add_argument("--diag-dir", default=os.path.join(ROOT, "gpurun_out", "long_stress_diag"),
+                    help="every rank's step every 50 steps (progress.txt) and Python stacks every 60 s "
+                         "(stacks/): a stall leaves evidence, and a slow run keeps writing")
     a = ap.parse_args()
     os.environ["ESGD_STRICT_HANDOFFS"] = str(a.strict)
+    if a.diag_dir:   # inherited by the spawned ranks (r06p: a run silent for 180 s left nothing)
+        os.makedirs(a.diag_dir, exist_ok=True)
+        os.environ.setdefault("ESGD_PROGRESS_FILE", os.path.join(a.diag_dir, "progress.txt"))
+        os.environ.setdefault("ESGD_HANG_DUMP_DIR", os.path.join(a.diag_dir, "stacks"))
+        os.environ.setdefault("ESGD_HANG_DUMP_S", "60")
     if a.pipelined:
         return pipelined(a)
     if a.device_flags:
