@@ -1335,8 +1335,9 @@ static int batch_flush_locked() {
     // counter), but the stream's next launch starts only once every workgroup of this one
     // was dispatched and left -- so the grid is kept to what the GPU can hold beside the
     // other ranks' launches: with 8 ranks on one GPU, 8 x 65 workgroups of the fan-in-8
-    // kernel (2 per CU) were all of it, and the five-launch rounds' spinning pairing
-    // kernels left some launch short (r04zp).  Ranks sharing a GPU get half
+    // kernel (2 per CU) were all of it, and the five-launch rounds' pairing kernels (then
+    // 256 spinning workgroups each; one since round 6) left some launch short (r04zp,
+    // DESIGN.md §5).  Ranks sharing a GPU get half
     // their share; one rank per GPU keeps kBatchWorkers (far below the chip's capacity).
     const int capacity = round_batch_capacity(g_pend[0].s->dtype, g_pend[0].s->world);
     const int sharing = ranks_on_my_device();
