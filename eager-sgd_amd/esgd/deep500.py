@@ -299,6 +299,13 @@ class AllreduceModule(_module_base()):
     def is_cuda_supported(self) -> bool:
         return self.op.supports_cuda()
 
+    def close(self):
+        """Unregister the op and delete it (its schedule: collective once a round ran, so every
+        rank closes its modules in the same order, as AllreduceOp.close)."""
+        if self.op.handle:
+            _LIVE.pop(self.op.handle, None)
+            self.op.close()
+
     def forward(self, grad, last=None):
         import torch
         return torch.ops.esgd.allreducef(grad, grad if last is None else last, self.op.handle, self.divisor)

@@ -736,6 +736,8 @@ def op_torch_registered(rank, world, shapes=((1000,), (64, 33), (4099,))):
             ok.append(bool(np.array_equal(got.view(np.uint32), want.view(np.uint32))))
             ok.append(bool(torch.count_nonzero(i.grad).item() == 0))
     comm.barrier()
+    for m in mods:   # every rank in the same order: the schedules' deletion is collective
+        m.close()
     comm.finalize()
     return {"ok": ok, "nodes": nodes}
 

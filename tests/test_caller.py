@@ -69,3 +69,7 @@ def test_registered_torch_op_sits_in_traced_graphs():
     with FakeTensorMode():
         y = torch.ops.esgd.allreducef(torch.empty(4, 3), torch.empty(4, 3), ar.op.handle, 2.0)
     assert tuple(y.shape) == (4, 3) and y.dtype == torch.float32
+    handle = ar.op.handle
+    ar.close()   # unregistered: the operator no longer reaches it
+    with pytest.raises(RuntimeError, match="no live op"):
+        torch.ops.esgd.allreducef(torch.ones(4, 3), torch.ones(4, 3), handle, 2.0)
