@@ -348,22 +348,38 @@ static void *ffref_c1_main(void *p) {
  * reference's ff.c:72 starts one progress pthread beside each MPI rank): rank r's progress
  * thread on cpus[2r], its main thread on cpus[2r + 1] (cpus NULL or ncpus < 2P: unpinned,
  * the scheduler's choice -- round 5's figures moved 1.7x between boxes that way). */
-static void ffref_pin(pthread_t t, const int *cpus, int ncpus, int i) {
-    if (!cpus || i >= ncpus) return;
-    cpu_set_t set;
-    CPU_ZERO(&set);
-    CPU_SET(cpus[i], &set);
-    (void)pthread_setaffinity_np(t, sizeof(set), &set);
+static void ffref_start(pthread_t *t, void *(*fn)(void *), void *arg, const int *cpus, int i) {
+    pthread_attr_t at;
+    pthread_attr_init(&at);
+    if (cpus) {   /* pinned from its first instruction, not after the create */
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        CPU_SET(cpus[i], &set);
+        (void)pthread_attr_setaffinity_np(&at, sizeof(set), &set);
+    }
+    pthread_create(t, &at, fn, arg);
+    pthread_attr_destroy(&at);
 }
 
 double ffref_time_c1_pinned(int P, uint32_t count, int reps, const int *cpus, int ncpus, int *ok) {
     if (P < 1 || P > 64 || reps < 1) return -1.0;
     if (ncpus < 2 * P) cpus = NULL;
     const size_t bytes = (size_t)count * 4;
+    /* the buffers are allocated and first touched (Linux places a page on the NUMA node of
+     * the CPU that first writes it) by this thread pinned to the ranks' cores for the while,
+     * so they sit on those cores' node, not on whichever node the caller happened to run */
+    cpu_set_t caller, ranks;
+    const int repin = cpus && pthread_getaffinity_np(pthread_self(), sizeof(caller), &caller) == 0;
+    if (repin) {
+        CPU_ZERO(&ranks);
+        for (int i = 0; i < 2 * P; ++i) CPU_SET(cpus[i], &ranks);
+        (void)pthread_setaffinity_np(pthread_self(), sizeof(ranks), &ranks);
+    }
     float *bufs[5][64];
     for (int k = 0; k < 5; ++k)
         for (int r = 0; r < P; ++r) { bufs[k][r] = (float *)malloc(bytes ? bytes : 4); memset(bufs[k][r], 0, bytes); }
     for (int r = 0; r < P; ++r) ffref_fill_uniform_f32(0x5EEDE56Dull, r, bufs[3][r], count);
+    if (repin) (void)pthread_setaffinity_np(pthread_self(), sizeof(caller), &caller);
     volatile int posted[64] = {0}, done[64] = {0}, ready[64] = {0}, taken[64] = {0}, stop = 0;
     pthread_barrier_t bar;
     pthread_barrier_init(&bar, NULL, (unsigned)P);
@@ -372,10 +388,8 @@ double ffref_time_c1_pinned(int P, uint32_t count, int reps, const int *cpus, in
     for (int r = 0; r < P; ++r) {
         args[r] = (ffref_c1_arg){P, r, reps, count, bufs[0], bufs[1], bufs[2], bufs[3], bufs[4],
                                  posted, done, ready, taken, &bar, &stop};
-        pthread_create(&th[2 * r], NULL, ffref_c1_progress, &args[r]);
-        pthread_create(&th[2 * r + 1], NULL, ffref_c1_main, &args[r]);
-        ffref_pin(th[2 * r], cpus, ncpus, 2 * r);
-        ffref_pin(th[2 * r + 1], cpus, ncpus, 2 * r + 1);
+        ffref_start(&th[2 * r], ffref_c1_progress, &args[r], cpus, 2 * r);
+        ffref_start(&th[2 * r + 1], ffref_c1_main, &args[r], cpus, 2 * r + 1);
     }
     for (int i = 0; i < 2 * P; ++i) pthread_join(th[i], NULL);
     pthread_barrier_destroy(&bar);
