@@ -818,11 +818,18 @@ struct SmallRoundArgs {
     int strict;
 };
 
+// err (optional): a word that holds `value` once the round failed elsewhere in this kernel
+// (the leader's peer wait), checked every 64th poll -- a wait that can no longer succeed
+// ends then, not at the timeout
 __device__ __forceinline__ bool spin_all(uint32_t *flags, int world, uint32_t value, long long t0,
-                                         long long timeout) {
+                                         long long timeout, const uint32_t *err = nullptr) {
+    unsigned polls = 0;
     for (int q = 0; q < world; ++q) {
         while (int32_t(__hip_atomic_load(&flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - value) < 0) {
             if (wall_clock64() - t0 > timeout) return false;
+            if (err && (++polls & 63u) == 0 &&
+                __hip_atomic_load(const_cast<uint32_t *>(err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == value)
+                return false;
             __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -847,7 +854,8 @@ __device__ __forceinline__ bool block_wait(const SmallRoundArgs &a, const uint32
                 else __hip_atomic_store(gate, a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         } else if (threadIdx.x == 0) {
-            good = spin_all(gate, 1, a.value, t0, a.timeout);
+            // the leader records a failed wait in this rank's error word and raises no gate
+            good = spin_all(gate, 1, a.value, t0, a.timeout, a.err);
         }
         if (threadIdx.x == 0) {
             if (good) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
