@@ -125,6 +125,21 @@ def _cpu_model():
     return None
 
 
+def run_labels(world: int, devs, transport: str) -> dict:
+    """config.parallelism and config.transport from the devices the ranks actually used
+    (VERDICT r05 item 5): ranks sharing one GPU are a rehearsal, whose bytes never cross xGMI."""
+    n = len(set(devs))
+    if n == 1 and world > 1:
+        par, where = f"dp{world} ({world} ranks on one GPU: rehearsal)", "in one GPU's HBM"
+    elif n < world:
+        par, where = f"dp{world} ({world} ranks on {n} GPUs, shared)", "over xGMI and within shared GPUs' HBM"
+    else:
+        par, where = f"dp{world} (one rank per GPU)", "over xGMI"
+    if transport == "rccl":
+        return {"parallelism": par, "transport": "rccl p2p send/recv + tree kernel on a side stream"}
+    return {"parallelism": par, "transport": "ipc pull (reduce-scatter tree kernel + all-gather) " + where}
+
+
 def _baseline_cpus(P: int):
     """2P cores for the CPU baseline's P simulated ranks: the first 2P physical cores of this
     process's affinity set in id order (one thread of each SMT pair; rank r on the (2r,
@@ -1668,12 +1683,7 @@ def run_allreduce(args, rank, world):
                                f"{args.dtype} bucket per GPU, in place",
                    "bucket_bytes": S,
                    # what ran, from the ranks' devices: a 1-GPU rehearsal is labelled as one
-                   "parallelism": (f"dp{world} ({world} ranks on one GPU: rehearsal)" if len(set(devs)) == 1
-                                   else f"dp{world} ({world} ranks on {len(set(devs))} GPUs, shared)" if SHARED_GPU
-                                   else f"dp{world} (one rank per GPU)"),
-                   "transport": ("rccl p2p send/recv + tree kernel on a side stream" if transport == "rccl"
-                                 else "ipc pull (reduce-scatter tree kernel + all-gather) " +
-                                 ("in one GPU's HBM" if SHARED_GPU else "over xGMI"))},
+                   **run_labels(world, devs, transport)},
         "algbw_GBs": round(algbw, 2), "busbw_GBs": round(busbw, 2),
         "xgmi_frac": None if SHARED_GPU else round(t_min / t_step, 4),
         "roofline": None if SHARED_GPU else {

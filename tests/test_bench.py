@@ -7,6 +7,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 from conftest import ROOT
 
 PROBE = r"""
@@ -86,3 +88,59 @@ def test_rank_stdout_carries_only_the_json_line():
     assert lines[0] == "python chatter before"
     assert [json.loads(x) for x in lines[1:]] == [{"metric": "m", "value": 1.0}]
     assert "[Gloo]" in r.stderr and "chatter after" in r.stderr
+
+
+def test_run_labels_follow_the_devices():
+    # the line says what ran -- ranks sharing one GPU are a rehearsal
+    import bench
+    assert bench.run_labels(2, [0, 0], "ipc") == {
+        "parallelism": "dp2 (2 ranks on one GPU: rehearsal)",
+        "transport": "ipc pull (reduce-scatter tree kernel + all-gather) in one GPU's HBM"}
+    one = bench.run_labels(8, list(range(8)), "ipc")
+    assert one["parallelism"] == "dp8 (one rank per GPU)" and one["transport"].endswith("over xGMI")
+    mixed = bench.run_labels(4, [0, 0, 1, 1], "ipc")
+    assert mixed["parallelism"] == "dp4 (4 ranks on 2 GPUs, shared)" and "shared GPUs" in mixed["transport"]
+    assert bench.run_labels(2, [0, 1], "rccl")["transport"].startswith("rccl p2p")
+
+
+def test_baseline_cpus_one_thread_per_physical_core():
+    # the CPU baseline's core list: 2 cores per simulated rank, never two SMT siblings
+    import bench
+    allowed = sorted(os.sched_getaffinity(0))
+    cores = bench._baseline_cpus(1)
+    if cores is None:
+        pytest.skip("fewer than 2 physical cores here")
+    assert len(cores) == 2 and len(set(cores)) == 2 and set(cores) <= set(allowed)
+
+    def siblings(c):
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                return f.read().strip()
+        except OSError:
+            return str(c)
+    assert siblings(cores[0]) != siblings(cores[1])
+    assert bench._baseline_cpus(10 ** 6) is None      # more than the host has: unpinned
+
+
+def test_pinned_c1_harness_is_correct_and_pinned():
+    # the oracle's C1-shaped harness with its threads on given cores: the every-rank result
+    # is the tree's; pinning changes only placement
+    import bench
+    from oracle import ffref
+    cores = bench._baseline_cpus(2)
+    if cores is None:
+        pytest.skip("fewer than 4 physical cores here")
+    t, ok = ffref.time_c1(2, 4096, 3, cpus=cores)
+    assert ok and t > 0
+
+
+def test_wait_until_reaches_its_deadline():
+    # the straggler's delay (mp_workers.wait_until): asleep but for the last 2 ms, never early
+    import time
+
+    from mp_workers import wait_until
+    for d in (0.0005, 0.01):
+        t0 = time.perf_counter()
+        wait_until(t0 + d)
+        el = time.perf_counter() - t0
+        assert d <= el < d + 0.02, (d, el)
