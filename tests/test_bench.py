@@ -1,7 +1,9 @@
-"""bench.py's launcher logic on the CPU (no device): a bare `bench.py --gpus N` must start
+"""bench.py's host logic on the CPU (no device): a bare `bench.py --gpus N` must start
 its own N ranks through torch.distributed.run -- before anything in the parent loads the
 HIP library -- and exit with their status (the reference's launcher
-starts its ranks the same way, test_scripts_imagenet/daint_eagersgd_imagenet.sh:2-5)."""
+starts its ranks the same way, test_scripts_imagenet/daint_eagersgd_imagenet.sh:2-5); the
+line's device-derived labels, the CPU baseline's core list and pinned harness, and the
+straggler's deadline wait (round 6)."""
 import json
 import os
 import subprocess
