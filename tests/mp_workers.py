@@ -123,8 +123,10 @@ def wait_until(deadline: float):
 
 
 def set_test_knobs(**knobs):
-    """The library's test hooks (ESGD_TEST, read at each use: runtime.cpp test_knob): e.g.
-    set_test_knobs(fail_exports=2, shadow=1); None values are left out."""
+    """The library's test hooks (ESGD_TEST, runtime.cpp test_knob): most are read once per
+    process, at the hook's first use, so set them before the first schedule (fail_connect is
+    read at every creation); e.g. set_test_knobs(fail_exports=2, shadow=1); None values are
+    left out."""
     have = dict(kv.split("=", 1) for kv in os.environ.get("ESGD_TEST", "").split(",") if "=" in kv)
     have.update({k: str(int(v)) for k, v in knobs.items() if v is not None})
     os.environ["ESGD_TEST"] = ",".join(f"{k}={v}" for k, v in have.items())
