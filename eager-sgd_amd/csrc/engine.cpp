@@ -249,6 +249,13 @@ static std::string sched_state(Sched &s) {
 
 static void fail_locked(Sched &s, int rc, const char *msg) {
     if (s.roctx_round) { roctxRangeStop(s.roctx_round); s.roctx_round = 0; }
+    // the failure contract across ranks: a round this rank joined and has not
+    // completed fails on every rank now -- peers' GPU flag waits and host queries watch this
+    // word -- rather than at their own timeouts.  A failure on the host side (a launch, a
+    // join, the wait limit) runs no kernel that would have recorded it; where the GPU did,
+    // it stored this same round.
+    if (s.world > 1 && s.sh && int32_t(s.cur - s.completed) > 0)
+        s.sh->gpu_err[s.rank].store(s.cur, std::memory_order_release);
     s.error = rc ? rc : ESGD_ERROR;
     snprintf(s.errmsg, sizeof(s.errmsg), "schedule %d round %u: %s", s.id, s.cur, msg);
     s.cv.notify_all();
