@@ -527,9 +527,9 @@ void gpu_trace_read(Sched &s, uint64_t out[6]) {
 void rccl_shutdown();
 
 // Per-schedule device words -- k_round_small's two arrival counters and two gates
-// ([0..3]), two unused ([4], [5]: the five-launch round's cache-maintenance gates until round
-// 6), the batched
-// rounds' words ([6..11], BatchDesc::ctr) and the five-launch round's failed round ([12]) -- one
+// ([0..3]), two unused ([4], [5]: the five-launch round's cache-maintenance gates until
+// round 6), the batched rounds' words ([6..11], BatchDesc::ctr) and the five-launch
+// round's failed round ([12]) -- one
 // allocation for the process: a hipMalloc per schedule, on the round path, is avoided
 // (host-side memory operations were seen to slow later peer-reading kernels).
 static uint32_t *g_ctr_pool = nullptr;
@@ -1337,8 +1337,8 @@ static int batch_flush_locked() {
     // other ranks' launches: with 8 ranks on one GPU, 8 x 65 workgroups of the fan-in-8
     // kernel (2 per CU) were all of it, and the five-launch rounds' pairing kernels (then
     // 256 spinning workgroups each; one since round 6) left some launch short (r04zp,
-    // DESIGN.md §5).  Ranks sharing a GPU get half
-    // their share; one rank per GPU keeps kBatchWorkers (far below the chip's capacity).
+    // DESIGN.md §5).  Ranks sharing a GPU get half their share; one rank per GPU keeps
+    // kBatchWorkers (far below the chip's capacity).
     const int capacity = round_batch_capacity(g_pend[0].s->dtype, g_pend[0].s->world);
     const int sharing = ranks_on_my_device();
     const int cap = capacity / (sharing > 1 ? 2 * sharing : 1) - 1;
